@@ -1,0 +1,93 @@
+"""ctypes binding of libbcosgpu.so (include/bcos_gpu.h).
+
+The product path is the HIP library: if it is missing or cannot be loaded this module raises --
+there is no CPU fallback anywhere in the package.
+"""
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libbcosgpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "bcos_gpu.h")
+
+OK, E_ARG, E_HIP, E_NODEV, E_EMPTY = 0, -1, -2, -3, -4
+KECCAK256, SM3 = 0, 1
+SUITE_SECP256K1, SUITE_SM2 = 0, 1
+MERKLE_NEW, MERKLE_OLD = 0, 1
+
+
+class BcosGpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"bcosgpu error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+_P = ctypes.c_void_p
+_U8P = ctypes.c_char_p
+_SZ = ctypes.c_size_t
+_I = ctypes.c_int
+
+_SIGS = {
+    "bcosgpu_version": (_I, []),
+    "bcosgpu_device_count": (_I, []),
+    "bcosgpu_init": (_I, [_I]),
+    "bcosgpu_last_error": (ctypes.c_char_p, []),
+    "bcosgpu_merkle_size": (ctypes.c_uint64, [ctypes.c_uint64, _I]),
+    "bcosgpu_hash_batch": (_I, [_I, _P, _P, _SZ, _P]),
+    "bcosgpu_keccak256_batch": (_I, [_P, _P, _SZ, _P]),
+    "bcosgpu_sm3_batch": (_I, [_P, _P, _SZ, _P]),
+    "bcosgpu_hash_batch_dev": (_I, [_I, _P, _P, _SZ, _P, _P]),
+    "bcosgpu_merkle_root": (_I, [_I, _I, _I, _P, _SZ, _P, _P]),
+    "bcosgpu_merkle_root_dev": (_I, [_I, _I, _P, _SZ, _P, _P, _P]),
+    "bcosgpu_secp256k1_recover_batch": (_I, [_P, _P, _SZ, _P, _P, _P]),
+    "bcosgpu_secp256k1_recover_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P, _P]),
+    "bcosgpu_sm2_verify_batch": (_I, [_P, _P, _SZ, _P, _P]),
+    "bcosgpu_sm2_verify_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P]),
+    "bcosgpu_secp256k1_sign_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P, _P]),
+    "bcosgpu_sm2_sign_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P]),
+    "bcosgpu_tx_verify_batch": (_I, [_I, _P, _P, _P, _P, _SZ, _P, _P, _P]),
+    "bcosgpu_tx_verify_batch_dev": (_I, [_I, _P, _P, _P, _P, _SZ, _P, _P, _P, _P]),
+    "bcosgpu_wedpr_secp256k1_recover_public_key": (ctypes.c_int8, [_P, _P, _P]),
+    "bcosgpu_wedpr_sm2_verify": (ctypes.c_int8, [_P, _P, _P]),
+}
+
+
+def header_symbols():
+    """Every function declared in include/bcos_gpu.h."""
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(bcosgpu_\w+)\s*\(", text)))
+
+
+def lib():
+    """Load libbcosgpu.so (raises OSError when the HIP build is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} not built: run `make -C fisco-bcos_amd` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise BcosGpuError(rc, lib().bcosgpu_last_error().decode(errors="replace"))
+    return rc
+
+
+_inited = set()
+
+
+def ensure_device(device=0):
+    """Initialise the engine on `device` (fails loudly without a gfx950 GPU)."""
+    if device not in _inited:
+        check(lib().bcosgpu_init(device))
+        _inited.add(device)

@@ -1,0 +1,231 @@
+"""Host-side mirror of the reference's crypto interfaces, backed by the HIP engine.
+
+Mirrors (same names, argument meaning and error behaviour):
+  bcos::crypto::Hash / Keccak256 / SM3         bcos-crypto/bcos-crypto/interfaces/crypto/Hash.h:37-72,
+                                               hash/Keccak256.h:39-51, hash/SM3.h:39-50
+  bcos::crypto::SignatureCrypto::recover/verify interfaces/crypto/Signature.h:40-58
+    Secp256k1Crypto                            signature/secp256k1/Secp256k1Crypto.{h,cpp}
+    SM2Crypto / FastSM2Crypto                  signature/sm2/SM2Crypto.cpp:66-92, fastsm2/FastSM2Crypto.h
+  bcos::crypto::merkle::Merkle<Hasher,width>   merkle/Merkle.h:36-262 (generateMerkle :170-208)
+  bcos::protocol::calculateMerkleProofRoot     bcos-protocol/bcos-protocol/ParallelMerkleProof.cpp:32-69
+  bcos::crypto::CryptoSuite::calculateAddress  interfaces/crypto/CryptoSuite.h:56-59
+Single-item calls keep the reference's exception semantics (recover raises InvalidSignature, an empty
+Merkle input raises ValueError like std::invalid_argument); *_batch calls return per-item verdicts.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ensure_device, lib
+
+
+class InvalidSignature(Exception):
+    """bcos::crypto::InvalidSignature (signature/Exceptions.h)."""
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _u8(a, shape=None):
+    a = np.ascontiguousarray(np.frombuffer(a, dtype=np.uint8) if isinstance(a, (bytes, bytearray)) else a,
+                             dtype=np.uint8)
+    return a if shape is None else a.reshape(shape)
+
+
+def pack_messages(msgs):
+    """list[bytes] -> (flat uint8 array, uint64 offsets[n+1])"""
+    offsets = np.zeros(len(msgs) + 1, dtype=np.uint64)
+    if msgs:
+        offsets[1:] = np.cumsum([len(m) for m in msgs], dtype=np.uint64)
+    data = np.frombuffer(b"".join(msgs), dtype=np.uint8) if msgs else np.zeros(0, dtype=np.uint8)
+    return np.ascontiguousarray(data), offsets
+
+
+class Hash:
+    """bcos::crypto::Hash: hash(bytesConstRef) -> h256 (Hash.h:44)."""
+    HASH_SIZE = 32
+    kind = None
+
+    def hash(self, data: bytes) -> bytes:
+        return self.hash_batch([bytes(data)])[0]
+
+    def hash_batch(self, msgs):
+        out = self.hash_packed(*pack_messages(list(msgs)))
+        return [out[i].tobytes() for i in range(len(msgs))]
+
+    def hash_packed(self, data, offsets):
+        """data: uint8[...], offsets: uint64[n+1] -> uint8[n, 32]"""
+        ensure_device()
+        n = len(offsets) - 1
+        out = np.zeros((n, 32), dtype=np.uint8)
+        if n:
+            d = data if len(data) else np.zeros(1, dtype=np.uint8)
+            check(lib().bcosgpu_hash_batch(self.kind, _ptr(d), _ptr(offsets), n, _ptr(out)))
+        return out
+
+    def empty_hash(self):
+        return self.hash(b"")
+
+
+class Keccak256(Hash):
+    kind = _lib.KECCAK256
+
+
+class SM3(Hash):
+    kind = _lib.SM3
+
+
+def right160(h: bytes) -> bytes:
+    """bcos::right160 (bcos-utilities/bcos-utilities/FixedBytes.h:666-671)."""
+    return h[12:32]
+
+
+class Merkle:
+    """bcos::crypto::merkle::Merkle<Hasher, width> (Merkle.h:36); default width 2 (Merkle.h:36)."""
+
+    def __init__(self, hasher: Hash, width: int = 2):
+        if width < 2:
+            raise ValueError("Width too short, at least 2")
+        self.hasher, self.width = hasher, width
+
+    def generate_merkle(self, origin_hashes):
+        """generateMerkle (Merkle.h:170-208) -> the output vector as a list of 32-byte entries."""
+        leaves = _u8(b"".join(bytes(h) for h in origin_hashes)).reshape(-1, 32)
+        n = leaves.shape[0]
+        if n == 0:
+            raise ValueError("Empty input")
+        ensure_device()
+        size = int(lib().bcosgpu_merkle_size(n, self.width))
+        levels = np.zeros((size, 32), dtype=np.uint8)
+        root = np.zeros(32, dtype=np.uint8)
+        check(lib().bcosgpu_merkle_root(self.hasher.kind, self.width, _lib.MERKLE_NEW, _ptr(leaves), n,
+                                        _ptr(root), _ptr(levels)))
+        return [levels[i].tobytes() for i in range(size)]
+
+    def root(self, leaves):
+        """Root only (last element of generateMerkle's output); leaves: uint8[n,32] or list of bytes."""
+        leaves = _u8(b"".join(bytes(h) for h in leaves) if isinstance(leaves, list) else leaves).reshape(-1, 32)
+        n = leaves.shape[0]
+        if n == 0:
+            raise ValueError("Empty input")
+        ensure_device()
+        root = np.zeros(32, dtype=np.uint8)
+        check(lib().bcosgpu_merkle_root(self.hasher.kind, self.width, _lib.MERKLE_NEW, _ptr(leaves), n,
+                                        _ptr(root), None))
+        return root.tobytes()
+
+
+def calculate_merkle_proof_root(hasher: Hash, leaves) -> bytes:
+    """protocol::calculateMerkleProofRoot (ParallelMerkleProof.cpp:32-69)."""
+    leaves = _u8(b"".join(bytes(h) for h in leaves) if isinstance(leaves, list) else leaves).reshape(-1, 32)
+    ensure_device()
+    root = np.zeros(32, dtype=np.uint8)
+    n = leaves.shape[0]
+    d = leaves if n else np.zeros((1, 32), dtype=np.uint8)
+    check(lib().bcosgpu_merkle_root(hasher.kind, 16, _lib.MERKLE_OLD, _ptr(d), n, _ptr(root), None))
+    return root.tobytes()
+
+
+class SignatureCrypto:
+    """bcos::crypto::SignatureCrypto (Signature.h:31-59)."""
+    SIG_LEN = None
+
+    def recover(self, hash32: bytes, sig: bytes) -> bytes:
+        pubs, ok = self.recover_batch(_u8(hash32, (1, 32)), [bytes(sig)])
+        if not ok[0]:
+            raise InvalidSignature("invalid signature: recover failed, msgHash : " + bytes(hash32).hex())
+        return pubs[0].tobytes()
+
+
+class Secp256k1Crypto(SignatureCrypto):
+    """Secp256k1Crypto (Secp256k1Crypto.h:37-72); recover -> wedpr_secp256k1_recover_public_key."""
+    SIG_LEN = 65
+
+    def recover_batch(self, hashes, sigs, want_address=False):
+        """hashes uint8[n,32]; sigs uint8[n,65] (or list of bytes; non-65-byte entries fail).
+        Returns (pub uint8[n,64], ok bool[n]) or (pub, addr uint8[n,20], ok) with want_address."""
+        hashes = _u8(hashes).reshape(-1, 32)
+        n = hashes.shape[0]
+        bad = np.zeros(n, dtype=bool)
+        if isinstance(sigs, list):
+            arr = np.zeros((n, 65), dtype=np.uint8)
+            for i, s in enumerate(sigs):
+                if len(s) == 65:
+                    arr[i] = np.frombuffer(bytes(s), dtype=np.uint8)
+                else:
+                    bad[i] = True
+                    arr[i, 64] = 0xFF  # any v > 3 fails
+            sigs = arr
+        sigs = _u8(sigs).reshape(n, 65)
+        pub = np.zeros((n, 64), dtype=np.uint8)
+        addr = np.zeros((n, 20), dtype=np.uint8)
+        ok = np.zeros(n, dtype=np.uint8)
+        if n:
+            ensure_device()
+            check(lib().bcosgpu_secp256k1_recover_batch(_ptr(hashes), _ptr(sigs), n, _ptr(pub),
+                                                        _ptr(addr), _ptr(ok)))
+        okb = ok.astype(bool) & ~bad
+        return (pub, addr, okb) if want_address else (pub, okb)
+
+
+class SM2Crypto(SignatureCrypto):
+    """SM2Crypto / FastSM2Crypto: recover = verify against the embedded public key (SM2Crypto.cpp:81-92)."""
+    SIG_LEN = 128
+
+    def verify(self, pub: bytes, hash32: bytes, sig: bytes) -> bool:
+        """SM2Crypto::verify (SM2Crypto.cpp:66-79): only sig[0:64] is used, with the given pub."""
+        if len(sig) < 64 or len(pub) != 64:
+            return False
+        _, ok = self.recover_batch(_u8(hash32, (1, 32)), [bytes(sig[:64]) + bytes(pub)])
+        return bool(ok[0])
+
+    def recover_batch(self, hashes, sigs, want_address=False):
+        hashes = _u8(hashes).reshape(-1, 32)
+        n = hashes.shape[0]
+        bad = np.zeros(n, dtype=bool)
+        if isinstance(sigs, list):
+            arr = np.zeros((n, 128), dtype=np.uint8)
+            for i, s in enumerate(sigs):
+                if len(s) == 128:
+                    arr[i] = np.frombuffer(bytes(s), dtype=np.uint8)
+                else:
+                    bad[i] = True  # SignatureDataWithPub: pub must be exactly 64 bytes
+            sigs = arr
+        sigs = _u8(sigs).reshape(n, 128)
+        addr = np.zeros((n, 20), dtype=np.uint8)
+        ok = np.zeros(n, dtype=np.uint8)
+        if n:
+            ensure_device()
+            check(lib().bcosgpu_sm2_verify_batch(_ptr(hashes), _ptr(sigs), n, _ptr(addr), _ptr(ok)))
+        okb = ok.astype(bool) & ~bad
+        pub = sigs[:, 64:128].copy()
+        return (pub, addr, okb) if want_address else (pub, okb)
+
+
+class CryptoSuite:
+    """bcos::crypto::CryptoSuite (CryptoSuite.h:33-67)."""
+
+    def __init__(self, hash_impl: Hash, signature_impl: SignatureCrypto):
+        self.hash_impl, self.signature_impl = hash_impl, signature_impl
+
+    def hash(self, data: bytes) -> bytes:
+        return self.hash_impl.hash(data)
+
+    def calculate_address(self, pub: bytes) -> bytes:
+        return right160(self.hash_impl.hash(pub))
+
+    @property
+    def suite(self):
+        return _lib.SUITE_SM2 if isinstance(self.signature_impl, SM2Crypto) else _lib.SUITE_SECP256K1
+
+
+def secp256k1_suite():
+    """Keccak256 + Secp256k1Crypto (ProtocolInitializer.cpp:102-124, sm_crypto = false)."""
+    return CryptoSuite(Keccak256(), Secp256k1Crypto())
+
+
+def sm_suite():
+    """SM3 + SM2 (ProtocolInitializer.cpp:102-124, sm_crypto = true)."""
+    return CryptoSuite(SM3(), SM2Crypto())

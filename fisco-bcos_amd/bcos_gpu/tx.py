@@ -1,0 +1,92 @@
+"""Transaction-side mirror: the tx-hash preimage and batched Transaction::verify.
+
+  bcostars::TransactionData fields         bcos-tars-protocol/bcos-tars-protocol/tars/Transaction.tars:2-11
+  impl_calculate<Hasher>(Transaction)      bcos-tars-protocol/bcos-tars-protocol/impl/TarsHashable.h:16-41
+      H(be32(version) || chainID || groupID || be64(blockLimit) || nonce || to || input || abi)
+  Transaction::verify                      bcos-framework/bcos-framework/protocol/Transaction.h:68-82
+  TransactionSync::importDownloadedTxs     bcos-txpool/bcos-txpool/sync/TransactionSync.cpp:496-575
+  BlockImpl::calculateTransactionRoot      bcos-tars-protocol/bcos-tars-protocol/protocol/BlockImpl.h:111-154
+"""
+import ctypes
+import struct
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ensure_device, lib
+from .crypto import CryptoSuite, Merkle, _ptr, pack_messages
+
+STATUS_NONE = 0  # TransactionStatus::None
+STATUS_INVALID_SIGNATURE = 1  # TransactionStatus::InvalidSignature (TxValidator.cpp:54-61)
+
+
+@dataclass
+class TransactionData:
+    """bcostars::TransactionData (Transaction.tars:2-11)."""
+    version: int = 0
+    chain_id: str = ""
+    group_id: str = ""
+    block_limit: int = 0
+    nonce: str = ""
+    to: str = ""
+    input: bytes = b""
+    abi: str = ""
+
+    def preimage(self) -> bytes:
+        """The bytes impl_calculate feeds the hasher, in order (TarsHashable.h:29-40)."""
+        return (struct.pack(">i", self.version) + self.chain_id.encode() + self.group_id.encode()
+                + struct.pack(">q", self.block_limit) + self.nonce.encode() + self.to.encode()
+                + bytes(self.input) + self.abi.encode())
+
+
+@dataclass
+class Transaction:
+    data: TransactionData
+    signature: bytes = b""
+    sender: bytes = b""
+
+    def hash(self, suite: CryptoSuite) -> bytes:
+        return suite.hash(self.data.preimage())
+
+
+def verify_packed(suite: CryptoSuite, pre, pre_off, sig, sig_off):
+    """Batched Transaction::verify over packed buffers.
+    Returns (txhash uint8[n,32], sender uint8[n,20], status uint8[n])."""
+    n = len(pre_off) - 1
+    txhash = np.zeros((n, 32), dtype=np.uint8)
+    sender = np.zeros((n, 20), dtype=np.uint8)
+    status = np.zeros(n, dtype=np.uint8)
+    if n:
+        ensure_device()
+        p = pre if len(pre) else np.zeros(1, dtype=np.uint8)
+        s = sig if len(sig) else np.zeros(1, dtype=np.uint8)
+        check(lib().bcosgpu_tx_verify_batch(suite.suite, _ptr(p), _ptr(pre_off), _ptr(s), _ptr(sig_off), n,
+                                            _ptr(txhash), _ptr(sender), _ptr(status)))
+    return txhash, sender, status
+
+
+def verify_transactions(suite: CryptoSuite, txs):
+    """importDownloadedTxs' parallel loop (TransactionSync.cpp:516-548) on the GPU: every tx whose
+    sender is unset is verified; tx.sender is set on success (Transaction.h:70-81).  Returns the
+    per-tx status list."""
+    todo = [i for i, t in enumerate(txs) if not t.sender]
+    status = [STATUS_NONE] * len(txs)
+    if not todo:
+        return status
+    pre, pre_off = pack_messages([txs[i].data.preimage() for i in todo])
+    sig, sig_off = pack_messages([bytes(txs[i].signature) for i in todo])
+    _, sender, st = verify_packed(suite, pre, pre_off, sig, sig_off)
+    for k, i in enumerate(todo):
+        if st[k] == 0:
+            txs[i].sender = sender[k].tobytes()
+        status[i] = int(st[k])
+    return status
+
+
+def calculate_transaction_root(suite: CryptoSuite, tx_hashes) -> bytes:
+    """BlockImpl::calculateTransactionRoot (BlockImpl.h:111-154): width-2 Merkle over the tx hashes;
+    no transactions -> the zero hash (:116-119)."""
+    if len(tx_hashes) == 0:
+        return bytes(32)
+    return Merkle(suite.hash_impl, 2).root(tx_hashes)

@@ -1,0 +1,362 @@
+// api.hip -- the C ABI (include/bcos_gpu.h): argument checks, per-device workspaces for the
+// host-pointer entry points, and the wedpr-shaped single-call shims.  No exceptions cross the ABI.
+#include <mutex>
+#include <string>
+#include <vector>
+#include <cstring>
+#include "engine.h"
+
+using namespace bcosgpu;
+
+namespace {
+
+thread_local std::string g_err;
+int set_err(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+int hip_err(hipError_t e, const char* what) {
+    return set_err(BCOSGPU_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_OK(call)                                   \
+    do {                                               \
+        hipError_t e_ = (call);                        \
+        if (e_ != hipSuccess) return hip_err(e_, #call); \
+    } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// One workspace per device for the synchronous host-pointer API; the mutex makes those entry
+// points safe to call from the reference's concurrent verifier pools (TxPool.h:48-49).
+struct Workspace {
+    std::mutex mu;
+    bool ready = false;
+    hipStream_t stream = nullptr;
+    DevBuf b[8];
+};
+std::mutex g_mu;
+std::vector<Workspace*> g_ws;
+
+int current_device(int* dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        return set_err(BCOSGPU_E_NODEV, "no HIP device visible");
+    }
+    HIP_OK(hipGetDevice(dev));
+    return 0;
+}
+
+int get_ws(Workspace** out) {
+    int dev = 0;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    rc = bcosgpu_init(dev);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(g_mu);
+    *out = g_ws[dev];
+    return 0;
+}
+
+inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
+
+}  // namespace
+
+extern "C" {
+
+int bcosgpu_version(void) { return BCOSGPU_VERSION; }
+
+int bcosgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+const char* bcosgpu_last_error(void) { return g_err.c_str(); }
+
+uint64_t bcosgpu_merkle_size(uint64_t n, int width) {
+    if (width < 2) return 0;
+    return n == 1 ? 1 : merkle_size(n, width);
+}
+
+int bcosgpu_init(int device) {
+    int n = bcosgpu_device_count();
+    if (n <= 0) return set_err(BCOSGPU_E_NODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return set_err(BCOSGPU_E_ARG, "device index out of range");
+    HIP_OK(hipSetDevice(device));
+    std::lock_guard<std::mutex> g(g_mu);
+    if (g_ws.size() < static_cast<size_t>(n)) g_ws.resize(n, nullptr);
+    if (!g_ws[device]) g_ws[device] = new Workspace();
+    Workspace* w = g_ws[device];
+    if (!w->ready) {
+        hipDeviceProp_t prop;
+        HIP_OK(hipGetDeviceProperties(&prop, device));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return set_err(BCOSGPU_E_NODEV, std::string("device is ") + prop.gcnArchName + ", built for gfx950");
+        HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+        int rc = ecc_init_tables(device);
+        if (rc) return set_err(rc, "ecc table setup failed");
+        w->ready = true;
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ hashing
+int bcosgpu_hash_batch_dev(int hasher, const uint8_t* d_data, const uint64_t* d_offsets, size_t n,
+                           uint8_t* d_out32, void* stream) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (n && (!d_data || !d_offsets || !d_out32)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_hash_batch(hasher, d_data, d_offsets, n, d_out32, as_stream(stream));
+    return rc ? hip_err(hipGetLastError(), "hash_batch launch") : 0;
+}
+
+int bcosgpu_hash_batch(int hasher, const uint8_t* data, const uint64_t* offsets, size_t n,
+                       uint8_t* out32) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (n == 0) return 0;
+    if (!data || !offsets || !out32) return set_err(BCOSGPU_E_ARG, "null pointer");
+    const uint64_t base = offsets[0], bytes = offsets[n] - base;
+    for (size_t i = 0; i < n; ++i)
+        if (offsets[i + 1] < offsets[i] || offsets[i + 1] - offsets[i] > 0xFFFFFFFFull)
+            return set_err(BCOSGPU_E_ARG, "offsets must be non-decreasing and messages < 4 GiB");
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    HIP_OK(w->b[0].ensure(bytes + 8));
+    HIP_OK(w->b[1].ensure((n + 1) * 8));
+    HIP_OK(w->b[2].ensure(n * 32));
+    std::vector<uint64_t> off(n + 1);
+    for (size_t i = 0; i <= n; ++i) off[i] = offsets[i] - base;
+    HIP_OK(hipMemcpyAsync(w->b[0].p, data + base, bytes, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[1].p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, w->stream));
+    rc = launch_hash_batch(hasher, w->b[0].as<uint8_t>(), w->b[1].as<uint64_t>(), n, w->b[2].as<uint8_t>(), w->stream);
+    if (rc) return hip_err(hipGetLastError(), "hash_batch launch");
+    HIP_OK(hipMemcpyAsync(out32, w->b[2].p, n * 32, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
+int bcosgpu_keccak256_batch(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32) {
+    return bcosgpu_hash_batch(BCOSGPU_KECCAK256, data, offsets, n, out32);
+}
+int bcosgpu_sm3_batch(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32) {
+    return bcosgpu_hash_batch(BCOSGPU_SM3, data, offsets, n, out32);
+}
+
+// ------------------------------------------------------------------ Merkle
+int bcosgpu_merkle_root_dev(int hasher, int width, const uint8_t* d_leaves32, size_t n,
+                            uint8_t* d_tree, uint8_t* d_root32, void* stream) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (n == 0) return set_err(BCOSGPU_E_EMPTY, "Empty input");
+    if (width < 2 || width > 64) return set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
+    if (!d_leaves32 || !d_tree) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_merkle(hasher, width, d_leaves32, n, d_tree, d_root32, as_stream(stream));
+    return rc ? hip_err(hipGetLastError(), "merkle launch") : 0;
+}
+
+int bcosgpu_merkle_root(int hasher, int width, int variant, const uint8_t* leaves32, size_t n,
+                        uint8_t* root32, uint8_t* levels) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (!root32 || (n && !leaves32)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    if (variant == BCOSGPU_MERKLE_NEW) {
+        if (n == 0) return set_err(BCOSGPU_E_EMPTY, "Empty input");
+        if (width < 2 || width > 64) return set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
+    } else if (variant != BCOSGPU_MERKLE_OLD) {
+        return set_err(BCOSGPU_E_ARG, "bad variant");
+    }
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    const uint64_t tree = variant == BCOSGPU_MERKLE_NEW ? bcosgpu_merkle_size(n, width) : merkle_size(n, 16) + 1;
+    HIP_OK(w->b[0].ensure(n * 32 + 32));
+    HIP_OK(w->b[1].ensure(tree * 32 + 32));
+    HIP_OK(w->b[2].ensure(32));
+    if (n) HIP_OK(hipMemcpyAsync(w->b[0].p, leaves32, n * 32, hipMemcpyHostToDevice, w->stream));
+    if (variant == BCOSGPU_MERKLE_NEW)
+        rc = launch_merkle(hasher, width, w->b[0].as<uint8_t>(), n, w->b[1].as<uint8_t>(), w->b[2].as<uint8_t>(), w->stream);
+    else
+        rc = launch_merkle_old(hasher, w->b[0].as<uint8_t>(), n, w->b[1].as<uint8_t>(), w->b[2].as<uint8_t>(), w->stream);
+    if (rc) return rc == BCOSGPU_E_ARG ? set_err(rc, "bad merkle arguments") : hip_err(hipGetLastError(), "merkle launch");
+    HIP_OK(hipMemcpyAsync(root32, w->b[2].p, 32, hipMemcpyDeviceToHost, w->stream));
+    if (levels && variant == BCOSGPU_MERKLE_NEW)
+        HIP_OK(hipMemcpyAsync(levels, w->b[1].p, tree * 32, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
+// ------------------------------------------------------------------ signatures
+int bcosgpu_secp256k1_recover_batch_dev(const uint8_t* d_hash32, const uint8_t* d_sig65, size_t n,
+                                        uint8_t* d_pub64, uint8_t* d_addr20, uint8_t* d_ok,
+                                        void* stream) {
+    if (n && (!d_hash32 || !d_sig65 || !d_ok)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_secp256k1_recover(d_hash32, d_sig65, 65, n, d_pub64, d_addr20, d_ok, as_stream(stream));
+    return rc ? set_err(rc, "secp256k1 recover launch failed") : 0;
+}
+
+int bcosgpu_secp256k1_recover_batch(const uint8_t* hash32, const uint8_t* sig65, size_t n,
+                                    uint8_t* pub64, uint8_t* addr20, uint8_t* ok) {
+    if (n == 0) return 0;
+    if (!hash32 || !sig65 || !ok) return set_err(BCOSGPU_E_ARG, "null pointer");
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    HIP_OK(w->b[0].ensure(n * 32));
+    HIP_OK(w->b[1].ensure(n * 65 + 8));
+    HIP_OK(w->b[2].ensure(n * 64));
+    HIP_OK(w->b[3].ensure(n * 20));
+    HIP_OK(w->b[4].ensure(n));
+    HIP_OK(hipMemcpyAsync(w->b[0].p, hash32, n * 32, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[1].p, sig65, n * 65, hipMemcpyHostToDevice, w->stream));
+    rc = launch_secp256k1_recover(w->b[0].as<uint8_t>(), w->b[1].as<uint8_t>(), 65, n,
+                                  pub64 ? w->b[2].as<uint8_t>() : nullptr,
+                                  addr20 ? w->b[3].as<uint8_t>() : nullptr, w->b[4].as<uint8_t>(), w->stream);
+    if (rc) return set_err(rc, "secp256k1 recover launch failed");
+    if (pub64) HIP_OK(hipMemcpyAsync(pub64, w->b[2].p, n * 64, hipMemcpyDeviceToHost, w->stream));
+    if (addr20) HIP_OK(hipMemcpyAsync(addr20, w->b[3].p, n * 20, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipMemcpyAsync(ok, w->b[4].p, n, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
+int bcosgpu_sm2_verify_batch_dev(const uint8_t* d_hash32, const uint8_t* d_sig128, size_t n,
+                                 uint8_t* d_addr20, uint8_t* d_ok, void* stream) {
+    if (n && (!d_hash32 || !d_sig128 || !d_ok)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_sm2_verify(d_hash32, d_sig128, 128, n, d_addr20, d_ok, as_stream(stream));
+    return rc ? set_err(rc, "sm2 verify launch failed") : 0;
+}
+
+int bcosgpu_sm2_verify_batch(const uint8_t* hash32, const uint8_t* sig128, size_t n,
+                             uint8_t* addr20, uint8_t* ok) {
+    if (n == 0) return 0;
+    if (!hash32 || !sig128 || !ok) return set_err(BCOSGPU_E_ARG, "null pointer");
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    HIP_OK(w->b[0].ensure(n * 32));
+    HIP_OK(w->b[1].ensure(n * 128));
+    HIP_OK(w->b[3].ensure(n * 20));
+    HIP_OK(w->b[4].ensure(n));
+    HIP_OK(hipMemcpyAsync(w->b[0].p, hash32, n * 32, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[1].p, sig128, n * 128, hipMemcpyHostToDevice, w->stream));
+    rc = launch_sm2_verify(w->b[0].as<uint8_t>(), w->b[1].as<uint8_t>(), 128, n,
+                           addr20 ? w->b[3].as<uint8_t>() : nullptr, w->b[4].as<uint8_t>(), w->stream);
+    if (rc) return set_err(rc, "sm2 verify launch failed");
+    if (addr20) HIP_OK(hipMemcpyAsync(addr20, w->b[3].p, n * 20, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipMemcpyAsync(ok, w->b[4].p, n, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
+int bcosgpu_secp256k1_sign_batch_dev(const uint8_t* d_sk32, const uint8_t* d_hash32, size_t n,
+                                     uint8_t* d_pub64, uint8_t* d_sig65, uint8_t* d_ok, void* stream) {
+    if (n && (!d_sk32 || !d_hash32 || !d_sig65 || !d_ok)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_secp256k1_sign(d_sk32, d_hash32, n, d_pub64, d_sig65, d_ok, as_stream(stream));
+    return rc ? set_err(rc, "secp256k1 sign launch failed") : 0;
+}
+
+int bcosgpu_sm2_sign_batch_dev(const uint8_t* d_sk32, const uint8_t* d_hash32, size_t n,
+                               uint8_t* d_sig128, uint8_t* d_ok, void* stream) {
+    if (n && (!d_sk32 || !d_hash32 || !d_sig128 || !d_ok)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_sm2_sign(d_sk32, d_hash32, n, d_sig128, d_ok, as_stream(stream));
+    return rc ? set_err(rc, "sm2 sign launch failed") : 0;
+}
+
+// ------------------------------------------------------------------ whole-tx admission
+int bcosgpu_tx_verify_batch_dev(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
+                                const uint8_t* d_sig, const uint64_t* d_sig_off, size_t n,
+                                uint8_t* d_txhash32, uint8_t* d_sender20, uint8_t* d_status,
+                                void* stream) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return set_err(BCOSGPU_E_ARG, "bad suite");
+    if (n && (!d_pre || !d_pre_off || !d_sig || !d_sig_off || !d_txhash32 || !d_sender20 || !d_status))
+        return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_tx_verify(suite, d_pre, d_pre_off, d_sig, d_sig_off, n, d_txhash32, d_sender20, d_status,
+                              as_stream(stream));
+    return rc ? set_err(rc, "tx verify launch failed") : 0;
+}
+
+int bcosgpu_tx_verify_batch(int suite, const uint8_t* pre, const uint64_t* pre_off,
+                            const uint8_t* sig, const uint64_t* sig_off, size_t n,
+                            uint8_t* txhash32, uint8_t* sender20, uint8_t* status) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return set_err(BCOSGPU_E_ARG, "bad suite");
+    if (n == 0) return 0;
+    if (!pre || !pre_off || !sig || !sig_off || !txhash32 || !sender20 || !status)
+        return set_err(BCOSGPU_E_ARG, "null pointer");
+    for (size_t i = 0; i < n; ++i)
+        if (pre_off[i + 1] < pre_off[i] || sig_off[i + 1] < sig_off[i] || pre_off[i + 1] - pre_off[i] > 0xFFFFFFFFull)
+            return set_err(BCOSGPU_E_ARG, "offsets must be non-decreasing");
+    const uint64_t pb = pre_off[0], pbytes = pre_off[n] - pb, sb = sig_off[0], sbytes = sig_off[n] - sb;
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    HIP_OK(w->b[0].ensure(pbytes + 8));
+    HIP_OK(w->b[1].ensure((n + 1) * 8));
+    HIP_OK(w->b[2].ensure(sbytes + 8));
+    HIP_OK(w->b[3].ensure((n + 1) * 8));
+    HIP_OK(w->b[4].ensure(n * 32));
+    HIP_OK(w->b[5].ensure(n * 20));
+    HIP_OK(w->b[6].ensure(n));
+    std::vector<uint64_t> po(n + 1), so(n + 1);
+    for (size_t i = 0; i <= n; ++i) { po[i] = pre_off[i] - pb; so[i] = sig_off[i] - sb; }
+    HIP_OK(hipMemcpyAsync(w->b[0].p, pre + pb, pbytes, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[1].p, po.data(), (n + 1) * 8, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[2].p, sig + sb, sbytes, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[3].p, so.data(), (n + 1) * 8, hipMemcpyHostToDevice, w->stream));
+    rc = launch_tx_verify(suite, w->b[0].as<uint8_t>(), w->b[1].as<uint64_t>(), w->b[2].as<uint8_t>(),
+                          w->b[3].as<uint64_t>(), n, w->b[4].as<uint8_t>(), w->b[5].as<uint8_t>(),
+                          w->b[6].as<uint8_t>(), w->stream);
+    if (rc) return set_err(rc, "tx verify launch failed");
+    HIP_OK(hipMemcpyAsync(txhash32, w->b[4].p, n * 32, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipMemcpyAsync(sender20, w->b[5].p, n * 20, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipMemcpyAsync(status, w->b[6].p, n, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
+// ------------------------------------------------------------------ wedpr-ABI shims
+int8_t bcosgpu_wedpr_secp256k1_recover_public_key(const bcosgpu_CInputBuffer* hash,
+                                                   const bcosgpu_CInputBuffer* sig,
+                                                   bcosgpu_COutputBuffer* pub) {
+    if (!hash || !sig || !pub || hash->len != 32 || pub->len < 64) return -1;
+    if (sig->len != 65) return -1;  // SECP256K1_SIGNATURE_LEN (Secp256k1Crypto.h:29)
+    uint8_t ok = 0;
+    if (bcosgpu_secp256k1_recover_batch(reinterpret_cast<const uint8_t*>(hash->data),
+                                        reinterpret_cast<const uint8_t*>(sig->data), 1,
+                                        reinterpret_cast<uint8_t*>(pub->data), nullptr, &ok))
+        return -1;
+    return ok ? 0 : -1;
+}
+
+int8_t bcosgpu_wedpr_sm2_verify(const bcosgpu_CInputBuffer* pub, const bcosgpu_CInputBuffer* hash,
+                                 const bcosgpu_CInputBuffer* sig) {
+    if (!pub || !hash || !sig || hash->len != 32 || sig->len != 64 || pub->len != 64) return -1;
+    uint8_t s[128], ok = 0;
+    std::memcpy(s, sig->data, 64);
+    std::memcpy(s + 64, pub->data, 64);
+    if (bcosgpu_sm2_verify_batch(reinterpret_cast<const uint8_t*>(hash->data), s, 1, nullptr, &ok)) return -1;
+    return ok ? 0 : -1;
+}
+
+}  // extern "C"

@@ -1,0 +1,33 @@
+// engine.h -- internal launcher declarations shared by the kernel TUs and the C ABI (api.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/bcos_gpu.h"
+
+namespace bcosgpu {
+
+// hash_kernels.hip
+int launch_hash_batch(int hasher, const uint8_t* d_data, const uint64_t* d_off, uint64_t n,
+                      uint8_t* d_out, hipStream_t st);
+uint64_t merkle_size(uint64_t n, int width);
+int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
+                  uint8_t* d_root, hipStream_t st);
+int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* d_scratch,
+                      uint8_t* d_root, hipStream_t st);
+
+// ecc_kernels.hip
+int ecc_init_tables(int device);
+int launch_secp256k1_recover(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t sig_stride,
+                             uint64_t n, uint8_t* d_pub, uint8_t* d_addr, uint8_t* d_ok,
+                             hipStream_t st);
+int launch_sm2_verify(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t sig_stride, uint64_t n,
+                      uint8_t* d_addr, uint8_t* d_ok, hipStream_t st);
+int launch_secp256k1_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint8_t* d_pub,
+                          uint8_t* d_sig, uint8_t* d_ok, hipStream_t st);
+int launch_sm2_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint8_t* d_sig,
+                    uint8_t* d_ok, hipStream_t st);
+int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
+                     const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n,
+                     uint8_t* d_txhash, uint8_t* d_sender, uint8_t* d_status, hipStream_t st);
+
+}  // namespace bcosgpu

@@ -1,0 +1,166 @@
+// hash_kernels.hip -- batch hashing and Merkle level kernels (gfx950).
+//
+// Replaces, for batches:
+//   Hash::hash(bytesConstRef)             bcos-crypto/bcos-crypto/interfaces/crypto/Hash.h:44
+//     (Keccak256::hash hash/Keccak256.h:39-51, SM3::hash hash/SM3.h:39-50)
+//   Merkle<Hasher,width>::generateMerkle  bcos-crypto/bcos-crypto/merkle/Merkle.h:170-208
+//     (per-level calculateLevelHashes :243-261 -> merkle_level_kernel, one node per lane)
+//   protocol::calculateMerkleProofRoot    bcos-protocol/bcos-protocol/ParallelMerkleProof.cpp:32-69
+#include "hash_device.h"
+#include "engine.h"
+
+namespace bcosgpu {
+
+// One message per lane; message i = data[off[i] .. off[i+1]).
+template <int H>
+__global__ __launch_bounds__(256) void hash_batch_kernel(const uint8_t* __restrict__ data,
+                                                         const uint64_t* __restrict__ off,
+                                                         uint64_t n, uint8_t* __restrict__ out) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a = off[i], b = off[i + 1];
+    const uint32_t len = static_cast<uint32_t>(b - a);
+    ByteReader rd(data + a, len);
+    uint32_t d[8];
+    if (H == KECCAK256) keccak256_msg(rd, len, d);
+    else sm3_msg(rd, len, d);
+    store_digest(H, out + 32 * i, d);
+}
+
+// One Merkle node per lane: out[i] = H(in[i*W] || ... || in[min((i+1)*W, nin) - 1]).
+// W = 0 selects the runtime width `w`.
+template <int H, int W>
+__global__ __launch_bounds__(256) void merkle_level_kernel(const uint8_t* __restrict__ in,
+                                                           uint64_t nin, int w,
+                                                           uint8_t* __restrict__ out,
+                                                           uint64_t nout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= nout) return;
+    const uint64_t width = W ? W : w;
+    const uint64_t first = i * width;
+    const uint64_t cnt = (nin - first) < width ? (nin - first) : width;
+    const uint32_t len = static_cast<uint32_t>(cnt * 32u);
+    AlignedReader rd(in + first * 32, len);
+    uint32_t d[8];
+    if (H == KECCAK256) keccak256_msg(rd, len, d);
+    else sm3_msg(rd, len, d);
+    store_digest(H, out + 32 * i, d);
+}
+
+// Count records of the reference's output vector (Merkle.h:189-204, setNumberToHash :213-217):
+// entry = uint32 big-endian level size in bytes 0..3, zero elsewhere.
+struct LevelTable {
+    uint64_t pos[64];
+    uint32_t count[64];
+    int nlevels;
+};
+__global__ void merkle_counts_kernel(uint8_t* tree, LevelTable t) {
+    const int l = threadIdx.x;
+    if (l >= t.nlevels) return;
+    uint32_t* e = reinterpret_cast<uint32_t*>(tree + 32 * t.pos[l]);
+    e[0] = bswap32(t.count[l]);
+#pragma unroll
+    for (int k = 1; k < 8; ++k) e[k] = 0;
+}
+
+// root = H(top) of the legacy algorithm (ParallelMerkleProof.cpp:68); len 0 -> H("") (:35-38).
+template <int H>
+__global__ void hash_one_kernel(const uint8_t* in, uint32_t len, uint8_t* out) {
+    if (threadIdx.x != 0) return;
+    AlignedReader rd(in, len);
+    uint32_t d[8];
+    if (H == KECCAK256) keccak256_msg(rd, len, d);
+    else sm3_msg(rd, len, d);
+    store_digest(H, out, d);
+}
+
+__global__ void copy32_kernel(const uint8_t* src, uint8_t* dst) {
+    if (threadIdx.x < 8)
+        reinterpret_cast<uint32_t*>(dst)[threadIdx.x] = reinterpret_cast<const uint32_t*>(src)[threadIdx.x];
+}
+
+static inline unsigned grid_for(uint64_t n, unsigned bs) { return static_cast<unsigned>((n + bs - 1) / bs); }
+
+int launch_hash_batch(int hasher, const uint8_t* d_data, const uint64_t* d_off, uint64_t n,
+                      uint8_t* d_out, hipStream_t st) {
+    if (n == 0) return 0;
+    if (hasher == SM3)
+        hipLaunchKernelGGL(hash_batch_kernel<SM3>, dim3(grid_for(n, 256)), dim3(256), 0, st, d_data, d_off, n, d_out);
+    else
+        hipLaunchKernelGGL(hash_batch_kernel<KECCAK256>, dim3(grid_for(n, 256)), dim3(256), 0, st, d_data, d_off, n, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+static void launch_level(int hasher, int width, const uint8_t* in, uint64_t nin, uint8_t* out,
+                         uint64_t nout, hipStream_t st) {
+    dim3 g(grid_for(nout, 256)), b(256);
+#define LVL(HH, WW) hipLaunchKernelGGL((merkle_level_kernel<HH, WW>), g, b, 0, st, in, nin, width, out, nout)
+    if (hasher == SM3) {
+        if (width == 2) LVL(SM3, 2); else if (width == 16) LVL(SM3, 16); else LVL(SM3, 0);
+    } else {
+        if (width == 2) LVL(KECCAK256, 2); else if (width == 16) LVL(KECCAK256, 16); else LVL(KECCAK256, 0);
+    }
+#undef LVL
+}
+
+uint64_t merkle_size(uint64_t n, int width) {
+    uint64_t nodes = 0;
+    while (n > 1) {
+        n = (n + width - 1) / width;
+        nodes += n + 1;
+    }
+    return nodes;
+}
+
+int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
+                  uint8_t* d_root, hipStream_t st) {
+    if (n == 0 || width < 2 || width > 64) return BCOSGPU_E_ARG;
+    if (n == 1) {  // Merkle.h:177-182
+        hipLaunchKernelGGL(copy32_kernel, dim3(1), dim3(64), 0, st, d_leaves, d_tree);
+        if (d_root) hipLaunchKernelGGL(copy32_kernel, dim3(1), dim3(64), 0, st, d_leaves, d_root);
+        return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+    }
+    LevelTable t{};
+    uint64_t pos = 0, nin = n;
+    const uint8_t* in = d_leaves;
+    while (nin > 1) {
+        const uint64_t nout = (nin + width - 1) / width;
+        if (t.nlevels >= 64) return BCOSGPU_E_ARG;
+        t.pos[t.nlevels] = pos;
+        t.count[t.nlevels] = static_cast<uint32_t>(nout);
+        ++t.nlevels;
+        uint8_t* out = d_tree + 32 * (pos + 1);
+        launch_level(hasher, width, in, nin, out, nout, st);
+        in = out;
+        pos += nout + 1;
+        nin = nout;
+    }
+    hipLaunchKernelGGL(merkle_counts_kernel, dim3(1), dim3(64), 0, st, d_tree, t);
+    if (d_root) hipLaunchKernelGGL(copy32_kernel, dim3(1), dim3(64), 0, st, d_tree + 32 * (pos - 1), d_root);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* d_scratch,
+                      uint8_t* d_root, hipStream_t st) {
+    // d_scratch: >= 32 * (ceil(n/16) + ceil(n/256) + ...) bytes; levels ping into it
+    if (n == 0) {
+        if (hasher == SM3) hipLaunchKernelGGL(hash_one_kernel<SM3>, dim3(1), dim3(64), 0, st, d_leaves, 0u, d_root);
+        else hipLaunchKernelGGL(hash_one_kernel<KECCAK256>, dim3(1), dim3(64), 0, st, d_leaves, 0u, d_root);
+        return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+    }
+    const uint8_t* in = d_leaves;
+    uint64_t nin = n, pos = 0;
+    while (nin > 1) {
+        const uint64_t nout = (nin + 15) / 16;
+        uint8_t* out = d_scratch + 32 * pos;
+        launch_level(hasher, 16, in, nin, out, nout, st);
+        in = out;
+        pos += nout;
+        nin = nout;
+    }
+    if (hasher == SM3) hipLaunchKernelGGL(hash_one_kernel<SM3>, dim3(1), dim3(64), 0, st, in, 32u, d_root);
+    else hipLaunchKernelGGL(hash_one_kernel<KECCAK256>, dim3(1), dim3(64), 0, st, in, 32u, d_root);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+}  // namespace bcosgpu

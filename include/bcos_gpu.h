@@ -1,0 +1,141 @@
+/*
+ * bcos_gpu.h -- C ABI of the MI355X batch-verification engine for FISCO-BCOS's tx-admission and
+ * block-check hot path (libbcosgpu.so).
+ *
+ * Drop-in boundary.  The reference reaches this path through
+ *   - bcos::crypto::SignatureCrypto::recover / verify   bcos-crypto/bcos-crypto/interfaces/crypto/Signature.h:40-58
+ *   - bcos::crypto::Hash::hash                          bcos-crypto/bcos-crypto/interfaces/crypto/Hash.h:44
+ *   - bcos::crypto::merkle::Merkle<H,width>             bcos-crypto/bcos-crypto/merkle/Merkle.h:170-208
+ * and, one level down, the wedpr / TASSL C ABI those classes bind (int8 return code, caller-owned
+ * buffers): wedpr_secp256k1_recover_public_key (Secp256k1Crypto.cpp:79-93), wedpr_secp256k1_verify
+ * (:51-63), fast_sm2_verify / wedpr_sm2_verify (fastsm2/fast_sm2.h:31-40, sm2/SM2Crypto.h:60-66).
+ * This header exports (a) batch entry points -- what the batch sites TransactionSync::importDownloadedTxs
+ * (bcos-txpool/bcos-txpool/sync/TransactionSync.cpp:516-548) and BlockImpl::calculateTransactionRoot
+ * (bcos-tars-protocol/bcos-tars-protocol/protocol/BlockImpl.h:111-154) are rewired to -- and
+ * (b) single-call shims with the exact wedpr signatures, so SignatureCrypto implementations can be
+ * swapped without touching their callers.  include/bcos_gpu.hpp wraps (a) in the reference's C++
+ * interface shapes; INTEGRATION.md shows the binding.
+ *
+ * Conventions: all functions return 0 on success and a negative BCOSGPU_E_* code on an API error
+ * (never throw across the ABI); per-item crypto verdicts are written to caller-allocated ok[] /
+ * status[] arrays (1 = valid / 0 = InvalidSignature for ok[]; 0 = ok, 1 = InvalidSignature for status[]).
+ * Byte layouts are the reference's: 32-byte big-endian scalars and digests, 64-byte X||Y public keys
+ * without the 0x04 prefix (Secp256k1KeyPair.h:29, SM2KeyPair.h:31), secp256k1 signatures r||s||v
+ * (65 B, v = recovery id 0..3, SignatureDataWithV.h:43-61), SM2 signatures r||s||pub (128 B,
+ * SignatureDataWithPub.h:55-64).  Functions are thread-safe.
+ *
+ * *_dev functions take DEVICE pointers and a hipStream_t (as void*; NULL = the legacy default
+ * stream) and are stream-ordered: nothing is synchronised, nothing is allocated per call except the
+ * engine's grow-only workspaces.  Device output pointers must be 4-byte aligned.  The other
+ * functions take HOST pointers and return after the results are copied back.
+ */
+#ifndef BCOS_GPU_H
+#define BCOS_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BCOSGPU_VERSION 1
+
+/* error codes */
+#define BCOSGPU_OK 0
+#define BCOSGPU_E_ARG (-1)    /* invalid argument (size, width, null pointer) */
+#define BCOSGPU_E_HIP (-2)    /* HIP runtime error (see bcosgpu_last_error) */
+#define BCOSGPU_E_NODEV (-3)  /* no usable gfx950 device */
+#define BCOSGPU_E_EMPTY (-4)  /* empty Merkle input: the reference throws std::invalid_argument (Merkle.h:172-175) */
+
+/* hashers (Hash implementations: hash/Keccak256.h, hash/SM3.h) */
+#define BCOSGPU_KECCAK256 0
+#define BCOSGPU_SM3 1
+/* signature suites (libinitializer/ProtocolInitializer.cpp:102-124) */
+#define BCOSGPU_SUITE_SECP256K1 0 /* Keccak256 + Secp256k1Crypto */
+#define BCOSGPU_SUITE_SM2 1       /* SM3 + (Fast)SM2Crypto */
+/* Merkle variants */
+#define BCOSGPU_MERKLE_NEW 0 /* Merkle<H,width>::generateMerkle (Merkle.h:170-208) */
+#define BCOSGPU_MERKLE_OLD 1 /* calculateMerkleProofRoot, width 16 (ParallelMerkleProof.cpp:32-69) */
+
+int bcosgpu_version(void);
+/* Number of visible HIP devices (0 when none). */
+int bcosgpu_device_count(void);
+/* Select the calling thread's device and build its constant tables (idempotent). */
+int bcosgpu_init(int device);
+/* Last error message of the calling thread. */
+const char* bcosgpu_last_error(void);
+/* Bytes of the reference's Merkle output vector, in 32-byte entries (Merkle.h:224-236 getMerkleSize). */
+uint64_t bcosgpu_merkle_size(uint64_t n, int width);
+
+/* ---------------------------------------------------------------- hashing (Hash::hash, batched) */
+/* message i = data[offsets[i] .. offsets[i+1]), n+1 offsets; out32 = n x 32-byte digests */
+int bcosgpu_hash_batch(int hasher, const uint8_t* data, const uint64_t* offsets, size_t n,
+                       uint8_t* out32);
+int bcosgpu_keccak256_batch(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32);
+int bcosgpu_sm3_batch(const uint8_t* data, const uint64_t* offsets, size_t n, uint8_t* out32);
+int bcosgpu_hash_batch_dev(int hasher, const uint8_t* d_data, const uint64_t* d_offsets, size_t n,
+                           uint8_t* d_out32, void* stream);
+
+/* ---------------------------------------------------------------- Merkle (Merkle<H,width>) */
+/* root32 receives the root; levels (nullable) receives bcosgpu_merkle_size(n,width) x 32 bytes laid
+ * out as the reference's output vector: per level a count record (uint32 big-endian in bytes 0..3,
+ * zero elsewhere) followed by the level's nodes; for n == 1 the single leaf.  variant OLD ignores
+ * width (always 16) and levels; n == 0 returns H("") for OLD and BCOSGPU_E_EMPTY for NEW. */
+int bcosgpu_merkle_root(int hasher, int width, int variant, const uint8_t* leaves32, size_t n,
+                        uint8_t* root32, uint8_t* levels);
+/* d_tree must hold bcosgpu_merkle_size(n,width) x 32 bytes (>= 32 for n == 1). */
+int bcosgpu_merkle_root_dev(int hasher, int width, const uint8_t* d_leaves32, size_t n,
+                            uint8_t* d_tree, uint8_t* d_root32, void* stream);
+
+/* ---------------------------------------------------------------- signatures (SignatureCrypto, batched) */
+/* secp256k1 public-key recovery (Secp256k1Crypto::recover, Secp256k1Crypto.h:57-60).
+ * pub64 / addr20 nullable; addr20 = right160(Keccak256(pub)) (calculateAddress, KeyPair.h:30-33). */
+int bcosgpu_secp256k1_recover_batch(const uint8_t* hash32, const uint8_t* sig65, size_t n,
+                                    uint8_t* pub64, uint8_t* addr20, uint8_t* ok);
+int bcosgpu_secp256k1_recover_batch_dev(const uint8_t* d_hash32, const uint8_t* d_sig65, size_t n,
+                                        uint8_t* d_pub64, uint8_t* d_addr20, uint8_t* d_ok,
+                                        void* stream);
+/* SM2 verify with the embedded public key (SM2Crypto::recover, SM2Crypto.cpp:81-92).
+ * addr20 = right160(SM3(pub)), nullable. */
+int bcosgpu_sm2_verify_batch(const uint8_t* hash32, const uint8_t* sig128, size_t n,
+                             uint8_t* addr20, uint8_t* ok);
+int bcosgpu_sm2_verify_batch_dev(const uint8_t* d_hash32, const uint8_t* d_sig128, size_t n,
+                                 uint8_t* d_addr20, uint8_t* d_ok, void* stream);
+/* Key derivation + deterministic signing (SignatureCrypto::createKeyPair / sign), used to build
+ * synthetic signed batches on the device.  Nonce k = H(sk || hash) mod n (H = Keccak256 for
+ * secp256k1, SM3 for SM2); sig65 = r||s||v (low-S, libsecp256k1 convention), sig128 = r||s||pub.
+ * ok[i] = 0 when sk is out of range or the nonce is degenerate. */
+int bcosgpu_secp256k1_sign_batch_dev(const uint8_t* d_sk32, const uint8_t* d_hash32, size_t n,
+                                     uint8_t* d_pub64, uint8_t* d_sig65, uint8_t* d_ok, void* stream);
+int bcosgpu_sm2_sign_batch_dev(const uint8_t* d_sk32, const uint8_t* d_hash32, size_t n,
+                               uint8_t* d_sig128, uint8_t* d_ok, void* stream);
+
+/* ---------------------------------------------------------------- whole-tx admission (Transaction::verify, batched) */
+/* Transaction::verify (bcos-framework/.../protocol/Transaction.h:68-82) for n transactions:
+ * txhash = H(preimage) (TarsHashable.h:16-41), pub = recover(txhash, sig), sender = right160(H(pub)).
+ * preimage i = pre[pre_off[i] .. pre_off[i+1]); signature i = sig[sig_off[i] .. sig_off[i+1]).
+ * status[i] = 0 (ok) or 1 (TransactionStatus::InvalidSignature); sender20 zero when invalid. */
+int bcosgpu_tx_verify_batch(int suite, const uint8_t* pre, const uint64_t* pre_off,
+                            const uint8_t* sig, const uint64_t* sig_off, size_t n,
+                            uint8_t* txhash32, uint8_t* sender20, uint8_t* status);
+int bcosgpu_tx_verify_batch_dev(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
+                                const uint8_t* d_sig, const uint64_t* d_sig_off, size_t n,
+                                uint8_t* d_txhash32, uint8_t* d_sender20, uint8_t* d_status,
+                                void* stream);
+
+/* ---------------------------------------------------------------- wedpr-ABI single-call shims */
+/* Same layout as wedpr-crypto's CInputBuffer / COutputBuffer; return 0 (WEDPR_SUCCESS) or -1. */
+typedef struct { const char* data; uintptr_t len; } bcosgpu_CInputBuffer;
+typedef struct { char* data; uintptr_t len; } bcosgpu_COutputBuffer;
+/* wedpr_secp256k1_recover_public_key (Secp256k1Crypto.cpp:79-93) */
+int8_t bcosgpu_wedpr_secp256k1_recover_public_key(const bcosgpu_CInputBuffer* hash,
+                                                   const bcosgpu_CInputBuffer* sig,
+                                                   bcosgpu_COutputBuffer* pub);
+/* fast_sm2_verify / wedpr_sm2_verify (fast_sm2.cpp:139-227): sig = r||s (64 B), pub = 64 B */
+int8_t bcosgpu_wedpr_sm2_verify(const bcosgpu_CInputBuffer* pub, const bcosgpu_CInputBuffer* hash,
+                                 const bcosgpu_CInputBuffer* sig);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

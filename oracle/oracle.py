@@ -1,0 +1,163 @@
+"""ctypes binding of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and
+only as the checker / timed CPU baseline.  See oracle/oracle.h for the reference citations.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+KECCAK256, SM3 = 0, 1
+SUITE_SECP256K1, SUITE_SM2 = 0, 1
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "liboracle.so"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        sigs = {
+            "oracle_keccak256": (None, [P, S, P]), "oracle_sm3": (None, [P, S, P]),
+            "oracle_hash": (None, [I, P, S, P]),
+            "oracle_hash_batch": (None, [I, P, P, S, P, I]),
+            "oracle_merkle": (I, [I, I, P, S, P, P, I]), "oracle_merkle_size": (S, [S, I]),
+            "oracle_merkle_old": (None, [I, P, S, P]),
+            "oracle_secp256k1_recover": (I, [P, P, S, P]), "oracle_secp256k1_pubkey": (I, [P, P]),
+            "oracle_secp256k1_sign": (I, [P, P, P, P]), "oracle_secp256k1_verify": (I, [P, P, P, S]),
+            "oracle_sm2_recover": (I, [P, P, S, P]), "oracle_sm2_pubkey": (I, [P, P]),
+            "oracle_sm2_sign": (I, [P, P, P, P]), "oracle_sm2_za": (None, [P, P]),
+            "oracle_tx_verify_batch": (None, [I, P, P, P, P, S, P, P, P, I]),
+            "oracle_secp256k1_recover_batch": (None, [P, P, S, P, P, I]),
+            "oracle_sm2_verify_batch": (None, [P, P, S, P, I]),
+        }
+        for k, (r, a) in sigs.items():
+            f = getattr(L, k)
+            f.restype = r
+            f.argtypes = a
+        _lib = L
+    return _lib
+
+
+def _b(x):
+    return ctypes.c_char_p(bytes(x))
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def keccak256(m: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().oracle_keccak256(_b(m), len(m), out)
+    return out.raw
+
+
+def sm3(m: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().oracle_sm3(_b(m), len(m), out)
+    return out.raw
+
+
+def hash_(hasher, m):
+    return sm3(m) if hasher == SM3 else keccak256(m)
+
+
+def hash_packed(hasher, data, offsets, nthreads=1):
+    n = len(offsets) - 1
+    out = np.zeros((n, 32), dtype=np.uint8)
+    d = data if len(data) else np.zeros(1, dtype=np.uint8)
+    lib().oracle_hash_batch(hasher, _p(d), _p(offsets), n, _p(out), nthreads)
+    return out
+
+
+def merkle(hasher, width, leaves, want_tree=False, nthreads=1):
+    """leaves: uint8[n,32].  Returns root bytes (and the full output vector)."""
+    leaves = np.ascontiguousarray(leaves, dtype=np.uint8).reshape(-1, 32)
+    n = leaves.shape[0]
+    root = ctypes.create_string_buffer(32)
+    size = 1 if n == 1 else lib().oracle_merkle_size(n, width)
+    tree = np.zeros((max(size, 1), 32), dtype=np.uint8) if want_tree else None
+    rc = lib().oracle_merkle(hasher, width, _p(leaves) if n else None, n, root,
+                             _p(tree) if want_tree else None, nthreads)
+    if rc:
+        raise ValueError("Empty input")
+    return (root.raw, tree) if want_tree else root.raw
+
+
+def merkle_old(hasher, leaves):
+    leaves = np.ascontiguousarray(leaves, dtype=np.uint8).reshape(-1, 32)
+    root = ctypes.create_string_buffer(32)
+    lib().oracle_merkle_old(hasher, _p(leaves) if leaves.shape[0] else None, leaves.shape[0], root)
+    return root.raw
+
+
+def secp256k1_recover(h, sig):
+    pub = ctypes.create_string_buffer(64)
+    rc = lib().oracle_secp256k1_recover(_b(h), _b(sig), len(sig), pub)
+    return pub.raw if rc == 0 else None
+
+
+def secp256k1_pubkey(sk):
+    pub = ctypes.create_string_buffer(64)
+    return pub.raw if lib().oracle_secp256k1_pubkey(_b(sk), pub) == 0 else None
+
+
+def secp256k1_sign(sk, h, k):
+    sig = ctypes.create_string_buffer(65)
+    return sig.raw if lib().oracle_secp256k1_sign(_b(sk), _b(h), _b(k), sig) == 0 else None
+
+
+def secp256k1_verify(pub, h, sig):
+    return lib().oracle_secp256k1_verify(_b(pub), _b(h), _b(sig), len(sig)) == 0
+
+
+def sm2_recover(h, sig):
+    pub = ctypes.create_string_buffer(64)
+    return pub.raw if lib().oracle_sm2_recover(_b(h), _b(sig), len(sig), pub) == 0 else None
+
+
+def sm2_pubkey(sk):
+    pub = ctypes.create_string_buffer(64)
+    return pub.raw if lib().oracle_sm2_pubkey(_b(sk), pub) == 0 else None
+
+
+def sm2_sign(sk, h, k):
+    sig = ctypes.create_string_buffer(128)
+    return sig.raw if lib().oracle_sm2_sign(_b(sk), _b(h), _b(k), sig) == 0 else None
+
+
+def tx_verify_packed(suite, pre, pre_off, sig, sig_off, nthreads=1):
+    n = len(pre_off) - 1
+    txhash = np.zeros((n, 32), dtype=np.uint8)
+    sender = np.zeros((n, 20), dtype=np.uint8)
+    status = np.zeros(n, dtype=np.uint8)
+    lib().oracle_tx_verify_batch(suite, _p(pre), _p(pre_off), _p(sig), _p(sig_off), n, _p(txhash),
+                                 _p(sender), _p(status), nthreads)
+    return txhash, sender, status
+
+
+def secp256k1_recover_batch(hashes, sigs, nthreads=1):
+    n = hashes.shape[0]
+    pub = np.zeros((n, 64), dtype=np.uint8)
+    ok = np.zeros(n, dtype=np.uint8)
+    lib().oracle_secp256k1_recover_batch(_p(hashes), _p(sigs), n, _p(pub), _p(ok), nthreads)
+    return pub, ok.astype(bool)
+
+
+def sm2_verify_batch(hashes, sigs, nthreads=1):
+    n = hashes.shape[0]
+    ok = np.zeros(n, dtype=np.uint8)
+    lib().oracle_sm2_verify_batch(_p(hashes), _p(sigs), n, _p(ok), nthreads)
+    return ok.astype(bool)

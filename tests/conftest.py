@@ -1,0 +1,49 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fisco-bcos_amd"))
+sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (runs on the MI355X box)")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as o
+    o.build()
+    return o
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def kat():
+    return load_golden("kat.json")
+
+
+@pytest.fixture(scope="session")
+def merkle_golden():
+    return load_golden("merkle.json")
+
+
+@pytest.fixture(scope="session")
+def ecc_golden():
+    return load_golden("ecc_openssl.json")
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """The HIP engine on device 0; the GPU tests fail (never skip to a fallback) without it."""
+    import bcos_gpu
+    bcos_gpu.ensure_device(0)
+    return bcos_gpu

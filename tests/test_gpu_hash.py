@@ -1,0 +1,114 @@
+"""GPU parity: batch Keccak256 / SM3 and the Merkle kernels against the oracle and the golden vectors.
+
+Mirrors HashTest.cpp (KATs), testMerkle.cpp (widths 2..16, counts 0..63, empty throws) and
+merkleBench (100k leaves), plus sizes past the level boundaries and 1M leaves.
+"""
+import hashlib
+import struct
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _bench_leaves(n):
+    return np.frombuffer(b"".join(hashlib.new("sm3", struct.pack("<Q", i)).digest() for i in range(n)),
+                         dtype=np.uint8).reshape(n, 32)
+
+
+def test_hash_kats(gpu, kat):
+    for v in kat["hash"]:
+        h = gpu.Keccak256() if v["hasher"] == "keccak256" else gpu.SM3()
+        assert h.hash(v["msg"].encode()).hex() == v["digest"]
+
+
+@pytest.mark.parametrize("hasher", [0, 1])
+def test_hash_batch_ragged(gpu, oracle, hasher):
+    rng = np.random.default_rng(11 + hasher)
+    lens = list(range(0, 300)) + list(rng.integers(0, 2000, size=700))
+    msgs = [rng.bytes(int(n)) for n in lens]
+    data, off = gpu.pack_messages(msgs)
+    h = gpu.SM3() if hasher else gpu.Keccak256()
+    got = h.hash_packed(data, off)
+    want = oracle.hash_packed(hasher, data, off, nthreads=8)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("hasher", [0, 1])
+def test_hash_batch_large_unaligned(gpu, oracle, hasher):
+    """100k tx-sized messages (150-170 B) packed back to back at arbitrary byte offsets."""
+    rng = np.random.default_rng(5)
+    lens = rng.integers(150, 171, size=100_000)
+    off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    got = (gpu.SM3() if hasher else gpu.Keccak256()).hash_packed(data, off)
+    assert np.array_equal(got, oracle.hash_packed(hasher, data, off, nthreads=16))
+
+
+def test_merkle_golden(gpu, merkle_golden):
+    cache = {}
+    for c in merkle_golden["cases"]:
+        n = c["n"]
+        if n not in cache:
+            cache[n] = _bench_leaves(n)
+        h = gpu.SM3() if c["hasher"] == "sm3" else gpu.Keccak256()
+        leaves = [cache[n][i].tobytes() for i in range(n)]
+        if c["variant"] == "old":
+            assert gpu.calculate_merkle_proof_root(h, cache[n]).hex() == c["root"], c
+            continue
+        if "tree" in c:
+            tree = gpu.Merkle(h, c["width"]).generate_merkle(leaves)
+            assert [e.hex() for e in tree] == c["tree"], c
+        assert gpu.Merkle(h, c["width"]).root(cache[n]).hex() == c["root"], c
+
+
+def test_merkle_property_small(gpu, oracle):
+    """testMerkle.cpp:62-142 shape: widths 2..16 x counts 1..63, full output vector equal."""
+    rng = np.random.default_rng(3)
+    for width in range(2, 17):
+        for n in range(1, 64):
+            leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+            for hasher, H in ((0, gpu.Keccak256()), (1, gpu.SM3())):
+                if (width + n + hasher) % 3:
+                    continue
+                got = gpu.Merkle(H, width).generate_merkle([leaves[i].tobytes() for i in range(n)])
+                _, want = oracle.merkle(hasher, width, leaves, want_tree=True)
+                assert got == [want[i].tobytes() for i in range(want.shape[0])], (width, n, hasher)
+
+
+def test_merkle_empty_throws(gpu):
+    with pytest.raises(ValueError):
+        gpu.Merkle(gpu.SM3(), 2).generate_merkle([])
+    assert gpu.calculate_merkle_proof_root(gpu.SM3(), []) == hashlib.new("sm3", b"").digest()
+
+
+@pytest.mark.parametrize("width", [2, 16])
+@pytest.mark.parametrize("hasher", [0, 1])
+def test_merkle_1m(gpu, oracle, width, hasher):
+    rng = np.random.default_rng(width + hasher)
+    leaves = rng.integers(0, 256, size=(1_000_000, 32), dtype=np.uint8)
+    H = gpu.SM3() if hasher else gpu.Keccak256()
+    assert gpu.Merkle(H, width).root(leaves) == oracle.merkle(hasher, width, leaves, nthreads=16)
+
+
+def test_device_api_torch(gpu, oracle):
+    """The *_dev entry points on HBM-resident torch tensors, launched on torch's stream."""
+    import torch
+    from bcos_gpu import device
+    rng = np.random.default_rng(9)
+    msgs = [rng.bytes(int(n)) for n in rng.integers(0, 400, size=4096)]
+    data, off = gpu.pack_messages(msgs)
+    d_data = torch.from_numpy(data.copy()).cuda()
+    d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+    d_out = torch.zeros((len(msgs), 32), dtype=torch.uint8, device="cuda")
+    device.hash_batch(device.KECCAK256, d_data, d_off, d_out)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy(), oracle.hash_packed(0, data, off))
+    leaves = d_out
+    tree = torch.zeros((device.merkle_size(4096, 2), 32), dtype=torch.uint8, device="cuda")
+    root = torch.zeros(32, dtype=torch.uint8, device="cuda")
+    device.merkle_root(device.KECCAK256, 2, leaves, tree, root)
+    torch.cuda.synchronize()
+    assert root.cpu().numpy().tobytes() == oracle.merkle(0, 2, d_out.cpu().numpy())
