@@ -66,6 +66,13 @@ def lib():
     """Load libbcosgpu.so (raises OSError when the HIP build is missing)."""
     global _lib
     if _lib is None:
+        # torch ships its own HIP runtime (torch/lib/libamdhip64.so, soname libamdhip64.so.7); load
+        # it first so libbcosgpu.so binds to that same runtime instead of a second copy from
+        # /opt/rocm -- two HIP runtimes in one process cannot share devices, pointers or streams.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} not built: run `make -C fisco-bcos_amd` (or __graft_entry__.build())")
         L = ctypes.CDLL(LIB_PATH)

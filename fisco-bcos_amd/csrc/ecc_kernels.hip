@@ -1,10 +1,750 @@
-// ecc_kernels.hip -- placeholder until the ECC kernels land (fails loudly, never silently).
+// ecc_kernels.hip -- secp256k1 public-key recovery, SM2 verification, deterministic signing and the
+// fused tx-admission kernel (gfx950, one signature per lane, integer ALU only).
+//
+// Replaces (per item, batched):
+//   Secp256k1Crypto::recover -> wedpr_secp256k1_recover_public_key
+//       bcos-crypto/bcos-crypto/signature/secp256k1/Secp256k1Crypto.cpp:79-93 (libsecp256k1 semantics)
+//   SM2Crypto::recover -> verify -> fast_sm2_verify / sm2_do_verify
+//       bcos-crypto/bcos-crypto/signature/sm2/SM2Crypto.cpp:66-92, fastsm2/fast_sm2.cpp:139-227
+//   Transaction::verify (hash -> recover -> right160(H(pub)))
+//       bcos-framework/bcos-framework/protocol/Transaction.h:68-82
+//
+// Scalar multiplication:
+//   fixed base G : 8-bit comb, table[32][256] of affine multiples b*2^(8i)*G in HBM (512 KiB per
+//                  curve, L2-resident), 32 mixed additions and no doublings.
+//   variable base: radix-16 Booth recoding (digits in [-8, 8]) over a register-resident table of
+//                  1P..8P; every lane runs the same 65-window schedule (no divergence).
+#include <mutex>
+#include "ec.h"
 #include "engine.h"
+#include "hash_device.h"
+
 namespace bcosgpu {
-int ecc_init_tables(int) { return 0; }
-int launch_secp256k1_recover(const uint8_t*, const uint8_t*, uint32_t, uint64_t, uint8_t*, uint8_t*, uint8_t*, hipStream_t) { return BCOSGPU_E_ARG; }
-int launch_sm2_verify(const uint8_t*, const uint8_t*, uint32_t, uint64_t, uint8_t*, uint8_t*, hipStream_t) { return BCOSGPU_E_ARG; }
-int launch_secp256k1_sign(const uint8_t*, const uint8_t*, uint64_t, uint8_t*, uint8_t*, uint8_t*, hipStream_t) { return BCOSGPU_E_ARG; }
-int launch_sm2_sign(const uint8_t*, const uint8_t*, uint64_t, uint8_t*, uint8_t*, hipStream_t) { return BCOSGPU_E_ARG; }
-int launch_tx_verify(int, const uint8_t*, const uint64_t*, const uint8_t*, const uint64_t*, uint64_t, uint8_t*, uint8_t*, uint8_t*, hipStream_t) { return BCOSGPU_E_ARG; }
+
+// ------------------------------------------------------------------ curve constants (internal form)
+__device__ __constant__ static const uint32_t kK1Gx[8] = {0x16f81798u, 0x59f2815bu, 0x2dce28d9u, 0x029bfcdbu,
+                                                       0xce870b07u, 0x55a06295u, 0xf9dcbbacu, 0x79be667eu};
+__device__ __constant__ static const uint32_t kK1Gy[8] = {0xfb10d4b8u, 0x9c47d08fu, 0xa6855419u, 0xfd17b448u,
+                                                       0x0e1108a8u, 0x5da4fbfcu, 0x26a3c465u, 0x483ada77u};
+// p - n (recid & 2 requires r < p - n)
+__device__ __constant__ static const uint32_t kK1PminusN[8] = {0x2fc9baeeu, 0x402da172u, 0x50b75fc4u, 0x45512319u,
+                                                            0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u};
+__device__ __constant__ static const uint32_t kN1Half[8] = {0x681b20a0u, 0xdfe92f46u, 0x57a4501du, 0x5d576e73u,
+                                                         0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu};
+// SM2 (Montgomery form mod p)
+__device__ __constant__ static const uint32_t kSM2Gx[8] = {0xf418029eu, 0x61328990u, 0xdca6c050u, 0x3e7981edu,
+                                                        0xac24c3c3u, 0xd6a1ed99u, 0xe1c13b05u, 0x91167a5eu};
+__device__ __constant__ static const uint32_t kSM2Gy[8] = {0x3c2d0dddu, 0xc1354e59u, 0x8d3295fau, 0xc1f5e578u,
+                                                        0x6e2a48f8u, 0x8d4cfb06u, 0x81d735bdu, 0x63cd65d4u};
+__device__ __constant__ static const uint32_t kSM2B[8] = {0x2bc0dd42u, 0x90d23063u, 0xe9b537abu, 0x71cf379au,
+                                                       0x5ea51c3cu, 0x52798150u, 0xba20e2c8u, 0x240fe188u};
+// Z_A = SM3(ENTL || "1234567812345678" || a || b || xG || yG || xA || yA) (fast_sm2.cpp:34,203):
+// SM3 state after the key-independent first 128 bytes, the next 4 constant words and bytes 144..145.
+__device__ __constant__ static const uint32_t kZaMid[8] = {0xadadedb5u, 0x0446043fu, 0x08a87aceu, 0xe86d2243u,
+                                                        0x8e232383u, 0xbfc81fe2u, 0xcf9117c8u, 0x4707011du};
+__device__ __constant__ static const uint32_t kZaW32[4] = {0x2153d0a9u, 0x877cc62au, 0x474002dfu, 0x32e52139u};
+static constexpr uint32_t kZaC36 = 0xf0a00000u;
+
+// ------------------------------------------------------------------ per-device G tables
+static constexpr int kCombWindows = 32;
+static constexpr int kCombEntries = 256;
+static constexpr size_t kTabWords = static_cast<size_t>(kCombWindows) * kCombEntries * 16;
+static std::mutex g_tab_mu;
+static uint32_t* g_tab_k1[64];
+static uint32_t* g_tab_sm2[64];
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ void load_be256(fe& r, const uint8_t* p) {
+    ByteReader rd(p, 32);
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
+    fe_from_be_words(r, w);
 }
+__device__ __forceinline__ void load_be256_aligned(fe& r, const uint8_t* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1];
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    fe_from_be_words(r, w);
+}
+__device__ __forceinline__ void store_be256(uint8_t* p, const fe& a) {
+    uint32_t w[8];
+    fe_to_be_words(w, a);
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    q[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+__device__ __forceinline__ void store_be256_u32(uint8_t* p, const fe& a) {
+    uint32_t w[8];
+    fe_to_be_words(w, a);
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = w[i];
+}
+__device__ __forceinline__ void shr8(fe& k) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) k.v[i] = __builtin_amdgcn_alignbit(k.v[i + 1], k.v[i], 8);
+    k.v[7] >>= 8;
+}
+__device__ __forceinline__ void shl4(fe& k) {
+#pragma unroll
+    for (int i = 7; i > 0; --i) k.v[i] = __builtin_amdgcn_alignbit(k.v[i], k.v[i - 1], 28);
+    k.v[0] <<= 4;
+}
+__device__ __forceinline__ void shl1(fe& k) {
+#pragma unroll
+    for (int i = 7; i > 0; --i) k.v[i] = __builtin_amdgcn_alignbit(k.v[i], k.v[i - 1], 31);
+    k.v[0] <<= 1;
+}
+// x mod n for x < 2^256 (n > 2^255)
+__device__ __forceinline__ void reduce_once(fe& x, const uint32_t* n) {
+    fe t;
+    const uint32_t bw = fe_sub_k(t, x, n);
+    fe_cmov(x, t, bw == 0);
+}
+
+// ------------------------------------------------------------------ scalar multiplication
+// acc = k * G via the 8-bit comb table (k plain, < 2^256)
+template <class C>
+__device__ __forceinline__ void comb_mul(Jac& acc, const fe& k_plain, const uint32_t* __restrict__ tab) {
+    fe k;
+    fe_copy(k, k_plain);
+    C::set_inf(acc);
+#pragma unroll 1
+    for (int i = 0; i < kCombWindows; ++i) {
+        const uint32_t b = k.v[0] & 255u;
+        shr8(k);
+        const uint4* e = reinterpret_cast<const uint4*>(tab + (static_cast<size_t>(i) * kCombEntries + b) * 16);
+        const uint4 q0 = e[0], q1 = e[1], q2 = e[2], q3 = e[3];
+        Aff T;
+        T.x.v[0] = q0.x; T.x.v[1] = q0.y; T.x.v[2] = q0.z; T.x.v[3] = q0.w;
+        T.x.v[4] = q1.x; T.x.v[5] = q1.y; T.x.v[6] = q1.z; T.x.v[7] = q1.w;
+        T.y.v[0] = q2.x; T.y.v[1] = q2.y; T.y.v[2] = q2.z; T.y.v[3] = q2.w;
+        T.y.v[4] = q3.x; T.y.v[5] = q3.y; T.y.v[6] = q3.z; T.y.v[7] = q3.w;
+        Jac S;
+        C::madd(S, acc, T);
+        C::cmov(acc, S, b != 0u);
+    }
+}
+
+// acc = k * P, radix-16 Booth recoding over the table 1P..8P (k plain, < 2^256)
+template <class C, class F>
+__device__ __forceinline__ void booth_mul(Jac& acc, const fe& k_plain, const Aff& P) {
+    Jac T[8];
+    C::from_aff(T[0], P);
+    C::dbl(T[1], T[0]);
+    C::madd(T[2], T[1], P);
+    C::dbl(T[3], T[1]);
+    C::madd(T[4], T[3], P);
+    C::dbl(T[5], T[2]);
+    C::madd(T[6], T[5], P);
+    C::dbl(T[7], T[3]);
+    fe k;
+    fe_copy(k, k_plain);
+    C::set_inf(acc);
+    C::cmov(acc, T[0], (k.v[7] >> 31) != 0u);  // digit 64 = bit 255
+#pragma unroll 1
+    for (int i = 63; i >= 0; --i) {
+        C::dbl(acc, acc);
+        C::dbl(acc, acc);
+        C::dbl(acc, acc);
+        C::dbl(acc, acc);
+        const uint32_t top = k.v[7];
+        const uint32_t W = top >> 28, c = (top >> 27) & 1u;
+        const int d = static_cast<int>(W + c) - static_cast<int>((W >> 3) << 4);
+        shl4(k);
+        const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+        Jac S;
+        fe_copy(S.X, T[0].X); fe_copy(S.Y, T[0].Y); fe_copy(S.Z, T[0].Z); S.inf = false;
+#pragma unroll
+        for (int q = 1; q < 8; ++q) {
+            const bool take = m == static_cast<uint32_t>(q);
+            fe_cmov(S.X, T[q].X, take);
+            fe_cmov(S.Y, T[q].Y, take);
+            fe_cmov(S.Z, T[q].Z, take);
+        }
+        fe ny;
+        F::neg(ny, S.Y);
+        fe_cmov(S.Y, ny, d < 0);
+        Jac R;
+        C::add(R, acc, S);
+        C::cmov(acc, R, d != 0);
+    }
+}
+
+// ------------------------------------------------------------------ table construction
+template <class C, class F>
+__global__ __launch_bounds__(256) void comb_table_kernel(uint32_t* tab, int sm2) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= kCombWindows * kCombEntries) return;
+    const int i = idx / kCombEntries;
+    uint32_t b = static_cast<uint32_t>(idx % kCombEntries);
+    if (b == 0) b = 1;  // unused slot: a valid point, never selected
+    fe k;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) k.v[q] = (q == (i >> 2)) ? (b << ((i & 3) * 8)) : 0u;
+    Aff G;
+    fe gx, gy;
+    fe_set(gx, sm2 ? kSM2Gx : kK1Gx);
+    fe_set(gy, sm2 ? kSM2Gy : kK1Gy);
+    fe_copy(G.x, gx);
+    fe_copy(G.y, gy);
+    Jac acc, S;
+    C::set_inf(acc);
+#pragma unroll 1
+    for (int bit = 255; bit >= 0; --bit) {
+        C::dbl(acc, acc);
+        const bool set = (k.v[7] >> 31) != 0u;
+        shl1(k);
+        C::madd(S, acc, G);
+        C::cmov(acc, S, set);
+    }
+    Aff A;
+    C::to_aff(A, acc);
+    F::normalize(A.x);
+    F::normalize(A.y);
+    uint32_t* o = tab + static_cast<size_t>(idx) * 16;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        o[w] = A.x.v[w];
+        o[8 + w] = A.y.v[w];
+    }
+}
+
+int ecc_init_tables(int device) {
+    std::lock_guard<std::mutex> g(g_tab_mu);
+    if (device < 0 || device >= 64) return BCOSGPU_E_ARG;
+    if (g_tab_k1[device] && g_tab_sm2[device]) return 0;
+    uint32_t *k1 = nullptr, *sm2 = nullptr;
+    if (hipMalloc(&k1, kTabWords * 4) != hipSuccess) return BCOSGPU_E_HIP;
+    if (hipMalloc(&sm2, kTabWords * 4) != hipSuccess) return BCOSGPU_E_HIP;
+    const int n = kCombWindows * kCombEntries;
+    hipLaunchKernelGGL((comb_table_kernel<CurveK1, FieldK1>), dim3((n + 255) / 256), dim3(256), 0, 0, k1, 0);
+    hipLaunchKernelGGL((comb_table_kernel<CurveSM2, FieldP2>), dim3((n + 255) / 256), dim3(256), 0, 0, sm2, 1);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return BCOSGPU_E_HIP;
+    g_tab_k1[device] = k1;
+    g_tab_sm2[device] = sm2;
+    return 0;
+}
+
+static int tables(const uint32_t** k1, const uint32_t** sm2) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BCOSGPU_E_NODEV;
+    if (!g_tab_k1[dev]) return BCOSGPU_E_NODEV;  // bcosgpu_init(dev) not called
+    *k1 = g_tab_k1[dev];
+    *sm2 = g_tab_sm2[dev];
+    return 0;
+}
+
+// ------------------------------------------------------------------ secp256k1 recover (one lane)
+// libsecp256k1 secp256k1_ecdsa_recover as wedpr calls it: reject v > 3, r or s not in [1, n-1],
+// (v & 2) with r >= p - n, x not on the curve, Q = infinity.  pub = (x, y) canonical, plain.
+__device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const uint8_t* sig, uint32_t siglen,
+                                                       const uint32_t* tab, fe& px, fe& py) {
+    if (siglen != 65u) return false;
+    ByteReader rd(sig, 65);
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
+    fe r, s;
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
+    fe_from_be_words(s, w);
+    const uint32_t v = rd.word(16) & 0xffu;
+    bool ok = v <= 3u;
+    ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, ParamN1::M);
+    fe x;
+    fe_copy(x, r);
+    if (v & 2u) {
+        ok = ok && fe_lt_k(r, kK1PminusN);
+        fe_add_k(x, r, ParamN1::M);
+    }
+    // y = sqrt(x^3 + 7)
+    fe rhs, y, t, seven;
+    FieldK1::sqr(t, x);
+    FieldK1::mul(rhs, t, x);
+    fe_zero(seven);
+    seven.v[0] = 7;
+    FieldK1::add(rhs, rhs, seven);
+    FieldK1::sqrt_cand(y, rhs);
+    FieldK1::sqr(t, y);
+    ok = ok && FieldK1::eq(t, rhs);
+    FieldK1::normalize(y);
+    fe ny;
+    FieldK1::neg(ny, y);
+    FieldK1::normalize(ny);
+    fe_cmov(y, ny, (y.v[0] & 1u) != (v & 1u));
+    // u1 = -e / r, u2 = s / r (mod n)
+    fe e;
+    fe_copy(e, hash_be);
+    reduce_once(e, ParamN1::M);
+    fe rr = r;
+    if (!ok) {  // keep the arithmetic well-defined on rejected lanes
+        fe_zero(rr);
+        rr.v[0] = 1;
+    }
+    fe rm, rinv, u1, u2;
+    FieldN1::from_plain(rm, rr);
+    FieldN1::inv(rinv, rm);
+    FieldN1::mul(u1, e, rinv);
+    FieldN1::neg(u1, u1);
+    fe ss = s;
+    if (!ok) fe_zero(ss);
+    FieldN1::mul(u2, ss, rinv);
+    // Q = u1*G + u2*R
+    Aff R;
+    fe_copy(R.x, x);
+    fe_copy(R.y, y);
+    Jac QG, QR, Q;
+    comb_mul<CurveK1>(QG, u1, tab);
+    booth_mul<CurveK1, FieldK1>(QR, u2, R);
+    CurveK1::add(Q, QG, QR);
+    ok = ok && !Q.inf;
+    Aff A;
+    CurveK1::to_aff(A, Q);
+    FieldK1::normalize(A.x);
+    FieldK1::normalize(A.y);
+    fe_copy(px, A.x);
+    fe_copy(py, A.y);
+    return ok;
+}
+
+// pub -> right160(Keccak256(pub)) as 5 little-endian memory words
+__device__ __forceinline__ void keccak_address(uint32_t a[5], const fe& x, const fe& y) {
+    uint32_t m[16], d[8];
+    fe_to_be_words(m, x);
+    fe_to_be_words(m + 8, y);
+    keccak256_64(m, d);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) a[i] = d[3 + i];
+}
+// pub (plain) -> right160(SM3(pub))
+__device__ __forceinline__ void sm3_address(uint32_t a[5], const fe& x, const fe& y) {
+    uint32_t m[16], d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        m[j] = x.v[7 - j];
+        m[8 + j] = y.v[7 - j];
+    }
+    sm3_64(m, d);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) a[i] = bswap32(d[3 + i]);
+}
+
+// ------------------------------------------------------------------ SM2 (one lane)
+// e = SM3(Z_A || hash) as 8 big-endian words; X, Y: public key as big-endian word arrays
+__device__ __forceinline__ void sm2_e(uint32_t e[8], const uint32_t X[8], const uint32_t Y[8], const fe& hash_be) {
+    uint32_t V[8], W[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) V[i] = kZaMid[i];
+    // block 2: bytes 128..191 = words 32..47
+#pragma unroll
+    for (int j = 0; j < 4; ++j) W[j] = kZaW32[j];
+    W[4] = kZaC36 | (X[0] >> 16);
+#pragma unroll
+    for (int j = 1; j < 8; ++j) W[4 + j] = (X[j - 1] << 16) | (X[j] >> 16);
+    W[12] = (X[7] << 16) | (Y[0] >> 16);
+#pragma unroll
+    for (int j = 1; j < 4; ++j) W[12 + j] = (Y[j - 1] << 16) | (Y[j] >> 16);
+    sm3_compress(V, W);
+    // block 3: words 48..63
+#pragma unroll
+    for (int j = 0; j < 4; ++j) W[j] = (Y[j + 3] << 16) | (Y[j + 4] >> 16);
+    W[4] = (Y[7] << 16) | 0x8000u;
+#pragma unroll
+    for (int j = 5; j < 15; ++j) W[j] = 0;
+    W[15] = 210u * 8u;
+    sm3_compress(V, W);
+    // e = SM3(Z_A || hash): 64 bytes -> 2 blocks
+    uint32_t V2[8];
+    sm3_init(V2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) W[j] = V[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) W[8 + j] = hash_be.v[7 - j];
+    sm3_compress(V2, W);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) W[j] = 0;
+    W[0] = 0x80000000u;
+    W[15] = 512u;
+    sm3_compress(V2, W);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = V2[i];
+}
+
+// sm2_do_verify semantics (GB/T 32918.2): pub must be on the curve with coordinates < p,
+// r, s in [1, n-1], t = r + s mod n != 0, accept iff (e + x1) mod n == r for (x1, y1) = sG + tP.
+// The comparison is done projectively (X == (r - e mod n [+ n]) * Z^2), so no inversion.
+__device__ __forceinline__ bool sm2_verify_lane(const fe& hash_be, const uint8_t* sig, uint32_t siglen,
+                                                const uint32_t* tab, fe& px, fe& py) {
+    if (siglen != 128u) return false;
+    ByteReader rd(sig, 128);
+    uint32_t w[8], X[8], Y[8];
+    fe r, s;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
+    fe_from_be_words(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        X[i] = bswap32(rd.word(16 + i));
+        Y[i] = bswap32(rd.word(24 + i));
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        px.v[i] = X[7 - i];
+        py.v[i] = Y[7 - i];
+    }
+    bool ok = fe_lt_k(px, ParamP2::M) && fe_lt_k(py, ParamP2::M);
+    ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN2::M) && fe_lt_k(s, ParamN2::M);
+    Aff P;
+    FieldP2::from_plain(P.x, px);
+    FieldP2::from_plain(P.y, py);
+    fe b;
+    fe_set(b, kSM2B);
+    ok = ok && CurveSM2::on_curve(P, b);
+    fe t;
+    FieldN2::add(t, r, s);
+    ok = ok && !fe_is_zero_raw(t);
+    uint32_t eb[8];
+    sm2_e(eb, X, Y, hash_be);
+    fe e;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e.v[i] = eb[7 - i];
+    reduce_once(e, ParamN2::M);
+    Jac QG, QP, Q;
+    comb_mul<CurveSM2>(QG, s, tab);
+    booth_mul<CurveSM2, FieldP2>(QP, t, P);
+    CurveSM2::add(Q, QG, QP);
+    ok = ok && !Q.inf;
+    // x1 = X / Z^2 must be congruent to r - e (mod n): x1 = c or c + n (when c + n < p)
+    fe c, c2, cm, z2, rhs;
+    FieldN2::sub(c, r, e);
+    FieldP2::sqr(z2, Q.Z);
+    FieldP2::from_plain(cm, c);
+    FieldP2::mul(rhs, cm, z2);
+    bool match = FieldP2::eq(rhs, Q.X);
+    const uint32_t carry = fe_add_k(c2, c, ParamN2::M);
+    const bool v2 = carry == 0u && fe_lt_k(c2, ParamP2::M);
+    if (v2) {
+        FieldP2::from_plain(cm, c2);
+        FieldP2::mul(rhs, cm, z2);
+        match = match || FieldP2::eq(rhs, Q.X);
+    }
+    return ok && match;
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ __launch_bounds__(256) void secp256k1_recover_kernel(const uint8_t* __restrict__ hash,
+                                                                const uint8_t* __restrict__ sig, uint32_t stride,
+                                                                uint64_t n, const uint32_t* __restrict__ tab,
+                                                                uint8_t* __restrict__ pub, uint8_t* __restrict__ addr,
+                                                                uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe h, x, y;
+    load_be256_aligned(h, hash + 32 * i);
+    const bool ok = secp256k1_recover_lane(h, sig + static_cast<uint64_t>(stride) * i, 65u, tab, x, y);
+    if (!ok) {
+        fe_zero(x);
+        fe_zero(y);
+    }
+    if (pub) {
+        store_be256(pub + 64 * i, x);
+        store_be256(pub + 64 * i + 32, y);
+    }
+    if (addr) {
+        uint32_t a[5] = {0, 0, 0, 0, 0};
+        if (ok) keccak_address(a, x, y);
+        uint32_t* o = reinterpret_cast<uint32_t*>(addr + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = a[k];
+    }
+    okout[i] = ok ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void sm2_verify_kernel(const uint8_t* __restrict__ hash,
+                                                         const uint8_t* __restrict__ sig, uint32_t stride,
+                                                         uint64_t n, const uint32_t* __restrict__ tab,
+                                                         uint8_t* __restrict__ addr, uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe h, x, y;
+    load_be256_aligned(h, hash + 32 * i);
+    const bool ok = sm2_verify_lane(h, sig + static_cast<uint64_t>(stride) * i, 128u, tab, x, y);
+    if (addr) {
+        uint32_t a[5] = {0, 0, 0, 0, 0};
+        if (ok) sm3_address(a, x, y);
+        uint32_t* o = reinterpret_cast<uint32_t*>(addr + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = a[k];
+    }
+    okout[i] = ok ? 1 : 0;
+}
+
+// Transaction::verify for a batch: tx hash of the preimage, recover / verify, sender address.
+template <int SUITE>
+__global__ __launch_bounds__(256) void tx_verify_kernel(const uint8_t* __restrict__ pre,
+                                                        const uint64_t* __restrict__ pre_off,
+                                                        const uint8_t* __restrict__ sig,
+                                                        const uint64_t* __restrict__ sig_off, uint64_t n,
+                                                        const uint32_t* __restrict__ tab,
+                                                        uint8_t* __restrict__ txhash, uint8_t* __restrict__ sender,
+                                                        uint8_t* __restrict__ status) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a = pre_off[i], b = pre_off[i + 1];
+    const uint32_t len = static_cast<uint32_t>(b - a);
+    ByteReader rd(pre + a, len);
+    uint32_t d[8];
+    if (SUITE == BCOSGPU_SUITE_SM2) sm3_msg(rd, len, d);
+    else keccak256_msg(rd, len, d);
+    store_digest(SUITE == BCOSGPU_SUITE_SM2 ? SM3 : KECCAK256, txhash + 32 * i, d);
+    fe h;
+    if (SUITE == BCOSGPU_SUITE_SM2) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h.v[k] = d[7 - k];
+    } else {
+        fe_from_be_words(h, d);
+    }
+    const uint64_t sa = sig_off[i], sb = sig_off[i + 1];
+    const uint64_t slen64 = sb - sa;
+    const uint32_t slen = slen64 > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(slen64);
+    fe x, y;
+    uint32_t ad[5] = {0, 0, 0, 0, 0};
+    bool ok;
+    if (SUITE == BCOSGPU_SUITE_SM2) {
+        ok = sm2_verify_lane(h, sig + sa, slen, tab, x, y);
+        if (ok) sm3_address(ad, x, y);
+    } else {
+        ok = secp256k1_recover_lane(h, sig + sa, slen, tab, x, y);
+        if (ok) keccak_address(ad, x, y);
+    }
+    uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = ad[k];
+    status[i] = ok ? 0 : 1;
+}
+
+// Key derivation + deterministic ECDSA signing, libsecp256k1 conventions (low-S, recid).
+// k = Keccak256(sk || hash) mod n.
+__global__ __launch_bounds__(256) void secp256k1_sign_kernel(const uint8_t* __restrict__ sk32,
+                                                             const uint8_t* __restrict__ hash32, uint64_t n,
+                                                             const uint32_t* __restrict__ tab,
+                                                             uint8_t* __restrict__ pub, uint8_t* __restrict__ sigout,
+                                                             uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4* skw = reinterpret_cast<const uint4*>(sk32 + 32 * i);
+    const uint4* hw = reinterpret_cast<const uint4*>(hash32 + 32 * i);
+    const uint4 s0 = skw[0], s1 = skw[1], h0 = hw[0], h1 = hw[1];
+    const uint32_t m[16] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w,
+                            h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    fe d, e, k;
+    fe_from_be_words(d, m);
+    fe_from_be_words(e, m + 8);
+    uint32_t kd[8];
+    keccak256_64(m, kd);
+    fe_from_be_words(k, kd);
+    reduce_once(k, ParamN1::M);
+    reduce_once(e, ParamN1::M);
+    bool ok = !fe_is_zero_raw(d) && fe_lt_k(d, ParamN1::M) && !fe_is_zero_raw(k);
+    Jac P, R;
+    Aff PA, RA;
+    comb_mul<CurveK1>(P, d, tab);
+    comb_mul<CurveK1>(R, k, tab);
+    CurveK1::to_aff(PA, P);
+    CurveK1::to_aff(RA, R);
+    FieldK1::normalize(PA.x);
+    FieldK1::normalize(PA.y);
+    FieldK1::normalize(RA.x);
+    FieldK1::normalize(RA.y);
+    uint32_t recid = RA.y.v[0] & 1u;
+    fe r;
+    fe_copy(r, RA.x);
+    if (!fe_lt_k(r, ParamN1::M)) recid |= 2u;
+    reduce_once(r, ParamN1::M);
+    ok = ok && !fe_is_zero_raw(r);
+    // s = k^-1 (e + r d) mod n
+    fe km, kinv, dm, rd, t, s;
+    fe kk = k;
+    if (fe_is_zero_raw(kk)) kk.v[0] = 1;
+    FieldN1::from_plain(km, kk);
+    FieldN1::inv(kinv, km);
+    FieldN1::from_plain(dm, d);
+    FieldN1::mul(rd, r, dm);
+    FieldN1::add(t, e, rd);
+    FieldN1::mul(s, t, kinv);
+    ok = ok && !fe_is_zero_raw(s);
+    fe half;
+    fe_set(half, kN1Half);
+    if (fe_lt(half, s)) {
+        FieldN1::neg(s, s);
+        recid ^= 1u;
+    }
+    store_be256(pub + 64 * i, PA.x);
+    store_be256(pub + 64 * i + 32, PA.y);
+    uint8_t* so = sigout + 65 * i;
+    uint32_t rw[8], sw[8];
+    fe_to_be_words(rw, r);
+    fe_to_be_words(sw, s);
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+        so[q] = static_cast<uint8_t>(rw[q >> 2] >> ((q & 3) * 8));
+        so[32 + q] = static_cast<uint8_t>(sw[q >> 2] >> ((q & 3) * 8));
+    }
+    so[64] = static_cast<uint8_t>(recid);
+    okout[i] = ok ? 1 : 0;
+}
+
+// SM2 key derivation + signing (GB/T 32918.2), k = SM3(sk || hash) mod n; sig = r || s || pub.
+__global__ __launch_bounds__(256) void sm2_sign_kernel(const uint8_t* __restrict__ sk32,
+                                                       const uint8_t* __restrict__ hash32, uint64_t n,
+                                                       const uint32_t* __restrict__ tab,
+                                                       uint8_t* __restrict__ sigout, uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe d, h;
+    load_be256_aligned(d, sk32 + 32 * i);
+    load_be256_aligned(h, hash32 + 32 * i);
+    // k = SM3(sk || hash)
+    uint32_t W[16], V[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        W[j] = d.v[7 - j];
+        W[8 + j] = h.v[7 - j];
+    }
+    sm3_init(V);
+    sm3_compress(V, W);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) W[j] = 0;
+    W[0] = 0x80000000u;
+    W[15] = 512u;
+    sm3_compress(V, W);
+    fe k;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) k.v[j] = V[7 - j];
+    reduce_once(k, ParamN2::M);
+    fe nm1;
+    fe_set(nm1, ParamN2::M);
+    nm1.v[0] -= 1;  // n - 1 (low limb of n is odd and > 0)
+    bool ok = !fe_is_zero_raw(d) && fe_lt(d, nm1) && !fe_is_zero_raw(k);
+    Jac P, K;
+    Aff PA, KA;
+    comb_mul<CurveSM2>(P, d, tab);
+    comb_mul<CurveSM2>(K, k, tab);
+    CurveSM2::to_aff(PA, P);
+    CurveSM2::to_aff(KA, K);
+    fe px, py, x1;
+    FieldP2::to_plain(px, PA.x);
+    FieldP2::to_plain(py, PA.y);
+    FieldP2::to_plain(x1, KA.x);
+    uint32_t X[8], Y[8], eb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        X[j] = px.v[7 - j];
+        Y[j] = py.v[7 - j];
+    }
+    sm2_e(eb, X, Y, h);
+    fe e;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e.v[j] = eb[7 - j];
+    reduce_once(e, ParamN2::M);
+    reduce_once(x1, ParamN2::M);
+    fe r, t, s;
+    FieldN2::add(r, e, x1);
+    ok = ok && !fe_is_zero_raw(r);
+    FieldN2::add(t, r, k);
+    ok = ok && !fe_is_zero_raw(t);
+    fe one, dp1, dm, inv, rd;
+    fe_zero(one);
+    one.v[0] = 1;
+    FieldN2::add(dp1, d, one);
+    if (fe_is_zero_raw(dp1)) dp1.v[0] = 1;
+    FieldN2::from_plain(dm, dp1);
+    FieldN2::inv(inv, dm);
+    fe dmm;
+    FieldN2::from_plain(dmm, d);
+    FieldN2::mul(rd, r, dmm);
+    FieldN2::sub(t, k, rd);
+    FieldN2::mul(s, t, inv);
+    ok = ok && !fe_is_zero_raw(s);
+    uint8_t* so = sigout + 128 * i;
+    uint32_t w[8];
+    const fe* parts[4] = {&r, &s, &px, &py};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        fe_to_be_words(w, *parts[p]);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) reinterpret_cast<uint32_t*>(so + 32 * p)[q] = w[q];
+    }
+    okout[i] = ok ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ launchers
+static inline unsigned grid_of(uint64_t n) { return static_cast<unsigned>((n + 255) / 256); }
+
+int launch_secp256k1_recover(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride, uint64_t n,
+                             uint8_t* d_pub, uint8_t* d_addr, uint8_t* d_ok, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int rc = tables(&k1, &sm2);
+    if (rc) return rc;
+    hipLaunchKernelGGL(secp256k1_recover_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, k1,
+                       d_pub, d_addr, d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_sm2_verify(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride, uint64_t n, uint8_t* d_addr,
+                      uint8_t* d_ok, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int rc = tables(&k1, &sm2);
+    if (rc) return rc;
+    hipLaunchKernelGGL(sm2_verify_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, sm2, d_addr,
+                       d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_secp256k1_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint8_t* d_pub, uint8_t* d_sig,
+                          uint8_t* d_ok, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int rc = tables(&k1, &sm2);
+    if (rc) return rc;
+    if (!d_pub) return BCOSGPU_E_ARG;
+    hipLaunchKernelGGL(secp256k1_sign_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_sk, d_hash, n, k1, d_pub, d_sig,
+                       d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_sm2_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint8_t* d_sig, uint8_t* d_ok,
+                    hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int rc = tables(&k1, &sm2);
+    if (rc) return rc;
+    hipLaunchKernelGGL(sm2_sign_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_sk, d_hash, n, sm2, d_sig, d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off, const uint8_t* d_sig,
+                     const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash, uint8_t* d_sender, uint8_t* d_status,
+                     hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int rc = tables(&k1, &sm2);
+    if (rc) return rc;
+    if (suite == BCOSGPU_SUITE_SM2)
+        hipLaunchKernelGGL(tx_verify_kernel<BCOSGPU_SUITE_SM2>, dim3(grid_of(n)), dim3(256), 0, st, d_pre, d_pre_off,
+                           d_sig, d_sig_off, n, sm2, d_txhash, d_sender, d_status);
+    else
+        hipLaunchKernelGGL(tx_verify_kernel<BCOSGPU_SUITE_SECP256K1>, dim3(grid_of(n)), dim3(256), 0, st, d_pre,
+                           d_pre_off, d_sig, d_sig_off, n, k1, d_txhash, d_sender, d_status);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+}  // namespace bcosgpu

@@ -1,0 +1,483 @@
+// fe.h -- 256-bit modular arithmetic for gfx950, 8 x 32-bit limbs per lane (little-endian limbs).
+//
+// Two reduction strategies, chosen per modulus:
+//  * FieldK1  -- secp256k1 base field p = 2^256 - 2^32 - 977.  512-bit Comba product
+//                (v_mad_u64_u32 + v_addc_co_u32 per partial product), then a pseudo-Mersenne fold
+//                T = L + H*(2^32 + 977).  Values are kept "weakly reduced" in [0, 2^256);
+//                normalize() gives the canonical residue.
+//  * Mont<P>  -- Comba-interleaved ("FIPS") Montgomery multiplication, R = 2^256, for the SM2
+//                base field (m' = 1, one zero limb skipped) and both group orders.  Values in
+//                Montgomery form, fully reduced (< m).
+// Each partial product is one v_mad_u64_u32 whose carry-out feeds one v_addc_co_u32 (inline asm,
+// so the compiler cannot fall back to compare-and-select carry detection).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bcosgpu {
+
+struct fe {
+    uint32_t v[8];
+};
+
+// acc(64) + c2(32) += a * b   -- 96-bit column accumulator of the Comba product
+#define BG_MADC(acc, c2, a, b)                                                                 \
+    do {                                                                                       \
+        uint64_t cc_;                                                                          \
+        asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32_e64 %2, %1, %2, 0, %1"          \
+            : "+v"(acc), "=&s"(cc_), "+v"(c2)                                                  \
+            : "v"(a), "v"(b));                                                                 \
+    } while (0)
+// same with a compile-time constant multiplier (lives in an SGPR)
+#define BG_MADC_K(acc, c2, a, k)                                                               \
+    do {                                                                                       \
+        uint64_t cc_;                                                                          \
+        asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32_e64 %2, %1, %2, 0, %1"          \
+            : "+v"(acc), "=&s"(cc_), "+v"(c2)                                                  \
+            : "v"(a), "s"(k));                                                                 \
+    } while (0)
+
+__device__ __forceinline__ void fe_copy(fe& r, const fe& a) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = a.v[i];
+}
+__device__ __forceinline__ void fe_set(fe& r, const uint32_t k[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = k[i];
+}
+__device__ __forceinline__ void fe_zero(fe& r) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = 0;
+}
+__device__ __forceinline__ uint32_t fe_is_zero_raw(const fe& a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.v[i];
+    return o == 0;
+}
+__device__ __forceinline__ uint32_t fe_eq_raw(const fe& a, const fe& b) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o |= a.v[i] ^ b.v[i];
+    return o == 0;
+}
+// r = c ? a : r   (per lane, branch-free)
+__device__ __forceinline__ void fe_cmov(fe& r, const fe& a, bool c) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = c ? a.v[i] : r.v[i];
+}
+// a < b as 256-bit integers
+__device__ __forceinline__ bool fe_lt(const fe& a, const fe& b) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        x = static_cast<uint64_t>(a.v[i]) - b.v[i] - (x >> 63);
+    }
+    return (x >> 63) != 0;
+}
+__device__ __forceinline__ bool fe_lt_k(const fe& a, const uint32_t* k) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x = static_cast<uint64_t>(a.v[i]) - k[i] - (x >> 63);
+    return (x >> 63) != 0;
+}
+// r = a + b (mod 2^256), returns carry
+__device__ __forceinline__ uint32_t fe_add_raw(fe& r, const fe& a, const fe& b) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        x += static_cast<uint64_t>(a.v[i]) + b.v[i];
+        r.v[i] = static_cast<uint32_t>(x);
+        x >>= 32;
+    }
+    return static_cast<uint32_t>(x);
+}
+// r = a - b (mod 2^256), returns borrow
+__device__ __forceinline__ uint32_t fe_sub_raw(fe& r, const fe& a, const fe& b) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        x = static_cast<uint64_t>(a.v[i]) - b.v[i] - (x >> 63);
+        r.v[i] = static_cast<uint32_t>(x);
+    }
+    return static_cast<uint32_t>(x >> 63);
+}
+__device__ __forceinline__ uint32_t fe_sub_k(fe& r, const fe& a, const uint32_t* k) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        x = static_cast<uint64_t>(a.v[i]) - k[i] - (x >> 63);
+        r.v[i] = static_cast<uint32_t>(x);
+    }
+    return static_cast<uint32_t>(x >> 63);
+}
+__device__ __forceinline__ uint32_t fe_add_k(fe& r, const fe& a, const uint32_t* k) {
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        x += static_cast<uint64_t>(a.v[i]) + k[i];
+        r.v[i] = static_cast<uint32_t>(x);
+        x >>= 32;
+    }
+    return static_cast<uint32_t>(x);
+}
+
+// 256 x 256 -> 512-bit product, Comba (column) order.
+__device__ __forceinline__ void mul_512(uint32_t r[16], const fe& a, const fe& b) {
+    uint64_t acc = 0;
+    uint32_t c2 = 0;
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = k - i;
+            if (j >= 0 && j < 8) BG_MADC(acc, c2, a.v[i], b.v[j]);
+        }
+        r[k] = static_cast<uint32_t>(acc);
+        acc = (acc >> 32) | (static_cast<uint64_t>(c2) << 32);
+        c2 = 0;
+    }
+    r[15] = static_cast<uint32_t>(acc);
+}
+
+// 256-bit square: off-diagonal products once, doubled, plus the diagonal.
+__device__ __forceinline__ void sqr_512(uint32_t r[16], const fe& a) {
+    uint64_t acc = 0;
+    uint32_t c2 = 0;
+    uint32_t t[16];
+    t[0] = 0;
+#pragma unroll
+    for (int k = 1; k < 14; ++k) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = k - i;
+            if (j > i && j < 8) BG_MADC(acc, c2, a.v[i], a.v[j]);
+        }
+        t[k] = static_cast<uint32_t>(acc);
+        acc = (acc >> 32) | (static_cast<uint64_t>(c2) << 32);
+        c2 = 0;
+    }
+    t[14] = static_cast<uint32_t>(acc);
+    t[15] = static_cast<uint32_t>(acc >> 32);
+    // double: t <<= 1 (t < 2^479 so the shift cannot overflow 512 bits)
+#pragma unroll
+    for (int k = 15; k > 0; --k) t[k] = __builtin_amdgcn_alignbit(t[k], t[k - 1], 31);
+    t[0] = 0;
+    // add diagonal squares a_i^2 at columns 2i, 2i+1
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t sq = static_cast<uint64_t>(a.v[i]) * a.v[i];
+        x += static_cast<uint64_t>(t[2 * i]) + static_cast<uint32_t>(sq);
+        r[2 * i] = static_cast<uint32_t>(x);
+        x >>= 32;
+        x += static_cast<uint64_t>(t[2 * i + 1]) + static_cast<uint32_t>(sq >> 32);
+        r[2 * i + 1] = static_cast<uint32_t>(x);
+        x >>= 32;
+    }
+}
+
+// ============================================================================ secp256k1 base field
+struct FieldK1 {
+    // p = 2^256 - c, c = 2^32 + 977
+    static constexpr uint32_t P[8] = {0xfffffc2fu, 0xfffffffeu, 0xffffffffu, 0xffffffffu,
+                                      0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+
+    // r += f * c for f < 2^32 (f small in practice); returns the carry out of 2^256
+    __device__ static __forceinline__ uint32_t add_fc(fe& r, uint32_t f) {
+        uint64_t x = static_cast<uint64_t>(f) * 977u + r.v[0];
+        r.v[0] = static_cast<uint32_t>(x);
+        x = (x >> 32) + r.v[1] + f;
+        r.v[1] = static_cast<uint32_t>(x);
+        x >>= 32;
+#pragma unroll
+        for (int i = 2; i < 8; ++i) {
+            x += r.v[i];
+            r.v[i] = static_cast<uint32_t>(x);
+            x >>= 32;
+        }
+        return static_cast<uint32_t>(x);
+    }
+    // r -= f * c for f in {0, 1}; returns the borrow
+    __device__ static __forceinline__ uint32_t sub_fc(fe& r, uint32_t f) {
+        uint64_t x = static_cast<uint64_t>(r.v[0]) - f * 977u;
+        r.v[0] = static_cast<uint32_t>(x);
+        x = static_cast<uint64_t>(r.v[1]) - f - (x >> 63);
+        r.v[1] = static_cast<uint32_t>(x);
+#pragma unroll
+        for (int i = 2; i < 8; ++i) {
+            x = static_cast<uint64_t>(r.v[i]) - (x >> 63);
+            r.v[i] = static_cast<uint32_t>(x);
+        }
+        return static_cast<uint32_t>(x >> 63);
+    }
+
+    // reduce a 512-bit value to [0, 2^256)
+    __device__ static __forceinline__ void reduce(fe& o, const uint32_t t[16]) {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            acc += static_cast<uint64_t>(t[8 + k]) * 977u + t[k];
+            if (k) acc += t[7 + k];
+            o.v[k] = static_cast<uint32_t>(acc);
+            acc >>= 32;
+        }
+        acc += t[15];  // top < 2^33
+        const uint32_t top_lo = static_cast<uint32_t>(acc), top_hi = static_cast<uint32_t>(acc >> 32);
+        // o += top * (2^32 + 977), top = top_hi * 2^32 + top_lo
+        uint64_t x = static_cast<uint64_t>(top_lo) * 977u + o.v[0];
+        o.v[0] = static_cast<uint32_t>(x);
+        x = (x >> 32) + static_cast<uint64_t>(top_hi) * 977u + top_lo + o.v[1];
+        o.v[1] = static_cast<uint32_t>(x);
+        x = (x >> 32) + top_hi + o.v[2];
+        o.v[2] = static_cast<uint32_t>(x);
+        x >>= 32;
+#pragma unroll
+        for (int i = 3; i < 8; ++i) {
+            x += o.v[i];
+            o.v[i] = static_cast<uint32_t>(x);
+            x >>= 32;
+        }
+        add_fc(o, static_cast<uint32_t>(x));  // 2^256 wrapped once more: cannot carry again
+    }
+
+    __device__ static __forceinline__ void mul(fe& r, const fe& a, const fe& b) {
+        uint32_t t[16];
+        mul_512(t, a, b);
+        reduce(r, t);
+    }
+    __device__ static __forceinline__ void sqr(fe& r, const fe& a) {
+        uint32_t t[16];
+        sqr_512(t, a);
+        reduce(r, t);
+    }
+    __device__ static __forceinline__ void add(fe& r, const fe& a, const fe& b) {
+        uint32_t c = fe_add_raw(r, a, b);
+        c = add_fc(r, c);
+        add_fc(r, c);
+    }
+    __device__ static __forceinline__ void sub(fe& r, const fe& a, const fe& b) {
+        uint32_t bw = fe_sub_raw(r, a, b);
+        bw = sub_fc(r, bw);
+        sub_fc(r, bw);
+    }
+    // canonical residue in [0, p)
+    __device__ static __forceinline__ void normalize(fe& a) {
+        fe t;
+        fe_copy(t, a);
+        const uint32_t c = add_fc(t, 1u);  // a >= p  <=>  a + c >= 2^256
+        fe_cmov(a, t, c != 0);
+    }
+    __device__ static __forceinline__ bool is_zero(const fe& a) {
+        fe t;
+        fe_copy(t, a);
+        normalize(t);
+        return fe_is_zero_raw(t);
+    }
+    __device__ static __forceinline__ bool eq(const fe& a, const fe& b) {
+        fe t;
+        sub(t, a, b);
+        return is_zero(t);
+    }
+    __device__ static __forceinline__ void neg(fe& r, const fe& a) {
+        fe z;
+        fe_zero(z);
+        sub(r, z, a);
+    }
+    __device__ static __forceinline__ void from_plain(fe& r, const fe& a) { fe_copy(r, a); }
+    __device__ static __forceinline__ void to_plain(fe& r, const fe& a) {
+        fe_copy(r, a);
+        normalize(r);
+    }
+    __device__ static __forceinline__ void set_one(fe& r) {
+        fe_zero(r);
+        r.v[0] = 1;
+    }
+    __device__ static __forceinline__ void sqr_n(fe& r, const fe& a, int n) {
+        sqr(r, a);
+        for (int i = 1; i < n; ++i) sqr(r, r);
+    }
+    // x^(2^223 - 1) building blocks of libsecp256k1-style addition chains
+    __device__ static __forceinline__ void chain223(fe& x223, fe& x22, fe& x2, fe& x3, const fe& a) {
+        fe t, x6, x9, x11, x44, x88, x176, x220;
+        sqr(t, a); mul(x2, t, a);
+        sqr(t, x2); mul(x3, t, a);
+        sqr_n(t, x3, 3); mul(x6, t, x3);
+        sqr_n(t, x6, 3); mul(x9, t, x3);
+        sqr_n(t, x9, 2); mul(x11, t, x2);
+        sqr_n(t, x11, 11); mul(x22, t, x11);
+        sqr_n(t, x22, 22); mul(x44, t, x22);
+        sqr_n(t, x44, 44); mul(x88, t, x44);
+        sqr_n(t, x88, 88); mul(x176, t, x88);
+        sqr_n(t, x176, 44); mul(x220, t, x44);
+        sqr_n(t, x220, 3); mul(x223, t, x3);
+    }
+    // a^(p-2)
+    __device__ static __forceinline__ void inv(fe& r, const fe& a) {
+        fe x223, x22, x2, x3, t;
+        chain223(x223, x22, x2, x3, a);
+        sqr_n(t, x223, 23); mul(t, t, x22);
+        sqr_n(t, t, 5); mul(t, t, a);
+        sqr_n(t, t, 3); mul(t, t, x2);
+        sqr_n(t, t, 2); mul(r, t, a);
+    }
+    // a^((p+1)/4): a square root when one exists
+    __device__ static __forceinline__ void sqrt_cand(fe& r, const fe& a) {
+        fe x223, x22, x2, x3, t;
+        chain223(x223, x22, x2, x3, a);
+        sqr_n(t, x223, 23); mul(t, t, x22);
+        sqr_n(t, t, 6); mul(t, t, x2);
+        sqr_n(r, t, 2);
+    }
+};
+
+// ============================================================================ Montgomery fields
+struct ParamP2 {  // SM2 base field
+    static constexpr uint32_t M[8] = {0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu,
+                                      0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu};
+    static constexpr uint32_t MINV = 0x1u;
+    static constexpr uint32_t R2[8] = {0x00000003u, 0x00000002u, 0xffffffffu, 0x00000002u,
+                                       0x00000001u, 0x00000001u, 0x00000002u, 0x00000004u};
+    static constexpr uint32_t ONE[8] = {0x00000001u, 0x00000000u, 0xffffffffu, 0x00000000u,
+                                        0x00000000u, 0x00000000u, 0x00000000u, 0x00000001u};
+    static constexpr uint32_t EXP_INV[8] = {0xfffffffdu, 0xffffffffu, 0x00000000u, 0xffffffffu,
+                                            0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu};
+};
+struct ParamN1 {  // secp256k1 group order
+    static constexpr uint32_t M[8] = {0xd0364141u, 0xbfd25e8cu, 0xaf48a03bu, 0xbaaedce6u,
+                                      0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+    static constexpr uint32_t MINV = 0x5588b13fu;
+    static constexpr uint32_t R2[8] = {0x67d7d140u, 0x896cf214u, 0x0e7cf878u, 0x741496c2u,
+                                       0x5bcd07c6u, 0xe697f5e4u, 0x81c69bc5u, 0x9d671cd5u};
+    static constexpr uint32_t ONE[8] = {0x2fc9bebfu, 0x402da173u, 0x50b75fc4u, 0x45512319u,
+                                        0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u};
+    static constexpr uint32_t EXP_INV[8] = {0xd036413fu, 0xbfd25e8cu, 0xaf48a03bu, 0xbaaedce6u,
+                                            0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+};
+struct ParamN2 {  // SM2 group order
+    static constexpr uint32_t M[8] = {0x39d54123u, 0x53bbf409u, 0x21c6052bu, 0x7203df6bu,
+                                      0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu};
+    static constexpr uint32_t MINV = 0x72350975u;
+    static constexpr uint32_t R2[8] = {0x7c114f20u, 0x901192afu, 0xde6fa2fau, 0x3464504au,
+                                       0x3affe0d4u, 0x620fc84cu, 0xa22b3d3bu, 0x1eb5e412u};
+    static constexpr uint32_t ONE[8] = {0xc62abeddu, 0xac440bf6u, 0xde39fad4u, 0x8dfc2094u,
+                                        0x00000000u, 0x00000000u, 0x00000000u, 0x00000001u};
+    static constexpr uint32_t EXP_INV[8] = {0x39d54121u, 0x53bbf409u, 0x21c6052bu, 0x7203df6bu,
+                                            0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu};
+};
+
+template <class P>
+struct Mont {
+    static constexpr const uint32_t* M = P::M;
+
+    // r = a * b * 2^-256 mod m (inputs < m, output < m)
+    __device__ static __forceinline__ void mul(fe& r, const fe& a, const fe& b) {
+        uint64_t acc = 0;
+        uint32_t c2 = 0, m[8], o[8];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int j = k - i;
+                if (j >= 0 && j < 8) BG_MADC(acc, c2, a.v[i], b.v[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int j = k - i;
+                if (i < k && j >= 1 && j < 8 && P::M[j] != 0u) BG_MADC_K(acc, c2, m[i], P::M[j]);
+            }
+            if (k < 8) {
+                m[k] = P::MINV == 1u ? static_cast<uint32_t>(acc) : static_cast<uint32_t>(acc) * P::MINV;
+                BG_MADC_K(acc, c2, m[k], P::M[0]);
+            } else {
+                o[k - 8] = static_cast<uint32_t>(acc);
+            }
+            acc = (acc >> 32) | (static_cast<uint64_t>(c2) << 32);
+            c2 = 0;
+        }
+        // result = o + top * 2^256 < 2m ; subtract m once if needed
+        const uint32_t top = static_cast<uint32_t>(acc);
+        fe t, u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t.v[i] = o[i];
+        const uint32_t bw = fe_sub_k(u, t, P::M);
+        const bool take = top != 0u || bw == 0u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.v[i] = take ? u.v[i] : t.v[i];
+    }
+    __device__ static __forceinline__ void sqr(fe& r, const fe& a) { mul(r, a, a); }
+    __device__ static __forceinline__ void add(fe& r, const fe& a, const fe& b) {
+        fe s, t;
+        const uint32_t c = fe_add_raw(s, a, b);
+        const uint32_t bw = fe_sub_k(t, s, P::M);
+        const bool take = c != 0u || bw == 0u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.v[i] = take ? t.v[i] : s.v[i];
+    }
+    __device__ static __forceinline__ void sub(fe& r, const fe& a, const fe& b) {
+        fe d, t;
+        const uint32_t bw = fe_sub_raw(d, a, b);
+        fe_add_k(t, d, P::M);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.v[i] = bw ? t.v[i] : d.v[i];
+    }
+    __device__ static __forceinline__ void neg(fe& r, const fe& a) {
+        fe z;
+        fe_zero(z);
+        sub(r, z, a);
+    }
+    __device__ static __forceinline__ void normalize(fe&) {}
+    __device__ static __forceinline__ bool is_zero(const fe& a) { return fe_is_zero_raw(a); }
+    __device__ static __forceinline__ bool eq(const fe& a, const fe& b) { return fe_eq_raw(a, b); }
+    __device__ static __forceinline__ void set_one(fe& r) { fe_set(r, P::ONE); }
+    // plain (< m) -> Montgomery form
+    __device__ static __forceinline__ void from_plain(fe& r, const fe& a) {
+        fe k;
+        fe_set(k, P::R2);
+        mul(r, a, k);
+    }
+    __device__ static __forceinline__ void to_plain(fe& r, const fe& a) {
+        fe one;
+        fe_zero(one);
+        one.v[0] = 1;
+        mul(r, a, one);
+    }
+    // a^(m-2) by left-to-right 4-bit fixed windows (wave-uniform window values)
+    __device__ static __forceinline__ void inv(fe& r, const fe& a) {
+        fe tab[16];
+        set_one(tab[0]);
+        fe_copy(tab[1], a);
+#pragma unroll
+        for (int i = 2; i < 16; ++i) mul(tab[i], tab[i - 1], a);
+        set_one(r);
+#pragma unroll 1
+        for (int w = 63; w >= 0; --w) {
+            if (w != 63) {
+                sqr(r, r); sqr(r, r); sqr(r, r); sqr(r, r);
+            }
+            const uint32_t nib = (P::EXP_INV[w >> 3] >> ((w & 7) * 4)) & 15u;
+            fe s;
+            fe_copy(s, tab[0]);
+#pragma unroll
+            for (int q = 1; q < 16; ++q) fe_cmov(s, tab[q], nib == static_cast<uint32_t>(q));
+            mul(r, r, s);
+        }
+    }
+};
+
+using FieldP2 = Mont<ParamP2>;
+using FieldN1 = Mont<ParamN1>;
+using FieldN2 = Mont<ParamN2>;
+
+// ---------------------------------------------------------------- byte conversions
+// 32 big-endian bytes (8 little-endian-loaded words w[0..7] in memory order) -> limbs
+__device__ __forceinline__ void fe_from_be_words(fe& r, const uint32_t w[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = __builtin_bswap32(w[7 - i]);
+}
+__device__ __forceinline__ void fe_to_be_words(uint32_t w[8], const fe& a) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[7 - i] = __builtin_bswap32(a.v[i]);
+}
+
+}  // namespace bcosgpu
