@@ -182,7 +182,7 @@ def test_sm2_verify_random_and_edge(gpu, oracle):
     _, addr, okg = gpu.SM2Crypto().recover_batch(h, sig, want_address=True)
     want = oracle.sm2_verify_batch(h, sig, nthreads=8)
     assert np.array_equal(okg, want)
-    assert want.sum() > n // 4
+    assert want.sum() >= n // 4
     for i in np.nonzero(want)[0][:200]:
         assert addr[i].tobytes() == oracle.sm3(sig[i, 64:].tobytes())[12:]
 
