@@ -42,6 +42,7 @@ _SIGS = {
     "bcosgpu_hash_batch_dev": (_I, [_I, _P, _P, _SZ, _P, _P]),
     "bcosgpu_merkle_root": (_I, [_I, _I, _I, _P, _SZ, _P, _P]),
     "bcosgpu_merkle_root_dev": (_I, [_I, _I, _P, _SZ, _P, _P, _P]),
+    "bcosgpu_merkle_frontier_dev": (_I, [_I, _I, _P, _SZ, _I, _P, _P, _P]),
     "bcosgpu_secp256k1_recover_batch": (_I, [_P, _P, _SZ, _P, _P, _P]),
     "bcosgpu_secp256k1_recover_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P, _P]),
     "bcosgpu_sm2_verify_batch": (_I, [_P, _P, _SZ, _P, _P]),

@@ -46,6 +46,13 @@ def merkle_root(hasher, width, leaves, tree, root, stream=None):
                                         _s(stream)))
 
 
+def merkle_frontier(hasher, width, leaves, levels, work, frontier, stream=None):
+    """Reference-tree level `levels` over a width^levels-aligned shard (bcosgpu_merkle_frontier_dev)."""
+    _dev(leaves)
+    check(lib().bcosgpu_merkle_frontier_dev(hasher, width, _p(leaves), leaves.shape[0], levels, _p(work),
+                                            _p(frontier), _s(stream)))
+
+
 def secp256k1_recover(hashes, sigs, pub, addr, ok, stream=None):
     """hashes uint8[n,32], sigs uint8[n,65] -> pub uint8[n,64] (or None), addr uint8[n,20] (or None), ok uint8[n]."""
     _dev(hashes)

@@ -1,0 +1,97 @@
+"""Multi-GPU sharding of the hot path (one process per GPU, torch.distributed over RCCL).
+
+Transactions shard by index with no data-path collective: each rank verifies its own contiguous
+range and keeps its verdicts / senders.  The only exchange is the block tx root:
+Merkle<H, width> (Merkle.h:170-208) groups every level from index 0, so when rank r's leaf range
+starts at a multiple of width^L, its level-L nodes are exactly the reference tree's level-L nodes for
+that range.  Each rank computes its frontier on its own GPU, ONE all-gather moves the frontiers
+(count-prefixed, fixed-size buffers, a few KB), and every rank finishes the top levels -- so the
+root is bit-identical to the single-device / reference root for any leaf count.
+"""
+import math
+
+import torch
+import torch.distributed as dist
+
+
+def choose_levels(n, world, width, target_frontier=64):
+    """Levels computed per shard: the largest L with world * target_frontier * width^L <= n
+    (so the gathered frontier stays small but every rank still has whole width^L blocks), and the
+    global level-L count >= 2 (the reference tree must have more than L levels)."""
+    L = 0
+    while True:
+        blk = width ** (L + 1)
+        if world * target_frontier * blk > n or math.ceil(n / blk) < 2:
+            break
+        L += 1
+    return L
+
+
+def shard_plan(n, world, width, levels):
+    """Contiguous leaf ranges [lo, hi) per rank; every lo is a multiple of width^levels."""
+    blk = width ** levels
+    per = math.ceil(n / (world * blk)) * blk
+    return [(min(r * per, n), min((r + 1) * per, n)) for r in range(world)]
+
+
+def sharded_merkle_root(frontier_fn, root_fn, n, width, levels, rank, world, dev, group=None):
+    """Root of the reference tree over n leaves sharded across `world` ranks.
+
+    frontier_fn(lo, hi) -> uint8 tensor [ceil((hi-lo)/width^levels), 32] on `dev`: this rank's
+        level-`levels` nodes (computed on its GPU; for levels == 0 the leaves themselves).
+    root_fn(frontier [m, 32]) -> uint8 tensor [32]: Merkle<H, width> root of the frontier.
+    """
+    plan = shard_plan(n, world, width, levels)
+    blk = width ** levels
+    lo, hi = plan[rank]
+    cap = math.ceil((plan[0][1] - plan[0][0]) / blk) if plan[0][1] > plan[0][0] else 1
+    buf = torch.zeros((cap + 1, 32), dtype=torch.uint8, device=dev)  # row 0: count record
+    if hi > lo:
+        f = frontier_fn(lo, hi)
+        m = f.shape[0]
+        buf[1:1 + m] = f
+    else:
+        m = 0
+    buf[0, :4] = torch.tensor(list(int(m).to_bytes(4, "big")), dtype=torch.uint8, device=dev)
+    gathered = torch.empty((world, cap + 1, 32), dtype=torch.uint8, device=dev)
+    if world > 1:
+        dist.all_gather_into_tensor(gathered.view(-1), buf.view(-1), group=group)
+    else:
+        gathered[0] = buf
+    parts = []
+    for r in range(world):
+        cnt = int.from_bytes(bytes(gathered[r, 0, :4].cpu().tolist()), "big")
+        if cnt:
+            parts.append(gathered[r, 1:1 + cnt])
+    frontier = torch.cat(parts, 0).contiguous()
+    return root_fn(frontier)
+
+
+def gpu_frontier_fn(hasher, width, levels, leaves):
+    """frontier_fn over a device-resident global leaf tensor (rank-local rows are used)."""
+    from . import device
+
+    def fn(lo, hi):
+        part = leaves[lo:hi].contiguous()
+        if levels == 0:
+            return part
+        m = math.ceil((hi - lo) / width ** levels)
+        work = torch.empty((2 * math.ceil((hi - lo) / width), 32), dtype=torch.uint8, device=leaves.device)
+        out = torch.empty((m, 32), dtype=torch.uint8, device=leaves.device)
+        device.merkle_frontier(hasher, width, part, levels, work, out)
+        return out
+
+    return fn
+
+
+def gpu_root_fn(hasher, width):
+    from . import device
+
+    def fn(frontier):
+        m = frontier.shape[0]
+        tree = torch.empty((max(device.merkle_size(m, width), 1), 32), dtype=torch.uint8, device=frontier.device)
+        root = torch.empty(32, dtype=torch.uint8, device=frontier.device)
+        device.merkle_root(hasher, width, frontier, tree, root)
+        return root
+
+    return fn

@@ -204,6 +204,16 @@ int bcosgpu_merkle_root(int hasher, int width, int variant, const uint8_t* leave
     return 0;
 }
 
+int bcosgpu_merkle_frontier_dev(int hasher, int width, const uint8_t* d_leaves32, size_t n, int levels,
+                                uint8_t* d_work, uint8_t* d_frontier, void* stream) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (n == 0) return set_err(BCOSGPU_E_EMPTY, "Empty input");
+    if (width < 2 || width > 64 || levels < 1 || levels > 63) return set_err(BCOSGPU_E_ARG, "bad width/levels");
+    if (!d_leaves32 || !d_work || !d_frontier) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_merkle_levels(hasher, width, d_leaves32, n, levels, d_work, d_frontier, as_stream(stream));
+    return rc ? hip_err(hipGetLastError(), "merkle frontier launch") : 0;
+}
+
 // ------------------------------------------------------------------ signatures
 int bcosgpu_secp256k1_recover_batch_dev(const uint8_t* d_hash32, const uint8_t* d_sig65, size_t n,
                                         uint8_t* d_pub64, uint8_t* d_addr20, uint8_t* d_ok,

@@ -31,6 +31,20 @@ __device__ __constant__ static const uint32_t kK1PminusN[8] = {0x2fc9baeeu, 0x40
                                                             0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u};
 __device__ __constant__ static const uint32_t kN1Half[8] = {0x681b20a0u, 0xdfe92f46u, 0x57a4501du, 0x5d576e73u,
                                                          0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu};
+// GLV endomorphism of secp256k1: lambda*(x, y) = (beta*x, y); split constants of libsecp256k1's
+// secp256k1_scalar_split_lambda (|k1|, |k2| < 2^128).  LAMBDA and MINUS_B2 in Montgomery form mod n.
+__device__ __constant__ static const uint32_t kGlvG1[8] = {0x45dbb031u, 0xe893209au, 0x71e8ca7fu, 0x3daa8a14u,
+                                                        0x9284eb15u, 0xe86c90e4u, 0xa7d46bcdu, 0x3086d221u};
+__device__ __constant__ static const uint32_t kGlvG2[8] = {0x8ac47f71u, 0x1571b4aeu, 0x9df506c6u, 0x221208acu,
+                                                        0x0abfe4c4u, 0x6f547fa9u, 0x010e8828u, 0xe4437ed6u};
+__device__ __constant__ static const uint32_t kGlvMB1[8] = {0x0abfe4c3u, 0x6f547fa9u, 0x010e8828u, 0xe4437ed6u,
+                                                         0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u};
+__device__ __constant__ static const uint32_t kGlvMB2M[8] = {0x6a144696u, 0x0cac5e50u, 0xf3ba5939u, 0x1e8a8dc5u,
+                                                          0xba244fceu, 0x176cdf65u, 0x8e173580u, 0xc25575ebu};
+__device__ __constant__ static const uint32_t kGlvLambdaM[8] = {0xc9926c9eu, 0xf07deb3du, 0x83c6944cu, 0x2c93e7adu,
+                                                             0x52697d91u, 0x73a96606u, 0x8558d639u, 0x53284017u};
+__device__ __constant__ static const uint32_t kGlvBeta[8] = {0x719501eeu, 0xc1396c28u, 0x12f58995u, 0x9cf04975u,
+                                                          0xac3434e9u, 0x6e64479eu, 0x657c0710u, 0x7ae96a2bu};
 // SM2 (Montgomery form mod p)
 __device__ __constant__ static const uint32_t kSM2Gx[8] = {0xf418029eu, 0x61328990u, 0xdca6c050u, 0x3e7981edu,
                                                         0xac24c3c3u, 0xd6a1ed99u, 0xe1c13b05u, 0x91167a5eu};
@@ -172,6 +186,116 @@ __device__ __forceinline__ void booth_mul(Jac& acc, const fe& k_plain, const Aff
     }
 }
 
+// k = k1 + k2*lambda (mod n) with |k1|, |k2| < 2^128 (libsecp256k1 split_lambda); returns the
+// magnitudes and signs.
+__device__ __forceinline__ void glv_split(fe& k1, bool& neg1, fe& k2, bool& neg2, const fe& k) {
+    uint32_t t[16];
+    fe g, c1, c2, x, y;
+    fe_set(g, kGlvG1);
+    mul_512(t, k, g);
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c1.v[i] = addc32(t[12 + i], i == 0 ? (t[11] >> 31) : 0u, c, c);
+#pragma unroll
+    for (int i = 4; i < 8; ++i) c1.v[i] = 0;
+    fe_set(g, kGlvG2);
+    mul_512(t, k, g);
+    c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c2.v[i] = addc32(t[12 + i], i == 0 ? (t[11] >> 31) : 0u, c, c);
+#pragma unroll
+    for (int i = 4; i < 8; ++i) c2.v[i] = 0;
+    fe_set(g, kGlvMB1);
+    mul_512(t, c1, g);  // < 2^256
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x.v[i] = t[i];
+    reduce_once(x, ParamN1::M);
+    fe_set(g, kGlvMB2M);
+    FieldN1::mul(y, c2, g);  // c2 * (-b2) mod n
+    FieldN1::add(k2, x, y);
+    fe_set(g, kGlvLambdaM);
+    FieldN1::mul(x, k2, g);  // k2 * lambda mod n
+    FieldN1::sub(k1, k, x);
+    fe half, nk;
+    fe_set(half, kN1Half);
+    neg1 = fe_lt(half, k1);
+    FieldN1::neg(nk, k1);
+    fe_cmov(k1, nk, neg1);
+    neg2 = fe_lt(half, k2);
+    FieldN1::neg(nk, k2);
+    fe_cmov(k2, nk, neg2);
+}
+
+__device__ __forceinline__ void shl4_128(fe& k) {
+#pragma unroll
+    for (int i = 3; i > 0; --i) k.v[i] = __builtin_amdgcn_alignbit(k.v[i], k.v[i - 1], 28);
+    k.v[0] <<= 4;
+}
+
+// one Booth digit of a 128-bit scalar held in k.v[0..3], window at bits 124..127
+__device__ __forceinline__ int booth_digit128(fe& k) {
+    const uint32_t top = k.v[3];
+    const uint32_t W = top >> 28, c = (top >> 27) & 1u;
+    shl4_128(k);
+    return static_cast<int>(W + c) - static_cast<int>((W >> 3) << 4);
+}
+
+// acc += (sign * d) * (phi ? lambda : 1) * P, T[j] = (j+1) P
+__device__ __forceinline__ void glv_add_digit(Jac& acc, const Jac T[8], int d, bool neg, bool phi) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    Jac S;
+    fe_copy(S.X, T[0].X); fe_copy(S.Y, T[0].Y); fe_copy(S.Z, T[0].Z); S.inf = false;
+#pragma unroll
+    for (int q = 1; q < 8; ++q) {
+        const bool take = m == static_cast<uint32_t>(q);
+        fe_cmov(S.X, T[q].X, take);
+        fe_cmov(S.Y, T[q].Y, take);
+        fe_cmov(S.Z, T[q].Z, take);
+    }
+    if (phi) {
+        fe b;
+        fe_set(b, kGlvBeta);
+        FieldK1::mul(S.X, S.X, b);
+    }
+    fe ny;
+    FieldK1::neg(ny, S.Y);
+    fe_cmov(S.Y, ny, (d < 0) != neg);
+    Jac R;
+    CurveK1::add(R, acc, S);
+    CurveK1::cmov(acc, R, d != 0);
+}
+
+// acc = k * P on secp256k1 via GLV: k1*P + k2*phi(P), 33 joint radix-16 Booth windows
+__device__ __forceinline__ void glv_mul_k1(Jac& acc, const fe& k, const Aff& P) {
+    fe k1, k2;
+    bool neg1, neg2;
+    glv_split(k1, neg1, k2, neg2, k);
+    Jac T[8];
+    CurveK1::from_aff(T[0], P);
+    CurveK1::dbl(T[1], T[0]);
+    CurveK1::madd(T[2], T[1], P);
+    CurveK1::dbl(T[3], T[1]);
+    CurveK1::madd(T[4], T[3], P);
+    CurveK1::dbl(T[5], T[2]);
+    CurveK1::madd(T[6], T[5], P);
+    CurveK1::dbl(T[7], T[3]);
+    CurveK1::set_inf(acc);
+    // digit 32 = bit 127 of each half
+    glv_add_digit(acc, T, static_cast<int>(k1.v[3] >> 31), neg1, false);
+    glv_add_digit(acc, T, static_cast<int>(k2.v[3] >> 31), neg2, true);
+#pragma unroll 1
+    for (int i = 31; i >= 0; --i) {
+        CurveK1::dbl(acc, acc);
+        CurveK1::dbl(acc, acc);
+        CurveK1::dbl(acc, acc);
+        CurveK1::dbl(acc, acc);
+        const int d1 = booth_digit128(k1);
+        const int d2 = booth_digit128(k2);
+        glv_add_digit(acc, T, d1, neg1, false);
+        glv_add_digit(acc, T, d2, neg2, true);
+    }
+}
+
 // ------------------------------------------------------------------ table construction
 template <class C, class F>
 __global__ __launch_bounds__(256) void comb_table_kernel(uint32_t* tab, int sm2) {
@@ -298,7 +422,7 @@ __device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const 
     fe_copy(R.y, y);
     Jac QG, QR, Q;
     comb_mul<CurveK1>(QG, u1, tab);
-    booth_mul<CurveK1, FieldK1>(QR, u2, R);
+    glv_mul_k1(QR, u2, R);
     CurveK1::add(Q, QG, QR);
     ok = ok && !Q.inf;
     Aff A;

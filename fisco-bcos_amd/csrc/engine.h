@@ -12,6 +12,8 @@ int launch_hash_batch(int hasher, const uint8_t* d_data, const uint64_t* d_off, 
 uint64_t merkle_size(uint64_t n, int width);
 int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
                   uint8_t* d_root, hipStream_t st);
+int launch_merkle_levels(int hasher, int width, const uint8_t* d_in, uint64_t n, int levels, uint8_t* d_work,
+                         uint8_t* d_out, hipStream_t st);
 int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* d_scratch,
                       uint8_t* d_root, hipStream_t st);
 

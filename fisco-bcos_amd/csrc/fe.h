@@ -66,60 +66,59 @@ __device__ __forceinline__ void fe_cmov(fe& r, const fe& a, bool c) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.v[i] = c ? a.v[i] : r.v[i];
 }
+// 32-bit add/sub with carry: lower to v_add_co_u32 / v_addc_co_u32 / v_sub(b)_co_u32 chains
+__device__ __forceinline__ uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t& cout) {
+    unsigned int co;
+    const uint32_t r = __builtin_addc(a, b, cin, &co);
+    cout = co;
+    return r;
+}
+__device__ __forceinline__ uint32_t subc32(uint32_t a, uint32_t b, uint32_t bin, uint32_t& bout) {
+    unsigned int bo;
+    const uint32_t r = __builtin_subc(a, b, bin, &bo);
+    bout = bo;
+    return r;
+}
 // a < b as 256-bit integers
 __device__ __forceinline__ bool fe_lt(const fe& a, const fe& b) {
-    uint64_t x = 0;
+    uint32_t bw = 0, t;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        x = static_cast<uint64_t>(a.v[i]) - b.v[i] - (x >> 63);
-    }
-    return (x >> 63) != 0;
+    for (int i = 0; i < 8; ++i) t = subc32(a.v[i], b.v[i], bw, bw);
+    (void)t;
+    return bw != 0;
 }
 __device__ __forceinline__ bool fe_lt_k(const fe& a, const uint32_t* k) {
-    uint64_t x = 0;
+    uint32_t bw = 0, t;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) x = static_cast<uint64_t>(a.v[i]) - k[i] - (x >> 63);
-    return (x >> 63) != 0;
+    for (int i = 0; i < 8; ++i) t = subc32(a.v[i], k[i], bw, bw);
+    (void)t;
+    return bw != 0;
 }
 // r = a + b (mod 2^256), returns carry
 __device__ __forceinline__ uint32_t fe_add_raw(fe& r, const fe& a, const fe& b) {
-    uint64_t x = 0;
+    uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        x += static_cast<uint64_t>(a.v[i]) + b.v[i];
-        r.v[i] = static_cast<uint32_t>(x);
-        x >>= 32;
-    }
-    return static_cast<uint32_t>(x);
+    for (int i = 0; i < 8; ++i) r.v[i] = addc32(a.v[i], b.v[i], c, c);
+    return c;
 }
 // r = a - b (mod 2^256), returns borrow
 __device__ __forceinline__ uint32_t fe_sub_raw(fe& r, const fe& a, const fe& b) {
-    uint64_t x = 0;
+    uint32_t bw = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        x = static_cast<uint64_t>(a.v[i]) - b.v[i] - (x >> 63);
-        r.v[i] = static_cast<uint32_t>(x);
-    }
-    return static_cast<uint32_t>(x >> 63);
+    for (int i = 0; i < 8; ++i) r.v[i] = subc32(a.v[i], b.v[i], bw, bw);
+    return bw;
 }
 __device__ __forceinline__ uint32_t fe_sub_k(fe& r, const fe& a, const uint32_t* k) {
-    uint64_t x = 0;
+    uint32_t bw = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        x = static_cast<uint64_t>(a.v[i]) - k[i] - (x >> 63);
-        r.v[i] = static_cast<uint32_t>(x);
-    }
-    return static_cast<uint32_t>(x >> 63);
+    for (int i = 0; i < 8; ++i) r.v[i] = subc32(a.v[i], k[i], bw, bw);
+    return bw;
 }
 __device__ __forceinline__ uint32_t fe_add_k(fe& r, const fe& a, const uint32_t* k) {
-    uint64_t x = 0;
+    uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        x += static_cast<uint64_t>(a.v[i]) + k[i];
-        r.v[i] = static_cast<uint32_t>(x);
-        x >>= 32;
-    }
-    return static_cast<uint32_t>(x);
+    for (int i = 0; i < 8; ++i) r.v[i] = addc32(a.v[i], k[i], c, c);
+    return c;
 }
 
 // 256 x 256 -> 512-bit product, Comba (column) order.
@@ -164,16 +163,12 @@ __device__ __forceinline__ void sqr_512(uint32_t r[16], const fe& a) {
     for (int k = 15; k > 0; --k) t[k] = __builtin_amdgcn_alignbit(t[k], t[k - 1], 31);
     t[0] = 0;
     // add diagonal squares a_i^2 at columns 2i, 2i+1
-    uint64_t x = 0;
+    uint32_t c = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint64_t sq = static_cast<uint64_t>(a.v[i]) * a.v[i];
-        x += static_cast<uint64_t>(t[2 * i]) + static_cast<uint32_t>(sq);
-        r[2 * i] = static_cast<uint32_t>(x);
-        x >>= 32;
-        x += static_cast<uint64_t>(t[2 * i + 1]) + static_cast<uint32_t>(sq >> 32);
-        r[2 * i + 1] = static_cast<uint32_t>(x);
-        x >>= 32;
+        const uint32_t lo = a.v[i] * a.v[i], hi = __umulhi(a.v[i], a.v[i]);
+        r[2 * i] = addc32(t[2 * i], lo, c, c);
+        r[2 * i + 1] = addc32(t[2 * i + 1], hi, c, c);
     }
 }
 
@@ -183,62 +178,59 @@ struct FieldK1 {
     static constexpr uint32_t P[8] = {0xfffffc2fu, 0xfffffffeu, 0xffffffffu, 0xffffffffu,
                                       0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
 
-    // r += f * c for f < 2^32 (f small in practice); returns the carry out of 2^256
+    // r += f * c for f in {0, 1}; returns the carry out of 2^256
     __device__ static __forceinline__ uint32_t add_fc(fe& r, uint32_t f) {
-        uint64_t x = static_cast<uint64_t>(f) * 977u + r.v[0];
-        r.v[0] = static_cast<uint32_t>(x);
-        x = (x >> 32) + r.v[1] + f;
-        r.v[1] = static_cast<uint32_t>(x);
-        x >>= 32;
+        uint32_t c = 0;
+        r.v[0] = addc32(r.v[0], f * 977u, 0, c);
+        r.v[1] = addc32(r.v[1], f, c, c);
 #pragma unroll
-        for (int i = 2; i < 8; ++i) {
-            x += r.v[i];
-            r.v[i] = static_cast<uint32_t>(x);
-            x >>= 32;
-        }
-        return static_cast<uint32_t>(x);
+        for (int i = 2; i < 8; ++i) r.v[i] = addc32(r.v[i], 0u, c, c);
+        return c;
     }
     // r -= f * c for f in {0, 1}; returns the borrow
     __device__ static __forceinline__ uint32_t sub_fc(fe& r, uint32_t f) {
-        uint64_t x = static_cast<uint64_t>(r.v[0]) - f * 977u;
-        r.v[0] = static_cast<uint32_t>(x);
-        x = static_cast<uint64_t>(r.v[1]) - f - (x >> 63);
-        r.v[1] = static_cast<uint32_t>(x);
+        uint32_t b = 0;
+        r.v[0] = subc32(r.v[0], f * 977u, 0, b);
+        r.v[1] = subc32(r.v[1], f, b, b);
 #pragma unroll
-        for (int i = 2; i < 8; ++i) {
-            x = static_cast<uint64_t>(r.v[i]) - (x >> 63);
-            r.v[i] = static_cast<uint32_t>(x);
-        }
-        return static_cast<uint32_t>(x >> 63);
+        for (int i = 2; i < 8; ++i) r.v[i] = subc32(r.v[i], 0u, b, b);
+        return b;
     }
 
-    // reduce a 512-bit value to [0, 2^256)
+    // reduce a 512-bit value T = L + H 2^256 to [0, 2^256):  T = L + H*977 + H*2^32 (mod p)
     __device__ static __forceinline__ void reduce(fe& o, const uint32_t t[16]) {
-        uint64_t acc = 0;
+        uint32_t lo[8], hi[8], u[8], c = 0, c2 = 0, c3 = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            acc += static_cast<uint64_t>(t[8 + k]) * 977u + t[k];
-            if (k) acc += t[7 + k];
-            o.v[k] = static_cast<uint32_t>(acc);
-            acc >>= 32;
+            lo[k] = t[8 + k] * 977u;
+            hi[k] = __umulhi(t[8 + k], 977u);
         }
-        acc += t[15];  // top < 2^33
-        const uint32_t top_lo = static_cast<uint32_t>(acc), top_hi = static_cast<uint32_t>(acc >> 32);
-        // o += top * (2^32 + 977), top = top_hi * 2^32 + top_lo
-        uint64_t x = static_cast<uint64_t>(top_lo) * 977u + o.v[0];
-        o.v[0] = static_cast<uint32_t>(x);
-        x = (x >> 32) + static_cast<uint64_t>(top_hi) * 977u + top_lo + o.v[1];
-        o.v[1] = static_cast<uint32_t>(x);
-        x = (x >> 32) + top_hi + o.v[2];
-        o.v[2] = static_cast<uint32_t>(x);
-        x >>= 32;
 #pragma unroll
-        for (int i = 3; i < 8; ++i) {
-            x += o.v[i];
-            o.v[i] = static_cast<uint32_t>(x);
-            x >>= 32;
-        }
-        add_fc(o, static_cast<uint32_t>(x));  // 2^256 wrapped once more: cannot carry again
+        for (int k = 0; k < 8; ++k) u[k] = addc32(t[k], lo[k], c, c);      // L + lo
+        uint32_t u8 = c;
+        u[1] = addc32(u[1], hi[0], 0, c2);                                  // + hi << 32
+#pragma unroll
+        for (int k = 2; k < 8; ++k) u[k] = addc32(u[k], hi[k - 1], c2, c2);
+        u8 = addc32(u8, hi[7], c2, c2);
+        u[1] = addc32(u[1], t[8], 0, c3);                                   // + H << 32
+#pragma unroll
+        for (int k = 2; k < 8; ++k) u[k] = addc32(u[k], t[7 + k], c3, c3);
+        u8 = addc32(u8, t[15], c3, c3);
+        const uint32_t u9 = c2 + c3;  // top = u8 + u9 * 2^32 < 2^34
+        // second fold: + top * 977 + top * 2^32
+        const uint32_t m0 = u8 * 977u, m1 = __umulhi(u8, 977u) + u9 * 977u;
+        uint32_t d = 0, e = 0;
+        u[0] = addc32(u[0], m0, 0, d);
+        u[1] = addc32(u[1], m1, d, d);
+        u[2] = addc32(u[2], u9, d, d);
+#pragma unroll
+        for (int k = 3; k < 8; ++k) u[k] = addc32(u[k], 0u, d, d);
+        u[1] = addc32(u[1], u8, 0, e);
+#pragma unroll
+        for (int k = 2; k < 8; ++k) u[k] = addc32(u[k], 0u, e, e);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o.v[k] = u[k];
+        add_fc(o, d + e);  // the wrapped 2^256 (at most once): cannot carry again
     }
 
     __device__ static __forceinline__ void mul(fe& r, const fe& a, const fe& b) {

@@ -140,6 +140,26 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
+// `levels` Merkle levels of a shard whose first leaf index is a multiple of width^levels: the
+// shard's level-`levels` nodes are exactly the reference tree's nodes over that range (Merkle.h
+// groups every level from index 0).  Intermediate levels ping-pong through d_work
+// (>= 32 * ceil(n / width) bytes); the last level lands in d_out.
+int launch_merkle_levels(int hasher, int width, const uint8_t* d_in, uint64_t n, int levels, uint8_t* d_work,
+                         uint8_t* d_out, hipStream_t st) {
+    if (n == 0 || width < 2 || width > 64 || levels < 1) return BCOSGPU_E_ARG;
+    const uint8_t* in = d_in;
+    uint64_t nin = n;
+    const uint64_t half = 32 * ((n + width - 1) / width);
+    for (int l = 0; l < levels; ++l) {
+        const uint64_t nout = (nin + width - 1) / width;
+        uint8_t* out = (l + 1 == levels) ? d_out : d_work + ((l & 1) ? half : 0);
+        launch_level(hasher, width, in, nin, out, nout, st);
+        in = out;
+        nin = nout;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
 int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* d_scratch,
                       uint8_t* d_root, hipStream_t st) {
     // d_scratch: >= 32 * (ceil(n/16) + ceil(n/256) + ...) bytes; levels ping into it

@@ -87,6 +87,14 @@ int bcosgpu_merkle_root(int hasher, int width, int variant, const uint8_t* leave
 int bcosgpu_merkle_root_dev(int hasher, int width, const uint8_t* d_leaves32, size_t n,
                             uint8_t* d_tree, uint8_t* d_root32, void* stream);
 
+/* Multi-GPU tx root: compute `levels` levels of the reference tree over one shard of leaves.  The
+ * shard's first global leaf index must be a multiple of width^levels; then its ceil(n / width^levels)
+ * output nodes are exactly the reference's level-`levels` nodes for that range, and the root over the
+ * concatenated frontiers of all shards (bcosgpu_merkle_root*) equals the single-device root.
+ * d_work >= 64 * ceil(n / width) bytes; d_frontier receives ceil(n / width^levels) x 32 bytes. */
+int bcosgpu_merkle_frontier_dev(int hasher, int width, const uint8_t* d_leaves32, size_t n, int levels,
+                                uint8_t* d_work, uint8_t* d_frontier, void* stream);
+
 /* ---------------------------------------------------------------- signatures (SignatureCrypto, batched) */
 /* secp256k1 public-key recovery (Secp256k1Crypto::recover, Secp256k1Crypto.h:57-60).
  * pub64 / addr20 nullable; addr20 = right160(Keccak256(pub)) (calculateAddress, KeyPair.h:30-33). */
