@@ -9,6 +9,7 @@
 // per-lane predicated; a wave skips them when no lane takes them.
 #pragma once
 #include "fe.h"
+#include "modinv.h"
 
 namespace bcosgpu {
 
@@ -202,7 +203,7 @@ struct Curve {
     // affine coordinates in the field's internal form; returns false for infinity
     __device__ static __forceinline__ bool to_aff(Aff& A, const Jac& P) {
         fe zi, zi2, t;
-        F::inv(zi, P.Z);
+        FieldInv<F>::inv(zi, P.Z);
         F::sqr(zi2, zi);
         F::mul(A.x, P.X, zi2);
         F::mul(t, zi2, zi);

@@ -15,6 +15,7 @@
 //   variable base: radix-16 Booth recoding (digits in [-8, 8]) over a register-resident table of
 //                  1P..8P; every lane runs the same 65-window schedule (no divergence).
 #include <mutex>
+#include <type_traits>
 #include "ec.h"
 #include "engine.h"
 #include "hash_device.h"
@@ -240,49 +241,103 @@ __device__ __forceinline__ int booth_digit128(fe& k) {
     return static_cast<int>(W + c) - static_cast<int>((W >> 3) << 4);
 }
 
-// acc += (sign * d) * (phi ? lambda : 1) * P, T[j] = (j+1) P
-__device__ __forceinline__ void glv_add_digit(Jac& acc, const Jac T[8], int d, bool neg, bool phi) {
+// acc += (sign * d) * (phi ? lambda : 1) * P over an affine table T[j] = (j+1) P (mixed add)
+template <class C, class F>
+__device__ __forceinline__ void add_digit_aff(Jac& acc, const Aff T[8], int d, bool neg, bool phi) {
     const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
-    Jac S;
-    fe_copy(S.X, T[0].X); fe_copy(S.Y, T[0].Y); fe_copy(S.Z, T[0].Z); S.inf = false;
+    Aff S;
+    fe_copy(S.x, T[0].x);
+    fe_copy(S.y, T[0].y);
 #pragma unroll
     for (int q = 1; q < 8; ++q) {
-        const bool take = m == static_cast<uint32_t>(q);
-        fe_cmov(S.X, T[q].X, take);
-        fe_cmov(S.Y, T[q].Y, take);
-        fe_cmov(S.Z, T[q].Z, take);
+        const uint64_t take = __builtin_amdgcn_ballot_w64(m == static_cast<uint32_t>(q));
+        fe_cmov_mask(S.x, T[q].x, take);
+        fe_cmov_mask(S.y, T[q].y, take);
     }
     if (phi) {
         fe b;
         fe_set(b, kGlvBeta);
-        FieldK1::mul(S.X, S.X, b);
+        F::mul(S.x, S.x, b);
     }
     fe ny;
-    FieldK1::neg(ny, S.Y);
-    fe_cmov(S.Y, ny, (d < 0) != neg);
+    F::neg(ny, S.y);
+    fe_cmov(S.y, ny, (d < 0) != neg);
     Jac R;
-    CurveK1::add(R, acc, S);
-    CurveK1::cmov(acc, R, d != 0);
+    C::madd(R, acc, S);
+    C::cmov(acc, R, d != 0);
 }
 
-// acc = k * P on secp256k1 via GLV: k1*P + k2*phi(P), 33 joint radix-16 Booth windows
+// Table 1P..8P of an affine P, as Jacobian points.
+template <class C>
+__device__ __forceinline__ void multiples8(Jac T[8], const Aff& P) {
+    C::from_aff(T[0], P);
+    C::dbl(T[1], T[0]);
+    C::madd(T[2], T[1], P);
+    C::dbl(T[3], T[1]);
+    C::madd(T[4], T[3], P);
+    C::dbl(T[5], T[2]);
+    C::madd(T[6], T[5], P);
+    C::dbl(T[7], T[3]);
+}
+
+// Compile-time loop (LLVM declines to fully unroll loops whose bodies hold several field
+// multiplications, which would push the point tables out of registers into scratch).
+template <int I, int N>
+struct Unroll {
+    template <class Fn>
+    __device__ static __forceinline__ void run(Fn&& fn) {
+        if constexpr (I < N) {
+            fn(std::integral_constant<int, I>{});
+            Unroll<I + 1, N>::run(fn);
+        }
+    }
+};
+
+// Rescale T[0..7] (T[0].Z == 1) to the common Z = Zc = Z1*...*Z7 without an inversion; the
+// coordinates (X_j s_j^2, Y_j s_j^3), s_j = Zc / Z_j, are then AFFINE coordinates on the isomorphic
+// curve E': y^2 = x^3 + b Zc^6, where a = 0 is preserved (secp256k1), so the a = 0 doubling and the
+// mixed addition stay valid and the endomorphism (x, y) -> (beta x, y) still applies.  A point
+// (X, Y, Z) computed on E' is (X, Y, Z * Zc) on the real curve.
+__device__ __forceinline__ void coz_table_k1(Aff A[8], fe& Zc, const Jac T[8]) {
+    fe pre[8], suf[8];
+    FieldK1::set_one(pre[0]);
+    fe_copy(pre[1], T[1].Z);
+    Unroll<2, 8>::run([&](auto J) { FieldK1::mul(pre[J], pre[J - 1], T[J].Z); });   // pre[j] = Z1..Zj
+    FieldK1::set_one(suf[7]);
+    Unroll<0, 7>::run([&](auto J) {                                                  // suf[j] = Z(j+1)..Z7
+        constexpr int j = 6 - decltype(J)::value;
+        FieldK1::mul(suf[j], suf[j + 1], T[j + 1].Z);
+    });
+    fe_copy(Zc, pre[7]);
+    Unroll<0, 8>::run([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        fe sj, s2, s3;
+        if constexpr (j == 0) fe_copy(sj, suf[0]);
+        else if constexpr (j == 7) fe_copy(sj, pre[6]);
+        else FieldK1::mul(sj, pre[j - 1], suf[j]);
+        FieldK1::sqr(s2, sj);
+        FieldK1::mul(s3, s2, sj);
+        FieldK1::mul(A[j].x, T[j].X, s2);
+        FieldK1::mul(A[j].y, T[j].Y, s3);
+    });
+}
+
+// acc = k * P on secp256k1 via GLV: k1*P + k2*phi(P), 33 joint radix-16 Booth windows of mixed
+// additions against the co-Z table; result on the real curve.
 __device__ __forceinline__ void glv_mul_k1(Jac& acc, const fe& k, const Aff& P) {
-    fe k1, k2;
+    fe k1, k2, Zc;
     bool neg1, neg2;
     glv_split(k1, neg1, k2, neg2, k);
-    Jac T[8];
-    CurveK1::from_aff(T[0], P);
-    CurveK1::dbl(T[1], T[0]);
-    CurveK1::madd(T[2], T[1], P);
-    CurveK1::dbl(T[3], T[1]);
-    CurveK1::madd(T[4], T[3], P);
-    CurveK1::dbl(T[5], T[2]);
-    CurveK1::madd(T[6], T[5], P);
-    CurveK1::dbl(T[7], T[3]);
+    Aff A[8];
+    {
+        Jac T[8];
+        multiples8<CurveK1>(T, P);
+        coz_table_k1(A, Zc, T);
+    }
     CurveK1::set_inf(acc);
     // digit 32 = bit 127 of each half
-    glv_add_digit(acc, T, static_cast<int>(k1.v[3] >> 31), neg1, false);
-    glv_add_digit(acc, T, static_cast<int>(k2.v[3] >> 31), neg2, true);
+    add_digit_aff<CurveK1, FieldK1>(acc, A, static_cast<int>(k1.v[3] >> 31), neg1, false);
+    add_digit_aff<CurveK1, FieldK1>(acc, A, static_cast<int>(k2.v[3] >> 31), neg2, true);
 #pragma unroll 1
     for (int i = 31; i >= 0; --i) {
         CurveK1::dbl(acc, acc);
@@ -291,8 +346,52 @@ __device__ __forceinline__ void glv_mul_k1(Jac& acc, const fe& k, const Aff& P) 
         CurveK1::dbl(acc, acc);
         const int d1 = booth_digit128(k1);
         const int d2 = booth_digit128(k2);
-        glv_add_digit(acc, T, d1, neg1, false);
-        glv_add_digit(acc, T, d2, neg2, true);
+        add_digit_aff<CurveK1, FieldK1>(acc, A, d1, neg1, false);
+        add_digit_aff<CurveK1, FieldK1>(acc, A, d2, neg2, true);
+    }
+    FieldK1::mul(acc.Z, acc.Z, Zc);
+}
+
+// acc = k * P on SM2: the table 1P..8P is normalised to affine with one inversion (Montgomery's
+// trick over the 7 non-trivial Z), then 65 radix-16 Booth windows of mixed additions.
+__device__ __forceinline__ void booth_mul_sm2(Jac& acc, const fe& k_plain, const Aff& P) {
+    Aff A[8];
+    {
+        Jac T[8];
+        multiples8<CurveSM2>(T, P);
+        fe pre[8], inv, t;
+        FieldP2::set_one(pre[0]);
+        Unroll<1, 8>::run([&](auto J) { FieldP2::mul(pre[J], pre[J - 1], T[J].Z); });
+        FieldInv<FieldP2>::inv(inv, pre[7]);  // (Z1...Z7)^-1
+        fe_copy(A[0].x, P.x);
+        fe_copy(A[0].y, P.y);
+        Unroll<0, 7>::run([&](auto J) {
+            constexpr int j = 7 - decltype(J)::value;
+            fe zi, zi2, zi3;
+            FieldP2::mul(zi, inv, pre[j - 1]);  // Z_j^-1
+            FieldP2::mul(inv, inv, T[j].Z);     // (Z1..Z(j-1))^-1
+            FieldP2::sqr(zi2, zi);
+            FieldP2::mul(zi3, zi2, zi);
+            FieldP2::mul(A[j].x, T[j].X, zi2);
+            FieldP2::mul(A[j].y, T[j].Y, zi3);
+        });
+        (void)t;
+    }
+    fe k;
+    fe_copy(k, k_plain);
+    CurveSM2::set_inf(acc);
+    add_digit_aff<CurveSM2, FieldP2>(acc, A, static_cast<int>(k.v[7] >> 31), false, false);  // digit 64
+#pragma unroll 1
+    for (int i = 63; i >= 0; --i) {
+        CurveSM2::dbl(acc, acc);
+        CurveSM2::dbl(acc, acc);
+        CurveSM2::dbl(acc, acc);
+        CurveSM2::dbl(acc, acc);
+        const uint32_t top = k.v[7];
+        const uint32_t W = top >> 28, c = (top >> 27) & 1u;
+        const int d = static_cast<int>(W + c) - static_cast<int>((W >> 3) << 4);
+        shl4(k);
+        add_digit_aff<CurveSM2, FieldP2>(acc, A, d, false, false);
     }
 }
 
@@ -410,7 +509,7 @@ __device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const 
     }
     fe rm, rinv, u1, u2;
     FieldN1::from_plain(rm, rr);
-    FieldN1::inv(rinv, rm);
+    FieldInv<FieldN1>::inv(rinv, rm);
     FieldN1::mul(u1, e, rinv);
     FieldN1::neg(u1, u1);
     fe ss = s;
@@ -421,8 +520,8 @@ __device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const 
     fe_copy(R.x, x);
     fe_copy(R.y, y);
     Jac QG, QR, Q;
-    comb_mul<CurveK1>(QG, u1, tab);
     glv_mul_k1(QR, u2, R);
+    comb_mul<CurveK1>(QG, u1, tab);
     CurveK1::add(Q, QG, QR);
     ok = ok && !Q.inf;
     Aff A;
@@ -540,8 +639,8 @@ __device__ __forceinline__ bool sm2_verify_lane(const fe& hash_be, const uint8_t
     for (int i = 0; i < 8; ++i) e.v[i] = eb[7 - i];
     reduce_once(e, ParamN2::M);
     Jac QG, QP, Q;
+    booth_mul_sm2(QP, t, P);
     comb_mul<CurveSM2>(QG, s, tab);
-    booth_mul<CurveSM2, FieldP2>(QP, t, P);
     CurveSM2::add(Q, QG, QP);
     ok = ok && !Q.inf;
     // x1 = X / Z^2 must be congruent to r - e (mod n): x1 = c or c + n (when c + n < p)
@@ -697,7 +796,7 @@ __global__ __launch_bounds__(256) void secp256k1_sign_kernel(const uint8_t* __re
     fe kk = k;
     if (fe_is_zero_raw(kk)) kk.v[0] = 1;
     FieldN1::from_plain(km, kk);
-    FieldN1::inv(kinv, km);
+    FieldInv<FieldN1>::inv(kinv, km);
     FieldN1::from_plain(dm, d);
     FieldN1::mul(rd, r, dm);
     FieldN1::add(t, e, rd);
@@ -789,7 +888,7 @@ __global__ __launch_bounds__(256) void sm2_sign_kernel(const uint8_t* __restrict
     FieldN2::add(dp1, d, one);
     if (fe_is_zero_raw(dp1)) dp1.v[0] = 1;
     FieldN2::from_plain(dm, dp1);
-    FieldN2::inv(inv, dm);
+    FieldInv<FieldN2>::inv(inv, dm);
     fe dmm;
     FieldN2::from_plain(dmm, d);
     FieldN2::mul(rd, r, dmm);

@@ -79,6 +79,12 @@ __device__ __forceinline__ uint32_t subc32(uint32_t a, uint32_t b, uint32_t bin,
     bout = bo;
     return r;
 }
+// r = lane-in-mask ? a : r, as explicit v_cndmask_b32 (the compiler cannot turn a chain of these
+// into an indexed scratch array access, which it otherwise does for per-lane table selects)
+__device__ __forceinline__ void fe_cmov_mask(fe& r, const fe& a, uint64_t mask) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(r.v[i]) : "v"(a.v[i]), "s"(mask));
+}
 // a < b as 256-bit integers
 __device__ __forceinline__ bool fe_lt(const fe& a, const fe& b) {
     uint32_t bw = 0, t;
@@ -434,32 +440,69 @@ struct Mont {
         one.v[0] = 1;
         mul(r, a, one);
     }
-    // a^(m-2) by left-to-right 4-bit fixed windows (wave-uniform window values)
+    __device__ static __forceinline__ void sqr_n(fe& r, const fe& a, int n) {
+        sqr(r, a);
+        for (int i = 1; i < n; ++i) sqr(r, r);
+    }
+    // a^(m-2) for the group orders: their top 128 bits are [127 ones][0] (secp256k1 n) or
+    // [31 ones][0][96 ones] (SM2 n), done by x^(2^k - 1) chains; the low 128 bits by a
+    // square-and-multiply loop whose branch is wave-uniform (the exponent is a constant).
     __device__ static __forceinline__ void inv(fe& r, const fe& a) {
-        fe tab[16];
-        set_one(tab[0]);
-        fe_copy(tab[1], a);
-#pragma unroll
-        for (int i = 2; i < 16; ++i) mul(tab[i], tab[i - 1], a);
-        set_one(r);
+        fe x2, x3, x6, x12, x24, x31, x32, x48, x96, t;
+        sqr(t, a); mul(x2, t, a);
+        sqr(t, x2); mul(x3, t, a);
+        sqr_n(t, x3, 3); mul(x6, t, x3);
+        sqr_n(t, x6, 6); mul(x12, t, x6);
+        sqr_n(t, x12, 12); mul(x24, t, x12);
+        sqr_n(t, x24, 6); mul(t, t, x6);
+        sqr(t, t); mul(x31, t, a);
+        sqr(t, x31); mul(x32, t, a);
+        sqr_n(t, x24, 24); mul(x48, t, x24);
+        sqr_n(t, x48, 48); mul(x96, t, x48);
+        if (P::EXP_INV[7] == 0xffffffffu) {  // secp256k1 n: [127 ones][0]
+            fe x120, x126;
+            sqr_n(t, x96, 24); mul(x120, t, x24);
+            sqr_n(t, x120, 6); mul(x126, t, x6);
+            sqr(t, x126); mul(t, t, a);  // 127 ones
+            sqr(r, t);                   // 0
+        } else {  // SM2 n: [31 ones][0][96 ones]
+            sqr(t, x31);
+            sqr_n(t, t, 96); mul(r, t, x96);
+        }
 #pragma unroll 1
-        for (int w = 63; w >= 0; --w) {
-            if (w != 63) {
-                sqr(r, r); sqr(r, r); sqr(r, r); sqr(r, r);
-            }
-            const uint32_t nib = (P::EXP_INV[w >> 3] >> ((w & 7) * 4)) & 15u;
-            fe s;
-            fe_copy(s, tab[0]);
-#pragma unroll
-            for (int q = 1; q < 16; ++q) fe_cmov(s, tab[q], nib == static_cast<uint32_t>(q));
-            mul(r, r, s);
+        for (int bit = 127; bit >= 0; --bit) {
+            sqr(r, r);
+            if ((P::EXP_INV[bit >> 5] >> (bit & 31)) & 1u) mul(r, r, a);
         }
     }
 };
 
-using FieldP2 = Mont<ParamP2>;
 using FieldN1 = Mont<ParamN1>;
 using FieldN2 = Mont<ParamN2>;
+
+// SM2 base field: Montgomery arithmetic plus an addition chain for p - 2 =
+// [31 ones][0][128 ones][32 zeros][32 ones][30 ones][0][1]  (255 S + 13 M)
+struct FieldP2 : Mont<ParamP2> {
+    __device__ static __forceinline__ void inv(fe& r, const fe& a) {
+        fe x2, x3, x6, x12, x15, x30, x31, x32, x64, x128, t;
+        sqr(t, a); mul(x2, t, a);
+        sqr(t, x2); mul(x3, t, a);
+        sqr_n(t, x3, 3); mul(x6, t, x3);
+        sqr_n(t, x6, 6); mul(x12, t, x6);
+        sqr_n(t, x12, 3); mul(x15, t, x3);
+        sqr_n(t, x15, 15); mul(x30, t, x15);
+        sqr(t, x30); mul(x31, t, a);
+        sqr(t, x31); mul(x32, t, a);
+        sqr_n(t, x32, 32); mul(x64, t, x32);
+        sqr_n(t, x64, 64); mul(x128, t, x64);
+        sqr(t, x31);                        // [31 ones][0]
+        sqr_n(t, t, 128); mul(t, t, x128);  // [128 ones]
+        sqr_n(t, t, 32);                    // [32 zeros]
+        sqr_n(t, t, 32); mul(t, t, x32);    // [32 ones]
+        sqr_n(t, t, 30); mul(t, t, x30);    // [30 ones]
+        sqr_n(t, t, 2); mul(r, t, a);       // [0][1]
+    }
+};
 
 // ---------------------------------------------------------------- byte conversions
 // 32 big-endian bytes (8 little-endian-loaded words w[0..7] in memory order) -> limbs

@@ -1,0 +1,223 @@
+// modinv.h -- modular inversion by Bernstein-Yang "safegcd" divsteps (gfx950, one value per lane).
+//
+// Replaces Fermat exponentiation (~270-340 modular multiplications) with batches of 30 branch-free
+// divsteps on the low 32 bits, each followed by a 2x2 transition-matrix update of the full-width
+// (f, g) and (d, e) held as 9 signed 30-bit limbs (v_mad_i64_i32 accumulators).  590 divsteps bound
+// any 256-bit input; the loop stops early, wave-uniformly, once g == 0 in every lane of the wave
+// (further batches are then exact no-ops).  Values are plain residues in [0, m).
+#pragma once
+#include "fe.h"
+
+namespace bcosgpu {
+
+struct S30 {
+    int32_t v[9];
+};
+
+struct ModInfo30 {
+    int32_t m[9];    // modulus in signed-30 form
+    uint32_t inv30;  // m^-1 mod 2^30
+};
+
+__device__ __constant__ static const ModInfo30 kMod30K1P = {
+    {1073740847, 1073741819, 1073741823, 1073741823, 1073741823, 1073741823, 1073741823, 1073741823, 65535}, 769313487u};
+__device__ __constant__ static const ModInfo30 kMod30N1 = {
+    {271991105, 1061780019, 881460155, 733428139, 1073741498, 1073741823, 1073741823, 1073741823, 65535}, 712462017u};
+__device__ __constant__ static const ModInfo30 kMod30P2 = {
+    {1073741823, 1073741823, 15, 1073741760, 1073741823, 1073741823, 1073741823, 1073725439, 65535}, 1073741823u};
+__device__ __constant__ static const ModInfo30 kMod30N2 = {
+    {970277155, 250597412, 476074677, 16243400, 1073741682, 1073741823, 1073741823, 1073725439, 65535}, 231405195u};
+
+static constexpr int32_t kM30 = 0x3fffffff;
+
+__device__ __forceinline__ void fe_to_s30(S30& r, const fe& a) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int bit = 30 * i, w = bit >> 5, sh = bit & 31;
+        uint32_t x = a.v[w] >> sh;
+        if (sh > 2 && w + 1 < 8) x |= a.v[w + 1] << (32 - sh);
+        r.v[i] = static_cast<int32_t>(x & kM30);
+    }
+    r.v[8] = static_cast<int32_t>(a.v[7] >> 16);
+}
+// limbs normalised to [0, 2^30) with a non-negative top limb
+__device__ __forceinline__ void s30_to_fe(fe& r, const S30& a) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const int bit = 32 * w, i = bit / 30, sh = bit % 30;
+        uint32_t x = static_cast<uint32_t>(a.v[i]) >> sh;
+        if (i + 1 < 9) x |= static_cast<uint32_t>(a.v[i + 1]) << (30 - sh);
+        if (sh > 28 && i + 2 < 9) x |= static_cast<uint32_t>(a.v[i + 2]) << (60 - sh);
+        r.v[w] = x;
+    }
+}
+
+// 30 divsteps on the low bits of f, g; transition matrix (u, v, q, r) scaled by 2^30:
+// u f0 + v g0 = f 2^30, q f0 + r g0 = g 2^30.  zeta = -(delta + 1/2).
+__device__ __forceinline__ int32_t divsteps_30(int32_t zeta, uint32_t f, uint32_t g, int32_t t[4]) {
+    uint32_t u = 1, v = 0, q = 0, r = 1;
+#pragma unroll
+    for (int i = 0; i < 30; ++i) {
+        uint32_t c1 = static_cast<uint32_t>(zeta >> 31);  // zeta < 0
+        const uint32_t c2 = 0u - (g & 1u);                 // g odd
+        const uint32_t x = (f ^ c1) - c1, y = (u ^ c1) - c1, z = (v ^ c1) - c1;
+        g += x & c2;
+        q += y & c2;
+        r += z & c2;
+        c1 &= c2;
+        zeta = (zeta ^ static_cast<int32_t>(c1)) - 1;
+        f += g & c1;
+        u += q & c1;
+        v += r & c1;
+        g >>= 1;
+        u <<= 1;
+        v <<= 1;
+    }
+    t[0] = static_cast<int32_t>(u);
+    t[1] = static_cast<int32_t>(v);
+    t[2] = static_cast<int32_t>(q);
+    t[3] = static_cast<int32_t>(r);
+    return zeta;
+}
+
+// (f, g) <- t (f, g) / 2^30 (exact)
+__device__ __forceinline__ void update_fg_30(S30& f, S30& g, const int32_t t[4]) {
+    const int64_t u = t[0], v = t[1], q = t[2], r = t[3];
+    int64_t cf = u * f.v[0] + v * g.v[0];
+    int64_t cg = q * f.v[0] + r * g.v[0];
+    cf >>= 30;
+    cg >>= 30;
+#pragma unroll
+    for (int i = 1; i < 9; ++i) {
+        cf += u * f.v[i] + v * g.v[i];
+        cg += q * f.v[i] + r * g.v[i];
+        f.v[i - 1] = static_cast<int32_t>(cf) & kM30;
+        cf >>= 30;
+        g.v[i - 1] = static_cast<int32_t>(cg) & kM30;
+        cg >>= 30;
+    }
+    f.v[8] = static_cast<int32_t>(cf);
+    g.v[8] = static_cast<int32_t>(cg);
+}
+
+// (d, e) <- (t (d, e) + m (md, me)) / 2^30, md/me chosen so the division is exact; keeps d, e in
+// (-2m, m).
+__device__ __forceinline__ void update_de_30(S30& d, S30& e, const int32_t t[4], const ModInfo30& mi) {
+    const int32_t u = t[0], v = t[1], q = t[2], r = t[3];
+    const int32_t sd = d.v[8] >> 31, se = e.v[8] >> 31;
+    int32_t md = (u & sd) + (v & se);
+    int32_t me = (q & sd) + (r & se);
+    int64_t cd = static_cast<int64_t>(u) * d.v[0] + static_cast<int64_t>(v) * e.v[0];
+    int64_t ce = static_cast<int64_t>(q) * d.v[0] + static_cast<int64_t>(r) * e.v[0];
+    md -= static_cast<int32_t>((mi.inv30 * static_cast<uint32_t>(cd) + static_cast<uint32_t>(md)) & kM30);
+    me -= static_cast<int32_t>((mi.inv30 * static_cast<uint32_t>(ce) + static_cast<uint32_t>(me)) & kM30);
+    cd += static_cast<int64_t>(mi.m[0]) * md;
+    ce += static_cast<int64_t>(mi.m[0]) * me;
+    cd >>= 30;
+    ce >>= 30;
+#pragma unroll
+    for (int i = 1; i < 9; ++i) {
+        cd += static_cast<int64_t>(u) * d.v[i] + static_cast<int64_t>(v) * e.v[i];
+        ce += static_cast<int64_t>(q) * d.v[i] + static_cast<int64_t>(r) * e.v[i];
+        cd += static_cast<int64_t>(mi.m[i]) * md;
+        ce += static_cast<int64_t>(mi.m[i]) * me;
+        d.v[i - 1] = static_cast<int32_t>(cd) & kM30;
+        cd >>= 30;
+        e.v[i - 1] = static_cast<int32_t>(ce) & kM30;
+        ce >>= 30;
+    }
+    d.v[8] = static_cast<int32_t>(cd);
+    e.v[8] = static_cast<int32_t>(ce);
+}
+
+// r in (-2m, m) -> sign * r mod m in [0, m)
+__device__ __forceinline__ void normalize_30(S30& r, int32_t sign, const ModInfo30& mi) {
+    int32_t ca = r.v[8] >> 31;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] += mi.m[i] & ca;
+    const int32_t cn = sign >> 31;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = (r.v[i] ^ cn) - cn;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        r.v[i + 1] += r.v[i] >> 30;
+        r.v[i] &= kM30;
+    }
+    ca = r.v[8] >> 31;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] += mi.m[i] & ca;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        r.v[i + 1] += r.v[i] >> 30;
+        r.v[i] &= kM30;
+    }
+}
+
+// r = x^-1 mod m (x in [0, m); x = 0 gives 0)
+__device__ __forceinline__ void modinv_safegcd(fe& r, const fe& x, const ModInfo30& mi) {
+    S30 d, e, f, g;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        d.v[i] = 0;
+        e.v[i] = 0;
+        f.v[i] = mi.m[i];
+    }
+    e.v[0] = 1;
+    fe_to_s30(g, x);
+    int32_t zeta = -1;
+#pragma unroll 1
+    for (int it = 0; it < 20; ++it) {
+        int32_t t[4];
+        zeta = divsteps_30(zeta, static_cast<uint32_t>(f.v[0]), static_cast<uint32_t>(g.v[0]), t);
+        update_de_30(d, e, t, mi);
+        update_fg_30(f, g, t);
+        int32_t gz = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) gz |= g.v[i];
+        if (__builtin_amdgcn_ballot_w64(gz != 0) == 0) break;  // every lane done: the rest are no-ops
+    }
+    normalize_30(d, f.v[8], mi);
+    s30_to_fe(r, d);
+}
+
+// Field inversion used by the kernels (plain or Montgomery form in, same form out).
+// For Montgomery fields: safegcd of a*R gives a^-1 R^-1; multiplying by R^3 (Montgomery) gives a^-1 R.
+__device__ __constant__ static const uint32_t kR3P2[8] = {0x00000016u, 0x00000012u, 0xfffffff8u, 0x0000000eu,
+                                                       0x0000000cu, 0x0000000au, 0x00000009u, 0x0000001bu};
+__device__ __constant__ static const uint32_t kR3N1[8] = {0xe9ff41edu, 0x7bc0cfe0u, 0x44d4322cu, 0x00176484u,
+                                                       0xf1d0b2dau, 0xb1b31347u, 0x18ef116du, 0x555d800cu};
+__device__ __constant__ static const uint32_t kR3N2[8] = {0x0eaa0b85u, 0x6ff874c7u, 0xaabe8d32u, 0x87d0c315u,
+                                                       0x97185afcu, 0x4c4fbbb3u, 0xd574ea14u, 0xc813249cu};
+
+template <class F>
+struct FieldInv;
+template <>
+struct FieldInv<FieldK1> {
+    __device__ static __forceinline__ void inv(fe& r, const fe& a) {
+        fe t;
+        fe_copy(t, a);
+        FieldK1::normalize(t);
+        modinv_safegcd(r, t, kMod30K1P);
+    }
+};
+template <class P>
+__device__ __forceinline__ void mont_inv_safegcd(fe& r, const fe& a, const ModInfo30& mi, const uint32_t* r3) {
+    fe t, k;
+    modinv_safegcd(t, a, mi);
+    fe_set(k, r3);
+    Mont<P>::mul(r, t, k);
+}
+template <>
+struct FieldInv<FieldP2> {
+    __device__ static __forceinline__ void inv(fe& r, const fe& a) { mont_inv_safegcd<ParamP2>(r, a, kMod30P2, kR3P2); }
+};
+template <>
+struct FieldInv<FieldN1> {
+    __device__ static __forceinline__ void inv(fe& r, const fe& a) { mont_inv_safegcd<ParamN1>(r, a, kMod30N1, kR3N1); }
+};
+template <>
+struct FieldInv<FieldN2> {
+    __device__ static __forceinline__ void inv(fe& r, const fe& a) { mont_inv_safegcd<ParamN2>(r, a, kMod30N2, kR3N2); }
+};
+
+}  // namespace bcosgpu
