@@ -13,6 +13,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "fe_asm.h"
 
 namespace bcosgpu {
 
@@ -205,38 +206,13 @@ struct FieldK1 {
 
     // reduce a 512-bit value T = L + H 2^256 to [0, 2^256):  T = L + H*977 + H*2^32 (mod p)
     __device__ static __forceinline__ void reduce(fe& o, const uint32_t t[16]) {
-        uint32_t lo[8], hi[8], u[8], c = 0, c2 = 0, c3 = 0;
+        uint32_t lo[8], hi[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             lo[k] = t[8 + k] * 977u;
             hi[k] = __umulhi(t[8 + k], 977u);
         }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) u[k] = addc32(t[k], lo[k], c, c);      // L + lo
-        uint32_t u8 = c;
-        u[1] = addc32(u[1], hi[0], 0, c2);                                  // + hi << 32
-#pragma unroll
-        for (int k = 2; k < 8; ++k) u[k] = addc32(u[k], hi[k - 1], c2, c2);
-        u8 = addc32(u8, hi[7], c2, c2);
-        u[1] = addc32(u[1], t[8], 0, c3);                                   // + H << 32
-#pragma unroll
-        for (int k = 2; k < 8; ++k) u[k] = addc32(u[k], t[7 + k], c3, c3);
-        u8 = addc32(u8, t[15], c3, c3);
-        const uint32_t u9 = c2 + c3;  // top = u8 + u9 * 2^32 < 2^34
-        // second fold: + top * 977 + top * 2^32
-        const uint32_t m0 = u8 * 977u, m1 = __umulhi(u8, 977u) + u9 * 977u;
-        uint32_t d = 0, e = 0;
-        u[0] = addc32(u[0], m0, 0, d);
-        u[1] = addc32(u[1], m1, d, d);
-        u[2] = addc32(u[2], u9, d, d);
-#pragma unroll
-        for (int k = 3; k < 8; ++k) u[k] = addc32(u[k], 0u, d, d);
-        u[1] = addc32(u[1], u8, 0, e);
-#pragma unroll
-        for (int k = 2; k < 8; ++k) u[k] = addc32(u[k], 0u, e, e);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o.v[k] = u[k];
-        add_fc(o, d + e);  // the wrapped 2^256 (at most once): cannot carry again
+        k1_reduce_asm(o.v, t, lo, hi);
     }
 
     __device__ static __forceinline__ void mul(fe& r, const fe& a, const fe& b) {
@@ -249,22 +225,13 @@ struct FieldK1 {
         sqr_512(t, a);
         reduce(r, t);
     }
-    __device__ static __forceinline__ void add(fe& r, const fe& a, const fe& b) {
-        uint32_t c = fe_add_raw(r, a, b);
-        c = add_fc(r, c);
-        add_fc(r, c);
-    }
-    __device__ static __forceinline__ void sub(fe& r, const fe& a, const fe& b) {
-        uint32_t bw = fe_sub_raw(r, a, b);
-        bw = sub_fc(r, bw);
-        sub_fc(r, bw);
-    }
+    __device__ static __forceinline__ void add(fe& r, const fe& a, const fe& b) { k1_add_asm(r.v, a.v, b.v); }
+    __device__ static __forceinline__ void sub(fe& r, const fe& a, const fe& b) { k1_sub_asm(r.v, a.v, b.v); }
     // canonical residue in [0, p)
     __device__ static __forceinline__ void normalize(fe& a) {
         fe t;
-        fe_copy(t, a);
-        const uint32_t c = add_fc(t, 1u);  // a >= p  <=>  a + c >= 2^256
-        fe_cmov(a, t, c != 0);
+        k1_normalize_asm(t.v, a.v);
+        fe_copy(a, t);
     }
     __device__ static __forceinline__ bool is_zero(const fe& a) {
         fe t;
@@ -404,21 +371,8 @@ struct Mont {
         for (int i = 0; i < 8; ++i) r.v[i] = take ? u.v[i] : t.v[i];
     }
     __device__ static __forceinline__ void sqr(fe& r, const fe& a) { mul(r, a, a); }
-    __device__ static __forceinline__ void add(fe& r, const fe& a, const fe& b) {
-        fe s, t;
-        const uint32_t c = fe_add_raw(s, a, b);
-        const uint32_t bw = fe_sub_k(t, s, P::M);
-        const bool take = c != 0u || bw == 0u;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) r.v[i] = take ? t.v[i] : s.v[i];
-    }
-    __device__ static __forceinline__ void sub(fe& r, const fe& a, const fe& b) {
-        fe d, t;
-        const uint32_t bw = fe_sub_raw(d, a, b);
-        fe_add_k(t, d, P::M);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) r.v[i] = bw ? t.v[i] : d.v[i];
-    }
+    __device__ static __forceinline__ void add(fe& r, const fe& a, const fe& b) { mod_add_asm(r.v, a.v, b.v, P::M); }
+    __device__ static __forceinline__ void sub(fe& r, const fe& a, const fe& b) { mod_sub_asm(r.v, a.v, b.v, P::M); }
     __device__ static __forceinline__ void neg(fe& r, const fe& a) {
         fe z;
         fe_zero(z);
