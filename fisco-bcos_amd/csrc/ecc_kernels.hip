@@ -14,6 +14,7 @@
 //                  curve, L2-resident), 32 mixed additions and no doublings.
 //   variable base: radix-16 Booth recoding (digits in [-8, 8]) over a register-resident table of
 //                  1P..8P; every lane runs the same 65-window schedule (no divergence).
+#include <cstdlib>
 #include <mutex>
 #include <type_traits>
 #include "ec.h"
@@ -709,8 +710,10 @@ __global__ __launch_bounds__(256) void sm2_verify_kernel(const uint8_t* __restri
 }
 
 // Transaction::verify for a batch: tx hash of the preimage, recover / verify, sender address.
-template <int SUITE>
-__global__ __launch_bounds__(256) void tx_verify_kernel(const uint8_t* __restrict__ pre,
+// OCC = waves per SIMD the register allocation must allow: 1 (no spills, lowest per-tx latency:
+// small batches) or 2 (spills ~120 VGPRs to scratch but doubles the resident waves: large batches).
+template <int SUITE, int OCC>
+__global__ __launch_bounds__(256, OCC) void tx_verify_kernel(const uint8_t* __restrict__ pre,
                                                         const uint64_t* __restrict__ pre_off,
                                                         const uint8_t* __restrict__ sig,
                                                         const uint64_t* __restrict__ sig_off, uint64_t n,
@@ -907,6 +910,250 @@ __global__ __launch_bounds__(256) void sm2_sign_kernel(const uint8_t* __restrict
     okout[i] = ok ? 1 : 0;
 }
 
+// ------------------------------------------------------------------ split (latency) secp256k1 tx verify
+// Small batches are latency-bound: 10k txs fill 157 waves on 1,024 SIMDs, so one recovery per lane
+// leaves most of the chip idle.  Here a 256-thread workgroup owns 64 txs and its 4 waves (on the
+// CU's 4 SIMDs) run independent parts of every recovery concurrently, exchanging through LDS:
+//   phase A  wave 1: tx hash, r^-1 (safegcd), u1 = -e/r, u2 = s/r, GLV split of u2
+//            wave 2: y = sqrt(x^3 + 7), table 1R..8R, co-Z rescale -> LDS (affine on E')
+//   phase C  wave 0: k1 * R      wave 1: k2 * phi(R)   (32 radix-16 windows each, table in LDS)
+//            wave 2: u1 * G (comb)
+//   phase D  wave 0: sum on E', map to E, add the G part, affine, Keccak address, store
+// Results are bit-identical to tx_verify_kernel<0, *>.
+struct SplitLds {
+    uint32_t tab[8][16][64];  // [entry][x0..7, y0..7][lane]: conflict-free per-lane gathers
+    uint32_t zc[8][64];
+    uint32_t u1[8][64];
+    uint32_t k1[4][64];
+    uint32_t k2[4][64];
+    uint32_t flags[64];       // bit0 wave-1 checks ok, bit1 wave-2 checks ok, bit2 neg1, bit3 neg2
+    uint32_t pt[3][25][64];   // partial results: X, Y, Z, inf
+};
+
+__device__ __forceinline__ void lds_store_fe(uint32_t (*dst)[64], const fe& a, int lane) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dst[k][lane] = a.v[k];
+}
+__device__ __forceinline__ void lds_load_fe(fe& a, const uint32_t (*src)[64], int lane) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a.v[k] = src[k][lane];
+}
+__device__ __forceinline__ void lds_store_jac(uint32_t (*dst)[64], const Jac& P, int lane) {
+    lds_store_fe(dst, P.X, lane);
+    lds_store_fe(dst + 8, P.Y, lane);
+    lds_store_fe(dst + 16, P.Z, lane);
+    dst[24][lane] = P.inf ? 1u : 0u;
+}
+__device__ __forceinline__ void lds_load_jac(Jac& P, const uint32_t (*src)[64], int lane) {
+    lds_load_fe(P.X, src, lane);
+    lds_load_fe(P.Y, src + 8, lane);
+    lds_load_fe(P.Z, src + 16, lane);
+    P.inf = src[24][lane] != 0u;
+}
+
+// acc += (+-d) (phi ? lambda : 1) T[|d| - 1], T gathered per lane from the LDS table (on E')
+__device__ __forceinline__ void add_digit_lds(Jac& acc, const SplitLds& L, int lane, int d, bool neg, bool phi) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &L.tab[0][0][0] + m * (16 * 64) + lane;
+    Aff S;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        S.x.v[k] = base[k * 64];
+        S.y.v[k] = base[(8 + k) * 64];
+    }
+    if (phi) {
+        fe b;
+        fe_set(b, kGlvBeta);
+        FieldK1::mul(S.x, S.x, b);
+    }
+    fe ny;
+    FieldK1::neg(ny, S.y);
+    fe_cmov(S.y, ny, (d < 0) != neg);
+    Jac R;
+    CurveK1::madd(R, acc, S);
+    CurveK1::cmov(acc, R, d != 0);
+}
+
+__device__ __forceinline__ void glv_half_lds(Jac& acc, fe& k, bool neg, bool phi, const SplitLds& L, int lane) {
+    CurveK1::set_inf(acc);
+    add_digit_lds(acc, L, lane, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
+#pragma unroll 1
+    for (int i = 31; i >= 0; --i) {
+        CurveK1::dbl(acc, acc);
+        CurveK1::dbl(acc, acc);
+        CurveK1::dbl(acc, acc);
+        CurveK1::dbl(acc, acc);
+        add_digit_lds(acc, L, lane, booth_digit128(k), neg, phi);
+    }
+}
+
+// parse r, s, v of a 65-byte signature; ok = libsecp256k1 parse_compact + r, s != 0
+__device__ __forceinline__ bool parse_sig65(const uint8_t* sig, uint32_t siglen, fe& r, fe& s, uint32_t& v) {
+    if (siglen != 65u) {
+        fe_zero(r);
+        fe_zero(s);
+        v = 0;
+        return false;
+    }
+    ByteReader rd(sig, 65);
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
+    fe_from_be_words(s, w);
+    v = rd.word(16) & 0xffu;
+    return v <= 3u && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, ParamN1::M);
+}
+
+__global__ __launch_bounds__(256, 1) void tx_verify_split_kernel(const uint8_t* __restrict__ pre,
+                                                                 const uint64_t* __restrict__ pre_off,
+                                                                 const uint8_t* __restrict__ sig,
+                                                                 const uint64_t* __restrict__ sig_off, uint64_t n,
+                                                                 const uint32_t* __restrict__ tab,
+                                                                 uint8_t* __restrict__ txhash,
+                                                                 uint8_t* __restrict__ sender,
+                                                                 uint8_t* __restrict__ status) {
+    __shared__ SplitLds L;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
+    const bool active = i < n;
+    uint64_t sa = 0, sb = 0;
+    if (active) {
+        sa = sig_off[i];
+        sb = sig_off[i + 1];
+    }
+    const uint32_t slen = (sb - sa) > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(sb - sa);
+    // ---------------------------------------------------------------- phase A
+    if (wave == 1) {
+        if (active) {
+            const uint64_t a = pre_off[i], b = pre_off[i + 1];
+            const uint32_t len = static_cast<uint32_t>(b - a);
+            ByteReader rd(pre + a, len);
+            uint32_t d[8];
+            keccak256_msg(rd, len, d);
+            store_digest(KECCAK256, txhash + 32 * i, d);
+            fe e, r, s;
+            uint32_t v;
+            fe_from_be_words(e, d);
+            reduce_once(e, ParamN1::M);
+            const bool ok = parse_sig65(sig + sa, slen, r, s, v);
+            if (!ok) {
+                fe_zero(r);
+                r.v[0] = 1;
+                fe_zero(s);
+            }
+            fe rm, rinv, u1, u2, k1, k2;
+            FieldN1::from_plain(rm, r);
+            FieldInv<FieldN1>::inv(rinv, rm);
+            FieldN1::mul(u1, e, rinv);
+            FieldN1::neg(u1, u1);
+            FieldN1::mul(u2, s, rinv);
+            bool neg1, neg2;
+            glv_split(k1, neg1, k2, neg2, u2);
+            lds_store_fe(L.u1, u1, lane);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                L.k1[k][lane] = k1.v[k];
+                L.k2[k][lane] = k2.v[k];
+            }
+            L.flags[lane] = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
+        }
+    } else if (wave == 2) {
+        if (active) {
+            fe r, s;
+            uint32_t v;
+            bool ok = parse_sig65(sig + sa, slen, r, s, v);
+            fe x;
+            fe_copy(x, r);
+            if (v & 2u) {
+                ok = ok && fe_lt_k(r, kK1PminusN);
+                fe_add_k(x, r, ParamN1::M);
+            }
+            fe rhs, y, t, seven;
+            FieldK1::sqr(t, x);
+            FieldK1::mul(rhs, t, x);
+            fe_zero(seven);
+            seven.v[0] = 7;
+            FieldK1::add(rhs, rhs, seven);
+            FieldK1::sqrt_cand(y, rhs);
+            FieldK1::sqr(t, y);
+            ok = ok && FieldK1::eq(t, rhs);
+            FieldK1::normalize(y);
+            fe ny;
+            FieldK1::neg(ny, y);
+            FieldK1::normalize(ny);
+            fe_cmov(y, ny, (y.v[0] & 1u) != (v & 1u));
+            Aff R, A[8];
+            fe_copy(R.x, x);
+            fe_copy(R.y, y);
+            fe Zc;
+            {
+                Jac T[8];
+                multiples8<CurveK1>(T, R);
+                coz_table_k1(A, Zc, T);
+            }
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                lds_store_fe(L.tab[j], A[j].x, lane);
+                lds_store_fe(L.tab[j] + 8, A[j].y, lane);
+            });
+            lds_store_fe(L.zc, Zc, lane);
+            L.pt[2][24][lane] = ok ? 2u : 0u;  // wave-2 verdict travels in a scratch slot until phase C
+        }
+    }
+    __syncthreads();
+    // ---------------------------------------------------------------- phase C
+    uint32_t flags = 0;
+    if (active) flags = L.flags[lane] | L.pt[2][24][lane];
+    __syncthreads();
+    if (wave <= 1) {
+        if (active) {
+            fe k;
+            fe_zero(k);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) k.v[q] = wave == 0 ? L.k1[q][lane] : L.k2[q][lane];
+            const bool neg = wave == 0 ? (flags & 4u) != 0 : (flags & 8u) != 0;
+            Jac P;
+            glv_half_lds(P, k, neg, wave == 1, L, lane);
+            lds_store_jac(L.pt[wave], P, lane);
+        }
+    } else if (wave == 2) {
+        if (active) {
+            fe u1;
+            lds_load_fe(u1, L.u1, lane);
+            Jac PG;
+            comb_mul<CurveK1>(PG, u1, tab);
+            lds_store_jac(L.pt[2], PG, lane);
+        }
+    }
+    __syncthreads();
+    // ---------------------------------------------------------------- phase D
+    if (wave == 0 && active) {
+        Jac P0, P1, PG, Q, R;
+        lds_load_jac(P0, L.pt[0], lane);
+        lds_load_jac(P1, L.pt[1], lane);
+        lds_load_jac(PG, L.pt[2], lane);
+        fe Zc;
+        lds_load_fe(Zc, L.zc, lane);
+        CurveK1::add(Q, P0, P1);  // on E'
+        FieldK1::mul(Q.Z, Q.Z, Zc);  // -> E
+        CurveK1::add(R, Q, PG);
+        const bool ok = (flags & 3u) == 3u && !R.inf;
+        Aff A;
+        CurveK1::to_aff(A, R);
+        FieldK1::normalize(A.x);
+        FieldK1::normalize(A.y);
+        uint32_t ad[5] = {0, 0, 0, 0, 0};
+        if (ok) keccak_address(ad, A.x, A.y);
+        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = ad[k];
+        status[i] = ok ? 0 : 1;
+    }
+}
+
 // ------------------------------------------------------------------ launchers
 static inline unsigned grid_of(uint64_t n) { return static_cast<unsigned>((n + 255) / 256); }
 
@@ -954,6 +1201,21 @@ int launch_sm2_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
+static int tx_verify_occupancy(uint64_t n) {
+    const char* e = getenv("BCOSGPU_TXV_OCC");  // read per launch so tests can A/B both variants
+    const int forced = e ? atoi(e) : 0;
+    if (forced == 1 || forced == 2) return forced;
+    return n >= (1ull << 17) ? 2 : 1;  // >= 2 waves per SIMD of work on 256 CUs
+}
+
+// Split kernel (4 waves per 64 txs) while the batch leaves SIMDs idle; BCOSGPU_TXV_SPLIT=0/1 forces it.
+static bool use_split(uint64_t n) {
+    const char* e = getenv("BCOSGPU_TXV_SPLIT");
+    const int forced = e ? atoi(e) : -1;
+    if (forced == 0 || forced == 1) return forced == 1;
+    return n <= (1ull << 15);
+}
+
 int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off, const uint8_t* d_sig,
                      const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash, uint8_t* d_sender, uint8_t* d_status,
                      hipStream_t st) {
@@ -961,12 +1223,20 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
     const uint32_t *k1, *sm2;
     int rc = tables(&k1, &sm2);
     if (rc) return rc;
-    if (suite == BCOSGPU_SUITE_SM2)
-        hipLaunchKernelGGL(tx_verify_kernel<BCOSGPU_SUITE_SM2>, dim3(grid_of(n)), dim3(256), 0, st, d_pre, d_pre_off,
-                           d_sig, d_sig_off, n, sm2, d_txhash, d_sender, d_status);
-    else
-        hipLaunchKernelGGL(tx_verify_kernel<BCOSGPU_SUITE_SECP256K1>, dim3(grid_of(n)), dim3(256), 0, st, d_pre,
+    if (suite == BCOSGPU_SUITE_SECP256K1 && use_split(n)) {
+        hipLaunchKernelGGL(tx_verify_split_kernel, dim3(static_cast<unsigned>((n + 63) / 64)), dim3(256), 0, st, d_pre,
                            d_pre_off, d_sig, d_sig_off, n, k1, d_txhash, d_sender, d_status);
+        return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+    }
+    const int occ = tx_verify_occupancy(n);
+#define TXV(S, O, T) hipLaunchKernelGGL((tx_verify_kernel<S, O>), dim3(grid_of(n)), dim3(256), 0, st, d_pre, d_pre_off, \
+                                        d_sig, d_sig_off, n, T, d_txhash, d_sender, d_status)
+    if (suite == BCOSGPU_SUITE_SM2) {
+        if (occ == 2) TXV(BCOSGPU_SUITE_SM2, 2, sm2); else TXV(BCOSGPU_SUITE_SM2, 1, sm2);
+    } else {
+        if (occ == 2) TXV(BCOSGPU_SUITE_SECP256K1, 2, k1); else TXV(BCOSGPU_SUITE_SECP256K1, 1, k1);
+    }
+#undef TXV
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
