@@ -38,6 +38,16 @@ WORKLOADS = {
 }
 
 
+def _kernel_name(suite, n):
+    """Which tx-verify kernel the library launches for this batch (mirrors ecc_kernels.hip policy)."""
+    split = os.environ.get("BCOSGPU_TXV_SPLIT")
+    if suite == 0 and (split == "1" or (split != "0" and n <= (1 << 15))):
+        return "tx_verify_split_kernel"
+    occ = os.environ.get("BCOSGPU_TXV_OCC")
+    occ = int(occ) if occ in ("1", "2") else (2 if n >= (1 << 17) else 1)
+    return "tx_verify_kernel<%d,%d>" % (suite, occ)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -106,7 +116,7 @@ def main():
         achieved = n * f_per * MAC_PER_F / (kernel_ms * 1e-3)
         roofline = {"bound": "int-valu", "achieved": achieved / 1e12, "peak": PEAK_MAC_PER_S / 1e12,
                     "unit": "TMAC/s", "frac": achieved / PEAK_MAC_PER_S, "traffic": None,
-                    "kernel": "tx_verify_kernel<%d>" % suite, "kernel_ms": kernel_ms,
+                    "kernel": _kernel_name(suite, n), "kernel_ms": kernel_ms,
                     "work_per_unit": "%d F x %d MAC (SURVEY.md 8d)" % (f_per, MAC_PER_F)}
         cpu = None
         if not args.no_cpu_baseline:

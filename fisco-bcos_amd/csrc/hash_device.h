@@ -57,74 +57,89 @@ __device__ __constant__ static const uint64_t kKeccakRC[24] = {
     0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
     0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
-    return (x << r) | (x >> (64 - r));
+// Keccak-f[1600] on 32-bit halves (gfx950 has no 64-bit logic ops): theta folds into 3-input
+// v_bitop3 XORs (column parity: 2 per half; a ^ C[x-1] ^ rotl1(C[x+1]) in one), rho is a v_alignbit
+// pair, chi is one v_bitop3 (a ^ (~b & c)) per half -- ~180 VALU per round.  State lane x + 5y.
+struct KLane {
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t chi32(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xD2);  // a ^ (~b & c)
+}
+template <int R>
+__device__ __forceinline__ KLane rotl_lane(KLane x) {
+    if constexpr (R == 0) {
+        return x;
+    } else if constexpr (R < 32) {
+        return {__builtin_amdgcn_alignbit(x.lo, x.hi, 32 - R), __builtin_amdgcn_alignbit(x.hi, x.lo, 32 - R)};
+    } else if constexpr (R == 32) {
+        return {x.hi, x.lo};
+    } else {
+        return {__builtin_amdgcn_alignbit(x.hi, x.lo, 64 - R), __builtin_amdgcn_alignbit(x.lo, x.hi, 64 - R)};
+    }
 }
 
-// Keccak-f[1600], fully unrolled; state lane index x + 5y.
 __device__ __forceinline__ void keccak_f1600(uint64_t s[25]) {
+    KLane a[25];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) a[i] = {static_cast<uint32_t>(s[i]), static_cast<uint32_t>(s[i] >> 32)};
 #pragma unroll 1
     for (int round = 0; round < 24; ++round) {
-        uint64_t c0 = s[0] ^ s[5] ^ s[10] ^ s[15] ^ s[20];
-        uint64_t c1 = s[1] ^ s[6] ^ s[11] ^ s[16] ^ s[21];
-        uint64_t c2 = s[2] ^ s[7] ^ s[12] ^ s[17] ^ s[22];
-        uint64_t c3 = s[3] ^ s[8] ^ s[13] ^ s[18] ^ s[23];
-        uint64_t c4 = s[4] ^ s[9] ^ s[14] ^ s[19] ^ s[24];
-        uint64_t d0 = c4 ^ rotl64(c1, 1), d1 = c0 ^ rotl64(c2, 1), d2 = c1 ^ rotl64(c3, 1),
-                 d3 = c2 ^ rotl64(c4, 1), d4 = c3 ^ rotl64(c0, 1);
-        // theta + rho + pi: b[y + 5((2x+3y)%5)] = rotl(a[x+5y] ^ d[x], r[x][y])
-        uint64_t b0 = s[0] ^ d0;
-        uint64_t b10 = rotl64(s[1] ^ d1, 1);
-        uint64_t b20 = rotl64(s[2] ^ d2, 62);
-        uint64_t b5 = rotl64(s[3] ^ d3, 28);
-        uint64_t b15 = rotl64(s[4] ^ d4, 27);
-        uint64_t b16 = rotl64(s[5] ^ d0, 36);
-        uint64_t b1 = rotl64(s[6] ^ d1, 44);
-        uint64_t b11 = rotl64(s[7] ^ d2, 6);
-        uint64_t b21 = rotl64(s[8] ^ d3, 55);
-        uint64_t b6 = rotl64(s[9] ^ d4, 20);
-        uint64_t b7 = rotl64(s[10] ^ d0, 3);
-        uint64_t b17 = rotl64(s[11] ^ d1, 10);
-        uint64_t b2 = rotl64(s[12] ^ d2, 43);
-        uint64_t b12 = rotl64(s[13] ^ d3, 25);
-        uint64_t b22 = rotl64(s[14] ^ d4, 39);
-        uint64_t b23 = rotl64(s[15] ^ d0, 41);
-        uint64_t b8 = rotl64(s[16] ^ d1, 45);
-        uint64_t b18 = rotl64(s[17] ^ d2, 15);
-        uint64_t b3 = rotl64(s[18] ^ d3, 21);
-        uint64_t b13 = rotl64(s[19] ^ d4, 8);
-        uint64_t b14 = rotl64(s[20] ^ d0, 18);
-        uint64_t b24 = rotl64(s[21] ^ d1, 2);
-        uint64_t b9 = rotl64(s[22] ^ d2, 61);
-        uint64_t b19 = rotl64(s[23] ^ d3, 56);
-        uint64_t b4 = rotl64(s[24] ^ d4, 14);
+        KLane c[5], e[5], b[25];
+#pragma unroll
+        for (int x = 0; x < 5; ++x) {
+            c[x].lo = xor3(xor3(a[x].lo, a[x + 5].lo, a[x + 10].lo), a[x + 15].lo, a[x + 20].lo);
+            c[x].hi = xor3(xor3(a[x].hi, a[x + 5].hi, a[x + 10].hi), a[x + 15].hi, a[x + 20].hi);
+        }
+#pragma unroll
+        for (int x = 0; x < 5; ++x) e[x] = rotl_lane<1>(c[(x + 1) % 5]);
+        // theta + rho + pi: b[y + 5((2x+3y)%5)] = rotl(a[x+5y] ^ C[x-1] ^ rotl1(C[x+1]), r[x][y])
+#define KECCAK_TRP(SRC, R, DST, XM1, X) \
+    b[DST] = rotl_lane<R>(KLane{xor3(a[SRC].lo, c[XM1].lo, e[X].lo), xor3(a[SRC].hi, c[XM1].hi, e[X].hi)})
+        KECCAK_TRP(0, 0, 0, 4, 0);
+        KECCAK_TRP(1, 1, 10, 0, 1);
+        KECCAK_TRP(2, 62, 20, 1, 2);
+        KECCAK_TRP(3, 28, 5, 2, 3);
+        KECCAK_TRP(4, 27, 15, 3, 4);
+        KECCAK_TRP(5, 36, 16, 4, 0);
+        KECCAK_TRP(6, 44, 1, 0, 1);
+        KECCAK_TRP(7, 6, 11, 1, 2);
+        KECCAK_TRP(8, 55, 21, 2, 3);
+        KECCAK_TRP(9, 20, 6, 3, 4);
+        KECCAK_TRP(10, 3, 7, 4, 0);
+        KECCAK_TRP(11, 10, 17, 0, 1);
+        KECCAK_TRP(12, 43, 2, 1, 2);
+        KECCAK_TRP(13, 25, 12, 2, 3);
+        KECCAK_TRP(14, 39, 22, 3, 4);
+        KECCAK_TRP(15, 41, 23, 4, 0);
+        KECCAK_TRP(16, 45, 8, 0, 1);
+        KECCAK_TRP(17, 15, 18, 1, 2);
+        KECCAK_TRP(18, 21, 3, 2, 3);
+        KECCAK_TRP(19, 8, 13, 3, 4);
+        KECCAK_TRP(20, 18, 14, 4, 0);
+        KECCAK_TRP(21, 2, 24, 0, 1);
+        KECCAK_TRP(22, 61, 9, 1, 2);
+        KECCAK_TRP(23, 56, 19, 2, 3);
+        KECCAK_TRP(24, 14, 4, 3, 4);
+#undef KECCAK_TRP
         // chi + iota
-        s[0] = b0 ^ (~b1 & b2) ^ kKeccakRC[round];
-        s[1] = b1 ^ (~b2 & b3);
-        s[2] = b2 ^ (~b3 & b4);
-        s[3] = b3 ^ (~b4 & b0);
-        s[4] = b4 ^ (~b0 & b1);
-        s[5] = b5 ^ (~b6 & b7);
-        s[6] = b6 ^ (~b7 & b8);
-        s[7] = b7 ^ (~b8 & b9);
-        s[8] = b8 ^ (~b9 & b5);
-        s[9] = b9 ^ (~b5 & b6);
-        s[10] = b10 ^ (~b11 & b12);
-        s[11] = b11 ^ (~b12 & b13);
-        s[12] = b12 ^ (~b13 & b14);
-        s[13] = b13 ^ (~b14 & b10);
-        s[14] = b14 ^ (~b10 & b11);
-        s[15] = b15 ^ (~b16 & b17);
-        s[16] = b16 ^ (~b17 & b18);
-        s[17] = b17 ^ (~b18 & b19);
-        s[18] = b18 ^ (~b19 & b15);
-        s[19] = b19 ^ (~b15 & b16);
-        s[20] = b20 ^ (~b21 & b22);
-        s[21] = b21 ^ (~b22 & b23);
-        s[22] = b22 ^ (~b23 & b24);
-        s[23] = b23 ^ (~b24 & b20);
-        s[24] = b24 ^ (~b20 & b21);
+#pragma unroll
+        for (int y = 0; y < 25; y += 5) {
+#pragma unroll
+            for (int x = 0; x < 5; ++x) {
+                const KLane p = b[y + x], q = b[y + (x + 1) % 5], r = b[y + (x + 2) % 5];
+                a[y + x] = {chi32(p.lo, q.lo, r.lo), chi32(p.hi, q.hi, r.hi)};
+            }
+        }
+        const uint64_t rc = kKeccakRC[round];
+        a[0].lo ^= static_cast<uint32_t>(rc);
+        a[0].hi ^= static_cast<uint32_t>(rc >> 32);
     }
+#pragma unroll
+    for (int i = 0; i < 25; ++i) s[i] = (static_cast<uint64_t>(a[i].hi) << 32) | a[i].lo;
 }
 
 // Keccak-256 of a whole message through a reader (rate 136 B = 34 words, pad 0x01 ... 0x80).
@@ -177,8 +192,8 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) {
     return __builtin_amdgcn_alignbit(x, x, (32 - r) & 31);
 }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-__device__ __forceinline__ uint32_t sm3_p0(uint32_t x) { return x ^ rotl32(x, 9) ^ rotl32(x, 17); }
-__device__ __forceinline__ uint32_t sm3_p1(uint32_t x) { return x ^ rotl32(x, 15) ^ rotl32(x, 23); }
+__device__ __forceinline__ uint32_t sm3_p0(uint32_t x) { return xor3(x, rotl32(x, 9), rotl32(x, 17)); }
+__device__ __forceinline__ uint32_t sm3_p1(uint32_t x) { return xor3(x, rotl32(x, 15), rotl32(x, 23)); }
 
 __device__ __forceinline__ void sm3_init(uint32_t V[8]) {
     V[0] = 0x7380166fu; V[1] = 0x4914b2b9u; V[2] = 0x172442d7u; V[3] = 0xda8a0600u;
@@ -187,28 +202,35 @@ __device__ __forceinline__ void sm3_init(uint32_t V[8]) {
 
 // One compression; W[0..15] are the block's big-endian words.  Message expansion is computed on
 // the fly in a 16-word ring so only 16 words stay live.
+template <bool LOW>  // rounds 0..15 (xor FF/GG) or 16..63 (majority / choose)
+__device__ __forceinline__ void sm3_round(int j, uint32_t W[16], uint32_t& A, uint32_t& B, uint32_t& C, uint32_t& D,
+                                          uint32_t& E, uint32_t& F, uint32_t& G, uint32_t& H) {
+    // W[j+4] is needed for W'[j] = W[j] ^ W[j+4]
+    if (j >= 12) {
+        const int t = j + 4;  // expand W[t], t in [16, 68)
+        const uint32_t x = xor3(W[(t - 16) & 15], W[(t - 9) & 15], rotl32(W[(t - 3) & 15], 15));
+        W[t & 15] = xor3(sm3_p1(x), rotl32(W[(t - 13) & 15], 7), W[(t - 6) & 15]);
+    }
+    const uint32_t wj = W[j & 15], wj4 = W[(j + 4) & 15];
+    const uint32_t T = LOW ? 0x79cc4519u : 0x7a879d8au;
+    const uint32_t a12 = rotl32(A, 12);
+    const uint32_t SS1 = rotl32(a12 + E + rotl32(T, j & 31), 7);
+    const uint32_t SS2 = SS1 ^ a12;
+    // FF: xor / majority, GG: xor / choose -- one v_bitop3 each
+    const uint32_t FF = __builtin_amdgcn_bitop3_b32(A, B, C, LOW ? 0x96 : 0xE8);
+    const uint32_t GG = __builtin_amdgcn_bitop3_b32(E, F, G, LOW ? 0x96 : 0xCA);
+    const uint32_t TT1 = FF + D + SS2 + (wj ^ wj4);
+    const uint32_t TT2 = GG + H + SS1 + wj;
+    D = C; C = rotl32(B, 9); B = A; A = TT1;
+    H = G; G = rotl32(F, 19); F = E; E = sm3_p0(TT2);
+}
+
 __device__ __forceinline__ void sm3_compress(uint32_t V[8], uint32_t W[16]) {
     uint32_t A = V[0], B = V[1], C = V[2], D = V[3], E = V[4], F = V[5], G = V[6], H = V[7];
 #pragma unroll
-    for (int j = 0; j < 64; ++j) {
-        // W[j+4] is needed for W'[j] = W[j] ^ W[j+4]
-        if (j >= 12) {
-            const int t = j + 4;  // expand W[t], t in [16, 68)
-            uint32_t x = W[(t - 16) & 15] ^ W[(t - 9) & 15] ^ rotl32(W[(t - 3) & 15], 15);
-            W[t & 15] = sm3_p1(x) ^ rotl32(W[(t - 13) & 15], 7) ^ W[(t - 6) & 15];
-        }
-        const uint32_t wj = W[j & 15], wj4 = W[(j + 4) & 15];
-        const uint32_t T = j < 16 ? 0x79cc4519u : 0x7a879d8au;
-        const uint32_t a12 = rotl32(A, 12);
-        const uint32_t SS1 = rotl32(a12 + E + rotl32(T, j & 31), 7);
-        const uint32_t SS2 = SS1 ^ a12;
-        const uint32_t FF = j < 16 ? (A ^ B ^ C) : ((A & B) | (A & C) | (B & C));
-        const uint32_t GG = j < 16 ? (E ^ F ^ G) : ((E & F) | (~E & G));
-        const uint32_t TT1 = FF + D + SS2 + (wj ^ wj4);
-        const uint32_t TT2 = GG + H + SS1 + wj;
-        D = C; C = rotl32(B, 9); B = A; A = TT1;
-        H = G; G = rotl32(F, 19); F = E; E = sm3_p0(TT2);
-    }
+    for (int j = 0; j < 16; ++j) sm3_round<true>(j, W, A, B, C, D, E, F, G, H);
+#pragma unroll
+    for (int j = 16; j < 64; ++j) sm3_round<false>(j, W, A, B, C, D, E, F, G, H);
     V[0] ^= A; V[1] ^= B; V[2] ^= C; V[3] ^= D; V[4] ^= E; V[5] ^= F; V[6] ^= G; V[7] ^= H;
 }
 
