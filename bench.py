@@ -1,20 +1,30 @@
 #!/usr/bin/env python3
 """bench.py -- headline benchmark of the MI355X batch-verification engine.
 
-Workload (BASELINE.json configs[1], "C2"): per GPU, a batch of 10,000 synthetic secp256k1-signed
-transactions resident in HBM; one step = one pass of the hot path over the batch:
+Default workload (BASELINE.json configs[1], "C2"): per GPU, a batch of 10,000 synthetic
+secp256k1-signed transactions resident in HBM; one step = one pass of the hot path over the batch:
 Keccak256 tx hash of each preimage (TarsHashable.h:16-41) + ECDSA public-key recovery
 (Secp256k1Crypto.cpp:79-93) + sender = right160(Keccak256(pub)) (Transaction.h:68-82), i.e.
-bcosgpu_tx_verify_batch_dev.  --workload c3 runs configs[2] instead (1M SM2/SM3 txs on one GPU).
-Multi-GPU: one process per GPU, each verifies its own shard (weak scaling, no data-path
-collective); rank 0 prints one JSON line with the whole-job rate.
+bcosgpu_tx_verify_batch_dev.  Multi-GPU: one process per GPU, each verifies its own shard (weak
+scaling, no data-path collective); rank 0 prints one JSON line with the whole-job rate.
 
-Also reported (same line): the roofline of the dominant kernel from HIP events on the launch stream,
-the CPU baseline (the oracle restatement, multi-threaded, on a bounded sample), and the C1 Merkle
-rate (merkleBench: width-16 root over 100k 32-byte leaves).
+Other BASELINE.json configs (--workload):
+  c3  configs[2]: 1M SM2/SM3 txs per GPU (SM3 tx hash + SM2 verify + sender), weak scaling.
+  c4  configs[3]: 1M secp256k1 txs in TOTAL, sharded by index over the ranks (width^L-aligned shard
+      plan); step = verify the shard + the block tx root (width-2 Keccak Merkle, BlockImpl.h:111-154):
+      per-rank frontier, ONE RCCL all-gather over xGMI, top levels on every rank.  Strong scaling.
+  c5  configs[4]: PBFT block-verify replay, 64 blocks x 20k txs in TOTAL, blocks sharded over the
+      ranks; step = verify every tx of the rank's blocks + each block's tx root
+      (bcosgpu_merkle_roots_batch_dev, one launch per tree level for all blocks).  Strong scaling.
+
+Also reported (same line): the roofline of the dominant kernel (tx_verify) from HIP events on the
+launch stream, its HBM traffic from the committed rocprofv3 PMC pass of the same workload
+(profiles/), the CPU baseline (the oracle restatement, multi-threaded, on a bounded sample, rank 0 at
+N=1 only), and the C1 Merkle rate (merkleBench: width-16 root over 100k 32-byte leaves).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -31,10 +41,19 @@ F_SM2_VERIFY = 3210
 # integer-MAC peak of gfx950 (v_mad_u64_u32 lane-ops/s), measured by fisco-bcos_amd/tools/intbench.hip
 # on MI355X (profiles/r01_intbench.json)
 PEAK_MAC_PER_S = 3.0785e13
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_{}.json")
 
 WORKLOADS = {
-    "c2": dict(suite=0, n=10_000, name="C2: 10k synthetic secp256k1 txs / GPU: Keccak256 tx hash + ECDSA recover + sender"),
-    "c3": dict(suite=1, n=1_000_000, name="C3: 1M synthetic SM2/SM3 txs / GPU: SM3 tx hash + SM2 verify + sender"),
+    "c2": dict(suite=0, n=10_000, scaling="weak", metric="sigs_per_sec",
+               name="C2: 10k synthetic secp256k1 txs / GPU: Keccak256 tx hash + ECDSA recover + sender"),
+    "c3": dict(suite=1, n=1_000_000, scaling="weak", metric="sm2_verify_per_sec",
+               name="C3: 1M synthetic SM2/SM3 txs / GPU: SM3 tx hash + SM2 verify + sender"),
+    "c4": dict(suite=0, n=1_000_000, scaling="strong", metric="sigs_per_sec",
+               name="C4: 1M synthetic secp256k1 txs sharded over the GPUs: tx hash + recover + sender "
+                    "+ width-2 Keccak tx root (per-GPU frontier, RCCL all-gather)"),
+    "c5": dict(suite=0, n=64 * 20_000, blocks=64, scaling="strong", metric="sigs_per_sec",
+               name="C5: PBFT block-verify replay, 64 blocks x 20k secp256k1 txs sharded by block: "
+                    "recover + per-block width-2 Keccak tx root"),
 }
 
 
@@ -48,6 +67,31 @@ def _kernel_name(suite, n):
     return "tx_verify_kernel<%d,%d>" % (suite, occ)
 
 
+def _norm(name):
+    return name.replace("void ", "").replace("bcosgpu::", "").replace(" ", "").split("(")[0]
+
+
+def _traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of this workload
+    (tools/prof_summary.py; FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction)."""
+    path = PMC_FILE.format(workload)
+    try:
+        with open(path) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    for name, c in pmc.get("kernels", {}).items():
+        if _norm(name) == _norm(kernel) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            return (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, ROOT)
+    return None, None
+
+
+def _block_plan(nblocks, world, rank):
+    per = math.ceil(nblocks / world)
+    lo, hi = min(rank * per, nblocks), min((rank + 1) * per, nblocks)
+    return lo, hi
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -55,6 +99,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-merkle", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
 
@@ -63,7 +108,7 @@ def main():
     import torch.distributed as dist
 
     import bcos_gpu
-    from bcos_gpu import device, synth
+    from bcos_gpu import device, parallel, synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -73,17 +118,45 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     bcos_gpu.ensure_device(local)
     wl = WORKLOADS[args.workload]
-    suite, n = wl["suite"], wl["n"]
-
-    # ---- synthetic, device-resident shard of this rank (distinct keys/txs per rank)
-    b = synth.make_batch(suite, n, seed=0xF15C0BC5 + 7919 * rank)
-    txhash = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
-    sender = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
-    status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    suite = wl["suite"]
     stream = torch.cuda.current_stream()
 
-    def step():
-        device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, txhash, sender, status, stream)
+    # ---- this rank's share of the work
+    txroot = None
+    block_off = None
+    if args.workload == "c4":
+        txroot = parallel.gpu_sharded_tx_root(wl["n"], world, rank, device.KECCAK256, 2, "cuda")
+        lo, hi = txroot.local_range
+        n = hi - lo
+    elif args.workload == "c5":
+        per_block = wl["n"] // wl["blocks"]
+        blo, bhi = _block_plan(wl["blocks"], world, rank)
+        n = (bhi - blo) * per_block
+        block_off = np.arange(bhi - blo + 1, dtype=np.uint64) * np.uint64(per_block)
+        work = torch.empty(max(device.merkle_roots_work_size(n, bhi - blo, 2), 1), dtype=torch.uint8, device="cuda")
+        roots = torch.empty((max(bhi - blo, 1), 32), dtype=torch.uint8, device="cuda")
+    else:
+        n = wl["n"]
+    units_total = wl["n"] if wl["scaling"] == "strong" else wl["n"] * world
+
+    # ---- synthetic, device-resident batch of this rank (distinct keys/txs per rank)
+    b = synth.make_batch(suite, max(n, 1), seed=0xF15C0BC5 + 7919 * rank)
+    txhash = torch.empty((max(n, 1), 32), dtype=torch.uint8, device="cuda")
+    sender = torch.empty((max(n, 1), 20), dtype=torch.uint8, device="cuda")
+    status = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(k=None):
+        if k is not None:
+            ev[k][0].record(stream)
+        if n:
+            device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, txhash, sender, status, stream)
+        if k is not None:
+            ev[k][1].record(stream)
+        if txroot is not None:
+            txroot(txhash[:n])
+        elif block_off is not None and n:
+            device.merkle_roots_batch(device.KECCAK256, 2, txhash, block_off, work, roots, stream)
 
     for _ in range(args.warmup):
         step()
@@ -91,54 +164,58 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
+    for k in range(args.steps):
+        step(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one tx_verify kernel per step on this stream
+    kernel_ms = sum(a.elapsed_time(c) for a, c in ev) / args.steps  # tx_verify launch, on its stream
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    ok_frac = float((status == 0).float().mean().item())
+    ok_frac = float((status[:n] == 0).float().mean().item()) if n else 1.0
 
     if rank == 0:
-        total = n * world * args.steps
-        value = total / elapsed
+        value = units_total * args.steps / elapsed
         f_per = F_SECP_RECOVER if suite == 0 else F_SM2_VERIFY
+        kname = _kernel_name(suite, n)
         achieved = n * f_per * MAC_PER_F / (kernel_ms * 1e-3)
+        traffic, traffic_src = _traffic(args.workload, kname)
         roofline = {"bound": "int-valu", "achieved": achieved / 1e12, "peak": PEAK_MAC_PER_S / 1e12,
-                    "unit": "TMAC/s", "frac": achieved / PEAK_MAC_PER_S, "traffic": None,
-                    "kernel": _kernel_name(suite, n), "kernel_ms": kernel_ms,
+                    "unit": "TMAC/s", "frac": achieved / PEAK_MAC_PER_S, "traffic": traffic,
+                    "traffic_source": traffic_src, "kernel": kname, "kernel_ms": kernel_ms,
+                    "units_per_launch": n,
                     "work_per_unit": "%d F x %d MAC (SURVEY.md 8d)" % (f_per, MAC_PER_F)}
         cpu = None
-        if not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(b, suite, min(n, 20000), args.cpu_threads)
-        merkle = merkle_c1()
         line = {
-            "metric": "sigs_per_sec" if suite == 0 else "sm2_verify_per_sec",
-            "value": value, "unit": "tx/s (hash + recover/verify + sender)", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 (256-bit integer)",
+            "metric": wl["metric"],
+            "value": value, "unit": "tx/s (hash + recover/verify + sender%s)" % (
+                " + tx root" if args.workload in ("c4", "c5") else ""),
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": wl["scaling"], "vs_baseline": None,
+            "dtype": "u32 (256-bit integer)",
             "data": "synthetic (distinct key per tx, 1%% bit-flipped s, 0.1%% v=4; valid frac %.4f)" % ok_frac,
-            "config": {"workload": wl["name"], "txs_per_gpu": n, "parallelism": "dp%d (tx-index shards)" % world},
-            "roofline": roofline, "cpu_baseline": cpu, "merkle_c1": merkle,
+            "config": {"workload": wl["name"], "txs_total": units_total, "txs_rank0": n,
+                       "parallelism": "dp%d (%s)" % (world, "block shards" if args.workload == "c5" else "tx-index shards")},
+            "roofline": roofline, "cpu_baseline": cpu,
         }
-        print(json.dumps(line))
+        if not args.no_merkle:
+            line["merkle_c1"] = merkle_c1()
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def cpu_baseline(b, suite, sample, threads):
-    """The oracle (C restatement, multi-threaded) on `sample` txs of the same batch, host cores."""
+def cpu_baseline(b, suite, sample, threads, min_seconds=1.0):
+    """The oracle (C restatement, multi-threaded) on `sample` txs of the same batch, host cores,
+    repeated until >= min_seconds of wall time (~16 CPU-seconds at 16 threads)."""
     import numpy as np
     from oracle import oracle
     pre = b.pre.cpu().numpy()
@@ -146,11 +223,16 @@ def cpu_baseline(b, suite, sample, threads):
     sig = b.sig.cpu().numpy()
     sig_off = b.sig_off[: sample + 1].cpu().numpy().astype(np.uint64)
     oracle.tx_verify_packed(suite, pre, pre_off[:65], sig, sig_off[:65], nthreads=threads)  # warm-up
-    t0 = time.perf_counter()
-    oracle.tx_verify_packed(suite, pre, pre_off, sig, sig_off, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": sample / dt, "unit": "tx/s", "cores": threads, "kind": "port",
-            "sample": "%d txs of the same batch, oracle/ C restatement (4x64-bit Montgomery, 4-bit Straus), %d threads" % (sample, threads)}
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle.tx_verify_packed(suite, pre, pre_off, sig, sig_off, nthreads=threads)
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= min_seconds:
+            break
+    return {"value": reps * sample / dt, "unit": "tx/s", "cores": threads, "kind": "port",
+            "sample": "%d x %d txs of the same batch (%.1f s wall), oracle/ C restatement (4x64-bit Montgomery, "
+                      "4-bit Straus), %d threads" % (reps, sample, dt, threads)}
 
 
 def merkle_c1():

@@ -43,12 +43,19 @@ _SIGS = {
     "bcosgpu_merkle_root": (_I, [_I, _I, _I, _P, _SZ, _P, _P]),
     "bcosgpu_merkle_root_dev": (_I, [_I, _I, _P, _SZ, _P, _P, _P]),
     "bcosgpu_merkle_frontier_dev": (_I, [_I, _I, _P, _SZ, _I, _P, _P, _P]),
+    "bcosgpu_merkle_roots_work_size": (ctypes.c_uint64, [ctypes.c_uint64, _SZ, _I]),
+    "bcosgpu_merkle_roots_batch": (_I, [_I, _I, _P, _P, _SZ, _P]),
+    "bcosgpu_merkle_roots_batch_dev": (_I, [_I, _I, _P, _P, _SZ, _P, _P, _P]),
     "bcosgpu_secp256k1_recover_batch": (_I, [_P, _P, _SZ, _P, _P, _P]),
     "bcosgpu_secp256k1_recover_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P, _P]),
     "bcosgpu_sm2_verify_batch": (_I, [_P, _P, _SZ, _P, _P]),
     "bcosgpu_sm2_verify_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P]),
     "bcosgpu_secp256k1_sign_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P, _P]),
     "bcosgpu_sm2_sign_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P]),
+    "bcosgpu_verify_batch": (_I, [_I, _P, _P, _P, _SZ, _SZ, _P]),
+    "bcosgpu_verify_batch_dev": (_I, [_I, _P, _P, _P, _SZ, _SZ, _P, _P]),
+    "bcosgpu_ecrecover_batch": (_I, [_P, _SZ, _P, _P]),
+    "bcosgpu_ecrecover_batch_dev": (_I, [_P, _SZ, _P, _P, _P]),
     "bcosgpu_tx_verify_batch": (_I, [_I, _P, _P, _P, _P, _SZ, _P, _P, _P]),
     "bcosgpu_tx_verify_batch_dev": (_I, [_I, _P, _P, _P, _P, _SZ, _P, _P, _P, _P]),
     "bcosgpu_wedpr_secp256k1_recover_public_key": (ctypes.c_int8, [_P, _P, _P]),

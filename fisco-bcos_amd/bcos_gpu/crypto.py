@@ -116,6 +116,22 @@ class Merkle:
                                         _ptr(root), None))
         return root.tobytes()
 
+    def roots_batch(self, blocks):
+        """Roots of many independent trees in one engine call (bcosgpu_merkle_roots_batch).
+        blocks: list of uint8[n_b, 32] arrays (or lists of 32-byte strings).  An empty block yields
+        the zero hash, as BlockImpl::calculateTransactionRoot does (BlockImpl.h:114-119)."""
+        arrs = [_u8(b"".join(bytes(h) for h in b) if isinstance(b, list) else b).reshape(-1, 32) for b in blocks]
+        nb = len(arrs)
+        roots = np.zeros((max(nb, 1), 32), dtype=np.uint8)
+        if nb == 0:
+            return []
+        off = np.zeros(nb + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([a.shape[0] for a in arrs], dtype=np.uint64)
+        leaves = np.ascontiguousarray(np.concatenate(arrs, 0)) if off[-1] else np.zeros((1, 32), dtype=np.uint8)
+        ensure_device()
+        check(lib().bcosgpu_merkle_roots_batch(self.hasher.kind, self.width, _ptr(leaves), _ptr(off), nb, _ptr(roots)))
+        return [roots[i].tobytes() for i in range(nb)]
+
 
 def calculate_merkle_proof_root(hasher: Hash, leaves) -> bytes:
     """protocol::calculateMerkleProofRoot (ParallelMerkleProof.cpp:32-69)."""
@@ -131,6 +147,30 @@ def calculate_merkle_proof_root(hasher: Hash, leaves) -> bytes:
 class SignatureCrypto:
     """bcos::crypto::SignatureCrypto (Signature.h:31-59)."""
     SIG_LEN = None
+    SUITE = None
+
+    def verify(self, pub: bytes, hash32: bytes, sig: bytes) -> bool:
+        """SignatureCrypto::verify(pub, hash, sig) (Signature.h:40-46) with a known key; only
+        sig[0:64] = r || s is read (SM2Crypto.cpp:66-79; wedpr_secp256k1_verify, Secp256k1Crypto.cpp:51-63)."""
+        if len(sig) < 64 or len(pub) != 64:
+            return False
+        return bool(self.verify_batch(_u8(pub, (1, 64)), _u8(hash32, (1, 32)), _u8(bytes(sig[:64]), (1, 64)))[0])
+
+    def verify_batch(self, pubs, hashes, sigs):
+        """Batched verify (bcosgpu_verify_batch): pubs uint8[n,64], hashes uint8[n,32],
+        sigs uint8[n, stride >= 64] -> bool[n]  (sealer-signature checks, BlockValidator.cpp:141-182)."""
+        pubs = _u8(pubs).reshape(-1, 64)
+        n = pubs.shape[0]
+        hashes = _u8(hashes).reshape(n, 32)
+        sigs = _u8(sigs).reshape(n, -1) if n else np.zeros((0, 64), dtype=np.uint8)
+        if sigs.shape[1] < 64:
+            raise ValueError("signatures must hold at least r || s (64 bytes)")
+        ok = np.zeros(n, dtype=np.uint8)
+        if n:
+            ensure_device()
+            check(lib().bcosgpu_verify_batch(self.SUITE, _ptr(pubs), _ptr(hashes), _ptr(sigs), sigs.shape[1], n,
+                                             _ptr(ok)))
+        return ok.astype(bool)
 
     def recover(self, hash32: bytes, sig: bytes) -> bytes:
         pubs, ok = self.recover_batch(_u8(hash32, (1, 32)), [bytes(sig)])
@@ -142,6 +182,7 @@ class SignatureCrypto:
 class Secp256k1Crypto(SignatureCrypto):
     """Secp256k1Crypto (Secp256k1Crypto.h:37-72); recover -> wedpr_secp256k1_recover_public_key."""
     SIG_LEN = 65
+    SUITE = _lib.SUITE_SECP256K1
 
     def recover_batch(self, hashes, sigs, want_address=False):
         """hashes uint8[n,32]; sigs uint8[n,65] (or list of bytes; non-65-byte entries fail).
@@ -173,13 +214,7 @@ class Secp256k1Crypto(SignatureCrypto):
 class SM2Crypto(SignatureCrypto):
     """SM2Crypto / FastSM2Crypto: recover = verify against the embedded public key (SM2Crypto.cpp:81-92)."""
     SIG_LEN = 128
-
-    def verify(self, pub: bytes, hash32: bytes, sig: bytes) -> bool:
-        """SM2Crypto::verify (SM2Crypto.cpp:66-79): only sig[0:64] is used, with the given pub."""
-        if len(sig) < 64 or len(pub) != 64:
-            return False
-        _, ok = self.recover_batch(_u8(hash32, (1, 32)), [bytes(sig[:64]) + bytes(pub)])
-        return bool(ok[0])
+    SUITE = _lib.SUITE_SM2
 
     def recover_batch(self, hashes, sigs, want_address=False):
         hashes = _u8(hashes).reshape(-1, 32)

@@ -53,6 +53,24 @@ def merkle_frontier(hasher, width, leaves, levels, work, frontier, stream=None):
                                             _p(frontier), _s(stream)))
 
 
+def merkle_roots_work_size(total_leaves, nblocks, width):
+    return int(lib().bcosgpu_merkle_roots_work_size(total_leaves, nblocks, width))
+
+
+def merkle_roots_batch(hasher, width, leaves, block_off, work, roots, stream=None):
+    """Roots of many blocks' trees (bcosgpu_merkle_roots_batch_dev).  leaves uint8[N,32] (device),
+    block_off: host uint64 numpy array [nblocks+1] of row indices into `leaves`, work: uint8 device
+    tensor >= merkle_roots_work_size bytes, roots uint8[nblocks,32]."""
+    import ctypes
+    import numpy as np
+    _dev(leaves)
+    bo = np.ascontiguousarray(block_off, dtype=np.uint64)
+    nb = bo.size - 1
+    base = leaves[int(bo[0]):] if nb > 0 and int(bo[0]) < leaves.shape[0] else leaves
+    check(lib().bcosgpu_merkle_roots_batch_dev(hasher, width, _p(base), bo.ctypes.data_as(ctypes.c_void_p), nb,
+                                               _p(work), _p(roots), _s(stream)))
+
+
 def secp256k1_recover(hashes, sigs, pub, addr, ok, stream=None):
     """hashes uint8[n,32], sigs uint8[n,65] -> pub uint8[n,64] (or None), addr uint8[n,20] (or None), ok uint8[n]."""
     _dev(hashes)

@@ -95,3 +95,71 @@ def gpu_root_fn(hasher, width):
         return root
 
     return fn
+
+
+class ShardedTxRoot:
+    """The multi-GPU tx root as a preallocated, host-sync-free step (used by bench.py's C4 workload).
+
+    Every rank knows the shard plan, hence every rank's frontier size, so the exchange needs no count
+    records and no device->host read: the rank's level-L nodes are written straight into its fixed-size
+    send buffer, ONE all_gather_into_tensor (RCCL over xGMI on the GPU box, gloo in the CPU tests) moves
+    them, an index_select compacts the concatenated frontier on the device, and the top levels run on
+    the device (bcosgpu_merkle_root_dev).  `frontier_fn(local_leaves, levels, out)` and
+    `root_fn(frontier, root_out)` are injectable so the same exchange logic runs on CPU under gloo.
+    """
+
+    def __init__(self, n, world, rank, width, dev, frontier_fn, root_fn, levels=None, group=None):
+        self.n, self.world, self.rank, self.width, self.group = n, world, rank, width, group
+        self.levels = choose_levels(n, world, width) if levels is None else levels
+        self.plan = shard_plan(n, world, width, self.levels)
+        blk = width ** self.levels
+        self.counts = [math.ceil((hi - lo) / blk) if hi > lo else 0 for lo, hi in self.plan]
+        self.cap = max(max(self.counts), 1)
+        self.send = torch.zeros((self.cap, 32), dtype=torch.uint8, device=dev)
+        self.recv = torch.zeros((world * self.cap, 32), dtype=torch.uint8, device=dev)
+        idx = [r * self.cap + j for r, c in enumerate(self.counts) for j in range(c)]
+        self.index = torch.tensor(idx, dtype=torch.int64, device=dev)
+        self.frontier = torch.empty((len(idx), 32), dtype=torch.uint8, device=dev)
+        self.root = torch.empty(32, dtype=torch.uint8, device=dev)
+        self.frontier_fn, self.root_fn = frontier_fn, root_fn
+
+    @property
+    def local_range(self):
+        return self.plan[self.rank]
+
+    def __call__(self, local_leaves):
+        """local_leaves: this rank's rows [lo, hi) of the leaf vector -> the global root (device tensor)."""
+        m = self.counts[self.rank]
+        if m:
+            if self.levels == 0:
+                self.send[:m].copy_(local_leaves)
+            else:
+                self.frontier_fn(local_leaves, self.levels, self.send[:m])
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+        else:
+            self.recv.copy_(self.send)
+        torch.index_select(self.recv, 0, self.index, out=self.frontier)
+        self.root_fn(self.frontier, self.root)
+        return self.root
+
+
+def gpu_sharded_tx_root(n, world, rank, hasher, width, dev, group=None):
+    """ShardedTxRoot over libbcosgpu.so: frontier and top levels on the GPU."""
+    from . import device
+
+    shard = shard_plan(n, world, width, choose_levels(n, world, width))[rank]
+    work = torch.empty((max(2 * math.ceil(max(shard[1] - shard[0], 1) / width), 1), 32), dtype=torch.uint8,
+                       device=dev)
+    tree = {}
+
+    def frontier_fn(leaves, levels, out):
+        device.merkle_frontier(hasher, width, leaves, levels, work, out)
+
+    def root_fn(frontier, root):
+        m = frontier.shape[0]
+        if m not in tree:
+            tree[m] = torch.empty((max(device.merkle_size(m, width), 1), 32), dtype=torch.uint8, device=dev)
+        device.merkle_root(hasher, width, frontier, tree[m], root)
+
+    return ShardedTxRoot(n, world, rank, width, dev, frontier_fn, root_fn, group=group)

@@ -6,6 +6,11 @@
   Transaction::verify                      bcos-framework/bcos-framework/protocol/Transaction.h:68-82
   TransactionSync::importDownloadedTxs     bcos-txpool/bcos-txpool/sync/TransactionSync.cpp:496-575
   BlockImpl::calculateTransactionRoot      bcos-tars-protocol/bcos-tars-protocol/protocol/BlockImpl.h:111-154
+  bcostars::TransactionReceiptData         bcos-tars-protocol/bcos-tars-protocol/tars/TransactionReceipt.tars:2-23
+  impl_calculate<Hasher>(TransactionReceipt) TarsHashable.h:43-75
+      H(be32(version) || gasUsed || contractAddress || be32(status) || output
+        || for each log: (address || topic_0 || ... || data) || be64(blockNumber))
+  BlockImpl::calculateReceiptRoot          BlockImpl.h:156-183
 """
 import ctypes
 import struct
@@ -38,6 +43,45 @@ class TransactionData:
         return (struct.pack(">i", self.version) + self.chain_id.encode() + self.group_id.encode()
                 + struct.pack(">q", self.block_limit) + self.nonce.encode() + self.to.encode()
                 + bytes(self.input) + self.abi.encode())
+
+
+@dataclass
+class LogEntry:
+    """bcostars::LogEntry (TransactionReceipt.tars:2-6)."""
+    address: str = ""
+    topic: list = None
+    data: bytes = b""
+
+
+@dataclass
+class TransactionReceiptData:
+    """bcostars::TransactionReceiptData (TransactionReceipt.tars:8-16)."""
+    version: int = 0
+    gas_used: str = ""
+    contract_address: str = ""
+    status: int = 0
+    output: bytes = b""
+    log_entries: list = None
+    block_number: int = 0
+
+    def preimage(self) -> bytes:
+        """The bytes impl_calculate<Hasher>(TransactionReceipt) feeds the hasher (TarsHashable.h:54-73)."""
+        parts = [struct.pack(">i", self.version), self.gas_used.encode(), self.contract_address.encode(),
+                 struct.pack(">i", self.status), bytes(self.output)]
+        for log in self.log_entries or []:
+            parts.append(log.address.encode())
+            parts.extend(bytes(t) for t in (log.topic or []))
+            parts.append(bytes(log.data))
+        parts.append(struct.pack(">q", self.block_number))
+        return b"".join(parts)
+
+
+@dataclass
+class TransactionReceipt:
+    """bcostars::TransactionReceipt (TransactionReceipt.tars:18-22); a non-empty data_hash
+    short-circuits the hash (TarsHashable.h:47-51)."""
+    data: TransactionReceiptData
+    data_hash: bytes = b""
 
 
 @dataclass
@@ -82,6 +126,33 @@ def verify_transactions(suite: CryptoSuite, txs):
             txs[i].sender = sender[k].tobytes()
         status[i] = int(st[k])
     return status
+
+
+def _hashes_of(suite: CryptoSuite, items):
+    """impl_calculate over tx / receipt objects: a set dataHash is used as is (TarsHashable.h:20-24,
+    :47-51), the rest are hashed on the GPU in one batch."""
+    out = [bytes(getattr(it, "data_hash", b"") or b"") for it in items]
+    todo = [i for i, h in enumerate(out) if not h]
+    if todo:
+        data, off = pack_messages([items[i].data.preimage() for i in todo])
+        hs = suite.hash_impl.hash_packed(data, off)
+        for k, i in enumerate(todo):
+            out[i] = hs[k].tobytes()
+    return out
+
+
+def calculate_receipt_root(suite: CryptoSuite, receipts) -> bytes:
+    """BlockImpl::calculateReceiptRoot (BlockImpl.h:156-183): width-2 Merkle over the receipt hashes;
+    no receipts -> the zero hash (:159-163)."""
+    if len(receipts) == 0:
+        return bytes(32)
+    return Merkle(suite.hash_impl, 2).root(_hashes_of(suite, receipts))
+
+
+def calculate_roots_batch(suite: CryptoSuite, blocks_of_hashes):
+    """calculateTransactionRoot / calculateReceiptRoot for many blocks at once (one engine call,
+    bcosgpu_merkle_roots_batch); each block is a list of 32-byte hashes, empty -> zero hash."""
+    return Merkle(suite.hash_impl, 2).roots_batch(blocks_of_hashes)
 
 
 def calculate_transaction_root(suite: CryptoSuite, tx_hashes) -> bytes:

@@ -214,6 +214,56 @@ int bcosgpu_merkle_frontier_dev(int hasher, int width, const uint8_t* d_leaves32
     return rc ? hip_err(hipGetLastError(), "merkle frontier launch") : 0;
 }
 
+uint64_t bcosgpu_merkle_roots_work_size(uint64_t total_leaves, size_t nblocks, int width) {
+    if (width < 2 || width > 64) return 0;
+    return merkle_roots_work_bytes(total_leaves, nblocks, width);
+}
+
+static int check_block_off(const uint64_t* block_off, size_t nblocks) {
+    if (!block_off) return set_err(BCOSGPU_E_ARG, "null block offsets");
+    for (size_t b = 0; b < nblocks; ++b)
+        if (block_off[b + 1] < block_off[b] || block_off[b + 1] - block_off[b] > 0xFFFFFFFFull)
+            return set_err(BCOSGPU_E_ARG, "block offsets must be non-decreasing, blocks < 2^32 leaves");
+    return 0;
+}
+
+int bcosgpu_merkle_roots_batch_dev(int hasher, int width, const uint8_t* d_leaves32, const uint64_t* block_off,
+                                   size_t nblocks, uint8_t* d_work, uint8_t* d_roots32, void* stream) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (width < 2 || width > 64) return set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
+    if (nblocks == 0) return 0;
+    if (int rc = check_block_off(block_off, nblocks)) return rc;
+    if (!d_work || !d_roots32 || (block_off[nblocks] > block_off[0] && !d_leaves32))
+        return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_merkle_roots_batch(hasher, width, d_leaves32, block_off, nblocks, d_work, d_roots32,
+                                       as_stream(stream));
+    return rc ? hip_err(hipGetLastError(), "merkle roots launch") : 0;
+}
+
+int bcosgpu_merkle_roots_batch(int hasher, int width, const uint8_t* leaves32, const uint64_t* block_off,
+                               size_t nblocks, uint8_t* roots32) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (width < 2 || width > 64) return set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
+    if (nblocks == 0) return 0;
+    if (int rc = check_block_off(block_off, nblocks)) return rc;
+    const uint64_t total = block_off[nblocks] - block_off[0];
+    if (!roots32 || (total && !leaves32)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    HIP_OK(w->b[0].ensure(total * 32 + 32));
+    HIP_OK(w->b[1].ensure(merkle_roots_work_bytes(total, nblocks, width)));
+    HIP_OK(w->b[2].ensure(nblocks * 32));
+    if (total) HIP_OK(hipMemcpyAsync(w->b[0].p, leaves32, total * 32, hipMemcpyHostToDevice, w->stream));
+    rc = launch_merkle_roots_batch(hasher, width, w->b[0].as<uint8_t>(), block_off, nblocks, w->b[1].as<uint8_t>(),
+                                   w->b[2].as<uint8_t>(), w->stream);
+    if (rc) return hip_err(hipGetLastError(), "merkle roots launch");
+    HIP_OK(hipMemcpyAsync(roots32, w->b[2].p, nblocks * 32, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
 // ------------------------------------------------------------------ signatures
 int bcosgpu_secp256k1_recover_batch_dev(const uint8_t* d_hash32, const uint8_t* d_sig65, size_t n,
                                         uint8_t* d_pub64, uint8_t* d_addr20, uint8_t* d_ok,
@@ -291,6 +341,67 @@ int bcosgpu_sm2_sign_batch_dev(const uint8_t* d_sk32, const uint8_t* d_hash32, s
     if (n && (!d_sk32 || !d_hash32 || !d_sig128 || !d_ok)) return set_err(BCOSGPU_E_ARG, "null pointer");
     int rc = launch_sm2_sign(d_sk32, d_hash32, n, d_sig128, d_ok, as_stream(stream));
     return rc ? set_err(rc, "sm2 sign launch failed") : 0;
+}
+
+// ------------------------------------------------------------------ verify with a known key, ecRecover
+int bcosgpu_verify_batch_dev(int suite, const uint8_t* d_pub64, const uint8_t* d_hash32, const uint8_t* d_sig,
+                             size_t sig_stride, size_t n, uint8_t* d_ok, void* stream) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return set_err(BCOSGPU_E_ARG, "bad suite");
+    if (sig_stride < 64 || sig_stride > 0xFFFFFFFFull) return set_err(BCOSGPU_E_ARG, "signature stride must be >= 64");
+    if (n && (!d_pub64 || !d_hash32 || !d_sig || !d_ok)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_sig_verify(suite, d_pub64, d_hash32, d_sig, static_cast<uint32_t>(sig_stride), n, d_ok,
+                               as_stream(stream));
+    return rc ? set_err(rc, "verify launch failed") : 0;
+}
+
+int bcosgpu_verify_batch(int suite, const uint8_t* pub64, const uint8_t* hash32, const uint8_t* sig,
+                         size_t sig_stride, size_t n, uint8_t* ok) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return set_err(BCOSGPU_E_ARG, "bad suite");
+    if (sig_stride < 64 || sig_stride > 0xFFFFFFFFull) return set_err(BCOSGPU_E_ARG, "signature stride must be >= 64");
+    if (n == 0) return 0;
+    if (!pub64 || !hash32 || !sig || !ok) return set_err(BCOSGPU_E_ARG, "null pointer");
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    HIP_OK(w->b[0].ensure(n * 64));
+    HIP_OK(w->b[1].ensure(n * 32));
+    HIP_OK(w->b[2].ensure(n * sig_stride + 8));
+    HIP_OK(w->b[3].ensure(n));
+    HIP_OK(hipMemcpyAsync(w->b[0].p, pub64, n * 64, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[1].p, hash32, n * 32, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[2].p, sig, n * sig_stride, hipMemcpyHostToDevice, w->stream));
+    rc = launch_sig_verify(suite, w->b[0].as<uint8_t>(), w->b[1].as<uint8_t>(), w->b[2].as<uint8_t>(),
+                           static_cast<uint32_t>(sig_stride), n, w->b[3].as<uint8_t>(), w->stream);
+    if (rc) return set_err(rc, "verify launch failed");
+    HIP_OK(hipMemcpyAsync(ok, w->b[3].p, n, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
+int bcosgpu_ecrecover_batch_dev(const uint8_t* d_in128, size_t n, uint8_t* d_out32, uint8_t* d_ok, void* stream) {
+    if (n && (!d_in128 || !d_out32 || !d_ok)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_ecrecover(d_in128, n, d_out32, d_ok, as_stream(stream));
+    return rc ? set_err(rc, "ecrecover launch failed") : 0;
+}
+
+int bcosgpu_ecrecover_batch(const uint8_t* in128, size_t n, uint8_t* out32, uint8_t* ok) {
+    if (n == 0) return 0;
+    if (!in128 || !out32 || !ok) return set_err(BCOSGPU_E_ARG, "null pointer");
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    HIP_OK(w->b[0].ensure(n * 128));
+    HIP_OK(w->b[1].ensure(n * 32));
+    HIP_OK(w->b[2].ensure(n));
+    HIP_OK(hipMemcpyAsync(w->b[0].p, in128, n * 128, hipMemcpyHostToDevice, w->stream));
+    rc = launch_ecrecover(w->b[0].as<uint8_t>(), n, w->b[1].as<uint8_t>(), w->b[2].as<uint8_t>(), w->stream);
+    if (rc) return set_err(rc, "ecrecover launch failed");
+    HIP_OK(hipMemcpyAsync(out32, w->b[1].p, n * 32, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipMemcpyAsync(ok, w->b[2].p, n, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
 }
 
 // ------------------------------------------------------------------ whole-tx admission

@@ -463,19 +463,8 @@ static int tables(const uint32_t** k1, const uint32_t** sm2) {
 // ------------------------------------------------------------------ secp256k1 recover (one lane)
 // libsecp256k1 secp256k1_ecdsa_recover as wedpr calls it: reject v > 3, r or s not in [1, n-1],
 // (v & 2) with r >= p - n, x not on the curve, Q = infinity.  pub = (x, y) canonical, plain.
-__device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const uint8_t* sig, uint32_t siglen,
-                                                       const uint32_t* tab, fe& px, fe& py) {
-    if (siglen != 65u) return false;
-    ByteReader rd(sig, 65);
-    uint32_t w[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
-    fe r, s;
-    fe_from_be_words(r, w);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
-    fe_from_be_words(s, w);
-    const uint32_t v = rd.word(16) & 0xffu;
+__device__ __forceinline__ bool secp256k1_recover_rsv(const fe& hash_be, const fe& r, const fe& s, uint32_t v,
+                                                      const uint32_t* tab, fe& px, fe& py) {
     bool ok = v <= 3u;
     ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, ParamN1::M);
     fe x;
@@ -532,6 +521,21 @@ __device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const 
     fe_copy(px, A.x);
     fe_copy(py, A.y);
     return ok;
+}
+
+__device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const uint8_t* sig, uint32_t siglen,
+                                                       const uint32_t* tab, fe& px, fe& py) {
+    if (siglen != 65u) return false;
+    ByteReader rd(sig, 65);
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
+    fe r, s;
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
+    fe_from_be_words(s, w);
+    return secp256k1_recover_rsv(hash_be, r, s, rd.word(16) & 0xffu, tab, px, py);
 }
 
 // pub -> right160(Keccak256(pub)) as 5 little-endian memory words
@@ -600,23 +604,8 @@ __device__ __forceinline__ void sm2_e(uint32_t e[8], const uint32_t X[8], const 
 // sm2_do_verify semantics (GB/T 32918.2): pub must be on the curve with coordinates < p,
 // r, s in [1, n-1], t = r + s mod n != 0, accept iff (e + x1) mod n == r for (x1, y1) = sG + tP.
 // The comparison is done projectively (X == (r - e mod n [+ n]) * Z^2), so no inversion.
-__device__ __forceinline__ bool sm2_verify_lane(const fe& hash_be, const uint8_t* sig, uint32_t siglen,
-                                                const uint32_t* tab, fe& px, fe& py) {
-    if (siglen != 128u) return false;
-    ByteReader rd(sig, 128);
-    uint32_t w[8], X[8], Y[8];
-    fe r, s;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
-    fe_from_be_words(r, w);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
-    fe_from_be_words(s, w);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        X[i] = bswap32(rd.word(16 + i));
-        Y[i] = bswap32(rd.word(24 + i));
-    }
+__device__ __forceinline__ bool sm2_verify_rs(const fe& hash_be, const fe& r, const fe& s, const uint32_t X[8],
+                                              const uint32_t Y[8], const uint32_t* tab, fe& px, fe& py) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         px.v[i] = X[7 - i];
@@ -657,6 +646,99 @@ __device__ __forceinline__ bool sm2_verify_lane(const fe& hash_be, const uint8_t
         FieldP2::from_plain(cm, c2);
         FieldP2::mul(rhs, cm, z2);
         match = match || FieldP2::eq(rhs, Q.X);
+    }
+    return ok && match;
+}
+
+__device__ __forceinline__ bool sm2_verify_lane(const fe& hash_be, const uint8_t* sig, uint32_t siglen,
+                                                const uint32_t* tab, fe& px, fe& py) {
+    if (siglen != 128u) return false;
+    ByteReader rd(sig, 128);
+    uint32_t w[8], X[8], Y[8];
+    fe r, s;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
+    fe_from_be_words(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        X[i] = bswap32(rd.word(16 + i));
+        Y[i] = bswap32(rd.word(24 + i));
+    }
+    return sm2_verify_rs(hash_be, r, s, X, Y, tab, px, py);
+}
+
+// ------------------------------------------------------------------ secp256k1 verify (known key)
+// libsecp256k1 secp256k1_ecdsa_verify as wedpr_secp256k1_verify calls it (Secp256k1Crypto.cpp:51-63):
+// pub (x, y) < p on the curve, r, s in [1, n-1], low-S (s <= n/2), e = hash mod n,
+// (x1, .) = (e/s) G + (r/s) P, accept iff x1 mod n == r.  Only bytes 0..63 of the signature (r || s)
+// are read.  The comparison is projective (X == r Z^2, or (r + n) Z^2 when r + n < p): no inversion.
+__device__ __constant__ static const uint32_t kN1HalfPlus[8] = {0x681b20a1u, 0xdfe92f46u, 0x57a4501du, 0x5d576e73u,
+                                                            0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu};
+__device__ __forceinline__ bool secp256k1_verify_lane(const fe& hash_be, const uint8_t* sig, const uint8_t* pub,
+                                                      const uint32_t* tab) {
+    ByteReader rs(sig, 64), rp(pub, 64);
+    uint32_t w[8];
+    fe r, s, x, y;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rs.word(i);
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rs.word(8 + i);
+    fe_from_be_words(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rp.word(i);
+    fe_from_be_words(x, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rp.word(8 + i);
+    fe_from_be_words(y, w);
+    bool ok = fe_lt_k(x, FieldK1::P) && fe_lt_k(y, FieldK1::P);
+    {
+        fe l, rr, t, seven;
+        FieldK1::sqr(l, y);
+        FieldK1::sqr(t, x);
+        FieldK1::mul(rr, t, x);
+        fe_zero(seven);
+        seven.v[0] = 7;
+        FieldK1::add(rr, rr, seven);
+        ok = ok && FieldK1::eq(l, rr);
+    }
+    ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, kN1HalfPlus);
+    fe e;
+    fe_copy(e, hash_be);
+    reduce_once(e, ParamN1::M);
+    fe ss = s;
+    if (!ok) {  // keep the arithmetic well-defined on rejected lanes
+        fe_zero(ss);
+        ss.v[0] = 1;
+    }
+    fe sm, sinv, u1, u2;
+    FieldN1::from_plain(sm, ss);
+    FieldInv<FieldN1>::inv(sinv, sm);
+    FieldN1::mul(u1, e, sinv);
+    FieldN1::mul(u2, r, sinv);
+    Aff P;
+    fe_copy(P.x, x);
+    fe_copy(P.y, y);
+    if (!ok) {  // a valid point for the rejected lanes
+        fe_set(P.x, kK1Gx);
+        fe_set(P.y, kK1Gy);
+    }
+    Jac QG, QP, Q;
+    glv_mul_k1(QP, u2, P);
+    comb_mul<CurveK1>(QG, u1, tab);
+    CurveK1::add(Q, QG, QP);
+    ok = ok && !Q.inf;
+    fe z2, rhs, r2;
+    FieldK1::sqr(z2, Q.Z);
+    FieldK1::mul(rhs, r, z2);
+    bool match = FieldK1::eq(rhs, Q.X);
+    const uint32_t carry = fe_add_k(r2, r, ParamN1::M);
+    if (carry == 0u && fe_lt_k(r2, FieldK1::P)) {
+        FieldK1::mul(rhs, r2, z2);
+        match = match || FieldK1::eq(rhs, Q.X);
     }
     return ok && match;
 }
@@ -706,6 +788,69 @@ __global__ __launch_bounds__(256) void sm2_verify_kernel(const uint8_t* __restri
 #pragma unroll
         for (int k = 0; k < 5; ++k) o[k] = a[k];
     }
+    okout[i] = ok ? 1 : 0;
+}
+
+// SignatureCrypto::verify(pub, hash, sig) for a batch (sealer signatures: BlockValidator.cpp:141-182,
+// PBFTCacheProcessor.cpp:795-821).  SM2: SM2Crypto::verify reads the first 64 signature bytes (r || s)
+// and verifies against the GIVEN key (SM2Crypto.cpp:66-79); secp256k1: secp256k1_verify_lane.
+template <int SUITE>
+__global__ __launch_bounds__(256) void sig_verify_kernel(const uint8_t* __restrict__ pub,
+                                                         const uint8_t* __restrict__ hash,
+                                                         const uint8_t* __restrict__ sig, uint32_t stride,
+                                                         uint64_t n, const uint32_t* __restrict__ tab,
+                                                         uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe h;
+    load_be256_aligned(h, hash + 32 * i);
+    const uint8_t* sg = sig + static_cast<uint64_t>(stride) * i;
+    bool ok;
+    if (SUITE == BCOSGPU_SUITE_SM2) {
+        ByteReader rs(sg, 64), rp(pub + 64 * i, 64);
+        uint32_t w[8], X[8], Y[8];
+        fe r, s, x, y;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rs.word(k);
+        fe_from_be_words(r, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rs.word(8 + k);
+        fe_from_be_words(s, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            X[k] = bswap32(rp.word(k));
+            Y[k] = bswap32(rp.word(8 + k));
+        }
+        ok = sm2_verify_rs(h, r, s, X, Y, tab, x, y);
+    } else {
+        ok = secp256k1_verify_lane(h, sg, pub + 64 * i, tab);
+    }
+    okout[i] = ok ? 1 : 0;
+}
+
+// EVM ecRecover precompile (bcos-executor/src/vm/Precompiled.cpp:443-482) for a batch: input =
+// hash(32) || v(32) || r(32) || s(32); recid = (byte)(in[63] - 27) (the other 31 bytes of v are not
+// read); on success out = 12 zero bytes || right160(Keccak256(pub)), ok = 1; on failure the
+// precompile returns an empty output: out = zeros, ok = 0.
+__global__ __launch_bounds__(256) void ecrecover_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                        const uint32_t* __restrict__ tab,
+                                                        uint8_t* __restrict__ out, uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* p = in + 128 * i;
+    fe h, r, s, x, y;
+    load_be256_aligned(h, p);
+    load_be256_aligned(r, p + 64);
+    load_be256_aligned(s, p + 96);
+    const uint32_t v = (reinterpret_cast<const uint32_t*>(p)[15] >> 24) - 27u;
+    const bool ok = secp256k1_recover_rsv(h, r, s, v & 0xffu, tab, x, y);
+    uint32_t a[5] = {0, 0, 0, 0, 0};
+    if (ok) keccak_address(a, x, y);
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + 32 * i);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o[k] = 0u;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[3 + k] = a[k];
     okout[i] = ok ? 1 : 0;
 }
 
@@ -1198,6 +1343,30 @@ int launch_sm2_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint
     int rc = tables(&k1, &sm2);
     if (rc) return rc;
     hipLaunchKernelGGL(sm2_sign_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_sk, d_hash, n, sm2, d_sig, d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
+                      uint64_t n, uint8_t* d_ok, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int rc = tables(&k1, &sm2);
+    if (rc) return rc;
+    if (suite == BCOSGPU_SUITE_SM2)
+        hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SM2>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash, d_sig,
+                           stride, n, sm2, d_ok);
+    else
+        hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SECP256K1>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash,
+                           d_sig, stride, n, k1, d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_ecrecover(const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint8_t* d_ok, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int rc = tables(&k1, &sm2);
+    if (rc) return rc;
+    hipLaunchKernelGGL(ecrecover_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_in, n, k1, d_out, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 

@@ -14,6 +14,9 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
                   uint8_t* d_root, hipStream_t st);
 int launch_merkle_levels(int hasher, int width, const uint8_t* d_in, uint64_t n, int levels, uint8_t* d_work,
                          uint8_t* d_out, hipStream_t st);
+uint64_t merkle_roots_work_bytes(uint64_t total_leaves, uint64_t nblocks, int width);
+int launch_merkle_roots_batch(int hasher, int width, const uint8_t* d_leaves, const uint64_t* block_off,
+                              uint64_t nblocks, uint8_t* d_work, uint8_t* d_roots, hipStream_t st);
 int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* d_scratch,
                       uint8_t* d_root, hipStream_t st);
 
@@ -28,6 +31,9 @@ int launch_secp256k1_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n
                           uint8_t* d_sig, uint8_t* d_ok, hipStream_t st);
 int launch_sm2_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint8_t* d_sig,
                     uint8_t* d_ok, hipStream_t st);
+int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
+                      uint64_t n, uint8_t* d_ok, hipStream_t st);
+int launch_ecrecover(const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint8_t* d_ok, hipStream_t st);
 int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
                      const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n,
                      uint8_t* d_txhash, uint8_t* d_sender, uint8_t* d_status, hipStream_t st);

@@ -160,6 +160,100 @@ int launch_merkle_levels(int hasher, int width, const uint8_t* d_in, uint64_t n,
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
+// ------------------------------------------------------------------ many blocks' roots at once
+// BlockImpl::calculateTransactionRoot / calculateReceiptRoot (BlockImpl.h:111-183) for a batch of
+// blocks (sync catch-up, PBFT replay): every level of up to kSegBlocks independent trees is ONE
+// launch, one output node per lane.  A block whose tree is already a single node passes it through
+// (so all trees end on the same launch, and the last launch writes the roots in place); an empty
+// block yields the zero hash (BlockImpl.h:114-119).
+static constexpr int kSegBlocks = 64;
+struct SegLevel {
+    uint64_t in_off[kSegBlocks];       // first input node of block b, in 32-byte entries
+    uint32_t n_in[kSegBlocks];         // input nodes of block b at this level (0 = empty block)
+    uint32_t out_off[kSegBlocks + 1];  // prefix of output nodes per block
+    uint32_t nb;
+};
+
+template <int H, int W>
+__global__ __launch_bounds__(256) void merkle_seg_level_kernel(const uint8_t* __restrict__ in, int w,
+                                                               uint8_t* __restrict__ out, const SegLevel t) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= t.out_off[t.nb]) return;
+    int lo = 0, hi = static_cast<int>(t.nb) - 1;  // last b with out_off[b] <= i
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (t.out_off[mid] <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    const uint32_t j = i - t.out_off[lo], nin = t.n_in[lo];
+    uint32_t* dst = reinterpret_cast<uint32_t*>(out + 32ull * i);
+    if (nin <= 1u) {  // empty block -> zero hash; finished tree -> pass the root through
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(in + 32ull * t.in_off[lo]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dst[k] = nin ? src[k] : 0u;
+        return;
+    }
+    const uint32_t width = W ? W : static_cast<uint32_t>(w);
+    const uint32_t first = j * width;
+    const uint32_t cnt = (nin - first) < width ? (nin - first) : width;
+    const uint32_t len = cnt * 32u;
+    AlignedReader rd(in + 32ull * (t.in_off[lo] + first), len);
+    uint32_t d[8];
+    if (H == KECCAK256) keccak256_msg(rd, len, d);
+    else sm3_msg(rd, len, d);
+    store_digest(H, out + 32ull * i, d);
+}
+
+uint64_t merkle_roots_work_bytes(uint64_t total_leaves, uint64_t nblocks, int width) {
+    return 64ull * ((total_leaves + width - 1) / width + nblocks);
+}
+
+int launch_merkle_roots_batch(int hasher, int width, const uint8_t* d_leaves, const uint64_t* block_off,
+                              uint64_t nblocks, uint8_t* d_work, uint8_t* d_roots, hipStream_t st) {
+    if (width < 2 || width > 64) return BCOSGPU_E_ARG;
+    if (nblocks == 0) return 0;
+    const uint64_t total = block_off[nblocks] - block_off[0];
+    const uint64_t half = 32ull * ((total + width - 1) / width + nblocks);  // ping-pong halves
+    for (uint64_t c0 = 0; c0 < nblocks; c0 += kSegBlocks) {
+        const uint32_t nb = static_cast<uint32_t>(nblocks - c0 < kSegBlocks ? nblocks - c0 : kSegBlocks);
+        uint64_t cnt[kSegBlocks];
+        int L = 1;
+        for (uint32_t b = 0; b < nb; ++b) {
+            cnt[b] = block_off[c0 + b + 1] - block_off[c0 + b];
+            if (cnt[b] > 0xFFFFFFFFull) return BCOSGPU_E_ARG;
+            int l = 0;
+            for (uint64_t m = cnt[b]; m > 1; m = (m + width - 1) / width) ++l;
+            if (l > L) L = l;
+        }
+        const uint8_t* in = d_leaves;
+        SegLevel t{};
+        t.nb = nb;
+        for (uint32_t b = 0; b < nb; ++b) t.in_off[b] = block_off[c0 + b] - block_off[0];
+        for (int l = 0; l < L; ++l) {
+            uint32_t o = 0;
+            for (uint32_t b = 0; b < nb; ++b) {
+                t.n_in[b] = static_cast<uint32_t>(cnt[b]);
+                t.out_off[b] = o;
+                cnt[b] = cnt[b] <= 1 ? 1 : (cnt[b] + width - 1) / width;
+                o += static_cast<uint32_t>(cnt[b]);
+            }
+            t.out_off[nb] = o;
+            uint8_t* out = (l + 1 == L) ? d_roots + 32ull * c0 : d_work + ((l & 1) ? half : 0);
+            dim3 g(grid_for(o, 256)), blk(256);
+#define SEG(HH, WW) hipLaunchKernelGGL((merkle_seg_level_kernel<HH, WW>), g, blk, 0, st, in, width, out, t)
+            if (hasher == SM3) {
+                if (width == 2) SEG(SM3, 2); else if (width == 16) SEG(SM3, 16); else SEG(SM3, 0);
+            } else {
+                if (width == 2) SEG(KECCAK256, 2); else if (width == 16) SEG(KECCAK256, 16); else SEG(KECCAK256, 0);
+            }
+#undef SEG
+            in = out;
+            for (uint32_t b = 0; b < nb; ++b) t.in_off[b] = t.out_off[b];
+        }
+    }
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
 int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* d_scratch,
                       uint8_t* d_root, hipStream_t st) {
     // d_scratch: >= 32 * (ceil(n/16) + ceil(n/256) + ...) bytes; levels ping into it

@@ -1,12 +1,17 @@
-# Runs the GPU test suite and the rocprofv3 passes (kernel trace + separate PMC passes) on the MI355X box.
+# rocprofv3 passes for one bench workload on the MI355X box: kernel trace + stats, then separate
+# --pmc passes (FETCH_SIZE and WRITE_SIZE cannot share a pass), each under its own time limit.
+# usage: bash fisco-bcos_amd/tools/gpu_profile.sh <workload> <steps> <limit_s>
+# writes gpurun_out/prof/<workload>/{trace,fetch,write,sq}/ and gpurun_out/prof/<workload>.log
 set -o pipefail
-mkdir -p gpurun_out/prof
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_all.log 2>&1; echo "pytest rc=$?" >> gpurun_out/pytest_all.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o r01 -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/prof_trace.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/fetch -o r01 -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof_fetch.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/write -o r01 -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof_write.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d gpurun_out/prof/sq -o r01 -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/prof_sq.log 2>&1
-echo "prof rc=$?"
-tail -3 gpurun_out/pytest_all.log
-find gpurun_out/prof -name "*.csv" | head -20
+WL=${1:-c2}; STEPS=${2:-10}; LIM=${3:-180}
+OUT=gpurun_out/prof/$WL
+mkdir -p $OUT
+export TMPDIR=/tmp
+B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --no-cpu-baseline --no-merkle"
+timeout -k 10 $LIM rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 && \
+timeout -s KILL $LIM rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B > $OUT/fetch.log 2>&1 && \
+timeout -s KILL $LIM rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B > $OUT/write.log 2>&1 && \
+timeout -s KILL $LIM rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS --output-format csv -d $OUT/sq -o run -- $B > $OUT/sq.log 2>&1
+rc=$?
+echo "profile $WL rc=$rc"
+exit $rc

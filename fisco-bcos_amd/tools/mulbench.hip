@@ -1,0 +1,135 @@
+// mulbench.hip -- latency vs throughput of the 256-bit field arithmetic on gfx950, measured in
+// shader-clock cycles per operation (s_memtime) with 1 and 2 waves per SIMD.  Answers: is a lone
+// wave (the C2 / small-batch regime) issue-bound or dependency-latency-bound in FieldK1::mul?
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include "../csrc/fe.h"
+#include "../csrc/ec.h"
+
+using namespace bcosgpu;
+#define ITERS 2000
+
+__device__ __forceinline__ void seed_fe(fe& x, uint32_t s) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x.v[i] = s * 2654435761u + i * 40503u + 1u;
+    x.v[7] &= 0x7fffffffu;
+}
+
+template <int CHAINS>
+__global__ __launch_bounds__(256) void k_mul(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    fe x[CHAINS], y;
+    seed_fe(y, s + 99);
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) seed_fe(x[c], s + threadIdx.x + c);
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) FieldK1::mul(x[c], x[c], y);
+    }
+    const uint64_t t1 = clock64();
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) r ^= x[c].v[0] ^ x[c].v[7];
+    if (r == 0x12345678u) out[0] = r;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+template <int CHAINS>
+__global__ __launch_bounds__(256) void k_sqr(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    fe x[CHAINS];
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) seed_fe(x[c], s + threadIdx.x + c);
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) FieldK1::sqr(x[c], x[c]);
+    }
+    const uint64_t t1 = clock64();
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) r ^= x[c].v[0] ^ x[c].v[7];
+    if (r == 0x12345678u) out[0] = r;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+__global__ __launch_bounds__(256) void k_dbl(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    Jac P;
+    seed_fe(P.X, s + threadIdx.x);
+    seed_fe(P.Y, s + threadIdx.x + 7);
+    seed_fe(P.Z, s + threadIdx.x + 9);
+    P.inf = false;
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS / 8; ++it) CurveK1::dbl(P, P);
+    const uint64_t t1 = clock64();
+    if ((P.X.v[0] ^ P.Y.v[3]) == 0x12345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+template <int CHAINS>
+__global__ __launch_bounds__(256) void k_madchain(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    uint64_t acc[CHAINS];
+    uint32_t c2[CHAINS];
+    const uint32_t a = s * 7u + threadIdx.x, b = s ^ 0x9e3779b9u;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) { acc[c] = c; c2[c] = 0; }
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS * 8; ++it) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) BG_MADC(acc[c], c2[c], a, b);
+    }
+    const uint64_t t1 = clock64();
+    uint64_t r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) r ^= acc[c] ^ c2[c];
+    if (r == 0x12345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+template <class K>
+static void run(const char* name, K kern, int waves_per_simd, double ops_per_iter, int iters, uint64_t* d_cyc, uint32_t* d_out,
+                bool last) {
+    const int blocks = 256 * waves_per_simd;  // 4 waves per block, 256 CUs
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d_cyc, d_out, 1u);  // warm-up
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d_cyc, d_out, 2u);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    uint64_t* h = new uint64_t[blocks];
+    hipMemcpy(h, d_cyc, blocks * 8, hipMemcpyDeviceToHost);
+    double avg = 0;
+    for (int i = 0; i < blocks; ++i) avg += h[i];
+    avg /= blocks;
+    delete[] h;
+    const double per_op = avg / (iters * ops_per_iter);
+    const double lane_ops = double(blocks) * 256 * iters * ops_per_iter / (ms * 1e-3);
+    printf("  \"%s_occ%d\": {\"cycles_per_op_per_wave\": %.1f, \"lane_ops_per_s\": %.4e, \"ms\": %.3f}%s\n", name,
+           waves_per_simd, per_op, lane_ops, ms, last ? "" : ",");
+}
+
+int main() {
+    uint64_t* d_cyc;
+    uint32_t* d_out;
+    hipMalloc(&d_cyc, 4096 * 8);
+    hipMalloc(&d_out, 64);
+    hipDeviceProp_t p;
+    hipGetDeviceProperties(&p, 0);
+    printf("{\"device\": \"%s\", \"clock_khz\": %d,\n", p.gcnArchName, p.clockRate);
+    for (int occ = 1; occ <= 2; ++occ) {
+        run("madc_chain1", k_madchain<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
+        run("madc_chain2", k_madchain<2>, occ, 2, ITERS * 8, d_cyc, d_out, false);
+        run("madc_chain4", k_madchain<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
+        run("fk1_mul_chain1", k_mul<1>, occ, 1, ITERS, d_cyc, d_out, false);
+        run("fk1_mul_chain2", k_mul<2>, occ, 2, ITERS, d_cyc, d_out, false);
+        run("fk1_sqr_chain1", k_sqr<1>, occ, 1, ITERS, d_cyc, d_out, false);
+        run("fk1_sqr_chain2", k_sqr<2>, occ, 2, ITERS, d_cyc, d_out, false);
+        run("k1_dbl", k_dbl, occ, 1, ITERS / 8, d_cyc, d_out, occ == 2);
+    }
+    printf("}\n");
+    return 0;
+}

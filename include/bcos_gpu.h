@@ -95,6 +95,18 @@ int bcosgpu_merkle_root_dev(int hasher, int width, const uint8_t* d_leaves32, si
 int bcosgpu_merkle_frontier_dev(int hasher, int width, const uint8_t* d_leaves32, size_t n, int levels,
                                 uint8_t* d_work, uint8_t* d_frontier, void* stream);
 
+/* Many blocks' roots in one call: BlockImpl::calculateTransactionRoot / calculateReceiptRoot
+ * (bcos-tars-protocol/.../protocol/BlockImpl.h:111-183) for a batch of blocks, e.g. PBFT/sync replay.
+ * Block b's leaves are entries [block_off[b], block_off[b+1]) of leaves32 (block_off: HOST array of
+ * nblocks + 1 non-decreasing entry indices; leaves32 points at entry block_off[0]).  roots32[b] =
+ * Merkle<H,width> root of block b; an empty block yields the zero hash (BlockImpl.h:114-119).
+ * d_work >= bcosgpu_merkle_roots_work_size(block_off[nblocks] - block_off[0], nblocks, width) bytes. */
+uint64_t bcosgpu_merkle_roots_work_size(uint64_t total_leaves, size_t nblocks, int width);
+int bcosgpu_merkle_roots_batch(int hasher, int width, const uint8_t* leaves32, const uint64_t* block_off,
+                               size_t nblocks, uint8_t* roots32);
+int bcosgpu_merkle_roots_batch_dev(int hasher, int width, const uint8_t* d_leaves32, const uint64_t* block_off,
+                                   size_t nblocks, uint8_t* d_work, uint8_t* d_roots32, void* stream);
+
 /* ---------------------------------------------------------------- signatures (SignatureCrypto, batched) */
 /* secp256k1 public-key recovery (Secp256k1Crypto::recover, Secp256k1Crypto.h:57-60).
  * pub64 / addr20 nullable; addr20 = right160(Keccak256(pub)) (calculateAddress, KeyPair.h:30-33). */
@@ -117,6 +129,26 @@ int bcosgpu_secp256k1_sign_batch_dev(const uint8_t* d_sk32, const uint8_t* d_has
                                      uint8_t* d_pub64, uint8_t* d_sig65, uint8_t* d_ok, void* stream);
 int bcosgpu_sm2_sign_batch_dev(const uint8_t* d_sk32, const uint8_t* d_hash32, size_t n,
                                uint8_t* d_sig128, uint8_t* d_ok, void* stream);
+
+/* SignatureCrypto::verify(pub, hash, sig) with a KNOWN key (Signature.h:40-46), batched -- the sealer
+ * signature checks BlockValidator::checkSignatureList (bcos-pbft/.../engine/BlockValidator.cpp:141-182)
+ * and PBFTCacheProcessor::checkPrecommitWeight (.../cache/PBFTCacheProcessor.cpp:795-821).
+ *   secp256k1: secp256k1Verify -> wedpr_secp256k1_verify (Secp256k1Crypto.cpp:51-63), libsecp256k1
+ *              secp256k1_ecdsa_verify semantics (low-S required, pub on the curve);
+ *   SM2:       SM2Crypto::verify (SM2Crypto.cpp:66-79) -> sm2_do_verify against the given key.
+ * Item i: pub64 + 64 i, hash32 + 32 i, signature sig + sig_stride i (stride >= 64: 65 for r||s||v,
+ * 128 for r||s||pub; only bytes 0..63 = r||s are read).  ok[i] = 1 iff the signature verifies. */
+int bcosgpu_verify_batch(int suite, const uint8_t* pub64, const uint8_t* hash32, const uint8_t* sig,
+                         size_t sig_stride, size_t n, uint8_t* ok);
+int bcosgpu_verify_batch_dev(int suite, const uint8_t* d_pub64, const uint8_t* d_hash32, const uint8_t* d_sig,
+                             size_t sig_stride, size_t n, uint8_t* d_ok, void* stream);
+
+/* EVM ecRecover precompile (bcos-executor/src/vm/Precompiled.cpp:443-482), batched.  Input i =
+ * in128 + 128 i = hash(32) || v(32) || r(32) || s(32); the recovery id is (uint8_t)(in[63] - 27).
+ * On success out32 = 12 zero bytes || right160(Keccak256(pub)) and ok = 1; on failure the precompile
+ * returns an empty output: ok = 0 (out32 zero).  d_in128 must be 16-byte aligned. */
+int bcosgpu_ecrecover_batch(const uint8_t* in128, size_t n, uint8_t* out32, uint8_t* ok);
+int bcosgpu_ecrecover_batch_dev(const uint8_t* d_in128, size_t n, uint8_t* d_out32, uint8_t* d_ok, void* stream);
 
 /* ---------------------------------------------------------------- whole-tx admission (Transaction::verify, batched) */
 /* Transaction::verify (bcos-framework/.../protocol/Transaction.h:68-82) for n transactions:

@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "bcos_gpu.h"
@@ -88,6 +89,18 @@ public:
                        uint8_t* ok) const {
         check(bcosgpu_secp256k1_recover_batch(hashes, sigs, n, pubs, addrs, ok));
     }
+    /* Secp256k1Crypto::verify -> secp256k1Verify (Secp256k1Crypto.cpp:51-63): r || s = sig[0:64] */
+    bool verify(const uint8_t pub[64], const HashType& hash, const uint8_t* sig, size_t sig_len) const {
+        if (sig_len < 64) return false;
+        uint8_t ok = 0;
+        check(bcosgpu_verify_batch(BCOSGPU_SUITE_SECP256K1, pub, hash.data(), sig, 64, 1, &ok));
+        return ok != 0;
+    }
+    /* batch verify with known keys (sealer signatures): item i = pubs + 64 i, hashes + 32 i, sigs + stride i */
+    void verify_batch(const uint8_t* pubs, const uint8_t* hashes, const uint8_t* sigs, size_t stride, size_t n,
+                      uint8_t* ok) const {
+        check(bcosgpu_verify_batch(BCOSGPU_SUITE_SECP256K1, pubs, hashes, sigs, stride, n, ok));
+    }
 };
 
 class GpuSM2Crypto {
@@ -96,10 +109,13 @@ public:
     /* SM2Crypto::verify (SM2Crypto.cpp:66-79): only sig[0:64] is used */
     bool verify(const uint8_t pub[64], const HashType& hash, const uint8_t* sig, size_t sig_len) const {
         if (sig_len < SIGNATURE_LEN) return false;
-        uint8_t s[128], ok = 0;
-        for (int i = 0; i < 64; ++i) { s[i] = sig[i]; s[64 + i] = pub[i]; }
-        check(bcosgpu_sm2_verify_batch(hash.data(), s, 1, nullptr, &ok));
+        uint8_t ok = 0;
+        check(bcosgpu_verify_batch(BCOSGPU_SUITE_SM2, pub, hash.data(), sig, SIGNATURE_LEN, 1, &ok));
         return ok != 0;
+    }
+    void verify_batch(const uint8_t* pubs, const uint8_t* hashes, const uint8_t* sigs, size_t stride, size_t n,
+                      uint8_t* ok) const {
+        check(bcosgpu_verify_batch(BCOSGPU_SUITE_SM2, pubs, hashes, sigs, stride, n, ok));
     }
     /* SM2Crypto::recover (SM2Crypto.cpp:81-92): verify with the embedded key, return it */
     bytes recover(const HashType& hash, const uint8_t* sig, size_t sig_len) const {
@@ -143,6 +159,35 @@ template <int HASHER>
 inline HashType calculateTransactionRoot(const std::vector<HashType>& txHashes) {
     if (txHashes.empty()) return HashType{};
     return GpuMerkle<HASHER, 2>().root(txHashes);
+}
+
+/* calculateTransactionRoot / calculateReceiptRoot of many blocks in one engine call; an empty block
+ * gives the zero hash (BlockImpl.h:114-119, :159-163). */
+template <int HASHER>
+inline std::vector<HashType> calculateRoots(const std::vector<std::vector<HashType>>& blocks) {
+    std::vector<uint64_t> off(blocks.size() + 1, 0);
+    std::vector<HashType> leaves;
+    for (size_t b = 0; b < blocks.size(); ++b) {
+        leaves.insert(leaves.end(), blocks[b].begin(), blocks[b].end());
+        off[b + 1] = leaves.size();
+    }
+    std::vector<HashType> roots(blocks.size());
+    if (blocks.empty()) return roots;
+    static const HashType zero{};
+    check(bcosgpu_merkle_roots_batch(HASHER, 2, leaves.empty() ? zero.data() : leaves[0].data(), off.data(),
+                                     blocks.size(), roots[0].data()));
+    return roots;
+}
+
+/* EVM ecRecover precompile (bcos-executor/src/vm/Precompiled.cpp:443-482): {true, 32-byte output}
+ * on success, {true, {}} on failure; `in` is read as 128 zero-padded bytes. */
+inline std::pair<bool, bytes> ecRecover(const uint8_t* in, size_t len) {
+    alignas(16) uint8_t buf[128] = {0};
+    for (size_t i = 0; i < len && i < 128; ++i) buf[i] = in[i];
+    uint8_t out[32], ok = 0;
+    check(bcosgpu_ecrecover_batch(buf, 1, out, &ok));
+    if (!ok) return {true, bytes()};
+    return {true, bytes(out, out + 32)};
 }
 
 }  // namespace bcosgpu

@@ -161,3 +161,35 @@ def sm2_verify_batch(hashes, sigs, nthreads=1):
     ok = np.zeros(n, dtype=np.uint8)
     lib().oracle_sm2_verify_batch(_p(hashes), _p(sigs), n, _p(ok), nthreads)
     return ok.astype(bool)
+
+
+def ecrecover(data: bytes):
+    """EVM ecRecover precompile restated from bcos-executor/src/vm/Precompiled.cpp:443-482:
+    rsv = r || s || (byte)(in[63] - 27); success -> 12 zero bytes || right160(keccak256(pub)),
+    failure -> b"" (the precompile's empty output).  Input is read as 128 zero-padded bytes."""
+    d = bytes(data)[:128].ljust(128, b"\0")
+    rsv = d[64:128] + bytes([(d[63] - 27) & 0xFF])
+    pub = secp256k1_recover(d[0:32], rsv)
+    if pub is None:
+        return b""
+    return bytes(12) + keccak256(pub)[12:]
+
+
+def receipt_preimage(version, gas_used, contract_address, status, output, logs, block_number):
+    """impl_calculate<Hasher>(bcostars::TransactionReceipt) field order, restated from
+    bcos-tars-protocol/bcos-tars-protocol/impl/TarsHashable.h:54-73: be32(version), gasUsed,
+    contractAddress, be32(status), output, per log (address, topics..., data), be64(blockNumber).
+    logs: list of (address: str, topics: list[bytes], data: bytes)."""
+    out = bytearray()
+    out += (version & 0xFFFFFFFF).to_bytes(4, "big")
+    out += gas_used.encode()
+    out += contract_address.encode()
+    out += (status & 0xFFFFFFFF).to_bytes(4, "big")
+    out += bytes(output)
+    for address, topics, data in logs:
+        out += address.encode()
+        for t in topics:
+            out += bytes(t)
+        out += bytes(data)
+    out += (block_number & 0xFFFFFFFFFFFFFFFF).to_bytes(8, "big")
+    return bytes(out)

@@ -44,6 +44,20 @@ int main() {
     GpuSecp256k1Crypto secp;
     bytes pub = secp.recover(mh, sig.data(), sig.size());
     CHECK(hex(right160(k.hash(pub)).data(), 20) == "ceaccac640adf55b2028469bd36ba501f28b699d");
+    CHECK(secp.verify(pub.data(), mh, sig.data(), sig.size()));  // Secp256k1Crypto::verify, known key
+    {   // EVM ecRecover precompile input hash || v=27 || r || s (EVMPrecompiledTest.cpp:58-72)
+        bytes in(128, 0);
+        std::memcpy(in.data(), hb.data(), 32);
+        in[63] = 27;
+        std::memcpy(in.data() + 64, hb.data(), 32);
+        std::memcpy(in.data() + 96, s.data(), 32);
+        auto r = ecRecover(in.data(), in.size());
+        CHECK(r.first && r.second.size() == 32);
+        CHECK(hex(r.second.data(), 32) == "000000000000000000000000ceaccac640adf55b2028469bd36ba501f28b699d");
+        in[63] = 29;
+        r = ecRecover(in.data(), in.size());
+        CHECK(r.first && r.second.empty());
+    }
     sig[64] = 4;  // SignatureTest.cpp:156-162
     bool threw = false;
     try { secp.recover(mh, sig.data(), sig.size()); } catch (const InvalidSignature&) { threw = true; }
@@ -68,6 +82,11 @@ int main() {
     threw = false;
     try { GpuMerkle<BCOSGPU_SM3, 16>().generateMerkle({}, out); } catch (const std::invalid_argument&) { threw = true; }
     CHECK(threw);
+    // calculateTransactionRoot over a batch of blocks: Keccak width 2, n = 17 and an empty block
+    auto roots = calculateRoots<BCOSGPU_KECCAK256>({leaves, {}});
+    CHECK(roots.size() == 2);
+    CHECK(hex(roots[0].data(), 32) == "741f553a7d060d82679d4dd31c12fc647d3871226808312d8807ace6d4ac5b50");
+    CHECK(roots[1] == HashType{});
     printf(fails ? "adapter_test: %d failures\n" : "adapter_test: ok\n", fails);
     return fails ? 1 : 0;
 }

@@ -42,3 +42,27 @@ def test_tx_preimage_layout():
     assert p[:4] == b"\x00\x00\x00\x01" and p[4:16] == b"chain0group0"
     assert p[16:24] == (500).to_bytes(8, "big") and p[24:27] == b"123"
     assert p[27:67] == b"ab" * 20 and p[67:] == b"\x01\x02"
+
+
+def test_receipt_preimage_matches_oracle_restatement(oracle):
+    """TarsHashable.h:43-75 field order, host mirror vs the oracle's independent restatement."""
+    logs = [bcos_gpu.LogEntry(address="0x" + "11" * 20, topic=[b"\x01" * 32, b"\x02" * 32], data=b"xyz"),
+            bcos_gpu.LogEntry(address="", topic=[], data=b"")]
+    r = bcos_gpu.TransactionReceiptData(version=0, gas_used="21000", contract_address="", status=-1,
+                                        output=b"\x00\x01", log_entries=logs, block_number=77)
+    want = oracle.receipt_preimage(0, "21000", "", -1, b"\x00\x01",
+                                   [("0x" + "11" * 20, [b"\x01" * 32, b"\x02" * 32], b"xyz"), ("", [], b"")], 77)
+    assert r.preimage() == want
+    assert want[:4] == bytes(4) and want[4:9] == b"21000" and want[9:13] == b"\xff" * 4
+    assert want[-8:] == (77).to_bytes(8, "big")
+
+
+def test_oracle_ecrecover_vector(oracle, kat):
+    """EVMPrecompiledTest.cpp:58-72 through the precompile's input layout (Precompiled.cpp:443-482)."""
+    h = bytes.fromhex("38d18acb67d25c8bb9942764b62f18e17054f66a817bd4295423adf9ed98873e")
+    s = bytes.fromhex("789d1dd423d25f0772d2748d60f7e4b81bb14d086eba8e8e8efb6dcff8a4ae02")
+    inp = h + (27).to_bytes(32, "big") + h + s
+    assert oracle.ecrecover(inp).hex() == "00" * 12 + "ceaccac640adf55b2028469bd36ba501f28b699d"
+    assert oracle.ecrecover(h + (29).to_bytes(32, "big") + h + s) == b""
+    # only the last byte of v is read: (1 << 8) + 27 behaves as 27
+    assert oracle.ecrecover(h + ((1 << 8) + 27).to_bytes(32, "big") + h + s) == oracle.ecrecover(inp)

@@ -112,3 +112,67 @@ def test_sharded_root_gpu_single_process(gpu, oracle):
             root = parallel.gpu_root_fn(hasher, width)(fr.contiguous())
             torch.cuda.synchronize()
             assert bytes(root.cpu().tolist()) == oracle.merkle(hasher, width, leaves_h, nthreads=16)
+
+
+def _worker_sync_free(rank, world, port, cases, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "fisco-bcos_amd"))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from bcos_gpu import parallel
+    from oracle import oracle as o
+    out = []
+    for (hasher, width, n, seed) in cases:
+        leaves = np.random.default_rng(seed).integers(0, 256, size=(n, 32), dtype=np.uint8)
+
+        def frontier_fn(local, levels, dst):
+            dst.copy_(torch.from_numpy(_oracle_levels(o, hasher, width, local.numpy(), levels).copy()))
+
+        def root_fn(frontier, dst):
+            dst.copy_(torch.from_numpy(np.frombuffer(o.merkle(hasher, width, frontier.numpy()), dtype=np.uint8).copy()))
+
+        st = parallel.ShardedTxRoot(n, world, rank, width, "cpu", frontier_fn, root_fn)
+        lo, hi = st.local_range
+        r = st(torch.from_numpy(leaves[lo:hi].copy()))
+        r2 = st(torch.from_numpy(leaves[lo:hi].copy()))  # buffers are reused across steps
+        out.append((st.levels, bytes(r.tolist()), bytes(r2.tolist())))
+    if rank == 0:
+        q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_tx_root_sync_free_gloo(oracle, world):
+    """bench.py C4's exchange (parallel.ShardedTxRoot: fixed-size frontiers, one all-gather, on-device
+    compaction) equals the single-process root, including ranks with empty shards."""
+    cases = [(0, 2, 100_000, 11), (1, 2, 3, 12), (0, 16, 70_000, 13), (1, 2, 1, 14), (0, 2, 131_072, 15)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_sync_free, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for (hasher, width, n, seed), (L, got, got2) in zip(cases, res):
+        leaves = np.random.default_rng(seed).integers(0, 256, size=(n, 32), dtype=np.uint8)
+        assert got == got2 == oracle.merkle(hasher, width, leaves), (hasher, width, n, L)
+    assert any(L > 0 for L, _, _ in res)
+
+
+@pytest.mark.gpu
+def test_sharded_tx_root_gpu_world1(gpu, oracle):
+    """gpu_sharded_tx_root (bench C4's step) on one GPU equals the oracle root."""
+    from bcos_gpu import parallel
+    for hasher, width, n in ((0, 2, 1_000_000), (1, 2, 20_001)):
+        leaves_h = np.random.default_rng(n + 1).integers(0, 256, size=(n, 32), dtype=np.uint8)
+        st = parallel.gpu_sharded_tx_root(n, 1, 0, hasher, width, "cuda")
+        lo, hi = st.local_range
+        r = st(torch.from_numpy(leaves_h[lo:hi].copy()).cuda())
+        torch.cuda.synchronize()
+        assert bytes(r.cpu().tolist()) == oracle.merkle(hasher, width, leaves_h, nthreads=16)
