@@ -298,6 +298,7 @@ struct FieldK1 {
 
 // ============================================================================ Montgomery fields
 struct ParamP2 {  // SM2 base field
+    static constexpr bool SM2P = true;
     static constexpr uint32_t M[8] = {0xffffffffu, 0xffffffffu, 0x00000000u, 0xffffffffu,
                                       0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu};
     static constexpr uint32_t MINV = 0x1u;
@@ -309,6 +310,7 @@ struct ParamP2 {  // SM2 base field
                                             0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu};
 };
 struct ParamN1 {  // secp256k1 group order
+    static constexpr bool SM2P = false;
     static constexpr uint32_t M[8] = {0xd0364141u, 0xbfd25e8cu, 0xaf48a03bu, 0xbaaedce6u,
                                       0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
     static constexpr uint32_t MINV = 0x5588b13fu;
@@ -320,6 +322,7 @@ struct ParamN1 {  // secp256k1 group order
                                             0xfffffffeu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
 };
 struct ParamN2 {  // SM2 group order
+    static constexpr bool SM2P = false;
     static constexpr uint32_t M[8] = {0x39d54123u, 0x53bbf409u, 0x21c6052bu, 0x7203df6bu,
                                       0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu};
     static constexpr uint32_t MINV = 0x72350975u;
@@ -331,12 +334,55 @@ struct ParamN2 {  // SM2 group order
                                             0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu};
 };
 
+// Montgomery reduction specialised to the SM2 prime p = 2^256 - 2^224 - 2^96 + 2^64 - 1 (m' = 1):
+// adding q p 2^(32i) to the 512-bit T puts +q at word i+8, -q at i+7, -q at i+3, +q at i+2 and
+// clears word i (q = its current value), so the reduction needs no multiplications: a column sweep
+// with a signed 64-bit accumulator (v_lshl_add_u64 adds).  T < p^2 -> result < 2p -> one conditional
+// subtraction.  Replaces the 56 multiply-accumulates of the generic CIOS reduction.
+__device__ __forceinline__ void redc_sm2p(fe& r, const uint32_t t[16]) {
+    uint32_t q[8], o[8];
+    int64_t acc = 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        acc += static_cast<int64_t>(t[c]);
+        if (c >= 2 && c <= 9) acc += static_cast<int64_t>(q[c - 2]);
+        if (c >= 8) acc += static_cast<int64_t>(q[c - 8]);
+        int64_t neg = 0;
+        if (c >= 3 && c <= 10) neg += static_cast<int64_t>(q[c - 3]);
+        if (c >= 7 && c <= 14) neg += static_cast<int64_t>(q[c - 7]);
+        acc -= neg;
+        if (c < 8) {
+            q[c] = static_cast<uint32_t>(acc);
+            acc -= static_cast<int64_t>(q[c]);
+        } else {
+            o[c - 8] = static_cast<uint32_t>(acc);
+        }
+        acc >>= 32;
+    }
+    const uint32_t top = static_cast<uint32_t>(acc);  // 0 or 1
+    fe t2, u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t2.v[i] = o[i];
+    uint32_t bw = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) u.v[i] = subc32(t2.v[i], ParamP2::M[i], bw, bw);
+    const bool take = top != 0u || bw == 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = take ? u.v[i] : t2.v[i];
+}
+
 template <class P>
 struct Mont {
     static constexpr const uint32_t* M = P::M;
 
     // r = a * b * 2^-256 mod m (inputs < m, output < m)
     __device__ static __forceinline__ void mul(fe& r, const fe& a, const fe& b) {
+        if constexpr (P::SM2P) {
+            uint32_t t[16];
+            mul_512(t, a, b);
+            redc_sm2p(r, t);
+            return;
+        }
         uint64_t acc = 0;
         uint32_t c2 = 0, m[8], o[8];
 #pragma unroll
@@ -370,7 +416,15 @@ struct Mont {
 #pragma unroll
         for (int i = 0; i < 8; ++i) r.v[i] = take ? u.v[i] : t.v[i];
     }
-    __device__ static __forceinline__ void sqr(fe& r, const fe& a) { mul(r, a, a); }
+    __device__ static __forceinline__ void sqr(fe& r, const fe& a) {
+        if constexpr (P::SM2P) {
+            uint32_t t[16];
+            sqr_512(t, a);
+            redc_sm2p(r, t);
+        } else {
+            mul(r, a, a);
+        }
+    }
     __device__ static __forceinline__ void add(fe& r, const fe& a, const fe& b) { mod_add_asm(r.v, a.v, b.v, P::M); }
     __device__ static __forceinline__ void sub(fe& r, const fe& a, const fe& b) { mod_sub_asm(r.v, a.v, b.v, P::M); }
     __device__ static __forceinline__ void neg(fe& r, const fe& a) {

@@ -35,6 +35,31 @@ __global__ __launch_bounds__(256) void k_mul(uint64_t* cyc, uint32_t* out, uint3
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+template <class F>
+__global__ __launch_bounds__(256) void k_fmul(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    fe x, y;
+    seed_fe(y, s + 99);
+    seed_fe(x, s + threadIdx.x);
+    y.v[7] &= 0x0fffffffu;
+    x.v[7] &= 0x0fffffffu;
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS; ++it) F::mul(x, x, y);
+    const uint64_t t1 = clock64();
+    if ((x.v[0] ^ x.v[7]) == 0x12345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+template <class F>
+__global__ __launch_bounds__(256) void k_fsqr(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    fe x;
+    seed_fe(x, s + threadIdx.x);
+    x.v[7] &= 0x0fffffffu;
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS; ++it) F::sqr(x, x);
+    const uint64_t t1 = clock64();
+    if ((x.v[0] ^ x.v[7]) == 0x12345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 template <int CHAINS>
 __global__ __launch_bounds__(256) void k_sqr(uint64_t* cyc, uint32_t* out, uint32_t s) {
     fe x[CHAINS];
@@ -86,6 +111,88 @@ __global__ __launch_bounds__(256) void k_madchain(uint64_t* cyc, uint32_t* out, 
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// v_mad_u64_u32 without using the carry-out (acc = a*b + acc): the 26-bit-limb accumulation pattern
+template <int CHAINS>
+__global__ __launch_bounds__(256) void k_madnc(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    uint64_t acc[CHAINS];
+    const uint32_t a = s * 7u + threadIdx.x, b = s ^ 0x9e3779b9u;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) acc[c] = c;
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS * 8; ++it) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) {
+            uint64_t cc;
+            asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[c]), "=s"(cc) : "v"(a), "v"(b));
+        }
+    }
+    const uint64_t t1 = clock64();
+    uint64_t r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) r ^= acc[c];
+    if (r == 0x12345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+// 64-bit adds via v_lshl_add_u64 (gfx940+): acc = (x << 1) + acc
+template <int CHAINS>
+__global__ __launch_bounds__(256) void k_lshladd(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    uint64_t acc[CHAINS];
+    const uint64_t b = s ^ 0x9e3779b9u;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) acc[c] = c + threadIdx.x;
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS * 8; ++it) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) asm volatile("v_lshl_add_u64 %0, %1, 1, %0" : "+v"(acc[c]) : "v"(b));
+    }
+    const uint64_t t1 = clock64();
+    uint64_t r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) r ^= acc[c];
+    if (r == 0x12345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+// plain 32-bit adds
+template <int CHAINS>
+__global__ __launch_bounds__(256) void k_add(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    uint32_t x[CHAINS];
+    const uint32_t b = s ^ 0x9e3779b9u;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) x[c] = c + threadIdx.x;
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS * 8; ++it) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) asm volatile("v_add_u32_e32 %0, %1, %0" : "+v"(x[c]) : "v"(b));
+    }
+    const uint64_t t1 = clock64();
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) r ^= x[c];
+    if (r == 0x12345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+// v_mul_lo + v_mul_hi pairs (32x32 -> 64 without mad)
+template <int CHAINS>
+__global__ __launch_bounds__(256) void k_mulpair(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    uint32_t x[CHAINS], y[CHAINS];
+    const uint32_t b = s ^ 0x9e3779b9u;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) { x[c] = c + threadIdx.x; y[c] = c; }
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS * 8; ++it) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) {
+            asm volatile("v_mul_lo_u32 %0, %1, %2\n\tv_mul_hi_u32 %1, %1, %2" : "=&v"(y[c]), "+v"(x[c]) : "v"(b));
+        }
+    }
+    const uint64_t t1 = clock64();
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) r ^= x[c] ^ y[c];
+    if (r == 0x12345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 template <class K>
 static void run(const char* name, K kern, int waves_per_simd, double ops_per_iter, int iters, uint64_t* d_cyc, uint32_t* d_out,
                 bool last) {
@@ -121,6 +228,13 @@ int main() {
     hipGetDeviceProperties(&p, 0);
     printf("{\"device\": \"%s\", \"clock_khz\": %d,\n", p.gcnArchName, p.clockRate);
     for (int occ = 1; occ <= 2; ++occ) {
+        run("madnc_chain1", k_madnc<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
+        run("madnc_chain4", k_madnc<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
+        run("lshladd_chain1", k_lshladd<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
+        run("lshladd_chain4", k_lshladd<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
+        run("add_chain1", k_add<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
+        run("add_chain4", k_add<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
+        run("mulpair_chain4", k_mulpair<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
         run("madc_chain1", k_madchain<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
         run("madc_chain2", k_madchain<2>, occ, 2, ITERS * 8, d_cyc, d_out, false);
         run("madc_chain4", k_madchain<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
@@ -128,6 +242,10 @@ int main() {
         run("fk1_mul_chain2", k_mul<2>, occ, 2, ITERS, d_cyc, d_out, false);
         run("fk1_sqr_chain1", k_sqr<1>, occ, 1, ITERS, d_cyc, d_out, false);
         run("fk1_sqr_chain2", k_sqr<2>, occ, 2, ITERS, d_cyc, d_out, false);
+        run("p2_mul", k_fmul<FieldP2>, occ, 1, ITERS, d_cyc, d_out, false);
+        run("p2_sqr", k_fsqr<FieldP2>, occ, 1, ITERS, d_cyc, d_out, false);
+        run("n2_mul_generic", k_fmul<FieldN2>, occ, 1, ITERS, d_cyc, d_out, false);
+        run("n2_sqr_generic", k_fsqr<FieldN2>, occ, 1, ITERS, d_cyc, d_out, false);
         run("k1_dbl", k_dbl, occ, 1, ITERS / 8, d_cyc, d_out, occ == 2);
     }
     printf("}\n");
