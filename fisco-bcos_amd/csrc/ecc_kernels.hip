@@ -268,6 +268,43 @@ __device__ __forceinline__ void add_digit_aff(Jac& acc, const Aff T[8], int d, b
     C::cmov(acc, R, d != 0);
 }
 
+// Same, with the table's x-coordinates in a per-wave LDS slice laid out [entry][word][lane] (a
+// conflict-free per-lane gather of 8 dwords) and the y-coordinates in VGPRs: frees 64 VGPRs, so the
+// occupancy-2 kernels stop spilling the table to scratch.
+template <class C, class F>
+__device__ __forceinline__ void add_digit_ldsx(Jac& acc, const uint32_t* ldsx, const fe Y[8], int d, bool neg,
+                                               bool phi) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    Aff S;
+    const uint32_t* b = ldsx + m * 512u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) S.x.v[k] = b[k * 64];
+    fe_copy(S.y, Y[0]);
+#pragma unroll
+    for (int q = 1; q < 8; ++q) fe_cmov_mask(S.y, Y[q], __builtin_amdgcn_ballot_w64(m == static_cast<uint32_t>(q)));
+    if (phi) {
+        fe bt;
+        fe_set(bt, kGlvBeta);
+        F::mul(S.x, S.x, bt);
+    }
+    fe ny;
+    F::neg(ny, S.y);
+    fe_cmov(S.y, ny, (d < 0) != neg);
+    Jac R;
+    C::madd(R, acc, S);
+    C::cmov(acc, R, d != 0);
+}
+
+// Moves the table's x-coordinates to the wave's LDS slice (ldsx already offset by the lane).
+__device__ __forceinline__ void table_x_to_lds(uint32_t* ldsx, const Aff A[8], fe Y[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ldsx[(j * 8 + k) * 64] = A[j].x.v[k];
+        fe_copy(Y[j], A[j].y);
+    }
+}
+
 // Table 1P..8P of an affine P, as Jacobian points.
 template <class C>
 __device__ __forceinline__ void multiples8(Jac T[8], const Aff& P) {
@@ -325,7 +362,8 @@ __device__ __forceinline__ void coz_table_k1(Aff A[8], fe& Zc, const Jac T[8]) {
 
 // acc = k * P on secp256k1 via GLV: k1*P + k2*phi(P), 33 joint radix-16 Booth windows of mixed
 // additions against the co-Z table; result on the real curve.
-__device__ __forceinline__ void glv_mul_k1(Jac& acc, const fe& k, const Aff& P) {
+template <bool LDS = false>
+__device__ __forceinline__ void glv_mul_k1(Jac& acc, const fe& k, const Aff& P, uint32_t* ldsx = nullptr) {
     fe k1, k2, Zc;
     bool neg1, neg2;
     glv_split(k1, neg1, k2, neg2, k);
@@ -336,6 +374,25 @@ __device__ __forceinline__ void glv_mul_k1(Jac& acc, const fe& k, const Aff& P) 
         coz_table_k1(A, Zc, T);
     }
     CurveK1::set_inf(acc);
+    if constexpr (LDS) {
+        fe Y[8];
+        table_x_to_lds(ldsx, A, Y);
+        add_digit_ldsx<CurveK1, FieldK1>(acc, ldsx, Y, static_cast<int>(k1.v[3] >> 31), neg1, false);
+        add_digit_ldsx<CurveK1, FieldK1>(acc, ldsx, Y, static_cast<int>(k2.v[3] >> 31), neg2, true);
+#pragma unroll 1
+        for (int i = 31; i >= 0; --i) {
+            CurveK1::dbl(acc, acc);
+            CurveK1::dbl(acc, acc);
+            CurveK1::dbl(acc, acc);
+            CurveK1::dbl(acc, acc);
+            const int d1 = booth_digit128(k1);
+            const int d2 = booth_digit128(k2);
+            add_digit_ldsx<CurveK1, FieldK1>(acc, ldsx, Y, d1, neg1, false);
+            add_digit_ldsx<CurveK1, FieldK1>(acc, ldsx, Y, d2, neg2, true);
+        }
+        FieldK1::mul(acc.Z, acc.Z, Zc);
+        return;
+    }
     // digit 32 = bit 127 of each half
     add_digit_aff<CurveK1, FieldK1>(acc, A, static_cast<int>(k1.v[3] >> 31), neg1, false);
     add_digit_aff<CurveK1, FieldK1>(acc, A, static_cast<int>(k2.v[3] >> 31), neg2, true);
@@ -355,7 +412,8 @@ __device__ __forceinline__ void glv_mul_k1(Jac& acc, const fe& k, const Aff& P) 
 
 // acc = k * P on SM2: the table 1P..8P is normalised to affine with one inversion (Montgomery's
 // trick over the 7 non-trivial Z), then 65 radix-16 Booth windows of mixed additions.
-__device__ __forceinline__ void booth_mul_sm2(Jac& acc, const fe& k_plain, const Aff& P) {
+template <bool LDS = false>
+__device__ __forceinline__ void booth_mul_sm2(Jac& acc, const fe& k_plain, const Aff& P, uint32_t* ldsx = nullptr) {
     Aff A[8];
     {
         Jac T[8];
@@ -381,6 +439,24 @@ __device__ __forceinline__ void booth_mul_sm2(Jac& acc, const fe& k_plain, const
     fe k;
     fe_copy(k, k_plain);
     CurveSM2::set_inf(acc);
+    if constexpr (LDS) {
+        fe Y[8];
+        table_x_to_lds(ldsx, A, Y);
+        add_digit_ldsx<CurveSM2, FieldP2>(acc, ldsx, Y, static_cast<int>(k.v[7] >> 31), false, false);
+#pragma unroll 1
+        for (int i = 63; i >= 0; --i) {
+            CurveSM2::dbl(acc, acc);
+            CurveSM2::dbl(acc, acc);
+            CurveSM2::dbl(acc, acc);
+            CurveSM2::dbl(acc, acc);
+            const uint32_t top = k.v[7];
+            const uint32_t W = top >> 28, c = (top >> 27) & 1u;
+            const int d = static_cast<int>(W + c) - static_cast<int>((W >> 3) << 4);
+            shl4(k);
+            add_digit_ldsx<CurveSM2, FieldP2>(acc, ldsx, Y, d, false, false);
+        }
+        return;
+    }
     add_digit_aff<CurveSM2, FieldP2>(acc, A, static_cast<int>(k.v[7] >> 31), false, false);  // digit 64
 #pragma unroll 1
     for (int i = 63; i >= 0; --i) {
@@ -463,8 +539,9 @@ static int tables(const uint32_t** k1, const uint32_t** sm2) {
 // ------------------------------------------------------------------ secp256k1 recover (one lane)
 // libsecp256k1 secp256k1_ecdsa_recover as wedpr calls it: reject v > 3, r or s not in [1, n-1],
 // (v & 2) with r >= p - n, x not on the curve, Q = infinity.  pub = (x, y) canonical, plain.
+template <bool LDS = false>
 __device__ __forceinline__ bool secp256k1_recover_rsv(const fe& hash_be, const fe& r, const fe& s, uint32_t v,
-                                                      const uint32_t* tab, fe& px, fe& py) {
+                                                      const uint32_t* tab, fe& px, fe& py, uint32_t* ldsx = nullptr) {
     bool ok = v <= 3u;
     ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, ParamN1::M);
     fe x;
@@ -510,7 +587,7 @@ __device__ __forceinline__ bool secp256k1_recover_rsv(const fe& hash_be, const f
     fe_copy(R.x, x);
     fe_copy(R.y, y);
     Jac QG, QR, Q;
-    glv_mul_k1(QR, u2, R);
+    glv_mul_k1<LDS>(QR, u2, R, ldsx);
     comb_mul<CurveK1>(QG, u1, tab);
     CurveK1::add(Q, QG, QR);
     ok = ok && !Q.inf;
@@ -523,8 +600,9 @@ __device__ __forceinline__ bool secp256k1_recover_rsv(const fe& hash_be, const f
     return ok;
 }
 
+template <bool LDS = false>
 __device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const uint8_t* sig, uint32_t siglen,
-                                                       const uint32_t* tab, fe& px, fe& py) {
+                                                       const uint32_t* tab, fe& px, fe& py, uint32_t* ldsx = nullptr) {
     if (siglen != 65u) return false;
     ByteReader rd(sig, 65);
     uint32_t w[8];
@@ -535,7 +613,7 @@ __device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const 
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
     fe_from_be_words(s, w);
-    return secp256k1_recover_rsv(hash_be, r, s, rd.word(16) & 0xffu, tab, px, py);
+    return secp256k1_recover_rsv<LDS>(hash_be, r, s, rd.word(16) & 0xffu, tab, px, py, ldsx);
 }
 
 // pub -> right160(Keccak256(pub)) as 5 little-endian memory words
@@ -604,8 +682,10 @@ __device__ __forceinline__ void sm2_e(uint32_t e[8], const uint32_t X[8], const 
 // sm2_do_verify semantics (GB/T 32918.2): pub must be on the curve with coordinates < p,
 // r, s in [1, n-1], t = r + s mod n != 0, accept iff (e + x1) mod n == r for (x1, y1) = sG + tP.
 // The comparison is done projectively (X == (r - e mod n [+ n]) * Z^2), so no inversion.
+template <bool LDS = false>
 __device__ __forceinline__ bool sm2_verify_rs(const fe& hash_be, const fe& r, const fe& s, const uint32_t X[8],
-                                              const uint32_t Y[8], const uint32_t* tab, fe& px, fe& py) {
+                                              const uint32_t Y[8], const uint32_t* tab, fe& px, fe& py,
+                                              uint32_t* ldsx = nullptr) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         px.v[i] = X[7 - i];
@@ -629,7 +709,7 @@ __device__ __forceinline__ bool sm2_verify_rs(const fe& hash_be, const fe& r, co
     for (int i = 0; i < 8; ++i) e.v[i] = eb[7 - i];
     reduce_once(e, ParamN2::M);
     Jac QG, QP, Q;
-    booth_mul_sm2(QP, t, P);
+    booth_mul_sm2<LDS>(QP, t, P, ldsx);
     comb_mul<CurveSM2>(QG, s, tab);
     CurveSM2::add(Q, QG, QP);
     ok = ok && !Q.inf;
@@ -650,8 +730,9 @@ __device__ __forceinline__ bool sm2_verify_rs(const fe& hash_be, const fe& r, co
     return ok && match;
 }
 
+template <bool LDS = false>
 __device__ __forceinline__ bool sm2_verify_lane(const fe& hash_be, const uint8_t* sig, uint32_t siglen,
-                                                const uint32_t* tab, fe& px, fe& py) {
+                                                const uint32_t* tab, fe& px, fe& py, uint32_t* ldsx = nullptr) {
     if (siglen != 128u) return false;
     ByteReader rd(sig, 128);
     uint32_t w[8], X[8], Y[8];
@@ -667,7 +748,7 @@ __device__ __forceinline__ bool sm2_verify_lane(const fe& hash_be, const uint8_t
         X[i] = bswap32(rd.word(16 + i));
         Y[i] = bswap32(rd.word(24 + i));
     }
-    return sm2_verify_rs(hash_be, r, s, X, Y, tab, px, py);
+    return sm2_verify_rs<LDS>(hash_be, r, s, X, Y, tab, px, py, ldsx);
 }
 
 // ------------------------------------------------------------------ secp256k1 verify (known key)
@@ -887,11 +968,16 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(const uint8_t* __re
     fe x, y;
     uint32_t ad[5] = {0, 0, 0, 0, 0};
     bool ok;
+    // OCC 2: the variable-base table's x-coordinates live in LDS (16 KiB per wave, 128 KiB per CU
+    // at 2 workgroups per CU), the rest of the working set in 256 VGPRs
+    constexpr bool kLds = OCC == 2;
+    __shared__ uint32_t ldsx_all[kLds ? 4 * 4096 : 1];
+    uint32_t* ldsx = kLds ? ldsx_all + (threadIdx.x >> 6) * 4096 + (threadIdx.x & 63) : nullptr;
     if (SUITE == BCOSGPU_SUITE_SM2) {
-        ok = sm2_verify_lane(h, sig + sa, slen, tab, x, y);
+        ok = sm2_verify_lane<kLds>(h, sig + sa, slen, tab, x, y, ldsx);
         if (ok) sm3_address(ad, x, y);
     } else {
-        ok = secp256k1_recover_lane(h, sig + sa, slen, tab, x, y);
+        ok = secp256k1_recover_lane<kLds>(h, sig + sa, slen, tab, x, y, ldsx);
         if (ok) keccak_address(ad, x, y);
     }
     uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
