@@ -191,8 +191,10 @@ def main():
                     "units_per_launch": n,
                     "work_per_unit": "%d F x %d MAC (SURVEY.md 8d)" % (f_per, MAC_PER_F)}
         cpu = None
+        host_api = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(b, suite, min(n, 20000), args.cpu_threads)
+            host_api = host_api_rate(b, suite, n)
         line = {
             "metric": wl["metric"],
             "value": value, "unit": "tx/s (hash + recover/verify + sender%s)" % (
@@ -203,7 +205,7 @@ def main():
             "data": "synthetic (distinct key per tx, 1%% bit-flipped s, 0.1%% v=4; valid frac %.4f)" % ok_frac,
             "config": {"workload": wl["name"], "txs_total": units_total, "txs_rank0": n,
                        "parallelism": "dp%d (%s)" % (world, "block shards" if args.workload == "c5" else "tx-index shards")},
-            "roofline": roofline, "cpu_baseline": cpu,
+            "roofline": roofline, "cpu_baseline": cpu, "pcie_inclusive": host_api,
         }
         if not args.no_merkle:
             line["merkle_c1"] = merkle_c1()
@@ -233,6 +235,26 @@ def cpu_baseline(b, suite, sample, threads, min_seconds=1.0):
     return {"value": reps * sample / dt, "unit": "tx/s", "cores": threads, "kind": "port",
             "sample": "%d x %d txs of the same batch (%.1f s wall), oracle/ C restatement (4x64-bit Montgomery, "
                       "4-bit Straus), %d threads" % (reps, sample, dt, threads)}
+
+
+def host_api_rate(b, suite, n, reps=5):
+    """The same batch through the host-pointer ABI (bcosgpu_tx_verify_batch: H2D copy, kernel, D2H,
+    synchronise) -- the PCIe-inclusive rate a caller holding host buffers sees.  Not `value`."""
+    import numpy as np
+    import bcos_gpu
+    from bcos_gpu import tx
+    pre = np.ascontiguousarray(b.pre.cpu().numpy())
+    pre_off = np.ascontiguousarray(b.pre_off[: n + 1].cpu().numpy().astype(np.uint64))
+    sig = np.ascontiguousarray(b.sig.cpu().numpy())
+    sig_off = np.ascontiguousarray(b.sig_off[: n + 1].cpu().numpy().astype(np.uint64))
+    suite_obj = bcos_gpu.sm_suite() if suite else bcos_gpu.secp256k1_suite()
+    tx.verify_packed(suite_obj, pre, pre_off, sig, sig_off)  # warm-up (workspace growth)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tx.verify_packed(suite_obj, pre, pre_off, sig, sig_off)
+    dt = (time.perf_counter() - t0) / reps
+    return {"value": n / dt, "unit": "tx/s", "ms_per_batch": dt * 1e3,
+            "path": "bcosgpu_tx_verify_batch (host buffers: H2D + kernel + D2H + sync)"}
 
 
 def merkle_c1():
