@@ -61,7 +61,7 @@ def _kernel_name(suite, n):
     """Which tx-verify kernel the library launches for this batch (mirrors ecc_kernels.hip policy)."""
     split = os.environ.get("BCOSGPU_TXV_SPLIT")
     if suite == 0 and (split == "1" or (split != "0" and n <= (1 << 15))):
-        return "tx_verify_split_kernel"
+        return "tx_verify_split_kernel" if os.environ.get("BCOSGPU_TXV_COOP") == "0" else "tx_verify_coop_kernel"
     occ = os.environ.get("BCOSGPU_TXV_OCC")
     occ = int(occ) if occ in ("1", "2") else (2 if n >= (1 << 17) else 1)
     return "tx_verify_kernel<%d,%d>" % (suite, occ)

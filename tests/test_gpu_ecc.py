@@ -254,17 +254,20 @@ def test_synthetic_batch_device_path(gpu, oracle, suite):
 
 @pytest.mark.parametrize("suite", [0, 1])
 def test_tx_verify_kernel_variants_agree(gpu, oracle, suite, monkeypatch):
-    """Every launch variant (4-wave split kernel, occupancy 1 and 2) gives identical outputs."""
+    """Every launch variant (cooperative-pair and 4-wave split kernels, occupancy 1 and 2) gives
+    identical outputs."""
     import torch
     from bcos_gpu import device, synth
     n = 3000 + 17  # ragged last workgroup
     b = synth.make_batch(suite, n, seed=91, flip_frac=0.02, bad_v_frac=0.01)
     pre, po, sg, so = (x.cpu().numpy() for x in (b.pre, b.pre_off, b.sig, b.sig_off))
     wh, ws, wst = oracle.tx_verify_packed(suite, pre, po.astype(np.uint64), sg, so.astype(np.uint64), nthreads=16)
-    variants = [("1", "1"), ("0", "1"), ("0", "2")] if suite == 0 else [("0", "1"), ("0", "2")]
-    for split, occ in variants:
+    variants = [("1", "1", "1"), ("1", "1", "0"), ("0", "1", "0"), ("0", "2", "0")] if suite == 0 else \
+        [("0", "1", "0"), ("0", "2", "0")]
+    for split, occ, coop in variants:
         monkeypatch.setenv("BCOSGPU_TXV_SPLIT", split)
         monkeypatch.setenv("BCOSGPU_TXV_OCC", occ)
+        monkeypatch.setenv("BCOSGPU_TXV_COOP", coop)
         th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
         snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
         st = torch.empty(n, dtype=torch.uint8, device="cuda")
