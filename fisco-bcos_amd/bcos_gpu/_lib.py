@@ -46,6 +46,11 @@ _SIGS = {
     "bcosgpu_merkle_roots_work_size": (ctypes.c_uint64, [ctypes.c_uint64, _SZ, _I]),
     "bcosgpu_merkle_roots_batch": (_I, [_I, _I, _P, _P, _SZ, _P]),
     "bcosgpu_merkle_roots_batch_dev": (_I, [_I, _I, _P, _P, _SZ, _P, _P, _P]),
+    "bcosgpu_merkle_proof_stride": (ctypes.c_uint64, [ctypes.c_uint64, _I]),
+    "bcosgpu_merkle_proofs": (_I, [_I, _I, _P, _SZ, _P, _SZ, _P, _P]),
+    "bcosgpu_merkle_proofs_dev": (_I, [_I, _P, _SZ, _P, _P, _SZ, _P, _P, _P]),
+    "bcosgpu_merkle_verify_proofs": (_I, [_I, _P, ctypes.c_uint64, _P, _P, _P, _I, _SZ, _P]),
+    "bcosgpu_merkle_verify_proofs_dev": (_I, [_I, _P, ctypes.c_uint64, _P, _P, _P, _I, _SZ, _P, _P]),
     "bcosgpu_secp256k1_recover_batch": (_I, [_P, _P, _SZ, _P, _P, _P]),
     "bcosgpu_secp256k1_recover_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P, _P]),
     "bcosgpu_sm2_verify_batch": (_I, [_P, _P, _SZ, _P, _P]),

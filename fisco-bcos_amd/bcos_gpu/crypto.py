@@ -132,6 +132,61 @@ class Merkle:
         check(lib().bcosgpu_merkle_roots_batch(self.hasher.kind, self.width, _ptr(leaves), _ptr(off), nb, _ptr(roots)))
         return [roots[i].tobytes() for i in range(nb)]
 
+    def generate_merkle_proofs(self, leaves, indices):
+        """Batched generateMerkleProof(originHashes, merkle, index, out) (Merkle.h:121-168) on the GPU."""
+        leaves = _u8(b"".join(bytes(h) for h in leaves) if isinstance(leaves, list) else leaves).reshape(-1, 32)
+        n = leaves.shape[0]
+        if n == 0:
+            raise ValueError("Empty input")
+        idx = np.ascontiguousarray(np.asarray(indices, dtype=np.uint64).reshape(-1))
+        if idx.size and int(idx.max()) >= n:
+            raise ValueError("Out of range!")
+        m = idx.size
+        ensure_device()
+        stride = int(lib().bcosgpu_merkle_proof_stride(n, self.width))
+        proofs = np.zeros((max(m, 1), stride, 32), dtype=np.uint8)
+        plen = np.zeros(max(m, 1), dtype=np.uint32)
+        if m:
+            check(lib().bcosgpu_merkle_proofs(self.hasher.kind, self.width, _ptr(np.ascontiguousarray(leaves)), n, _ptr(idx),
+                                              m, _ptr(proofs), _ptr(plen)))
+        return [[proofs[q, e].tobytes() for e in range(int(plen[q]))] for q in range(m)]
+
+    def generate_merkle_proof(self, origin_hashes, which):
+        """generateMerkleProof: `which` is a leaf index, or a leaf hash (its first occurrence, Merkle.h:84-98)."""
+        leaves = _u8(b"".join(bytes(h) for h in origin_hashes) if isinstance(origin_hashes, list)
+                     else origin_hashes).reshape(-1, 32)
+        if isinstance(which, (bytes, bytearray)):
+            hits = np.nonzero((leaves == np.frombuffer(bytes(which), dtype=np.uint8)).all(axis=1))[0]
+            if hits.size == 0:
+                raise ValueError("Not found hash!")
+            which = int(hits[0])
+        return self.generate_merkle_proofs(leaves, [which])[0]
+
+    def verify_merkle_proofs(self, proofs, hashes, roots):
+        """Batched verifyMerkleProof (Merkle.h:45-81): list of proofs (lists of 32-byte entries), their leaf
+        hashes, and one root per proof (or one shared root).  Returns bool[m]; an empty proof raises."""
+        m = len(proofs)
+        if any(len(p) == 0 for p in proofs):
+            raise ValueError("Empty input proof!")
+        if m == 0:
+            return np.zeros(0, dtype=bool)
+        stride = max(len(p) for p in proofs)
+        buf = np.zeros((m, stride, 32), dtype=np.uint8)
+        plen = np.array([len(p) for p in proofs], dtype=np.uint32)
+        for q, p in enumerate(proofs):
+            buf[q, :len(p)] = np.frombuffer(b"".join(bytes(e) for e in p), dtype=np.uint8).reshape(-1, 32)
+        hs = _u8(b"".join(bytes(h) for h in hashes)).reshape(m, 32)
+        rs = _u8(b"".join(bytes(r) for r in roots) if isinstance(roots, list) else bytes(roots)).reshape(-1, 32)
+        ok = np.zeros(m, dtype=np.uint8)
+        ensure_device()
+        check(lib().bcosgpu_merkle_verify_proofs(self.hasher.kind, _ptr(buf), stride, _ptr(plen), _ptr(np.ascontiguousarray(hs)),
+                                                 _ptr(np.ascontiguousarray(rs)), 1 if rs.shape[0] == m and m > 1 else 0, m,
+                                                 _ptr(ok)))
+        return ok == 1
+
+    def verify_merkle_proof(self, proof, h, root):
+        return bool(self.verify_merkle_proofs([proof], [bytes(h)], bytes(root))[0])
+
 
 def calculate_merkle_proof_root(hasher: Hash, leaves) -> bytes:
     """protocol::calculateMerkleProofRoot (ParallelMerkleProof.cpp:32-69)."""

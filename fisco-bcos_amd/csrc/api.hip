@@ -264,6 +264,92 @@ int bcosgpu_merkle_roots_batch(int hasher, int width, const uint8_t* leaves32, c
     return 0;
 }
 
+// ------------------------------------------------------------------ Merkle proofs
+uint64_t bcosgpu_merkle_proof_stride(uint64_t n, int width) {
+    if (width < 2 || width > 64 || n == 0) return 0;
+    return merkle_proof_stride(n, width);
+}
+
+int bcosgpu_merkle_proofs_dev(int width, const uint8_t* d_leaves32, size_t n, const uint8_t* d_tree,
+                              const uint64_t* d_index, size_t m, uint8_t* d_proofs, uint32_t* d_proof_len, void* stream) {
+    if (width < 2 || width > 64) return set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
+    if (n == 0) return set_err(BCOSGPU_E_EMPTY, "Empty input");
+    if (m && (!d_leaves32 || !d_tree || !d_index || !d_proofs || !d_proof_len)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_merkle_proofs(width, d_leaves32, n, d_tree, d_index, m, d_proofs, d_proof_len, as_stream(stream));
+    return rc ? hip_err(hipGetLastError(), "merkle proofs launch") : 0;
+}
+
+int bcosgpu_merkle_proofs(int hasher, int width, const uint8_t* leaves32, size_t n, const uint64_t* index, size_t m,
+                          uint8_t* proofs, uint32_t* proof_len) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (width < 2 || width > 64) return set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
+    if (n == 0) return set_err(BCOSGPU_E_EMPTY, "Empty input");
+    if (m == 0) return 0;
+    if (!leaves32 || !index || !proofs || !proof_len) return set_err(BCOSGPU_E_ARG, "null pointer");
+    for (size_t q = 0; q < m; ++q)
+        if (index[q] >= n) return set_err(BCOSGPU_E_ARG, "Out of range!");  // Merkle.h:124-127
+    const uint64_t stride = merkle_proof_stride(n, width), tree = bcosgpu_merkle_size(n, width);
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    HIP_OK(w->b[0].ensure(n * 32));
+    HIP_OK(w->b[1].ensure(tree * 32 + 32));
+    HIP_OK(w->b[2].ensure(m * 8));
+    HIP_OK(w->b[3].ensure(m * stride * 32));
+    HIP_OK(w->b[4].ensure(m * 4));
+    HIP_OK(hipMemcpyAsync(w->b[0].p, leaves32, n * 32, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[2].p, index, m * 8, hipMemcpyHostToDevice, w->stream));
+    rc = launch_merkle(hasher, width, w->b[0].as<uint8_t>(), n, w->b[1].as<uint8_t>(), nullptr, w->stream);
+    if (!rc)
+        rc = launch_merkle_proofs(width, w->b[0].as<uint8_t>(), n, w->b[1].as<uint8_t>(), w->b[2].as<uint64_t>(), m,
+                                  w->b[3].as<uint8_t>(), w->b[4].as<uint32_t>(), w->stream);
+    if (rc) return hip_err(hipGetLastError(), "merkle proofs launch");
+    HIP_OK(hipMemcpyAsync(proofs, w->b[3].p, m * stride * 32, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipMemcpyAsync(proof_len, w->b[4].p, m * 4, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
+int bcosgpu_merkle_verify_proofs_dev(int hasher, const uint8_t* d_proofs, uint64_t stride, const uint32_t* d_proof_len,
+                                     const uint8_t* d_hashes32, const uint8_t* d_roots32, int per_proof_root, size_t m,
+                                     uint8_t* d_ok, void* stream) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (stride == 0 || stride > 0xFFFFFFFFull) return set_err(BCOSGPU_E_ARG, "bad proof stride");
+    if (m && (!d_proofs || !d_proof_len || !d_hashes32 || !d_roots32 || !d_ok)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_merkle_verify(hasher, d_proofs, stride, d_proof_len, d_hashes32, d_roots32, per_proof_root ? 1 : 0, m,
+                                  d_ok, as_stream(stream));
+    return rc ? hip_err(hipGetLastError(), "merkle verify launch") : 0;
+}
+
+int bcosgpu_merkle_verify_proofs(int hasher, const uint8_t* proofs, uint64_t stride, const uint32_t* proof_len,
+                                 const uint8_t* hashes32, const uint8_t* roots32, int per_proof_root, size_t m, uint8_t* ok) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (stride == 0 || stride > 0xFFFFFFFFull) return set_err(BCOSGPU_E_ARG, "bad proof stride");
+    if (m == 0) return 0;
+    if (!proofs || !proof_len || !hashes32 || !roots32 || !ok) return set_err(BCOSGPU_E_ARG, "null pointer");
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    const size_t nroots = per_proof_root ? m : 1;
+    HIP_OK(w->b[0].ensure(m * stride * 32));
+    HIP_OK(w->b[1].ensure(m * 4));
+    HIP_OK(w->b[2].ensure(m * 32));
+    HIP_OK(w->b[3].ensure(nroots * 32));
+    HIP_OK(w->b[4].ensure(m));
+    HIP_OK(hipMemcpyAsync(w->b[0].p, proofs, m * stride * 32, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[1].p, proof_len, m * 4, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[2].p, hashes32, m * 32, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[3].p, roots32, nroots * 32, hipMemcpyHostToDevice, w->stream));
+    rc = launch_merkle_verify(hasher, w->b[0].as<uint8_t>(), stride, w->b[1].as<uint32_t>(), w->b[2].as<uint8_t>(),
+                              w->b[3].as<uint8_t>(), per_proof_root ? 1 : 0, m, w->b[4].as<uint8_t>(), w->stream);
+    if (rc) return hip_err(hipGetLastError(), "merkle verify launch");
+    HIP_OK(hipMemcpyAsync(ok, w->b[4].p, m, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
 // ------------------------------------------------------------------ signatures
 int bcosgpu_secp256k1_recover_batch_dev(const uint8_t* d_hash32, const uint8_t* d_sig65, size_t n,
                                         uint8_t* d_pub64, uint8_t* d_addr20, uint8_t* d_ok,

@@ -17,6 +17,12 @@ int launch_merkle_levels(int hasher, int width, const uint8_t* d_in, uint64_t n,
 uint64_t merkle_roots_work_bytes(uint64_t total_leaves, uint64_t nblocks, int width);
 int launch_merkle_roots_batch(int hasher, int width, const uint8_t* d_leaves, const uint64_t* block_off,
                               uint64_t nblocks, uint8_t* d_work, uint8_t* d_roots, hipStream_t st);
+uint64_t merkle_proof_stride(uint64_t n, int width);
+int launch_merkle_proofs(int width, const uint8_t* d_leaves, uint64_t n, const uint8_t* d_tree, const uint64_t* d_index,
+                         uint64_t m, uint8_t* d_proofs, uint32_t* d_len, hipStream_t st);
+int launch_merkle_verify(int hasher, const uint8_t* d_proofs, uint64_t stride, const uint32_t* d_len,
+                         const uint8_t* d_hashes, const uint8_t* d_roots, int root_stride, uint64_t m, uint8_t* d_ok,
+                         hipStream_t st);
 int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* d_scratch,
                       uint8_t* d_root, hipStream_t st);
 

@@ -254,6 +254,159 @@ int launch_merkle_roots_batch(int hasher, int width, const uint8_t* d_leaves, co
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
+// ------------------------------------------------------------------ Merkle proofs
+// Merkle<H,width>::generateMerkleProof(originHashes, merkle, index, out) (Merkle.h:121-168) for a
+// batch of leaf indices: one proof per lane, gathered from the leaves and the reference-layout tree.
+// Proof = per level below the root: a count record (BE u32 in a 32-byte entry) and the group of
+// <= width siblings that contains the node; a 1-leaf tree's proof is the single leaf.
+struct ProofLevels {
+    uint64_t pos[64];    // tree entry of level l's count record (level 0 = leaves: unused)
+    uint64_t len[64];    // nodes at level l (level 0 = n)
+    int nlev;            // levels below the root
+};
+
+__device__ __forceinline__ void copy_entry(uint8_t* dst, const uint8_t* src) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    d[0] = s[0];
+    d[1] = s[1];
+}
+
+__global__ __launch_bounds__(256) void merkle_proof_kernel(const uint8_t* __restrict__ leaves, const uint8_t* __restrict__ tree,
+                                                           int width, const ProofLevels t, const uint64_t* __restrict__ index,
+                                                           uint64_t m, uint64_t stride, uint8_t* __restrict__ proofs,
+                                                           uint32_t* __restrict__ plen) {
+    const uint64_t q = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (q >= m) return;
+    uint8_t* out = proofs + 32ull * stride * q;
+    uint64_t idx = index[q];
+    if (t.nlev == 0) {  // n == 1 (Merkle.h:137-142)
+        copy_entry(out, tree);
+        plen[q] = 1;
+        return;
+    }
+    uint32_t e = 0;
+    idx -= idx % width;  // indexAlign (Merkle.h:211)
+    for (int l = 0; l < t.nlev; ++l) {
+        const uint64_t len = t.len[l];
+        const uint64_t cnt = (len - idx) < static_cast<uint64_t>(width) ? (len - idx) : static_cast<uint64_t>(width);
+        uint32_t* rec = reinterpret_cast<uint32_t*>(out + 32ull * e);
+        rec[0] = bswap32(static_cast<uint32_t>(cnt));
+#pragma unroll
+        for (int k = 1; k < 8; ++k) rec[k] = 0;
+        ++e;
+        const uint8_t* src = l == 0 ? leaves + 32ull * idx : tree + 32ull * (t.pos[l] + 1 + idx);
+        for (uint64_t j = 0; j < cnt; ++j) copy_entry(out + 32ull * (e + j), src + 32ull * j);
+        e += static_cast<uint32_t>(cnt);
+        idx /= width;
+        idx -= idx % width;
+    }
+    plen[q] = e;
+}
+
+// verifyMerkleProof(proof, hash, root) (Merkle.h:45-81), one proof per lane.  ok = 1 / 0, or 2 for an
+// empty proof (the reference throws std::invalid_argument{"Empty input proof!"}).  A count record
+// that runs past the proof is "false" (the reference reads out of range there).
+template <int H>
+__global__ __launch_bounds__(256) void merkle_verify_kernel(const uint8_t* __restrict__ proofs, uint64_t stride,
+                                                            const uint32_t* __restrict__ plen,
+                                                            const uint8_t* __restrict__ hashes,
+                                                            const uint8_t* __restrict__ roots, int root_stride,
+                                                            uint64_t m, uint8_t* __restrict__ ok) {
+    const uint64_t q = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (q >= m) return;
+    const uint8_t* pr = proofs + 32ull * stride * q;
+    const uint32_t len = plen[q] < stride ? plen[q] : static_cast<uint32_t>(stride);
+    if (plen[q] == 0) {
+        ok[q] = 2;
+        return;
+    }
+    uint32_t h[8];
+    const uint32_t* hs = reinterpret_cast<const uint32_t*>(hashes + 32ull * q);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = hs[k];
+    bool good = plen[q] <= stride;
+    if (len > 1) {
+        uint32_t it = 0;
+        while (good && it < len) {
+            const uint32_t cnt = bswap32(reinterpret_cast<const uint32_t*>(pr + 32ull * it)[0]);
+            ++it;
+            if (cnt > len - it) {
+                good = false;
+                break;
+            }
+            bool found = false;
+            for (uint32_t j = 0; j < cnt; ++j) {
+                const uint32_t* en = reinterpret_cast<const uint32_t*>(pr + 32ull * (it + j));
+                bool eq = true;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) eq = eq && en[k] == h[k];
+                found = found || eq;
+            }
+            if (!found) {
+                good = false;
+                break;
+            }
+            const uint32_t bytes = cnt * 32u;
+            AlignedReader rd(pr + 32ull * it, bytes);
+            uint32_t d[8];
+            if (H == KECCAK256) keccak256_msg(rd, bytes, d);
+            else sm3_msg(rd, bytes, d);
+            uint8_t tmp[32];
+            store_digest(H, tmp, d);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h[k] = reinterpret_cast<const uint32_t*>(tmp)[k];
+            it += cnt;
+        }
+    }
+    const uint32_t* rt = reinterpret_cast<const uint32_t*>(roots + 32ull * (root_stride ? q : 0));
+#pragma unroll
+    for (int k = 0; k < 8; ++k) good = good && h[k] == rt[k];
+    ok[q] = good ? 1 : 0;
+}
+
+uint64_t merkle_proof_stride(uint64_t n, int width) {
+    if (n <= 1) return 1;
+    uint64_t s = 0;
+    for (uint64_t len = n; len > 1; len = (len + width - 1) / width) s += 1 + (len < static_cast<uint64_t>(width) ? len : width);
+    return s;
+}
+
+int launch_merkle_proofs(int width, const uint8_t* d_leaves, uint64_t n, const uint8_t* d_tree, const uint64_t* d_index,
+                         uint64_t m, uint8_t* d_proofs, uint32_t* d_len, hipStream_t st) {
+    if (n == 0 || width < 2 || width > 64) return BCOSGPU_E_ARG;
+    if (m == 0) return 0;
+    ProofLevels t{};
+    uint64_t pos = 0, len = n;
+    while (len > 1) {
+        if (t.nlev >= 64) return BCOSGPU_E_ARG;
+        t.len[t.nlev] = len;
+        const uint64_t next = (len + width - 1) / width;
+        // level nlev's nodes are the children grouped at this step; their parents sit at tree entry pos
+        // (count record) + 1 ..; for l >= 1 the nodes of level l live at the previous record's position
+        t.pos[t.nlev] = t.nlev == 0 ? 0 : pos;
+        if (t.nlev > 0) pos += len + 1;
+        ++t.nlev;
+        len = next;
+    }
+    hipLaunchKernelGGL(merkle_proof_kernel, dim3(grid_for(m, 256)), dim3(256), 0, st, d_leaves, d_tree, width, t, d_index, m,
+                       merkle_proof_stride(n, width), d_proofs, d_len);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_merkle_verify(int hasher, const uint8_t* d_proofs, uint64_t stride, const uint32_t* d_len,
+                         const uint8_t* d_hashes, const uint8_t* d_roots, int root_stride, uint64_t m, uint8_t* d_ok,
+                         hipStream_t st) {
+    if (m == 0) return 0;
+    if (hasher == SM3)
+        hipLaunchKernelGGL(merkle_verify_kernel<SM3>, dim3(grid_for(m, 256)), dim3(256), 0, st, d_proofs, stride, d_len,
+                           d_hashes, d_roots, root_stride, m, d_ok);
+    else
+        hipLaunchKernelGGL(merkle_verify_kernel<KECCAK256>, dim3(grid_for(m, 256)), dim3(256), 0, st, d_proofs, stride,
+                           d_len, d_hashes, d_roots, root_stride, m, d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
 int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* d_scratch,
                       uint8_t* d_root, hipStream_t st) {
     // d_scratch: >= 32 * (ceil(n/16) + ceil(n/256) + ...) bytes; levels ping into it

@@ -107,6 +107,27 @@ int bcosgpu_merkle_roots_batch(int hasher, int width, const uint8_t* leaves32, c
 int bcosgpu_merkle_roots_batch_dev(int hasher, int width, const uint8_t* d_leaves32, const uint64_t* block_off,
                                    size_t nblocks, uint8_t* d_work, uint8_t* d_roots32, void* stream);
 
+/* Merkle proofs (Merkle<H,width>::generateMerkleProof / verifyMerkleProof, Merkle.h:45-168; callers
+ * Ledger::getTransactionProof and the RPC proof queries).  A proof is a sequence of 32-byte entries:
+ * per level below the root a count record (BE u32 in bytes 0..3) and the <= width nodes of the group
+ * that contains the node (for a 1-leaf tree: the single leaf).  Proofs are written at a fixed stride
+ * of bcosgpu_merkle_proof_stride(n, width) entries; proof_len[q] = entries used.
+ * Index >= n is BCOSGPU_E_ARG ("Out of range!", Merkle.h:124-127).  Verification: ok[q] = 1 / 0, or
+ * 2 for an empty proof (the reference throws std::invalid_argument{"Empty input proof!"}).  Roots: one
+ * per proof (per_proof_root = 1) or one shared root (0). */
+uint64_t bcosgpu_merkle_proof_stride(uint64_t n, int width);
+int bcosgpu_merkle_proofs(int hasher, int width, const uint8_t* leaves32, size_t n, const uint64_t* index, size_t m,
+                          uint8_t* proofs, uint32_t* proof_len);
+/* d_tree = the output vector of bcosgpu_merkle_root_dev for the same leaves and width */
+int bcosgpu_merkle_proofs_dev(int width, const uint8_t* d_leaves32, size_t n, const uint8_t* d_tree,
+                              const uint64_t* d_index, size_t m, uint8_t* d_proofs, uint32_t* d_proof_len, void* stream);
+int bcosgpu_merkle_verify_proofs(int hasher, const uint8_t* proofs, uint64_t stride, const uint32_t* proof_len,
+                                 const uint8_t* hashes32, const uint8_t* roots32, int per_proof_root, size_t m,
+                                 uint8_t* ok);
+int bcosgpu_merkle_verify_proofs_dev(int hasher, const uint8_t* d_proofs, uint64_t stride, const uint32_t* d_proof_len,
+                                     const uint8_t* d_hashes32, const uint8_t* d_roots32, int per_proof_root, size_t m,
+                                     uint8_t* d_ok, void* stream);
+
 /* ---------------------------------------------------------------- signatures (SignatureCrypto, batched) */
 /* secp256k1 public-key recovery (Secp256k1Crypto::recover, Secp256k1Crypto.h:57-60).
  * pub64 / addr20 nullable; addr20 = right160(Keccak256(pub)) (calculateAddress, KeyPair.h:30-33). */

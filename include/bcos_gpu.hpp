@@ -145,6 +145,25 @@ public:
         check(bcosgpu_merkle_root(HASHER, static_cast<int>(width), BCOSGPU_MERKLE_NEW, originHashes[0].data(),
                                   originHashes.size(), root.data(), out[0].data()));
     }
+    /* generateMerkleProof(originHashes, index, out) (Merkle.h:121-168): out is replaced (the reference
+     * appends to a caller-cleared vector); index out of range throws std::invalid_argument */
+    void generateMerkleProof(const std::vector<HashType>& originHashes, uint64_t index, std::vector<HashType>& out) const {
+        if (originHashes.empty()) throw std::invalid_argument("Empty input");
+        if (index >= originHashes.size()) throw std::invalid_argument("Out of range!");
+        out.resize(bcosgpu_merkle_proof_stride(originHashes.size(), static_cast<int>(width)));
+        uint32_t len = 0;
+        check(bcosgpu_merkle_proofs(HASHER, static_cast<int>(width), originHashes[0].data(), originHashes.size(), &index,
+                                    1, out[0].data(), &len));
+        out.resize(len);
+    }
+    /* verifyMerkleProof(proof, hash, root) (Merkle.h:45-81); an empty proof throws std::invalid_argument */
+    bool verifyMerkleProof(const std::vector<HashType>& proof, const HashType& hash, const HashType& root) const {
+        if (proof.empty()) throw std::invalid_argument("Empty input proof!");
+        const uint32_t len = static_cast<uint32_t>(proof.size());
+        uint8_t ok = 0;
+        check(bcosgpu_merkle_verify_proofs(HASHER, proof[0].data(), proof.size(), &len, hash.data(), root.data(), 0, 1, &ok));
+        return ok == 1;
+    }
     HashType root(const std::vector<HashType>& originHashes) const {
         if (originHashes.empty()) throw std::invalid_argument("Empty input");
         HashType r{};

@@ -193,3 +193,53 @@ def receipt_preimage(version, gas_used, contract_address, status, output, logs, 
         out += bytes(data)
     out += (block_number & 0xFFFFFFFFFFFFFFFF).to_bytes(8, "big")
     return bytes(out)
+
+
+def _count_record(c):
+    return int(c).to_bytes(4, "big") + bytes(28)
+
+
+def merkle_proof(hasher, width, leaves, index):
+    """Merkle<H,width>::generateMerkleProof(originHashes, merkle, index, out), restated from
+    bcos-crypto/bcos-crypto/merkle/Merkle.h:121-168 over this oracle's tree (list of 32-byte entries)."""
+    leaves = np.ascontiguousarray(leaves, dtype=np.uint8).reshape(-1, 32)
+    n = leaves.shape[0]
+    if index >= n:
+        raise ValueError("Out of range!")
+    _, tree = merkle(hasher, width, leaves, want_tree=True)
+    if n == 1:
+        return [tree[0].tobytes()]
+    index -= (index + width) % width  # indexAlign (Merkle.h:211)
+    count = min(n - index, width)
+    out = [_count_record(count)] + [leaves[j].tobytes() for j in range(index, index + count)]
+    pos = 0
+    while pos < tree.shape[0]:
+        index //= width
+        index -= (index + width) % width
+        level_len = int.from_bytes(tree[pos, :4].tobytes(), "big")
+        pos += 1
+        if level_len == 1:
+            break
+        nxt = min(level_len - index, width)
+        out.append(_count_record(nxt))
+        out += [tree[pos + j].tobytes() for j in range(index, index + nxt)]
+        pos += level_len
+    return out
+
+
+def merkle_verify_proof(hasher, proof, h, root):
+    """verifyMerkleProof (Merkle.h:45-81); empty proof raises like std::invalid_argument."""
+    if len(proof) == 0:
+        raise ValueError("Empty input proof!")
+    h = bytes(h)
+    if len(proof) > 1:
+        it = 0
+        while it < len(proof):
+            count = int.from_bytes(proof[it][:4], "big")
+            it += 1
+            group = proof[it:it + count]
+            if len(group) < count or h not in group:
+                return False
+            h = hash_(hasher, b"".join(group))
+            it += count
+    return h == bytes(root)

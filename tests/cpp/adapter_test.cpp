@@ -82,6 +82,17 @@ int main() {
     threw = false;
     try { GpuMerkle<BCOSGPU_SM3, 16>().generateMerkle({}, out); } catch (const std::invalid_argument&) { threw = true; }
     CHECK(threw);
+    // Merkle proofs (testMerkle.cpp:91-121): every leaf verifies, a zero hash does not, empty proof throws
+    GpuMerkle<BCOSGPU_SM3, 16> m16;
+    for (uint64_t i = 0; i < leaves.size(); ++i) {
+        std::vector<HashType> proof;
+        m16.generateMerkleProof(leaves, i, proof);
+        CHECK(m16.verifyMerkleProof(proof, leaves[i], out.back()));
+        CHECK(!m16.verifyMerkleProof(proof, HashType{}, out.back()));
+    }
+    threw = false;
+    try { m16.verifyMerkleProof({}, leaves[0], out.back()); } catch (const std::invalid_argument&) { threw = true; }
+    CHECK(threw);
     // calculateTransactionRoot over a batch of blocks: Keccak width 2, n = 17 and an empty block
     auto roots = calculateRoots<BCOSGPU_KECCAK256>({leaves, {}});
     CHECK(roots.size() == 2);

@@ -144,3 +144,39 @@ def test_receipt_and_tx_roots(gpu, oracle):
         assert gpu.calculate_receipt_root(suite, []) == bytes(32)
         roots = gpu.calculate_roots_batch(suite, [list(leaves[:10]), [], list(leaves)])
         assert roots == [oracle.merkle(hasher, 2, leaves[:10]), bytes(32), oracle.merkle(hasher, 2, leaves)]
+
+
+@pytest.mark.parametrize("hasher,width", [(0, 2), (1, 2), (0, 16), (1, 3)])
+def test_merkle_proofs_vs_oracle(gpu, oracle, hasher, width):
+    """generateMerkleProof for every leaf of several trees == the oracle's restatement of Merkle.h:121-168;
+    verifyMerkleProof on the GPU == the oracle's (Merkle.h:45-81), incl. the reference test's negative
+    cases (testMerkle.cpp:91-121)."""
+    rng = np.random.default_rng(71 + width + hasher)
+    h = gpu.SM3() if hasher else gpu.Keccak256()
+    mk = gpu.Merkle(h, width)
+    for n in (1, 2, 3, width, width + 1, 17, 100, 257):
+        leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        root = oracle.merkle(hasher, width, leaves)
+        got = mk.generate_merkle_proofs(leaves, list(range(n)))
+        want = [oracle.merkle_proof(hasher, width, leaves, i) for i in range(n)]
+        assert got == want, n
+        proofs, hashes, expect = [], [], []
+        for i in range(n):
+            proofs.append(got[i]); hashes.append(leaves[i].tobytes()); expect.append(True)
+            proofs.append(got[i]); hashes.append(bytes(32)); expect.append(False)
+            if len(got[i]) > 1:
+                bad = list(got[i])
+                bad[int(rng.integers(0, len(bad)))] = bytes(32)
+                proofs.append(bad); hashes.append(leaves[i].tobytes())
+                expect.append(oracle.merkle_verify_proof(hasher, bad, leaves[i].tobytes(), root))
+        ok = mk.verify_merkle_proofs(proofs, hashes, [root] * len(proofs))
+        assert list(ok) == expect
+        assert mk.verify_merkle_proof(got[0], leaves[0].tobytes(), root)
+        assert mk.generate_merkle_proof(leaves, leaves[n - 1].tobytes()) == want[int(np.nonzero(
+            (leaves == leaves[n - 1]).all(axis=1))[0][0])]
+        with pytest.raises(ValueError):
+            mk.generate_merkle_proofs(leaves, [n])
+        with pytest.raises(ValueError):
+            mk.verify_merkle_proof([], leaves[0].tobytes(), root)
+    with pytest.raises(ValueError):
+        mk.generate_merkle_proof(rng.integers(0, 256, size=(4, 32), dtype=np.uint8), bytes(32))

@@ -112,3 +112,27 @@ def test_merkle_empty_throws(oracle):  # Merkle.h:172-175, testMerkle.cpp
     with pytest.raises(ValueError):
         oracle.merkle(oracle.SM3, 2, np.zeros((0, 32), dtype=np.uint8))
     assert oracle.merkle_old(oracle.SM3, np.zeros((0, 32), dtype=np.uint8)) == oracle.sm3(b"")
+
+
+def test_merkle_proof_restatement(oracle):
+    """The oracle's generateMerkleProof / verifyMerkleProof restatement against the reference's own
+    properties (testMerkle.cpp:91-121): every leaf's proof verifies against the root, a zero hash does
+    not, a proof with one entry replaced by zeros does not (when longer than 1), out of range raises,
+    an empty proof raises."""
+    rng = np.random.default_rng(77)
+    for width in (2, 3, 16):
+        for n in (1, 2, 3, 5, 17, 40):
+            leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+            root = oracle.merkle(0, width, leaves)
+            for i in range(n):
+                proof = oracle.merkle_proof(0, width, leaves, i)
+                assert oracle.merkle_verify_proof(0, proof, leaves[i].tobytes(), root)
+                assert not oracle.merkle_verify_proof(0, proof, bytes(32), root)
+                if len(proof) > 1:
+                    bad = list(proof)
+                    bad[int(rng.integers(0, len(bad)))] = bytes(32)
+                    assert not oracle.merkle_verify_proof(0, bad, leaves[i].tobytes(), root)
+            with pytest.raises(ValueError):
+                oracle.merkle_proof(0, width, leaves, n)
+            with pytest.raises(ValueError):
+                oracle.merkle_verify_proof(0, [], leaves[0].tobytes(), root)
