@@ -43,7 +43,7 @@ def chain(first, rest, dst, a, b):
     return lines
 
 
-def render(sig, locals_, ops, body, doc):
+def render(sig, locals_, ops, body, doc, clobbers='"vcc"'):
     outs, ins = ops.constraints()
     s = [f"// {doc}", f"__device__ __forceinline__ void {sig} {{"]
     if locals_:
@@ -53,7 +53,7 @@ def render(sig, locals_, ops, body, doc):
         s.append(f'        "{ln}' + ('\\n\\t"' if i + 1 < len(body) else '"'))
     s.append(f"        : {outs}")
     s.append(f"        : {ins}")
-    s.append('        : "vcc");')
+    s.append(f'        : {clobbers});')
     s.append("}")
     return "\n".join(s) + "\n"
 
@@ -69,14 +69,25 @@ def k1_addsub(sub):
     f, c, prop = (("v_sub_co_u32_e32", "v_subb_co_u32_e32", "v_subbrev_co_u32_e32") if sub else
                   ("v_add_co_u32_e32", "v_addc_co_u32_e32", "v_addc_co_u32_e32"))
     body = chain(f, c, R, A, B)
-    for _ in range(2):  # fold the carry/borrow out of 2^256 twice: 2^256 == 2^32 + 977 (mod p)
-        body += [f"v_cndmask_b32_e64 {T0}, 0, {K}, vcc", f"v_cndmask_b32_e64 {T1}, 0, 1, vcc",
-                 f"{f} {R[0]}, vcc, {R[0]}, {T0}", f"{c} {R[1]}, vcc, {R[1]}, {T1}, vcc"]
-        body += [f"{prop} {R[i]}, vcc, 0, {R[i]}, vcc" for i in range(2, 8)]
+    # fold the carry/borrow out of 2^256: 2^256 == 2^32 + 977 (mod p).  The fold touches words 0-1;
+    # it propagates into words 2-7 (and then needs a second fold) only when word 1 over/underflows,
+    # probability ~2^-32 per lane, so that tail is branched over unless some lane of the wave needs it
+    # (it adds each lane's own carry, 0 for the others).  s_nop covers the VALU-writes-VCC ->
+    # SALU-reads-VCC latency.
+    def fold():
+        return [f"v_cndmask_b32_e64 {T0}, 0, {K}, vcc", f"v_cndmask_b32_e64 {T1}, 0, 1, vcc",
+                f"{f} {R[0]}, vcc, {R[0]}, {T0}", f"{c} {R[1]}, vcc, {R[1]}, {T1}, vcc"]
+    body += fold()
+    body += ["s_nop 4", "s_cmp_eq_u64 vcc, 0", "s_cbranch_scc1 2f"]
+    body += [f"{prop} {R[i]}, vcc, 0, {R[i]}, vcc" for i in range(2, 8)]
+    body += fold()
+    body += [f"{prop} {R[i]}, vcc, 0, {R[i]}, vcc" for i in range(2, 8)]
+    body += ["2:"]
     name = "k1_sub_asm" if sub else "k1_add_asm"
     return render(f"{name}(uint32_t r[8], const uint32_t a[8], const uint32_t b[8])",
                   "uint32_t t0, t1; const uint32_t k977 = 977u;", ops, body,
-                  f"secp256k1 base field: r = a {'-' if sub else '+'} b (mod p), values in [0, 2^256)")
+                  f"secp256k1 base field: r = a {'-' if sub else '+'} b (mod p), values in [0, 2^256)",
+                  clobbers='"vcc", "scc"')
 
 
 def k1_normalize():
