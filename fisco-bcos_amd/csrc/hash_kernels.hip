@@ -6,6 +6,7 @@
 //   Merkle<Hasher,width>::generateMerkle  bcos-crypto/bcos-crypto/merkle/Merkle.h:170-208
 //     (per-level calculateLevelHashes :243-261 -> merkle_level_kernel, one node per lane)
 //   protocol::calculateMerkleProofRoot    bcos-protocol/bcos-protocol/ParallelMerkleProof.cpp:32-69
+#include <cstdlib>
 #include "hash_device.h"
 #include "engine.h"
 
@@ -112,10 +113,160 @@ uint64_t merkle_size(uint64_t n, int width) {
     return nodes;
 }
 
+// ------------------------------------------------------------------ fused Merkle tree (2 launches)
+// At merkleBench sizes the tree is latency-bound (a 512-byte width-16 node is 4 serial Keccak-f in one
+// lane), so the per-level launches of the generic path cost as much as the hashing at the top.  Here
+// one workgroup of B = width^k threads (the largest power of width <= 256) hashes B level-1 nodes and
+// then every level whose groups lie inside it, through LDS, writing each node into the reference's
+// output vector as it goes (groups align with workgroups because B is a power of width); a single
+// 1024-thread workgroup then finishes the top levels.  Same output vector as the per-level path.
+struct TreeLevels {
+    uint64_t pos[64];  // tree entry of the count record of level l + 1 (level 0 = leaves)
+    uint64_t cnt[64];  // nodes of level l + 1
+    int nlev;          // levels above the leaves (the last has one node)
+};
+
+template <int H>
+__device__ __forceinline__ void hash_nodes(const uint8_t* src, uint32_t cnt, uint32_t d[8]) {
+    const uint32_t len = cnt * 32u;
+    AlignedReader rd(src, len);
+    if (H == KECCAK256) keccak256_msg(rd, len, d);
+    else sm3_msg(rd, len, d);
+}
+
+template <int H, int W>
+__global__ __launch_bounds__(256) void merkle_wg_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w, int kin,
+                                                        uint8_t* __restrict__ tree, const TreeLevels t,
+                                                        uint8_t* __restrict__ root) {
+    __shared__ uint4 lds[2][256][2];
+    const uint32_t width = W ? W : static_cast<uint32_t>(w);
+    const uint32_t tid = threadIdx.x, B = blockDim.x;
+    uint64_t base = static_cast<uint64_t>(blockIdx.x) * B;  // first level-1 node of this workgroup
+    uint32_t nodes = static_cast<uint32_t>(t.cnt[0] - base < B ? t.cnt[0] - base : B);
+    uint32_t d[8];
+    if (tid < nodes) {
+        const uint64_t first = (base + tid) * width;
+        const uint32_t c = static_cast<uint32_t>(n - first < width ? n - first : width);
+        hash_nodes<H>(leaves + 32ull * first, c, d);
+        store_digest(H, tree + 32ull * (t.pos[0] + 1 + base + tid), d);
+        store_digest(H, reinterpret_cast<uint8_t*>(&lds[0][tid][0]), d);
+    }
+    int cur = 0;
+    const int top = kin + 1 < t.nlev ? kin + 1 : t.nlev;  // levels this kernel produces
+    for (int l = 1; l < top; ++l) {
+        __syncthreads();
+        const uint64_t nbase = base / width;
+        const uint32_t nn = (nodes + width - 1) / width;
+        if (tid < nn) {
+            const uint32_t c = nodes - tid * width < width ? nodes - tid * width : width;
+            hash_nodes<H>(reinterpret_cast<const uint8_t*>(&lds[cur][tid * width][0]), c, d);
+            store_digest(H, tree + 32ull * (t.pos[l] + 1 + nbase + tid), d);
+            store_digest(H, reinterpret_cast<uint8_t*>(&lds[cur ^ 1][tid][0]), d);
+        }
+        cur ^= 1;
+        nodes = nn;
+        base = nbase;
+    }
+    if (blockIdx.x == 0 && tid < static_cast<uint32_t>(t.nlev)) {  // count records (Merkle.h:189-204)
+        uint32_t* e = reinterpret_cast<uint32_t*>(tree + 32ull * t.pos[tid]);
+        e[0] = bswap32(static_cast<uint32_t>(t.cnt[tid]));
+#pragma unroll
+        for (int k = 1; k < 8; ++k) e[k] = 0;
+    }
+    if (top == t.nlev && root) {  // the whole tree fit in this (single) workgroup
+        __syncthreads();
+        if (tid == 0) {
+            const uint4* r = &lds[cur][0][0];
+            reinterpret_cast<uint4*>(root)[0] = r[0];
+            reinterpret_cast<uint4*>(root)[1] = r[1];
+        }
+    }
+}
+
+// levels [l0, t.nlev) (0-based, level l0 - 1 already in the tree) in ONE workgroup; root copy
+template <int H, int W>
+__global__ __launch_bounds__(1024) void merkle_top_kernel(int w, int l0, uint8_t* __restrict__ tree, const TreeLevels t,
+                                                          uint8_t* __restrict__ root) {
+    const uint32_t width = W ? W : static_cast<uint32_t>(w);
+    for (int l = l0; l < t.nlev; ++l) {
+        const uint64_t nin = t.cnt[l - 1];
+        const uint8_t* in = tree + 32ull * (t.pos[l - 1] + 1);
+        for (uint64_t j = threadIdx.x; j < t.cnt[l]; j += blockDim.x) {
+            const uint64_t first = j * width;
+            const uint32_t c = static_cast<uint32_t>(nin - first < width ? nin - first : width);
+            uint32_t d[8];
+            hash_nodes<H>(in + 32ull * first, c, d);
+            store_digest(H, tree + 32ull * (t.pos[l] + 1 + j), d);
+        }
+        __syncthreads();
+    }
+    if (root && threadIdx.x < 2) {
+        const uint4* r = reinterpret_cast<const uint4*>(tree + 32ull * (t.pos[t.nlev - 1] + 1));
+        reinterpret_cast<uint4*>(root)[threadIdx.x] = r[threadIdx.x];
+    }
+}
+
+static constexpr uint64_t kTopKernelMaxIn = 16384;  // inputs per level the single-workgroup kernel takes
+
+int launch_merkle_levelwise(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
+                            uint8_t* d_root, hipStream_t st);
+
 int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
                   uint8_t* d_root, hipStream_t st) {
     if (n == 0 || width < 2 || width > 64) return BCOSGPU_E_ARG;
+    const char* lw = getenv("BCOSGPU_MERKLE_LEVELWISE");  // A/B switch to the one-launch-per-level path
+    if (lw && atoi(lw) == 1) return launch_merkle_levelwise(hasher, width, d_leaves, n, d_tree, d_root, st);
     if (n == 1) {  // Merkle.h:177-182
+        hipLaunchKernelGGL(copy32_kernel, dim3(1), dim3(64), 0, st, d_leaves, d_tree);
+        if (d_root) hipLaunchKernelGGL(copy32_kernel, dim3(1), dim3(64), 0, st, d_leaves, d_root);
+        return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+    }
+    TreeLevels t{};
+    uint64_t pos = 0;
+    for (uint64_t m = n; m > 1;) {
+        if (t.nlev >= 64) return BCOSGPU_E_ARG;
+        m = (m + width - 1) / width;
+        t.pos[t.nlev] = pos;
+        t.cnt[t.nlev] = m;
+        pos += m + 1;
+        ++t.nlev;
+    }
+    int kin = 0;
+    uint32_t B = 1;
+    while (B * static_cast<uint32_t>(width) <= 256u) {
+        B *= width;
+        ++kin;
+    }
+    const dim3 g1(static_cast<unsigned>((t.cnt[0] + B - 1) / B));
+#define WG(HH, WW) hipLaunchKernelGGL((merkle_wg_kernel<HH, WW>), g1, dim3(B), 0, st, d_leaves, n, width, kin, d_tree, t, d_root)
+    if (hasher == SM3) {
+        if (width == 2) WG(SM3, 2); else if (width == 16) WG(SM3, 16); else WG(SM3, 0);
+    } else {
+        if (width == 2) WG(KECCAK256, 2); else if (width == 16) WG(KECCAK256, 16); else WG(KECCAK256, 0);
+    }
+#undef WG
+    int l = kin + 1;  // next level (0-based) to compute
+    while (l < t.nlev && t.cnt[l - 1] > kTopKernelMaxIn) {  // wide middle levels: one launch each
+        launch_level(hasher, width, d_tree + 32ull * (t.pos[l - 1] + 1), t.cnt[l - 1], d_tree + 32ull * (t.pos[l] + 1),
+                     t.cnt[l], st);
+        ++l;
+    }
+    if (l < t.nlev) {
+#define TOP(HH, WW) hipLaunchKernelGGL((merkle_top_kernel<HH, WW>), dim3(1), dim3(1024), 0, st, width, l, d_tree, t, d_root)
+        if (hasher == SM3) {
+            if (width == 2) TOP(SM3, 2); else if (width == 16) TOP(SM3, 16); else TOP(SM3, 0);
+        } else {
+            if (width == 2) TOP(KECCAK256, 2); else if (width == 16) TOP(KECCAK256, 16); else TOP(KECCAK256, 0);
+        }
+#undef TOP
+    }
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_merkle_levelwise(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
+                            uint8_t* d_root, hipStream_t st) {
+    if (n == 0 || width < 2 || width > 64) return BCOSGPU_E_ARG;
+    if (n == 1) {
         hipLaunchKernelGGL(copy32_kernel, dim3(1), dim3(64), 0, st, d_leaves, d_tree);
         if (d_root) hipLaunchKernelGGL(copy32_kernel, dim3(1), dim3(64), 0, st, d_leaves, d_root);
         return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
