@@ -277,6 +277,98 @@ __device__ __forceinline__ void sm3_64(const uint32_t m_be[16], uint32_t out[8])
     for (int i = 0; i < 8; ++i) out[i] = V[i];
 }
 
+// ------------------------------------------------------------------ lane-cooperative Keccak-256
+// For latency-bound hashing (the top levels of a Merkle tree: one 512-byte width-16 node is 4 serial
+// permutations), one state is spread over 25 lanes of a 32-lane group, lane t = x + 5y holding
+// A[x][y] as two 32-bit halves; a wave runs two states.  A round is ~20 VALU + 18 ds_bpermute per lane
+// (theta: 4 column gathers + C[x-1], C[x+1]; pi: 1 gather; chi: 2 row gathers) instead of ~170 VALU
+// in one lane.  Both 32-lane groups of the wave must call it together (ds_bpermute is wave-wide).
+struct KeccakCoop {
+    int gl;            // lane within the 32-lane group
+    int col[4];        // bpermute byte addresses of the column mates (x, y + k), k = 1..4
+    int xm1, xp1, xp2; // (x - 1, y), (x + 1, y), (x + 2, y)
+    int pisrc;         // pi: source lane of this lane's B position
+    uint32_t sh;       // rho: 32 - (r mod 32), 0 when r mod 32 == 0
+    bool swap;         // rho: r >= 32
+    uint32_t m0;       // all-ones on lane 0 (iota)
+    __device__ KeccakCoop() {
+        const int lane = static_cast<int>(__lane_id());
+        gl = lane & 31;
+        const int base = lane & 32;
+        const int t = gl < 25 ? gl : 0;
+        const int x = t % 5, y = t / 5;
+        auto addr = [&](int xx, int yy) { return (base + ((xx + 5) % 5) + 5 * ((yy + 5) % 5)) * 4; };
+#pragma unroll
+        for (int k = 0; k < 4; ++k) col[k] = addr(x, y + 1 + k);
+        xm1 = addr(x - 1, y);
+        xp1 = addr(x + 1, y);
+        xp2 = addr(x + 2, y);
+        // destination (X, Y) = (x, y) of this lane takes source (x', y') with y' = X, 2x' + 3y' = Y (mod 5)
+        const int sx = ((3 * (y - 3 * x)) % 5 + 5) % 5;
+        pisrc = addr(sx, x);
+        constexpr uint8_t R[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
+                                   25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
+        const int r = R[t];
+        swap = r >= 32;
+        sh = (r & 31) ? 32u - (r & 31) : 0u;
+        m0 = gl == 0 ? 0xffffffffu : 0u;
+    }
+    __device__ __forceinline__ static uint32_t bp(int addr, uint32_t v) {
+        return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(addr, static_cast<int>(v)));
+    }
+    __device__ __forceinline__ void permute(uint32_t& lo, uint32_t& hi) const {
+#pragma unroll 1
+        for (int round = 0; round < 24; ++round) {
+            // theta
+            const uint32_t c_lo = xor3(xor3(lo, bp(col[0], lo), bp(col[1], lo)), bp(col[2], lo), bp(col[3], lo));
+            const uint32_t c_hi = xor3(xor3(hi, bp(col[0], hi), bp(col[1], hi)), bp(col[2], hi), bp(col[3], hi));
+            const uint32_t m_lo = bp(xm1, c_lo), m_hi = bp(xm1, c_hi);
+            const uint32_t p_lo = bp(xp1, c_lo), p_hi = bp(xp1, c_hi);
+            lo = xor3(lo, m_lo, __builtin_amdgcn_alignbit(p_lo, p_hi, 31));
+            hi = xor3(hi, m_hi, __builtin_amdgcn_alignbit(p_hi, p_lo, 31));
+            // rho (per-lane rotation) then pi (gather)
+            uint32_t a = swap ? hi : lo, b = swap ? lo : hi;
+            if (sh) {
+                const uint32_t na = __builtin_amdgcn_alignbit(a, b, sh), nb = __builtin_amdgcn_alignbit(b, a, sh);
+                a = na;
+                b = nb;
+            }
+            lo = bp(pisrc, a);
+            hi = bp(pisrc, b);
+            // chi + iota
+            const uint64_t rc = kKeccakRC[round];
+            const uint32_t n_lo = chi32(lo, bp(xp1, lo), bp(xp2, lo));
+            const uint32_t n_hi = chi32(hi, bp(xp1, hi), bp(xp2, hi));
+            lo = n_lo ^ (static_cast<uint32_t>(rc) & m0);
+            hi = n_hi ^ (static_cast<uint32_t>(rc >> 32) & m0);
+        }
+    }
+    // Keccak-256 of msg[0..len) (len a multiple of 8, msg 8-byte aligned, global or LDS memory);
+    // lanes gl < 4 return digest word gl (bytes 8 gl .. 8 gl + 7) in lo/hi.
+    __device__ __forceinline__ void hash(const uint8_t* msg, uint32_t len, uint32_t& lo, uint32_t& hi) const {
+        lo = 0;
+        hi = 0;
+        const uint32_t nblocks = len / 136u + 1u;
+        for (uint32_t blk = 0; blk < nblocks; ++blk) {
+            const uint32_t pos = blk * 136u + 8u * static_cast<uint32_t>(gl);
+            uint32_t wlo = 0, whi = 0;
+            if (gl < 17) {
+                if (pos < len) {
+                    const uint2 w = *reinterpret_cast<const uint2*>(msg + pos);
+                    wlo = w.x;
+                    whi = w.y;
+                } else if (pos == len) {
+                    wlo = 1u;  // Keccak pad byte 0x01 (OpenSSLHasher.h:74-79)
+                }
+                if (blk + 1 == nblocks && gl == 16) whi ^= 0x80000000u;  // final 0x80
+            }
+            lo ^= wlo;
+            hi ^= whi;
+            permute(lo, hi);
+        }
+    }
+};
+
 // Store a 32-byte digest.  Keccak words are little-endian lanes (byte order == memory order);
 // SM3 words are big-endian.
 __device__ __forceinline__ void store_digest(int hasher, uint8_t* dst, const uint32_t d[8]) {

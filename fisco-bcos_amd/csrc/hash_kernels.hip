@@ -134,15 +134,32 @@ __device__ __forceinline__ void hash_nodes(const uint8_t* src, uint32_t cnt, uin
     else sm3_msg(rd, len, d);
 }
 
+// One tree node cooperatively: every 32-lane group of the workgroup hashes node `base + group` of a
+// level (Keccak only; all groups of a wave run the permutation together, idle ones on a dummy input).
+// Lanes 0..3 of a group write the digest to dst (and dst2 when non-null).
+template <int W>
+__device__ __forceinline__ void coop_level_pass(const KeccakCoop& kc, const uint8_t* in, uint64_t nin, uint32_t width,
+                                                uint64_t j, uint64_t nout, uint8_t* dst, uint8_t* dst2) {
+    const bool act = j < nout;
+    const uint64_t first = act ? j * width : 0;
+    const uint32_t c = act ? static_cast<uint32_t>(nin - first < width ? nin - first : width) : 1u;
+    uint32_t lo, hi;
+    kc.hash(in + 32ull * first, 32u * c, lo, hi);
+    if (act && kc.gl < 4) {
+        *reinterpret_cast<uint2*>(dst + 8 * kc.gl) = make_uint2(lo, hi);
+        if (dst2) *reinterpret_cast<uint2*>(dst2 + 8 * kc.gl) = make_uint2(lo, hi);
+    }
+}
+
 template <int H, int W>
-__global__ __launch_bounds__(256) void merkle_wg_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w, int kin,
-                                                        uint8_t* __restrict__ tree, const TreeLevels t,
+__global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w, int kin,
+                                                        int B, uint8_t* __restrict__ tree, const TreeLevels t,
                                                         uint8_t* __restrict__ root) {
     __shared__ uint4 lds[2][256][2];
     const uint32_t width = W ? W : static_cast<uint32_t>(w);
-    const uint32_t tid = threadIdx.x, B = blockDim.x;
+    const uint32_t tid = threadIdx.x, groups = blockDim.x / 32;
     uint64_t base = static_cast<uint64_t>(blockIdx.x) * B;  // first level-1 node of this workgroup
-    uint32_t nodes = static_cast<uint32_t>(t.cnt[0] - base < B ? t.cnt[0] - base : B);
+    uint32_t nodes = static_cast<uint32_t>(t.cnt[0] - base < static_cast<uint64_t>(B) ? t.cnt[0] - base : B);
     uint32_t d[8];
     if (tid < nodes) {
         const uint64_t first = (base + tid) * width;
@@ -157,9 +174,15 @@ __global__ __launch_bounds__(256) void merkle_wg_kernel(const uint8_t* __restric
         __syncthreads();
         const uint64_t nbase = base / width;
         const uint32_t nn = (nodes + width - 1) / width;
-        if (tid < nn) {
+        const uint8_t* in = reinterpret_cast<const uint8_t*>(&lds[cur][0][0]);
+        if (H == KECCAK256 && nn <= groups) {  // latency-bound level: 25 lanes per node
+            const KeccakCoop kc;
+            const uint32_t g = tid / 32;
+            coop_level_pass<W>(kc, in, nodes, width, g, nn, tree + 32ull * (t.pos[l] + 1 + nbase + g),
+                               reinterpret_cast<uint8_t*>(&lds[cur ^ 1][g < 256 ? g : 0][0]));
+        } else if (tid < nn) {
             const uint32_t c = nodes - tid * width < width ? nodes - tid * width : width;
-            hash_nodes<H>(reinterpret_cast<const uint8_t*>(&lds[cur][tid * width][0]), c, d);
+            hash_nodes<H>(in + 32u * tid * width, c, d);
             store_digest(H, tree + 32ull * (t.pos[l] + 1 + nbase + tid), d);
             store_digest(H, reinterpret_cast<uint8_t*>(&lds[cur ^ 1][tid][0]), d);
         }
@@ -188,15 +211,22 @@ template <int H, int W>
 __global__ __launch_bounds__(1024) void merkle_top_kernel(int w, int l0, uint8_t* __restrict__ tree, const TreeLevels t,
                                                           uint8_t* __restrict__ root) {
     const uint32_t width = W ? W : static_cast<uint32_t>(w);
+    const uint32_t groups = blockDim.x / 32;
     for (int l = l0; l < t.nlev; ++l) {
         const uint64_t nin = t.cnt[l - 1];
         const uint8_t* in = tree + 32ull * (t.pos[l - 1] + 1);
-        for (uint64_t j = threadIdx.x; j < t.cnt[l]; j += blockDim.x) {
-            const uint64_t first = j * width;
-            const uint32_t c = static_cast<uint32_t>(nin - first < width ? nin - first : width);
-            uint32_t d[8];
-            hash_nodes<H>(in + 32ull * first, c, d);
-            store_digest(H, tree + 32ull * (t.pos[l] + 1 + j), d);
+        if (H == KECCAK256 && t.cnt[l] <= groups) {  // latency-bound level: 25 lanes per node
+            const KeccakCoop kc;
+            const uint32_t g = threadIdx.x / 32;
+            coop_level_pass<W>(kc, in, nin, width, g, t.cnt[l], tree + 32ull * (t.pos[l] + 1 + g), nullptr);
+        } else {
+            for (uint64_t j = threadIdx.x; j < t.cnt[l]; j += blockDim.x) {
+                const uint64_t first = j * width;
+                const uint32_t c = static_cast<uint32_t>(nin - first < width ? nin - first : width);
+                uint32_t d[8];
+                hash_nodes<H>(in + 32ull * first, c, d);
+                store_digest(H, tree + 32ull * (t.pos[l] + 1 + j), d);
+            }
         }
         __syncthreads();
     }
@@ -238,7 +268,11 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
         ++kin;
     }
     const dim3 g1(static_cast<unsigned>((t.cnt[0] + B - 1) / B));
-#define WG(HH, WW) hipLaunchKernelGGL((merkle_wg_kernel<HH, WW>), g1, dim3(B), 0, st, d_leaves, n, width, kin, d_tree, t, d_root)
+    // Keccak: enough 32-lane groups that the second level runs one cooperative pass (B / width nodes)
+    uint32_t threads = B;
+    if (hasher == KECCAK256 && kin >= 1 && 32u * (B / width) > threads && 32u * (B / width) <= 512u) threads = 32u * (B / width);
+    const dim3 b1(threads);
+#define WG(HH, WW) hipLaunchKernelGGL((merkle_wg_kernel<HH, WW>), g1, b1, 0, st, d_leaves, n, width, kin, static_cast<int>(B), d_tree, t, d_root)
     if (hasher == SM3) {
         if (width == 2) WG(SM3, 2); else if (width == 16) WG(SM3, 16); else WG(SM3, 0);
     } else {
