@@ -94,6 +94,41 @@ class Transaction:
         return suite.hash(self.data.preimage())
 
 
+class _TxDataView(ctypes.Structure):
+    """bcosgpu_TransactionData (include/bcos_gpu.h): pointers into the caller's fields."""
+    _fields_ = [("version", ctypes.c_int32),
+                ("chain_id", ctypes.c_char_p), ("chain_id_len", ctypes.c_size_t),
+                ("group_id", ctypes.c_char_p), ("group_id_len", ctypes.c_size_t),
+                ("block_limit", ctypes.c_int64),
+                ("nonce", ctypes.c_char_p), ("nonce_len", ctypes.c_size_t),
+                ("to", ctypes.c_char_p), ("to_len", ctypes.c_size_t),
+                ("input", ctypes.c_char_p), ("input_len", ctypes.c_size_t),
+                ("abi", ctypes.c_char_p), ("abi_len", ctypes.c_size_t)]
+
+
+def pack_preimages(datas):
+    """The native packer (bcosgpu_pack_tx_preimages, host C++): list[TransactionData] ->
+    (uint8 packed preimages, uint64 offsets[n+1]) in the SoA layout bcosgpu_tx_verify_batch takes."""
+    n = len(datas)
+    views = (_TxDataView * max(n, 1))()
+    keep = []
+    for i, d in enumerate(datas):
+        fields = [d.chain_id.encode(), d.group_id.encode(), d.nonce.encode(), d.to.encode(), bytes(d.input),
+                  d.abi.encode()]
+        keep.append(fields)
+        v = views[i]
+        v.version = d.version
+        v.block_limit = d.block_limit
+        for name, b in zip(("chain_id", "group_id", "nonce", "to", "input", "abi"), fields):
+            setattr(v, name, b)
+            setattr(v, name + "_len", len(b))
+    size = int(lib().bcosgpu_tx_preimage_size(views, n))
+    out = np.zeros(max(size, 1), dtype=np.uint8)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    check(lib().bcosgpu_pack_tx_preimages(views, n, _ptr(out), size, _ptr(off)))
+    return out[:size], off
+
+
 def verify_packed(suite: CryptoSuite, pre, pre_off, sig, sig_off):
     """Batched Transaction::verify over packed buffers.
     Returns (txhash uint8[n,32], sender uint8[n,20], status uint8[n])."""
@@ -118,7 +153,7 @@ def verify_transactions(suite: CryptoSuite, txs):
     status = [STATUS_NONE] * len(txs)
     if not todo:
         return status
-    pre, pre_off = pack_messages([txs[i].data.preimage() for i in todo])
+    pre, pre_off = pack_preimages([txs[i].data for i in todo])
     sig, sig_off = pack_messages([bytes(txs[i].signature) for i in todo])
     _, sender, st = verify_packed(suite, pre, pre_off, sig, sig_off)
     for k, i in enumerate(todo):

@@ -34,8 +34,10 @@ __global__ void k(const uint32_t* in, const int* op, int n, uint32_t* out) {
 
 static void parse(const char* h, uint32_t* w) {
     char buf[65];
-    snprintf(buf, sizeof buf, "%064s", h);
-    for (int j = 0; j < 64; ++j) if (buf[j] == ' ') buf[j] = '0';
+    const size_t len = strlen(h) < 64 ? strlen(h) : 64;
+    memset(buf, '0', 64);
+    memcpy(buf + 64 - len, h + strlen(h) - len, len);
+    buf[64] = 0;
     for (int q = 0; q < 8; ++q) {
         char part[9];
         memcpy(part, buf + 8 * (7 - q), 8);
@@ -60,11 +62,11 @@ int main() {
     if (!n) return 0;
     uint32_t *din, *dout;
     int* dop;
-    hipMalloc(&din, in.size() * 4);
-    hipMalloc(&dout, n * 32);
-    hipMalloc(&dop, n * 4);
-    hipMemcpy(din, in.data(), in.size() * 4, hipMemcpyHostToDevice);
-    hipMemcpy(dop, ops.data(), n * 4, hipMemcpyHostToDevice);
+    if (hipMalloc(&din, in.size() * 4) != hipSuccess || hipMalloc(&dout, n * 32) != hipSuccess ||
+        hipMalloc(&dop, n * 4) != hipSuccess ||
+        hipMemcpy(din, in.data(), in.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dop, ops.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return 1;
     hipLaunchKernelGGL(k, dim3((n + 255) / 256), dim3(256), 0, 0, din, dop, n, dout);
     std::vector<uint32_t> out(8 * n);
     if (hipMemcpy(out.data(), dout, n * 32, hipMemcpyDeviceToHost) != hipSuccess) return 1;

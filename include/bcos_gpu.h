@@ -184,6 +184,28 @@ int bcosgpu_tx_verify_batch_dev(int suite, const uint8_t* d_pre, const uint64_t*
                                 uint8_t* d_txhash32, uint8_t* d_sender20, uint8_t* d_status,
                                 void* stream);
 
+/* ---------------------------------------------------------------- host-side preimage packer */
+/* A view of bcostars::TransactionData (bcos-tars-protocol/.../tars/Transaction.tars:2-11): pointers
+ * into the caller's decoded transaction, nothing is copied until packing. */
+typedef struct {
+    int32_t version;
+    const char* chain_id;  size_t chain_id_len;
+    const char* group_id;  size_t group_id_len;
+    int64_t block_limit;
+    const char* nonce;     size_t nonce_len;
+    const char* to;        size_t to_len;
+    const uint8_t* input;  size_t input_len;
+    const char* abi;       size_t abi_len;
+} bcosgpu_TransactionData;
+/* Total preimage bytes of n transactions. */
+uint64_t bcosgpu_tx_preimage_size(const bcosgpu_TransactionData* txs, size_t n);
+/* Packs the tx-hash preimages impl_calculate<Hasher>(Transaction) hashes (TarsHashable.h:16-41:
+ * be32(version) || chainID || groupID || be64(blockLimit) || nonce || to || input || abi) back to
+ * back into out (cap bytes) and writes offsets[n+1] -- the SoA layout bcosgpu_tx_verify_batch* take.
+ * Host only (no device needed); multithreaded for large batches.  BCOSGPU_E_ARG if cap is too small. */
+int bcosgpu_pack_tx_preimages(const bcosgpu_TransactionData* txs, size_t n, uint8_t* out, uint64_t cap,
+                              uint64_t* offsets);
+
 /* ---------------------------------------------------------------- wedpr-ABI single-call shims */
 /* Same layout as wedpr-crypto's CInputBuffer / COutputBuffer; return 0 (WEDPR_SUCCESS) or -1. */
 typedef struct { const char* data; uintptr_t len; } bcosgpu_CInputBuffer;

@@ -243,3 +243,11 @@ def merkle_verify_proof(hasher, proof, h, root):
             h = hash_(hasher, b"".join(group))
             it += count
     return h == bytes(root)
+
+
+def tx_preimage(version, chain_id, group_id, block_limit, nonce, to, input_, abi):
+    """impl_calculate<Hasher>(bcostars::Transaction) field order, restated from
+    bcos-tars-protocol/bcos-tars-protocol/impl/TarsHashable.h:29-40."""
+    return ((version & 0xFFFFFFFF).to_bytes(4, "big") + chain_id.encode() + group_id.encode()
+            + (block_limit & 0xFFFFFFFFFFFFFFFF).to_bytes(8, "big") + nonce.encode() + to.encode() + bytes(input_)
+            + abi.encode())

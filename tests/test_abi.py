@@ -3,6 +3,8 @@
 import ctypes
 import subprocess
 
+import numpy as np
+
 import bcos_gpu
 from bcos_gpu import _lib
 
@@ -66,3 +68,26 @@ def test_oracle_ecrecover_vector(oracle, kat):
     assert oracle.ecrecover(h + (29).to_bytes(32, "big") + h + s) == b""
     # only the last byte of v is read: (1 << 8) + 27 behaves as 27
     assert oracle.ecrecover(h + ((1 << 8) + 27).to_bytes(32, "big") + h + s) == oracle.ecrecover(inp)
+
+
+def test_native_preimage_packer(oracle):
+    """bcosgpu_pack_tx_preimages (host C++) == the Python mirror == the oracle's restatement of
+    TarsHashable.h:29-40, for ragged batches incl. empty fields, negative version / blockLimit and a
+    batch large enough to take the threaded path."""
+    from bcos_gpu import tx
+    rng = np.random.default_rng(3)
+    for n in (0, 1, 7, 20000):
+        datas = []
+        for i in range(n):
+            datas.append(bcos_gpu.TransactionData(
+                version=int(rng.integers(-2, 3)), chain_id="chain%d" % (i % 3) if i % 5 else "",
+                group_id="group0", block_limit=int(rng.integers(-10, 10**12)), nonce=str(int(rng.integers(0, 10**18))),
+                to=rng.bytes(20).hex() if i % 4 else "", input=rng.bytes(int(rng.integers(0, 300))),
+                abi="" if i % 7 else "[{}]"))
+        data, off = tx.pack_preimages(datas)
+        assert len(off) == n + 1 and int(off[-1]) == len(data)
+        for i in (list(range(min(n, 50))) + ([n - 1] if n else [])):
+            d = datas[i]
+            got = data[int(off[i]):int(off[i + 1])].tobytes()
+            assert got == d.preimage() == oracle.tx_preimage(d.version, d.chain_id, d.group_id, d.block_limit,
+                                                             d.nonce, d.to, d.input, d.abi)
