@@ -1401,7 +1401,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_split_kernel(const uint8_t* 
 // four waves in phase A (each recomputes u1: hashing and one inversion are cheaper than a sync),
 // so phase C is the two cooperative GLV chains only.  Bit-identical to tx_verify_kernel<0, *>.
 #ifdef BCOSGPU_COOP_TIMING  // tools/coopbench.hip: phase timestamps of workgroup 0
-__device__ uint64_t g_coop_t[4][4];
+__device__ uint64_t g_coop_t[4][6];
 #define COOP_T(k) \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_coop_t[threadIdx.x >> 6][k] = clock64()
 #else
@@ -1416,7 +1416,7 @@ struct CoopLds {
     uint32_t flags[64];               // bit0 scalars ok, bit1 R ok, bit2 neg1, bit3 neg2
     uint4 ex[2][2][5][2][64];         // [chain][writer role][slot][word quad][lane]; slots 0-2: exchange 0, 3: 1, 4: 2
     uint32_t tabphx[8][8][64];        // beta * x of the table entries (chain 1's phi(R) table)
-    uint32_t pt[5][25][64];           // chain results 0/1, G partials 2..4 (X, Y, Z, inf)
+    uint32_t pt[4][25][64];           // chain results 0/1, G partials 2..3 (X, Y, Z, inf)
 };
 
 struct CoopCtx {
@@ -1749,12 +1749,12 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
             }
             L.flags[lane] = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
         }
-        // comb windows: wave 0 -> [0, 12), wave 3 -> [12, 24), wave 1 (after its split) -> [24, 32)
-        const int lo = wave == 0 ? 0 : (wave == 3 ? 12 : 24);
-        const int hi = wave == 0 ? 12 : (wave == 3 ? 24 : 32);
-        Jac G;
-        comb_range_k1(G, u1, tab, lo, hi);
-        coop_store_jac(L.pt[2 + (wave == 0 ? 0 : (wave == 3 ? 1 : 2))], G, lane);
+        // comb windows of u1 * G: wave 0 -> [0, 16), wave 3 -> [16, 32) (wave 1 has the GLV split)
+        if (wave != 1) {
+            Jac G;
+            comb_range_k1(G, u1, tab, wave == 0 ? 0 : 16, wave == 0 ? 16 : 32);
+            coop_store_jac(L.pt[wave == 0 ? 2 : 3], G, lane);
+        }
     }
     COOP_T(1);
     __syncthreads();
@@ -1783,13 +1783,11 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
     if (c.role == 0) coop_store_jac(L.pt[c.chain], acc, lane);
     __syncthreads();
     // ---------------------------------------------------------------- phase D
-    if (wave == 1) {  // G part: partials 0 + 1 + 2
-        Jac G0, G1, G2, S, T;
+    if (wave == 1) {  // G part: partials 0 + 1
+        Jac G0, G1, T;
         coop_load_jac(G0, L.pt[2], lane);
         coop_load_jac(G1, L.pt[3], lane);
-        coop_load_jac(G2, L.pt[4], lane);
-        CurveK1::add(S, G0, G1);
-        CurveK1::add(T, S, G2);
+        CurveK1::add(T, G0, G1);
         coop_store_jac(L.pt[2], T, lane);
     } else if (wave == 0) {  // R part on E', mapped to E
         Jac P0, P1, Q;
@@ -1809,7 +1807,9 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
         CurveK1::add(R, Q, G);
         const bool ok = (flags & 3u) == 3u && !R.inf;
         Aff A;
+        COOP_T(4);
         CurveK1::to_aff(A, R);
+        COOP_T(5);
         FieldK1::normalize(A.x);
         FieldK1::normalize(A.y);
         uint32_t ad[5] = {0, 0, 0, 0, 0};
