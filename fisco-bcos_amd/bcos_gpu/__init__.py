@@ -6,6 +6,7 @@ from ._lib import BcosGpuError, ensure_device, header_symbols, lib
 from .crypto import (SM3, CryptoSuite, Hash, InvalidSignature, Keccak256, Merkle, SM2Crypto,
                      Secp256k1Crypto, calculate_merkle_proof_root, pack_messages, right160,
                      secp256k1_suite, sm_suite)
+from . import tars
 from .tx import (LogEntry, Transaction, TransactionData, TransactionReceipt, TransactionReceiptData,
                  calculate_receipt_root, calculate_roots_batch, calculate_transaction_root, verify_packed,
                  verify_transactions)

@@ -65,6 +65,11 @@ _SIGS = {
     "bcosgpu_tx_verify_batch_dev": (_I, [_I, _P, _P, _P, _P, _SZ, _P, _P, _P, _P]),
     "bcosgpu_tx_preimage_size": (ctypes.c_uint64, [_P, _SZ]),
     "bcosgpu_pack_tx_preimages": (_I, [_P, _SZ, _P, ctypes.c_uint64, _P]),
+    "bcosgpu_tars_decode_work_size": (ctypes.c_uint64, [_SZ]),
+    "bcosgpu_tars_tx_decode_dev": (_I, [_P, _P, _SZ, _P, _P, _P, _P, _P, _P, ctypes.c_uint64, _P]),
+    "bcosgpu_tars_tx_verify_batch": (_I, [_I, _P, _P, _SZ, _I, _I, _P, _P, _P]),
+    "bcosgpu_tars_tx_verify_batch_dev": (_I, [_I, _P, _P, _SZ, _I, _I, _P, _P, _P, _P, _P, ctypes.c_uint64, _P, _P,
+                                              _P, _P]),
     "bcosgpu_wedpr_secp256k1_recover_public_key": (ctypes.c_int8, [_P, _P, _P]),
     "bcosgpu_wedpr_sm2_verify": (ctypes.c_int8, [_P, _P, _P]),
 }

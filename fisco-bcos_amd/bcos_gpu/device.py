@@ -101,3 +101,30 @@ def tx_verify(suite, pre, pre_off, sig, sig_off, txhash, sender, status, stream=
     n = pre_off.numel() - 1
     check(lib().bcosgpu_tx_verify_batch_dev(suite, _p(pre), _p(pre_off), _p(sig), _p(sig_off), n, _p(txhash),
                                             _p(sender), _p(status), _s(stream)))
+
+
+def tars_decode_work_size(n):
+    return int(lib().bcosgpu_tars_decode_work_size(n))
+
+
+def tars_tx_decode(enc, enc_off, pre, pre_off, sig, sig_off, dec_status, work, stream=None):
+    """Device Tars decode of n transactions into the packed preimage / signature layout
+    (bcosgpu_tars_tx_decode_dev); dec_status may be None."""
+    _dev(enc)
+    n = enc_off.numel() - 1
+    check(lib().bcosgpu_tars_tx_decode_dev(_p(enc), _p(enc_off), n, _p(pre), _p(pre_off), _p(sig), _p(sig_off),
+                                           None if dec_status is None else _p(dec_status), _p(work),
+                                           work.numel() * work.element_size(), _s(stream)))
+
+
+def tars_tx_verify(suite, enc, enc_off, pre, pre_off, sig, sig_off, work, txhash, sender, status, check_sig=True,
+                   check_hash=False, stream=None):
+    """Device createTransaction: decode + hash (+ Transaction::verify when check_sig)
+    (bcosgpu_tars_tx_verify_batch_dev)."""
+    _dev(enc)
+    n = enc_off.numel() - 1
+    check(lib().bcosgpu_tars_tx_verify_batch_dev(suite, _p(enc), _p(enc_off), n, int(bool(check_sig)),
+                                                 int(bool(check_hash)), _p(pre),
+                                                 _p(pre_off), _p(sig), _p(sig_off), _p(work),
+                                                 work.numel() * work.element_size(), _p(txhash), _p(sender),
+                                                 _p(status), _s(stream)))

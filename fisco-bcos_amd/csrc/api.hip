@@ -542,6 +542,85 @@ int bcosgpu_tx_verify_batch(int suite, const uint8_t* pre, const uint64_t* pre_o
     return 0;
 }
 
+// ------------------------------------------------------------------ Tars-encoded transactions
+uint64_t bcosgpu_tars_decode_work_size(size_t n) { return tars_decode_work_bytes(n); }
+
+int bcosgpu_tars_tx_decode_dev(const uint8_t* d_enc, const uint64_t* d_enc_off, size_t n, uint8_t* d_pre,
+                               uint64_t* d_pre_off, uint8_t* d_sig, uint64_t* d_sig_off, uint8_t* d_dec_status,
+                               void* d_work, uint64_t work_bytes, void* stream) {
+    if (n == 0) return 0;
+    if (!d_enc || !d_enc_off || !d_pre || !d_pre_off || !d_sig || !d_sig_off || !d_work)
+        return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_tars_tx_decode(d_enc, d_enc_off, n, d_pre, d_pre_off, d_sig, d_sig_off, d_dec_status, d_work,
+                                   work_bytes, as_stream(stream));
+    if (rc == BCOSGPU_E_ARG) return set_err(rc, "work buffer too small or batch too large");
+    return rc ? hip_err(hipGetLastError(), "tars decode launch") : 0;
+}
+
+int bcosgpu_tars_tx_verify_batch_dev(int suite, const uint8_t* d_enc, const uint64_t* d_enc_off, size_t n,
+                                     int check_sig, int check_hash, uint8_t* d_pre, uint64_t* d_pre_off, uint8_t* d_sig,
+                                     uint64_t* d_sig_off, void* d_work, uint64_t work_bytes, uint8_t* d_txhash32,
+                                     uint8_t* d_sender20, uint8_t* d_status, void* stream) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return set_err(BCOSGPU_E_ARG, "bad suite");
+    if (n == 0) return 0;
+    if (!d_enc || !d_enc_off || !d_pre || !d_pre_off || !d_sig || !d_sig_off || !d_work || !d_txhash32 ||
+        !d_sender20 || !d_status)
+        return set_err(BCOSGPU_E_ARG, "null pointer");
+    hipStream_t st = as_stream(stream);
+    int rc = launch_tars_tx_decode(d_enc, d_enc_off, n, d_pre, d_pre_off, d_sig, d_sig_off, nullptr, d_work,
+                                   work_bytes, st);
+    if (rc == BCOSGPU_E_ARG) return set_err(rc, "work buffer too small or batch too large");
+    if (!rc && check_sig) {
+        rc = launch_tx_verify(suite, d_pre, d_pre_off, d_sig, d_sig_off, n, d_txhash32, d_sender20, d_status, st);
+    } else if (!rc) {  // checkSig = false: decode + hash only (TransactionFactoryImpl.h:52-60)
+        rc = launch_hash_batch(suite == BCOSGPU_SUITE_SM2 ? BCOSGPU_SM3 : BCOSGPU_KECCAK256, d_pre, d_pre_off, n,
+                               d_txhash32, st);
+        if (!rc && (hipMemsetAsync(d_sender20, 0, 20 * n, st) != hipSuccess ||
+                    hipMemsetAsync(d_status, 0, n, st) != hipSuccess))
+            rc = BCOSGPU_E_HIP;
+    }
+    if (!rc) rc = launch_tars_finish(d_enc, d_work, nullptr, d_txhash32, d_status, n, check_hash, st);
+    return rc ? hip_err(hipGetLastError(), "tars tx verify launch") : 0;
+}
+
+int bcosgpu_tars_tx_verify_batch(int suite, const uint8_t* enc, const uint64_t* enc_off, size_t n, int check_sig,
+                                 int check_hash, uint8_t* txhash32, uint8_t* sender20, uint8_t* status) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return set_err(BCOSGPU_E_ARG, "bad suite");
+    if (n == 0) return 0;
+    if (!enc || !enc_off || !txhash32 || !sender20 || !status) return set_err(BCOSGPU_E_ARG, "null pointer");
+    for (size_t i = 0; i < n; ++i)
+        if (enc_off[i + 1] < enc_off[i]) return set_err(BCOSGPU_E_ARG, "offsets must be non-decreasing");
+    const uint64_t base = enc_off[0], bytes = enc_off[n] - base;
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    const uint64_t work = tars_decode_work_bytes(n);
+    HIP_OK(w->b[0].ensure(bytes + 8));
+    HIP_OK(w->b[1].ensure((n + 1) * 8));
+    HIP_OK(w->b[2].ensure(bytes + 12 * n + 8));  // preimages
+    HIP_OK(w->b[3].ensure(2 * (n + 1) * 8));     // preimage + signature offsets
+    HIP_OK(w->b[4].ensure(bytes + 8));           // signatures
+    HIP_OK(w->b[5].ensure(n * 53));              // txhash, sender, status
+    HIP_OK(w->b[6].ensure(work));
+    std::vector<uint64_t> off(n + 1);
+    for (size_t i = 0; i <= n; ++i) off[i] = enc_off[i] - base;
+    HIP_OK(hipMemcpyAsync(w->b[0].p, enc + base, bytes, hipMemcpyHostToDevice, w->stream));
+    HIP_OK(hipMemcpyAsync(w->b[1].p, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, w->stream));
+    uint64_t* pre_off = w->b[3].as<uint64_t>();
+    uint8_t* out = w->b[5].as<uint8_t>();
+    rc = bcosgpu_tars_tx_verify_batch_dev(suite, w->b[0].as<uint8_t>(), w->b[1].as<uint64_t>(), n, check_sig,
+                                          check_hash,
+                                          w->b[2].as<uint8_t>(), pre_off, w->b[4].as<uint8_t>(), pre_off + (n + 1),
+                                          w->b[6].p, work, out, out + 32 * n, out + 52 * n, w->stream);
+    if (rc) return rc;
+    HIP_OK(hipMemcpyAsync(txhash32, out, n * 32, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipMemcpyAsync(sender20, out + 32 * n, n * 20, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipMemcpyAsync(status, out + 52 * n, n, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
 // ------------------------------------------------------------------ wedpr-ABI shims
 int8_t bcosgpu_wedpr_secp256k1_recover_public_key(const bcosgpu_CInputBuffer* hash,
                                                    const bcosgpu_CInputBuffer* sig,

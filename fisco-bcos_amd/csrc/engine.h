@@ -44,4 +44,13 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
                      const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n,
                      uint8_t* d_txhash, uint8_t* d_sender, uint8_t* d_status, hipStream_t st);
 
+// tars_kernels.hip
+uint64_t tars_decode_work_bytes(uint64_t n);
+int launch_tars_tx_decode(const uint8_t* d_enc, const uint64_t* d_enc_off, uint64_t n, uint8_t* d_pre,
+                          uint64_t* d_pre_off, uint8_t* d_sig, uint64_t* d_sig_off, uint8_t* d_dec_status,
+                          void* d_work, uint64_t work_bytes, hipStream_t st);
+// d_dec may be null: the decode status kept in d_work by launch_tars_tx_decode(d_dec_status = null)
+int launch_tars_finish(const uint8_t* d_enc, const void* d_work, const uint8_t* d_dec, const uint8_t* d_txhash,
+                       uint8_t* d_status, uint64_t n, int check_hash, hipStream_t st);
+
 }  // namespace bcosgpu

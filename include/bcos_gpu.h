@@ -184,6 +184,31 @@ int bcosgpu_tx_verify_batch_dev(int suite, const uint8_t* d_pre, const uint64_t*
                                 uint8_t* d_txhash32, uint8_t* d_sender20, uint8_t* d_status,
                                 void* stream);
 
+/* ---------------------------------------------------------------- Tars-encoded transactions */
+/* Batched TransactionFactoryImpl::createTransaction(txData, checkSig, checkHash)
+ * (bcos-tars-protocol/bcos-tars-protocol/protocol/TransactionFactoryImpl.h:46-85), decode included:
+ * decode n Tars-encoded bcostars::Transaction (TransactionImpl.cpp:38-41 -> TarsSerializable.h:28-35, the
+ * tarscpp wire format), recompute the tx hash and, when check_sig, recover / verify the signature and
+ * derive the sender (sender = 0 otherwise).  Callers: JsonRpcImpl_2_0.cpp:443-444 (sendTransaction,
+ * checkSig false, checkHash true), TxPool.cpp:96 (pushed txs, checkSig false).
+ * Encoded tx i = enc[enc_off[i] .. enc_off[i+1]).  status[i]: 0 ok, 1 InvalidSignature (verify throws),
+ * 2 the decode throws, 3 check_hash != 0 and a non-empty dataHash differs from the recomputed hash. */
+int bcosgpu_tars_tx_verify_batch(int suite, const uint8_t* enc, const uint64_t* enc_off, size_t n, int check_sig,
+                                 int check_hash, uint8_t* txhash32, uint8_t* sender20, uint8_t* status);
+/* Work buffer for the device entry points below: >= bcosgpu_tars_decode_work_size(n) bytes. */
+uint64_t bcosgpu_tars_decode_work_size(size_t n);
+/* Device decode only: writes the packed preimages / signatures in the layout bcosgpu_tx_verify_batch_dev
+ * takes.  d_pre >= enc bytes + 12 n, d_sig >= enc bytes, d_pre_off / d_sig_off n + 1 entries,
+ * d_dec_status n bytes (0 / 2; may be null). */
+int bcosgpu_tars_tx_decode_dev(const uint8_t* d_enc, const uint64_t* d_enc_off, size_t n, uint8_t* d_pre,
+                               uint64_t* d_pre_off, uint8_t* d_sig, uint64_t* d_sig_off, uint8_t* d_dec_status,
+                               void* d_work, uint64_t work_bytes, void* stream);
+/* Device decode + verify, stream-ordered (the buffers as for bcosgpu_tars_tx_decode_dev). */
+int bcosgpu_tars_tx_verify_batch_dev(int suite, const uint8_t* d_enc, const uint64_t* d_enc_off, size_t n,
+                                     int check_sig, int check_hash, uint8_t* d_pre, uint64_t* d_pre_off, uint8_t* d_sig,
+                                     uint64_t* d_sig_off, void* d_work, uint64_t work_bytes, uint8_t* d_txhash32,
+                                     uint8_t* d_sender20, uint8_t* d_status, void* stream);
+
 /* ---------------------------------------------------------------- host-side preimage packer */
 /* A view of bcostars::TransactionData (bcos-tars-protocol/.../tars/Transaction.tars:2-11): pointers
  * into the caller's decoded transaction, nothing is copied until packing. */
