@@ -100,6 +100,7 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
+    ap.add_argument("--no-tars", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
 
@@ -214,6 +215,8 @@ def main():
         }
         if not args.no_merkle:
             line["merkle_c1"] = merkle_c1()
+        if world == 1 and n and not args.no_tars:
+            line["create_transaction"] = create_transaction_leg(b, suite, n, status[:n])
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
@@ -260,6 +263,42 @@ def host_api_rate(b, suite, n, reps=5):
     dt = (time.perf_counter() - t0) / reps
     return {"value": n / dt, "unit": "tx/s", "ms_per_batch": dt * 1e3,
             "path": "bcosgpu_tx_verify_batch (host buffers: H2D + kernel + D2H + sync)"}
+
+
+def create_transaction_leg(b, suite, n, want_status, reps=20):
+    """The same batch from raw Tars encodings (createTransaction(bytes, checkSig = true, checkHash = true),
+    TransactionFactoryImpl.h:46-85): device decode + pack + verify + hash check, HBM-resident.  Reported
+    beside `value` (which starts from packed preimages); decode_ms is the decode + pack share."""
+    import torch
+    from bcos_gpu import device, synth
+    enc, off = synth.tars_encodings(b)
+    pre = torch.empty(enc.numel() + 12 * n, dtype=torch.uint8, device="cuda")
+    sig = torch.empty(enc.numel(), dtype=torch.uint8, device="cuda")
+    pre_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    sig_off = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    work = torch.empty(device.tars_decode_work_size(n), dtype=torch.uint8, device="cuda")
+    th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        c.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(c) / reps
+
+    full = timed(lambda: device.tars_tx_verify(suite, enc, off, pre, pre_off, sig, sig_off, work, th, snd, st,
+                                               check_sig=True, check_hash=True))
+    same = bool(torch.equal(st, want_status))
+    dec = timed(lambda: device.tars_tx_decode(enc, off, pre, pre_off, sig, sig_off, None, work))
+    return {"value": n / (full * 1e-3), "unit": "tx/s", "ms_per_batch": full, "decode_ms": dec,
+            "bytes_per_tx": enc.numel() // n, "status_matches_packed_path": same,
+            "path": "bcosgpu_tars_tx_verify_batch_dev (decode + pack + verify + dataHash check)"}
 
 
 def merkle_c1():

@@ -97,3 +97,27 @@ def make_batch(suite, n, seed=0xF15C0BC5, flip_frac=0.01, bad_v_frac=0.001, dev=
             corrupted[badv] = 2
     sig_off = torch.arange(0, (n + 1) * sig_len, sig_len, dtype=torch.int64, device=dev)
     return SignedBatch(suite, pre, pre_off, sig.view(-1), sig_off, sig_len, corrupted, n)
+
+
+def tars_encodings(b: SignedBatch):
+    """The batch as Tars-encoded bcostars::Transaction bytes (TransactionImpl::encode), built on the
+    device from the fixed-layout preimages: data {chainID, groupID, blockLimit 500, nonce, to, input},
+    dataHash (the tx hash) and signature, in the exact bytes bcos_gpu.tars.encode_transaction writes.
+    Returns (uint8 enc[n * L], int64 offsets[n + 1])."""
+    n, dev = b.n, b.pre.device
+    pre = b.pre.view(n, PREIMAGE_LEN)
+    txhash = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    device.hash_batch(device.SM3 if b.suite == device.SUITE_SM2 else device.KECCAK256, b.pre, b.pre_off, txhash)
+
+    def const(bs):
+        return torch.tensor(list(bs), dtype=torch.uint8, device=dev).expand(n, len(bs))
+
+    sig_head = b"\x3d\x00\x01\x00\x80" if b.sig_len == 128 else b"\x3d\x00\x00" + bytes([b.sig_len])
+    cols = [const(b"\x1a\x26\x06"), pre[:, 4:10], const(b"\x36\x06"), pre[:, 10:16],
+            const(b"\x41\x01\xf4\x56\x13"), pre[:, 24:43], const(b"\x66\x28"), pre[:, 43:83],
+            const(b"\x7d\x00\x00\x44"), pre[:, 83:151], const(b"\x0b\x2d\x00\x00\x20"), txhash,
+            const(sig_head), b.sig.view(n, b.sig_len)]
+    enc = torch.cat(cols, dim=1).contiguous()
+    L = enc.shape[1]
+    off = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device=dev)
+    return enc.view(-1), off

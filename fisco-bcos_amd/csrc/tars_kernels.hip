@@ -51,10 +51,10 @@ __global__ __launch_bounds__(256) void tars_tx_decode_kernel(const uint8_t* __re
     dec_status[i] = ok ? 0 : 2;
 }
 
-__device__ __forceinline__ uint8_t* copy_bytes(uint8_t* dst, const uint8_t* src, uint32_t n) {
-    for (uint32_t k = 0; k < n; ++k) dst[k] = src[k];
-    return dst + n;
-}
+// Pack: a team of kPackTeam lanes per tx writes its preimage / signature bytes, consecutive lanes on
+// consecutive bytes, so the loads from the encoding and the stores to the packed buffers coalesce (one
+// lane per tx walking its own bytes touched a different cache line per lane per byte).
+constexpr int kPackTeam = 16;
 
 __global__ __launch_bounds__(256) void tars_tx_pack_kernel(const uint8_t* __restrict__ enc, uint64_t n,
                                                            const TxFields* __restrict__ fields,
@@ -62,41 +62,72 @@ __global__ __launch_bounds__(256) void tars_tx_pack_kernel(const uint8_t* __rest
                                                            const uint64_t* __restrict__ sig_off,
                                                            const uint8_t* __restrict__ dec_status,
                                                            uint8_t* __restrict__ pre, uint8_t* __restrict__ sig) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t i = t / kPackTeam;
+    const uint32_t l = static_cast<uint32_t>(t % kPackTeam);
     if (i >= n || dec_status[i]) return;
     const TxFields f = fields[i];
-    uint8_t* o = pre + pre_off[i];
+    // preimage segments: be32(version) | chainID | groupID | be64(blockLimit) | nonce | to | input | abi
+    const uint32_t e0 = 4, e1 = e0 + f.len[F_CHAIN], e2 = e1 + f.len[F_GROUP], e3 = e2 + 8,
+                   e4 = e3 + f.len[F_NONCE], e5 = e4 + f.len[F_TO], e6 = e5 + f.len[F_INPUT], e7 = e6 + f.len[F_ABI];
     const uint32_t v = static_cast<uint32_t>(f.version);
-    o[0] = v >> 24; o[1] = v >> 16; o[2] = v >> 8; o[3] = v;
-    o = copy_bytes(o + 4, enc + f.off[F_CHAIN], f.len[F_CHAIN]);
-    o = copy_bytes(o, enc + f.off[F_GROUP], f.len[F_GROUP]);
-    const uint64_t b = static_cast<uint64_t>(f.block_limit);
-    for (int k = 0; k < 8; ++k) o[k] = static_cast<uint8_t>(b >> (56 - 8 * k));
-    o = copy_bytes(o + 8, enc + f.off[F_NONCE], f.len[F_NONCE]);
-    o = copy_bytes(o, enc + f.off[F_TO], f.len[F_TO]);
-    o = copy_bytes(o, enc + f.off[F_INPUT], f.len[F_INPUT]);
-    copy_bytes(o, enc + f.off[F_ABI], f.len[F_ABI]);
-    copy_bytes(sig + sig_off[i], enc + f.off[F_SIG], f.len[F_SIG]);
+    const uint64_t bl = static_cast<uint64_t>(f.block_limit);
+    uint8_t* o = pre + pre_off[i];
+    for (uint32_t j = l; j < e7; j += kPackTeam) {
+        uint8_t x;
+        if (j < e0) {
+            x = static_cast<uint8_t>(v >> (24 - 8 * j));
+        } else if (j >= e2 && j < e3) {
+            x = static_cast<uint8_t>(bl >> (56 - 8 * (j - e2)));
+        } else {
+            uint64_t src;
+            if (j < e1) src = f.off[F_CHAIN] + (j - e0);
+            else if (j < e2) src = f.off[F_GROUP] + (j - e1);
+            else if (j < e4) src = f.off[F_NONCE] + (j - e3);
+            else if (j < e5) src = f.off[F_TO] + (j - e4);
+            else if (j < e6) src = f.off[F_INPUT] + (j - e5);
+            else src = f.off[F_ABI] + (j - e6);
+            x = enc[src];
+        }
+        o[j] = x;
+    }
+    uint8_t* so = sig + sig_off[i];
+    const uint8_t* si = enc + f.off[F_SIG];
+    for (uint32_t j = l; j < f.len[F_SIG]; j += kPackTeam) so[j] = si[j];
 }
 
 // createTransaction's verdict order (TransactionFactoryImpl.h:46-84): the decode throws (2), then with
-// checkHash a non-empty dataHash that differs from the recomputed hash throws (3, :61-77), then verify (1)
-__global__ void tars_finish_kernel(const uint8_t* __restrict__ enc, const TxFields* __restrict__ fields,
-                                   const uint8_t* __restrict__ dec, const uint8_t* __restrict__ txhash,
-                                   uint8_t* __restrict__ status, uint64_t n, int check_hash) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    if (dec[i]) {
-        status[i] = dec[i];
-        return;
+// checkHash a non-empty dataHash that differs from the recomputed hash throws (3, :62-78), then verify (1).
+// Eight lanes per tx compare four bytes each; a wave ballot combines them.
+__global__ __launch_bounds__(256) void tars_finish_kernel(const uint8_t* __restrict__ enc,
+                                                          const TxFields* __restrict__ fields,
+                                                          const uint8_t* __restrict__ dec,
+                                                          const uint8_t* __restrict__ txhash,
+                                                          uint8_t* __restrict__ status, uint64_t n, int check_hash) {
+    const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t i = t / 8;
+    const uint32_t l = static_cast<uint32_t>(t % 8);
+    bool differs = false;
+    uint8_t d = 0;
+    if (i < n) {
+        d = dec[i];
+        if (!d && check_hash) {
+            const uint32_t len = fields[i].len[F_HASH];
+            if (len == 32) {
+                const uint8_t* h = enc + fields[i].off[F_HASH] + 4 * l;
+                const uint32_t want = reinterpret_cast<const uint32_t*>(txhash + 32 * i)[l];
+                const uint32_t got = h[0] | (h[1] << 8) | (h[2] << 16) | (static_cast<uint32_t>(h[3]) << 24);
+                differs = got != want;
+            } else if (len != 0) {
+                differs = true;
+            }
+        }
     }
-    if (!check_hash) return;
-    const uint32_t len = fields[i].len[F_HASH];
-    if (len == 0) return;
-    bool same = len == 32;
-    const uint8_t* h = enc + fields[i].off[F_HASH];
-    for (uint32_t k = 0; same && k < 32; ++k) same = h[k] == txhash[32 * i + k];
-    if (!same) status[i] = 3;
+    const uint64_t bad = __ballot(differs);  // every lane of the wave reaches this
+    const uint32_t lane = threadIdx.x & 63;
+    if (i >= n || l != 0) return;
+    if (d) status[i] = d;
+    else if ((bad >> lane) & 0xffull) status[i] = 3;
 }
 
 // Work buffer: fields[n] | pre_len[n] | sig_len[n] | dec_status[n] | scan temp storage
@@ -136,7 +167,8 @@ int launch_tars_tx_decode(const uint8_t* d_enc, const uint64_t* d_enc_off, uint6
     if (hipcub::DeviceScan::InclusiveSum(w, temp, pre_len, d_pre_off + 1, static_cast<int>(n), st) != hipSuccess ||
         hipcub::DeviceScan::InclusiveSum(w, temp, sig_len, d_sig_off + 1, static_cast<int>(n), st) != hipSuccess)
         return BCOSGPU_E_HIP;
-    hipLaunchKernelGGL(tars_tx_pack_kernel, dim3(grid), dim3(256), 0, st, d_enc, n, fields, d_pre_off, d_sig_off,
+    hipLaunchKernelGGL(tars_tx_pack_kernel, dim3(static_cast<unsigned>((n * kPackTeam + 255) / 256)), dim3(256), 0, st,
+                       d_enc, n, fields, d_pre_off, d_sig_off,
                        d_dec_status, d_pre, d_sig);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
@@ -147,7 +179,7 @@ int launch_tars_finish(const uint8_t* d_enc, const void* d_work, const uint8_t* 
     const uint8_t* w = static_cast<const uint8_t*>(d_work);
     const TxFields* fields = reinterpret_cast<const TxFields*>(w);
     if (!d_dec) d_dec = w + ((n * sizeof(TxFields) + 255) & ~255ull) + 2 * ((n * 8 + 255) & ~255ull);
-    hipLaunchKernelGGL(tars_finish_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, st, d_enc,
+    hipLaunchKernelGGL(tars_finish_kernel, dim3(static_cast<unsigned>((n * 8 + 255) / 256)), dim3(256), 0, st, d_enc,
                        fields, d_dec, d_txhash, d_status, n, check_hash);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }

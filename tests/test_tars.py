@@ -445,3 +445,23 @@ def test_gpu_device_decode_matches_packer(gpu):
     assert np.array_equal(pre.cpu().numpy()[:int(po[-1])], want_pre)
     assert np.array_equal(sig_off.cpu().numpy().astype(np.uint64), want_sig_off)
     assert np.array_equal(sig.cpu().numpy()[:len(want_sig)], want_sig)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("suite", [0, 1])
+def test_synth_tars_encodings_match_writer(gpu, suite):
+    """The bench's device-built encodings are byte-identical to TarsWriter's for the same transactions."""
+    from bcos_gpu import synth
+    b = synth.make_batch(suite, 64, seed=3 + suite, flip_frac=0.0, bad_v_frac=0.0)
+    enc, off = synth.tars_encodings(b)
+    enc, off = enc.cpu().numpy(), off.cpu().numpy()
+    pre = b.pre.cpu().numpy().reshape(64, -1)
+    sig = b.sig.cpu().numpy().reshape(64, -1)
+    cs = gpu.sm_suite() if suite else gpu.secp256k1_suite()
+    for i in range(64):
+        p = pre[i].tobytes()
+        d = TransactionData(version=0, chain_id=p[4:10].decode(), group_id=p[10:16].decode(), block_limit=500,
+                            nonce=p[24:43].decode(), to=p[43:83].decode(), input=p[83:151], abi="")
+        assert d.preimage() == p
+        want = encode_transaction(Transaction(d, signature=sig[i].tobytes()), data_hash=cs.hash(p))
+        assert enc[off[i]:off[i + 1]].tobytes() == want, i
