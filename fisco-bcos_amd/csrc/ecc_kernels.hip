@@ -1397,11 +1397,12 @@ __global__ __launch_bounds__(256, 1) void tx_verify_split_kernel(const uint8_t* 
 //   madd (7M + 4S):          a: Z1Z1, U2, HH, Z3 | b: Z1Z1, S2', S2, rr^2 -> a: J | b: V
 //                            -> a: rr (V - X3) | b: Y J        6 instead of 11
 // Both waves of a pair hold the whole point after every operation (they compute bit-identical
-// values), so the four waves run the same barrier schedule.  The G part u1*G is split over the
-// four waves in phase A (each recomputes u1: hashing and one inversion are cheaper than a sync),
-// so phase C is the two cooperative GLV chains only.  Bit-identical to tx_verify_kernel<0, *>.
+// values), so the four waves run the same barrier schedule.  Phase A needs no square root before
+// the table (the R chain runs on an isomorphic curve, see phase A), so the hash, r^-1, the R table,
+// the square root and the comb windows of u1*G run side by side on the four waves, and phase C is
+// the two cooperative GLV chains only.  Bit-identical to tx_verify_kernel<0, *>.
 #ifdef BCOSGPU_COOP_TIMING  // tools/coopbench.hip: phase timestamps of workgroup 0
-__device__ uint64_t g_coop_t[4][6];
+__device__ uint64_t g_coop_t[4][8];
 #define COOP_T(k) \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_coop_t[threadIdx.x >> 6][k] = clock64()
 #else
@@ -1416,8 +1417,22 @@ struct CoopLds {
     uint32_t flags[64];               // bit0 scalars ok, bit1 R ok, bit2 neg1, bit3 neg2
     uint4 ex[2][2][5][2][64];         // [chain][writer role][slot][word quad][lane]; slots 0-2: exchange 0, 3: 1, 4: 2
     uint32_t tabphx[8][8][64];        // beta * x of the table entries (chain 1's phi(R) table)
-    uint32_t pt[4][25][64];           // chain results 0/1, G partials 2..3 (X, Y, Z, inf)
+    uint32_t pt[5][25][64];           // chain results 0/1, G partials 2..4 (X, Y, Z, inf)
+    uint32_t xe[8][64];               // e = H(m) mod n (wave 3 -> waves 0, 1)
+    uint32_t xrinv[8][64];            // r^-1, Montgomery form (wave 0 -> waves 1, 3)
+    uint32_t ys[8][64];               // y of R with v's parity (wave 2 -> phase D)
+    uint32_t rflag[64];               // R verdict (wave 2)
+    uint32_t post[2];                 // phase-A hand-off flags: 0 r^-1 ready, 1 e ready
 };
+
+// One-way hand-offs between waves inside phase A: the producer writes its per-lane values, then
+// releases the flag; the consumer acquires it.  Workgroup scope, so these are LDS-only fences.
+__device__ __forceinline__ void coop_post(uint32_t* f) {
+    __hip_atomic_store(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void coop_wait(uint32_t* f) {
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(1);
+}
 
 struct CoopCtx {
     CoopLds* L;
@@ -1663,78 +1678,106 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
         pb = pre_off[i + 1];
     }
     const uint32_t slen = (sb - sa) > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(sb - sa);
+    if (threadIdx.x == 0) {
+        L.post[0] = 0u;
+        L.post[1] = 0u;
+    }
+    __syncthreads();
     // ---------------------------------------------------------------- phase A
-    if (wave == 2) {
-        fe r, s;
-        uint32_t v = 0;
-        bool ok = false;
-        if (active) ok = parse_sig65(sig + sa, slen, r, s, v);
-        else { fe_zero(r); fe_zero(s); }
-        fe x;
+    // R = (x, y) is needed through y only at the very end: the R chain runs on the isomorphic curve
+    // E_w: Y^2 = X^3 + 7 w^3 (w = x^3 + 7), where R' = (w x, w^2) needs no square root, and a point
+    // (X, Y, Z) of E_w is (X, Y, Z y) on E.  So the square root runs beside the table instead of
+    // before it.  Schedule: wave 0 inverts r, wave 3 hashes (they swap r^-1 and e through LDS flags),
+    // wave 1 builds the R' table and then the GLV split, wave 2 takes the square root; the comb
+    // windows of u1 * G go to waves 0 and 3 and the tail of wave 1.
+    fe r, s;
+    uint32_t v = 0;
+    bool ok = false;
+    if (active) ok = parse_sig65(sig + sa, slen, r, s, v);
+    else { fe_zero(r); fe_zero(s); }
+    if (wave == 1 || wave == 2) {
+        fe x, rhs, t, seven;
         fe_copy(x, r);
+        bool okr = ok;
         if (v & 2u) {
-            ok = ok && fe_lt_k(r, kK1PminusN);
+            okr = okr && fe_lt_k(r, kK1PminusN);
             fe_add_k(x, r, ParamN1::M);
         }
-        fe rhs, y, t, seven;
         FieldK1::sqr(t, x);
         FieldK1::mul(rhs, t, x);
         fe_zero(seven);
         seven.v[0] = 7;
-        FieldK1::add(rhs, rhs, seven);
-        FieldK1::sqrt_cand(y, rhs);
-        FieldK1::sqr(t, y);
-        ok = ok && FieldK1::eq(t, rhs);
-        FieldK1::normalize(y);
-        fe ny;
-        FieldK1::neg(ny, y);
-        FieldK1::normalize(ny);
-        fe_cmov(y, ny, (y.v[0] & 1u) != (v & 1u));
-        Aff R, A[8];
-        fe_copy(R.x, x);
-        fe_copy(R.y, y);
-        fe Zc;
-        {
-            Jac T[8];
-            multiples8<CurveK1>(T, R);
-            coz_table_k1(A, Zc, T);
+        FieldK1::add(rhs, rhs, seven);  // w
+        if (wave == 2) {
+            fe y;
+            FieldK1::sqrt_cand(y, rhs);
+            FieldK1::sqr(t, y);
+            okr = okr && FieldK1::eq(t, rhs);
+            FieldK1::normalize(y);
+            fe ny;
+            FieldK1::neg(ny, y);
+            FieldK1::normalize(ny);
+            fe_cmov(y, ny, (y.v[0] & 1u) != (v & 1u));
+            lds_store_fe(L.ys, y, lane);
+            L.rflag[lane] = okr ? 2u : 0u;
+            COOP_T(6);
+        } else {
+            Aff R, A[8];
+            FieldK1::mul(R.x, rhs, x);  // w x
+            FieldK1::sqr(R.y, rhs);     // w^2
+            fe Zc;
+            {
+                Jac T[8];
+                multiples8<CurveK1>(T, R);
+                coz_table_k1(A, Zc, T);
+            }
+            fe beta;
+            fe_set(beta, kGlvBeta);
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                lds_store_fe(L.tab[j], A[j].x, lane);
+                lds_store_fe(L.tab[j] + 8, A[j].y, lane);
+                fe bx;
+                FieldK1::mul(bx, A[j].x, beta);
+                lds_store_fe(L.tabphx[j], bx, lane);
+            });
+            lds_store_fe(L.zc, Zc, lane);
+            COOP_T(6);
         }
-        fe beta;
-        fe_set(beta, kGlvBeta);
-        Unroll<0, 8>::run([&](auto J) {
-            constexpr int j = decltype(J)::value;
-            lds_store_fe(L.tab[j], A[j].x, lane);
-            lds_store_fe(L.tab[j] + 8, A[j].y, lane);
-            fe bx;
-            FieldK1::mul(bx, A[j].x, beta);
-            lds_store_fe(L.tabphx[j], bx, lane);
-        });
-        lds_store_fe(L.zc, Zc, lane);
-        L.pt[1][24][lane] = ok ? 2u : 0u;  // R verdict travels in a scratch slot until phase C
-    } else {
-        // every other wave: tx hash, r^-1, u1 = -e/r; wave 1 also u2 and its GLV split; waves 0, 1, 3
-        // each take a third-ish of the comb windows of u1 * G
-        fe e, r, s;
-        uint32_t v = 0;
-        bool ok = false;
+    }
+    if (!ok) {  // scalars of a rejected signature: any well-defined values (the verdict is already 1)
+        fe_zero(r);
+        r.v[0] = 1;
+        fe_zero(s);
+    }
+    if (wave == 3) {
         uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (active) {
             const uint32_t len = static_cast<uint32_t>(pb - pa);
             ByteReader rd(pre + pa, len);
             keccak256_msg(rd, len, d);
-            if (wave == 1) store_digest(KECCAK256, txhash + 32 * i, d);
-            ok = parse_sig65(sig + sa, slen, r, s, v);
+            store_digest(KECCAK256, txhash + 32 * i, d);
         }
+        fe e;
         fe_from_be_words(e, d);
         reduce_once(e, ParamN1::M);
-        if (!ok) {
-            fe_zero(r);
-            r.v[0] = 1;
-            fe_zero(s);
-        }
-        fe rm, rinv, u1;
+        lds_store_fe(L.xe, e, lane);
+        coop_post(&L.post[1]);
+        COOP_T(7);
+    } else if (wave == 0) {
+        fe rm, rinv;
         FieldN1::from_plain(rm, r);
         FieldInv<FieldN1>::inv(rinv, rm);
+        lds_store_fe(L.xrinv, rinv, lane);
+        coop_post(&L.post[0]);
+        COOP_T(7);
+    }
+    if (wave != 2) {
+        coop_wait(&L.post[0]);
+        coop_wait(&L.post[1]);
+        fe e, rinv, u1;
+        lds_load_fe(e, L.xe, lane);
+        lds_load_fe(rinv, L.xrinv, lane);
         FieldN1::mul(u1, e, rinv);
         FieldN1::neg(u1, u1);
         if (wave == 1) {
@@ -1749,17 +1792,18 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
             }
             L.flags[lane] = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
         }
-        // comb windows of u1 * G: wave 0 -> [0, 16), wave 3 -> [16, 32) (wave 1 has the GLV split)
-        if (wave != 1) {
-            Jac G;
-            comb_range_k1(G, u1, tab, wave == 0 ? 0 : 16, wave == 0 ? 16 : 32);
-            coop_store_jac(L.pt[wave == 0 ? 2 : 3], G, lane);
-        }
+        // comb windows of u1 * G: wave 0 [0, kCombW0), wave 3 [kCombW0, kCombW1), wave 1 [kCombW1, 32)
+        constexpr int kCombW0 = 12, kCombW1 = 24;
+        Jac G;
+        const int lo = wave == 0 ? 0 : wave == 3 ? kCombW0 : kCombW1;
+        const int hi = wave == 0 ? kCombW0 : wave == 3 ? kCombW1 : 32;
+        comb_range_k1(G, u1, tab, lo, hi);
+        coop_store_jac(L.pt[wave == 0 ? 2 : wave == 3 ? 3 : 4], G, lane);
     }
     COOP_T(1);
     __syncthreads();
     // ---------------------------------------------------------------- phase C: two cooperative GLV chains
-    const uint32_t flags = L.flags[lane] | L.pt[1][24][lane];
+    const uint32_t flags = L.flags[lane] | L.rflag[lane];
     CoopCtx c{&L, wave >> 1, wave & 1, lane};
     fe k;
     fe_zero(k);
@@ -1767,7 +1811,6 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
     for (int q = 0; q < 4; ++q) k.v[q] = L.k[c.chain][q][lane];
     const bool neg = c.chain == 0 ? (flags & 4u) != 0 : (flags & 8u) != 0;
     const bool phi = c.chain == 1;
-    __syncthreads();  // pt[1][24] (R verdict) is read before the chain results overwrite it
     Jac acc;
     CurveK1::set_inf(acc);
     coop_add_digit(acc, c, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
@@ -1783,19 +1826,23 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
     if (c.role == 0) coop_store_jac(L.pt[c.chain], acc, lane);
     __syncthreads();
     // ---------------------------------------------------------------- phase D
-    if (wave == 1) {  // G part: partials 0 + 1
-        Jac G0, G1, T;
+    if (wave == 1) {  // G part: partials 0 + 1 + 2
+        Jac G0, G1, T, U;
         coop_load_jac(G0, L.pt[2], lane);
         coop_load_jac(G1, L.pt[3], lane);
         CurveK1::add(T, G0, G1);
-        coop_store_jac(L.pt[2], T, lane);
-    } else if (wave == 0) {  // R part on E', mapped to E
+        coop_load_jac(G0, L.pt[4], lane);
+        CurveK1::add(U, T, G0);
+        coop_store_jac(L.pt[2], U, lane);
+    } else if (wave == 0) {  // R part: co-Z curve -> E_w (Z * Zc) -> E (Z * y)
         Jac P0, P1, Q;
         coop_load_jac(P0, L.pt[0], lane);
         coop_load_jac(P1, L.pt[1], lane);
-        fe Zc;
+        fe Zc, y;
         lds_load_fe(Zc, L.zc, lane);
+        lds_load_fe(y, L.ys, lane);
         CurveK1::add(Q, P0, P1);
+        FieldK1::mul(Zc, Zc, y);
         FieldK1::mul(Q.Z, Q.Z, Zc);
         coop_store_jac(L.pt[0], Q, lane);
     }

@@ -30,13 +30,16 @@ int main() {
         hipLaunchKernelGGL(tx_verify_coop_kernel, dim3((n + 63) / 64), dim3(256), 0, 0, dp, dpo, ds, dso, n, k1, dh, dsn, dst);
         hipDeviceSynchronize();
     }
-    uint64_t t[4][6];
+    uint64_t t[4][8];
     hipMemcpyFromSymbol(t, HIP_SYMBOL(g_coop_t), sizeof(t));
     printf("{\"cycles_since_start\": {");
     for (int w = 0; w < 4; ++w)
         printf("%s\"wave%d\": [%llu, %llu, %llu]", w ? ", " : "", w, (unsigned long long)(t[w][1] - t[w][0]),
                (unsigned long long)(t[w][2] - t[w][0]), (unsigned long long)(t[w][3] - t[w][0]));
-    printf("}, \"wave0_phase_d\": [%llu, %llu], \"probes\": \"end of phase A work, end of phase C loop, end of kernel; wave 0: before / after the affine inversion\"}\n",
+    printf("}, \"probes6_7\": [");
+    for (int w = 0; w < 4; ++w)
+        printf("%s[%llu, %llu]", w ? ", " : "", (unsigned long long)(t[w][6] - t[w][0]), (unsigned long long)(t[w][7] - t[w][0]));
+    printf("], \"wave0_phase_d\": [%llu, %llu], \"probes\": \"end of phase A work, end of phase C loop, end of kernel; wave 0: before / after the affine inversion\"}\n",
            (unsigned long long)(t[0][4] - t[0][0]), (unsigned long long)(t[0][5] - t[0][0]));
     return 0;
 }
