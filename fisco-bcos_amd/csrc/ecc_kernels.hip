@@ -1403,11 +1403,17 @@ __global__ __launch_bounds__(256, 1) void tx_verify_split_kernel(const uint8_t* 
 // the two cooperative GLV chains only.  Bit-identical to tx_verify_kernel<0, *>.
 #ifdef BCOSGPU_COOP_TIMING  // tools/coopbench.hip: phase timestamps of workgroup 0
 __device__ uint64_t g_coop_t[4][8];
+__device__ uint64_t g_dbl_t[4][8];
+#define DBL_T(k) \
+    if (c.probe && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][k] = clock64()
 #define COOP_T(k) \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_coop_t[threadIdx.x >> 6][k] = clock64()
 #else
 #define COOP_T(k) \
     do {          \
+    } while (0)
+#define DBL_T(k) \
+    do {         \
     } while (0)
 #endif
 struct CoopLds {
@@ -1437,6 +1443,7 @@ __device__ __forceinline__ void coop_wait(uint32_t* f) {
 struct CoopCtx {
     CoopLds* L;
     int chain, role, lane;
+    bool probe;  // BCOSGPU_COOP_TIMING: stamp the doubling phases (workgroup 0, one doubling)
     // An exchange slot is rewritten only after the barrier that follows the partner's read of it,
     // so one slot per (exchange, field element) suffices across consecutive operations.
     // Layout [quad][lane] of uint4: one fe is two conflict-free ds_write_b128 / ds_read_b128.
@@ -1459,6 +1466,7 @@ struct CoopCtx {
 // P = 2 P (a = 0, dbl-2009-l), P replicated on both waves of the pair.
 __device__ __forceinline__ void coop_dbl(Jac& P, const CoopCtx& c) {
     fe A, B, C, D, E, F, t, X3, Y3, Z3;
+    DBL_T(0);
     if (c.role == 0) {
         FieldK1::sqr(A, P.X);
         FieldK1::add(E, A, A);
@@ -1474,7 +1482,9 @@ __device__ __forceinline__ void coop_dbl(Jac& P, const CoopCtx& c) {
         c.put(0, 0, C);
         c.put(0, 1, t);
     }
+    DBL_T(1);
     __syncthreads();
+    DBL_T(2);
     if (c.role == 0) {
         c.get(0, 0, C);
         c.get(0, 1, t);
@@ -1502,7 +1512,9 @@ __device__ __forceinline__ void coop_dbl(Jac& P, const CoopCtx& c) {
         FieldK1::add(Z3, Z3, Z3);
         c.put(1, 0, Z3);
     }
+    DBL_T(3);
     __syncthreads();
+    DBL_T(4);
     if (c.role == 0) c.get(1, 0, Z3);
     else c.get(1, 0, Y3);
     fe_copy(P.X, X3);
@@ -1804,7 +1816,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
     __syncthreads();
     // ---------------------------------------------------------------- phase C: two cooperative GLV chains
     const uint32_t flags = L.flags[lane] | L.rflag[lane];
-    CoopCtx c{&L, wave >> 1, wave & 1, lane};
+    CoopCtx c{&L, wave >> 1, wave & 1, lane, false};
     fe k;
     fe_zero(k);
 #pragma unroll
@@ -1817,7 +1829,13 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
 #pragma unroll 1
     for (int w = 31; w >= 0; --w) {
         coop_dbl(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+        c.probe = blockIdx.x == 0 && w == 20;
+#endif
         coop_dbl(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+        c.probe = false;
+#endif
         coop_dbl(acc, c);
         coop_dbl(acc, c);
         coop_add_digit(acc, c, booth_digit128(k), neg, phi);

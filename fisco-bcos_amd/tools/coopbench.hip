@@ -39,6 +39,13 @@ int main() {
     printf("}, \"probes6_7\": [");
     for (int w = 0; w < 4; ++w)
         printf("%s[%llu, %llu]", w ? ", " : "", (unsigned long long)(t[w][6] - t[w][0]), (unsigned long long)(t[w][7] - t[w][0]));
+    uint64_t dt[4][8];
+    hipMemcpyFromSymbol(dt, HIP_SYMBOL(g_dbl_t), sizeof(dt));
+    printf("], \"dbl\": [");
+    for (int w = 0; w < 4; ++w)
+        printf("%s[%llu, %llu, %llu, %llu]", w ? ", " : "", (unsigned long long)(dt[w][1] - dt[w][0]),
+               (unsigned long long)(dt[w][2] - dt[w][0]), (unsigned long long)(dt[w][3] - dt[w][0]),
+               (unsigned long long)(dt[w][4] - dt[w][0]));
     printf("], \"wave0_phase_d\": [%llu, %llu], \"probes\": \"end of phase A work, end of phase C loop, end of kernel; wave 0: before / after the affine inversion\"}\n",
            (unsigned long long)(t[0][4] - t[0][0]), (unsigned long long)(t[0][5] - t[0][0]));
     return 0;

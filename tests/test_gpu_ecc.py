@@ -19,8 +19,8 @@ def _dev_sign(gpu, suite, sk, h):
     import torch
     from bcos_gpu import device
     n = sk.shape[0]
-    d_sk = torch.from_numpy(np.ascontiguousarray(sk)).cuda()
-    d_h = torch.from_numpy(np.ascontiguousarray(h)).cuda()
+    d_sk = torch.from_numpy(np.array(sk, dtype=np.uint8, copy=True)).cuda()
+    d_h = torch.from_numpy(np.array(h, dtype=np.uint8, copy=True)).cuda()
     ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
     if suite == 0:
         sig = torch.zeros((n, 65), dtype=torch.uint8, device="cuda")
