@@ -1391,9 +1391,8 @@ __global__ __launch_bounds__(256, 1) void tx_verify_split_kernel(const uint8_t* 
 // serial point-operation chain, not by the SIMD.  Here the two GLV halves each run on a PAIR of
 // waves that split every doubling and mixed addition by dependency level and trade intermediate
 // field elements through LDS:
-//   dbl  (2M + 5S, depth 3): a: A = X^2, F = (3A)^2 | b: B = Y^2, C = B^2, t = (X + B)^2
-//                            -> both: D, X3 | a: Y3 = E (D - X3) - 8C | b: Z3 = 2 Y Z
-//                            4 multiplications on the critical path instead of 7
+//   dbl  (3M + 4S, depth 2): a: A = X^2, F = (3A)^2, Z3 = 2 Y Z | b: B = Y^2, D = 4 X B, 8 B^2
+//                            -> both: X3, Y3 = E (D - X3) - 8C        4 instead of 7, one barrier
 //   madd (7M + 4S):          a: Z1Z1, U2, HH, Z3 | b: Z1Z1, S2', S2, rr^2 -> a: J | b: V
 //                            -> a: rr (V - X3) | b: Y J        6 instead of 11
 // Both waves of a pair hold the whole point after every operation (they compute bit-identical
@@ -1421,7 +1420,7 @@ struct CoopLds {
     uint32_t zc[8][64];
     uint32_t k[2][4][64];             // GLV halves
     uint32_t flags[64];               // bit0 scalars ok, bit1 R ok, bit2 neg1, bit3 neg2
-    uint4 ex[2][2][5][2][64];         // [chain][writer role][slot][word quad][lane]; slots 0-2: exchange 0, 3: 1, 4: 2
+    uint4 ex[2][2][6][2][64];         // [chain][writer role][slot][word quad][lane]; madd: 0-2 exchange 0, 3: 1, 4: 2; dbl: 0-2 | 3-5
     uint32_t tabphx[8][8][64];        // beta * x of the table entries (chain 1's phi(R) table)
     uint32_t pt[5][25][64];           // chain results 0/1, G partials 2..4 (X, Y, Z, inf)
     uint32_t xe[8][64];               // e = H(m) mod n (wave 3 -> waves 0, 1)
@@ -1455,6 +1454,17 @@ struct CoopCtx {
         p[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
         p[64] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
     }
+    __device__ __forceinline__ void puts(int s, const fe& a) const {  // raw slot index 0..5
+        uint4* p = &L->ex[chain][role][s][0][0] + lane;
+        p[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+        p[64] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+    }
+    __device__ __forceinline__ void gets(int s, fe& a) const {
+        const uint4* p = &L->ex[chain][role ^ 1][s][0][0] + lane;
+        const uint4 q0 = p[0], q1 = p[64];
+        a.v[0] = q0.x; a.v[1] = q0.y; a.v[2] = q0.z; a.v[3] = q0.w;
+        a.v[4] = q1.x; a.v[5] = q1.y; a.v[6] = q1.z; a.v[7] = q1.w;
+    }
     __device__ __forceinline__ void get(int x, int f, fe& a) const {  // the partner's value
         const uint4* p = slot(x, role ^ 1, f);
         const uint4 q0 = p[0], q1 = p[64];
@@ -1463,63 +1473,59 @@ struct CoopCtx {
     }
 };
 
-// P = 2 P (a = 0, dbl-2009-l), P replicated on both waves of the pair.
+// P = 2 P (a = 0, dbl-2009-l with D = 4 X B), P replicated on both waves of the pair; ONE exchange:
+//   a: A = X^2, E = 3A, F = E^2, Z3 = 2 Y Z | b: B = Y^2, D = 4 X B, C = B^2, C8 = 8 C
+//   -> both: X3 = F - 2D, Y3 = E (D - X3) - C8
+// The shifted passes (shl<k>, mul3) replace ten field additions.  S0 is the exchange buffer: slots
+// 0-2 (shared with coop_madd's exchange 0) or 3-5 (3, 4 shared with its exchanges 1, 2).  The four
+// doublings of a window use 0, 3, 0, 3, so a slot is rewritten only after the barrier that follows
+// the partner's last read of it (the madd rewrites 0-2 before its first barrier, two doublings after
+// the last read of buffer 0, and 3/4 only after its first/second barrier).
+template <int S0>
 __device__ __forceinline__ void coop_dbl(Jac& P, const CoopCtx& c) {
-    fe A, B, C, D, E, F, t, X3, Y3, Z3;
+    fe E, F, D, C8, Z3, X3, Y3, t;
     DBL_T(0);
     if (c.role == 0) {
+        fe A;
         FieldK1::sqr(A, P.X);
-        FieldK1::add(E, A, A);
-        FieldK1::add(E, E, A);
+        FieldK1::mul3(E, A);
         FieldK1::sqr(F, E);
-        c.put(0, 0, A);
-        c.put(0, 1, F);
+        c.puts(S0, E);
+        c.puts(S0 + 1, F);
+        FieldK1::mul(Z3, P.Y, P.Z);
+        FieldK1::template shl<1>(Z3, Z3);
+        c.puts(S0 + 2, Z3);
     } else {
+        fe B, C;
         FieldK1::sqr(B, P.Y);
+        FieldK1::mul(D, P.X, B);
+        FieldK1::template shl<2>(D, D);
+        c.puts(S0, D);
         FieldK1::sqr(C, B);
-        FieldK1::add(t, P.X, B);
-        FieldK1::sqr(t, t);
-        c.put(0, 0, C);
-        c.put(0, 1, t);
+        FieldK1::template shl<3>(C8, C);
+        c.puts(S0 + 1, C8);
     }
     DBL_T(1);
     __syncthreads();
     DBL_T(2);
     if (c.role == 0) {
-        c.get(0, 0, C);
-        c.get(0, 1, t);
+        c.gets(S0, D);
+        c.gets(S0 + 1, C8);
     } else {
-        c.get(0, 0, A);
-        c.get(0, 1, F);
-        FieldK1::add(E, A, A);
-        FieldK1::add(E, E, A);
+        c.gets(S0, E);
+        c.gets(S0 + 1, F);
+        c.gets(S0 + 2, Z3);
     }
-    FieldK1::sub(D, t, A);
-    FieldK1::sub(D, D, C);
-    FieldK1::add(D, D, D);
-    FieldK1::add(t, D, D);
+    FieldK1::template shl<1>(t, D);
     FieldK1::sub(X3, F, t);
-    if (c.role == 0) {
-        FieldK1::sub(t, D, X3);
-        FieldK1::mul(Y3, E, t);
-        FieldK1::add(C, C, C);
-        FieldK1::add(C, C, C);
-        FieldK1::add(C, C, C);
-        FieldK1::sub(Y3, Y3, C);
-        c.put(1, 0, Y3);
-    } else {
-        FieldK1::mul(Z3, P.Y, P.Z);
-        FieldK1::add(Z3, Z3, Z3);
-        c.put(1, 0, Z3);
-    }
+    FieldK1::sub(t, D, X3);
+    FieldK1::mul(Y3, E, t);
+    FieldK1::sub(Y3, Y3, C8);
     DBL_T(3);
-    __syncthreads();
-    DBL_T(4);
-    if (c.role == 0) c.get(1, 0, Z3);
-    else c.get(1, 0, Y3);
     fe_copy(P.X, X3);
     fe_copy(P.Y, Y3);
     fe_copy(P.Z, Z3);
+    DBL_T(4);
 }
 
 // P = P + Q (madd-2007-bl with the complete-addition special cases of CurveK1::madd), Q affine.
@@ -1541,7 +1547,7 @@ __device__ __forceinline__ void coop_madd(Jac& R, const Jac& P, const Aff& Q, co
         FieldK1::mul(u, Q.y, P.Z);
         FieldK1::mul(u, u, Z1Z1);         // S2
         FieldK1::sub(rr, u, P.Y);
-        FieldK1::add(rr, rr, rr);
+        FieldK1::template shl<1>(rr, rr);
         FieldK1::sqr(R2, rr);
         c.put(0, 0, rr);
         c.put(0, 1, R2);
@@ -1555,8 +1561,7 @@ __device__ __forceinline__ void coop_madd(Jac& R, const Jac& P, const Aff& Q, co
         c.get(0, 1, HH);
         c.get(0, 2, Z3);
     }
-    FieldK1::add(I, HH, HH);
-    FieldK1::add(I, I, I);
+    FieldK1::template shl<2>(I, HH);
     if (c.role == 0) {
         FieldK1::mul(J, H, I);
         c.put(1, 0, J);
@@ -1568,7 +1573,7 @@ __device__ __forceinline__ void coop_madd(Jac& R, const Jac& P, const Aff& Q, co
     if (c.role == 0) c.get(1, 0, V);
     else c.get(1, 0, J);
     FieldK1::sub(X3, R2, J);
-    FieldK1::add(t, V, V);
+    FieldK1::template shl<1>(t, V);
     FieldK1::sub(X3, X3, t);
     if (c.role == 0) {
         FieldK1::sub(t, V, X3);
@@ -1576,7 +1581,7 @@ __device__ __forceinline__ void coop_madd(Jac& R, const Jac& P, const Aff& Q, co
         c.put(2, 0, u);
     } else {
         FieldK1::mul(u, P.Y, J);
-        FieldK1::add(u, u, u);            // 2 Y J
+        FieldK1::template shl<1>(u, u);   // 2 Y J
         c.put(2, 0, u);
     }
     __syncthreads();
@@ -1828,16 +1833,16 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
     coop_add_digit(acc, c, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
 #pragma unroll 1
     for (int w = 31; w >= 0; --w) {
-        coop_dbl(acc, c);
+        coop_dbl<0>(acc, c);
 #ifdef BCOSGPU_COOP_TIMING
         c.probe = blockIdx.x == 0 && w == 20;
 #endif
-        coop_dbl(acc, c);
+        coop_dbl<3>(acc, c);
 #ifdef BCOSGPU_COOP_TIMING
         c.probe = false;
 #endif
-        coop_dbl(acc, c);
-        coop_dbl(acc, c);
+        coop_dbl<0>(acc, c);
+        coop_dbl<3>(acc, c);
         coop_add_digit(acc, c, booth_digit128(k), neg, phi);
     }
     COOP_T(2);

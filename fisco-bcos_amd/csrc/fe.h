@@ -227,6 +227,15 @@ struct FieldK1 {
     }
     __device__ static __forceinline__ void add(fe& r, const fe& a, const fe& b) { k1_add_asm(r.v, a.v, b.v); }
     __device__ static __forceinline__ void sub(fe& r, const fe& a, const fe& b) { k1_sub_asm(r.v, a.v, b.v); }
+    // r = 2^K a, r = 3a: one shifted pass and one fold instead of K (or 2) full additions
+    template <int K>
+    __device__ static __forceinline__ void shl(fe& r, const fe& a) {
+        static_assert(K >= 1 && K <= 3, "shift 1..3");
+        if (K == 1) k1_shl1_asm(r.v, a.v);
+        else if (K == 2) k1_shl2_asm(r.v, a.v);
+        else k1_shl3_asm(r.v, a.v);
+    }
+    __device__ static __forceinline__ void mul3(fe& r, const fe& a) { k1_add_shl1_asm(r.v, a.v, a.v); }
     // canonical residue in [0, p)
     __device__ static __forceinline__ void normalize(fe& a) {
         fe t;
@@ -427,6 +436,17 @@ struct Mont {
     }
     __device__ static __forceinline__ void add(fe& r, const fe& a, const fe& b) { mod_add_asm(r.v, a.v, b.v, P::M); }
     __device__ static __forceinline__ void sub(fe& r, const fe& a, const fe& b) { mod_sub_asm(r.v, a.v, b.v, P::M); }
+    template <int K>
+    __device__ static __forceinline__ void shl(fe& r, const fe& a) {
+        add(r, a, a);
+#pragma unroll
+        for (int k = 1; k < K; ++k) add(r, r, r);
+    }
+    __device__ static __forceinline__ void mul3(fe& r, const fe& a) {
+        fe t;
+        add(t, a, a);
+        add(r, t, a);
+    }
     __device__ static __forceinline__ void neg(fe& r, const fe& a) {
         fe z;
         fe_zero(z);

@@ -1,5 +1,5 @@
 // fetest.hip -- field-arithmetic vectors for tests/test_gpu_field.py: reads lines "op a b" (hex,
-// 256-bit, op in add/sub/mul/sqr/norm) from stdin, evaluates them with FieldK1 on the GPU (one
+// 256-bit, op in add/sub/mul/sqr/norm/shl1/shl2/shl3/mul3) from stdin, evaluates them with FieldK1 on the GPU (one
 // vector per lane), prints the canonical result per line.  Covers the rare carry/borrow tails of
 // the k1_add/k1_sub asm that random inputs almost never reach.
 #include <hip/hip_runtime.h>
@@ -25,6 +25,10 @@ __global__ void k(const uint32_t* in, const int* op, int n, uint32_t* out) {
         case 1: FieldK1::sub(r, a, b); break;
         case 2: FieldK1::mul(r, a, b); break;
         case 3: FieldK1::sqr(r, a); break;
+        case 5: FieldK1::shl<1>(r, a); break;
+        case 6: FieldK1::shl<2>(r, a); break;
+        case 7: FieldK1::shl<3>(r, a); break;
+        case 8: FieldK1::mul3(r, a); break;
         default: fe_copy(r, a); break;
     }
     FieldK1::normalize(r);
@@ -56,7 +60,8 @@ int main() {
         parse(b, w + 8);
         in.insert(in.end(), w, w + 16);
         const std::string o(op);
-        ops.push_back(o == "add" ? 0 : o == "sub" ? 1 : o == "mul" ? 2 : o == "sqr" ? 3 : 4);
+        ops.push_back(o == "add" ? 0 : o == "sub" ? 1 : o == "mul" ? 2 : o == "sqr" ? 3 : o == "shl1" ? 5
+                      : o == "shl2" ? 6 : o == "shl3" ? 7 : o == "mul3" ? 8 : 4);
     }
     const int n = static_cast<int>(ops.size());
     if (!n) return 0;

@@ -90,6 +90,60 @@ def k1_addsub(sub):
                   clobbers='"vcc", "scc"')
 
 
+def k1_shl_fold(K, R, T, M0):
+    """R (8 words) + T * 2^256 -> R + T * (2^32 + 977) (mod p), T < 2^24: words 0-1 inline, the
+    carry tail (probability ~2^-32 per lane) branched over unless some lane of the wave needs it."""
+    add, addc = "v_add_co_u32_e32", "v_addc_co_u32_e32"
+    b = [f"v_mul_u32_u24_e32 {M0}, {K}, {T}", f"{add} {R[0]}, vcc, {R[0]}, {M0}", f"{addc} {R[1]}, vcc, {R[1]}, {T}, vcc"]
+    b += ["s_nop 4", "s_cmp_eq_u64 vcc, 0", "s_cbranch_scc1 2f"]
+    b += [f"{addc} {R[i]}, vcc, 0, {R[i]}, vcc" for i in range(2, 8)]
+    # a carry out of 2^256 here leaves R < T * (2^32 + 977) < 2^57 - fold it once more (no further carry)
+    b += [f"v_cndmask_b32_e64 {M0}, 0, {K}, vcc", f"v_cndmask_b32_e64 {T}, 0, 1, vcc",
+          f"{add} {R[0]}, vcc, {R[0]}, {M0}", f"{addc} {R[1]}, vcc, {R[1]}, {T}, vcc"]
+    b += [f"{addc} {R[i]}, vcc, 0, {R[i]}, vcc" for i in range(2, 8)]
+    b += ["2:"]
+    return b
+
+
+def shifted(X, k, dst):
+    """dst[0..7] = low 256 bits of X << k (k in 1..3); returns the instructions (top word separate)."""
+    b = [f"v_lshlrev_b32_e32 {dst[0]}, {k}, {X[0]}"]
+    b += [f"v_alignbit_b32 {dst[i]}, {X[i]}, {X[i - 1]}, {32 - k}" for i in range(1, 8)]
+    return b
+
+
+def k1_shl(k):
+    ops = Ops()
+    r, t, m0 = ops.out("r"), ops.out("t", 1), ops.out("m0", 1)
+    a, kk = ops.inp("a"), ops.inp("k977", 1)
+    R = [ops.ref("out", r, i) for i in range(8)]
+    A = [ops.ref("in", a, i) for i in range(8)]
+    T, M0, K = ops.ref("out", t), ops.ref("out", m0), ops.ref("in", kk)
+    body = shifted(A, k, R) + [f"v_lshrrev_b32_e32 {T}, {32 - k}, {A[7]}"]
+    body += k1_shl_fold(K, R, T, M0)
+    return render(f"k1_shl{k}_asm(uint32_t r[8], const uint32_t a[8])", "uint32_t t, m0; const uint32_t k977 = 977u;",
+                  ops, body, f"secp256k1 base field: r = 2^{k} a (mod p), values in [0, 2^256)",
+                  clobbers='"vcc", "scc"')
+
+
+def k1_add_shl(k):
+    ops = Ops()
+    r, bs, t, m0 = ops.out("r"), ops.out("bs"), ops.out("t", 1), ops.out("m0", 1)
+    a, bb, kk = ops.inp("a"), ops.inp("b"), ops.inp("k977", 1)
+    R = [ops.ref("out", r, i) for i in range(8)]
+    BS = [ops.ref("out", bs, i) for i in range(8)]
+    A = [ops.ref("in", a, i) for i in range(8)]
+    B = [ops.ref("in", bb, i) for i in range(8)]
+    T, M0, K = ops.ref("out", t), ops.ref("out", m0), ops.ref("in", kk)
+    body = shifted(B, k, BS) + [f"v_lshrrev_b32_e32 {T}, {32 - k}, {B[7]}"]
+    body += chain("v_add_co_u32_e32", "v_addc_co_u32_e32", R, A, BS)
+    body += [f"v_addc_co_u32_e32 {T}, vcc, 0, {T}, vcc"]
+    body += k1_shl_fold(K, R, T, M0)
+    return render(f"k1_add_shl{k}_asm(uint32_t r[8], const uint32_t a[8], const uint32_t b[8])",
+                  "uint32_t bs[8], t, m0; const uint32_t k977 = 977u;", ops, body,
+                  f"secp256k1 base field: r = a + 2^{k} b (mod p), values in [0, 2^256)", clobbers='"vcc", "scc"')
+
+
 def k1_normalize():
     ops = Ops()
     r, t = ops.out("r"), ops.out("t")
@@ -185,7 +239,8 @@ def main():
              "// 256-bit carry chains as single inline-asm blocks, without the s_nop padding the compiler",
              "// inserts between dependent VCC carry steps on gfx950 (validated by tools/carrybench.hip).",
              "#pragma once", "#include <stdint.h>", "", "namespace bcosgpu {", "",
-             k1_addsub(False), k1_addsub(True), k1_normalize(), k1_reduce(), mod_add(), mod_sub(), "}  // namespace bcosgpu", ""]
+             k1_addsub(False), k1_addsub(True), k1_shl(1), k1_shl(2), k1_shl(3), k1_add_shl(1),
+             k1_normalize(), k1_reduce(), mod_add(), mod_sub(), "}  // namespace bcosgpu", ""]
     with open(OUT, "w") as f:
         f.write("\n".join(parts))
     print("wrote", os.path.normpath(OUT))

@@ -33,8 +33,23 @@ def _cases():
         t = rnd.randrange(0, C)          # sub: a - b + 2^256 = t < c forces the borrow tail
         b = rnd.randrange(t + 1, M)
         cases.append(("sub", t + M - b, b))
+    # shifted passes: 2^k a and 3a for a in [0, 2^256); the top bits shifted out fold back, and
+    # 2^k a close to a multiple of 2^256 (low two words near 2^64 - fold) drives the carry tail
+    for a in edge:
+        for op in ("shl1", "shl2", "shl3", "mul3"):
+            cases.append((op, a, 0))
+    for _ in range(300):
+        k = rnd.choice((1, 2, 3))
+        hi = rnd.randrange(2**k)
+        low = (rnd.randrange(M) >> 64 << 64) | (2**64 - 1 - rnd.randrange(C * (2**k)))
+        a = ((hi << 256) | low) >> k           # 2^k a = hi * 2^256 + low (up to the shifted-out bits)
+        cases.append(("shl%d" % k, a, 0))
+        cases.append(("mul3", rnd.randrange(M - 2**70, M), 0))
+        hi = rnd.randrange(1, 2**k)      # 2^k a = hi * 2^256 + (2^256 - small): the second fold
+        cases.append(("shl%d" % k, ((hi << 256) | (M - 1 - rnd.randrange(C * hi))) >> k, 0))
     for _ in range(500):
-        cases.append((rnd.choice(("add", "sub", "mul", "sqr")), rnd.randrange(M), rnd.randrange(M)))
+        cases.append((rnd.choice(("add", "sub", "mul", "sqr", "shl1", "shl2", "shl3", "mul3")),
+                      rnd.randrange(M), rnd.randrange(M)))
     return cases
 
 
@@ -48,5 +63,6 @@ def test_fieldk1_vs_python():
     got = [int(x, 16) for x in r.stdout.split()]
     assert len(got) == len(cases)
     for (op, a, b), g in zip(cases, got):
-        want = {"add": a + b, "sub": a - b, "mul": a * b, "sqr": a * a, "norm": a}[op] % P
+        want = {"add": a + b, "sub": a - b, "mul": a * b, "sqr": a * a, "norm": a, "shl1": 2 * a,
+                "shl2": 4 * a, "shl3": 8 * a, "mul3": 3 * a}[op] % P
         assert g == want, (op, hex(a), hex(b), hex(g), hex(want))
