@@ -38,6 +38,18 @@ struct fe {
             : "v"(a), "s"(k));                                                                 \
     } while (0)
 
+// 32 x 32 -> 64-bit product in one v_mad_u64_u32 (instead of a v_mul_lo_u32 / v_mul_hi_u32 pair)
+__device__ __forceinline__ uint64_t mul_wide(uint32_t a, uint32_t b) {
+    uint64_t r, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cc) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint64_t mul_wide_k(uint32_t a, uint32_t k) {
+    uint64_t r, cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cc) : "v"(a), "s"(k));
+    return r;
+}
+
 __device__ __forceinline__ void fe_copy(fe& r, const fe& a) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.v[i] = a.v[i];
@@ -173,7 +185,8 @@ __device__ __forceinline__ void sqr_512(uint32_t r[16], const fe& a) {
     uint32_t c = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint32_t lo = a.v[i] * a.v[i], hi = __umulhi(a.v[i], a.v[i]);
+        const uint64_t sq = mul_wide(a.v[i], a.v[i]);
+        const uint32_t lo = static_cast<uint32_t>(sq), hi = static_cast<uint32_t>(sq >> 32);
         r[2 * i] = addc32(t[2 * i], lo, c, c);
         r[2 * i + 1] = addc32(t[2 * i + 1], hi, c, c);
     }
@@ -209,8 +222,9 @@ struct FieldK1 {
         uint32_t lo[8], hi[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            lo[k] = t[8 + k] * 977u;
-            hi[k] = __umulhi(t[8 + k], 977u);
+            const uint64_t h = mul_wide_k(t[8 + k], 977u);
+            lo[k] = static_cast<uint32_t>(h);
+            hi[k] = static_cast<uint32_t>(h >> 32);
         }
         k1_reduce_asm(o.v, t, lo, hi);
     }
