@@ -62,12 +62,23 @@ __device__ __constant__ static const uint32_t kZaW32[4] = {0x2153d0a9u, 0x877cc6
 static constexpr uint32_t kZaC36 = 0xf0a00000u;
 
 // ------------------------------------------------------------------ per-device G tables
+// Two comb tables of affine b * 2^(B i) * G per curve, [window i][entry b][x0..7, y0..7]:
+//  * 8-bit  (B = 8, 32 windows x 256, 512 KiB): L2-resident; the latency-bound small-batch kernels
+//    (cooperative / split), whose lone waves would stall on every HBM gather;
+//  * 16-bit (B = 16, 16 windows x 65536, 64 MiB): half the mixed additions (16 instead of 32) for
+//    the throughput kernels, which hide the gather latency (one window prefetched, 2 waves/SIMD).
 static constexpr int kCombWindows = 32;
 static constexpr int kCombEntries = 256;
 static constexpr size_t kTabWords = static_cast<size_t>(kCombWindows) * kCombEntries * 16;
+static constexpr int kWideBits = 16;
+static constexpr int kWideWindows = 256 / kWideBits;
+static constexpr uint32_t kWideEntries = 1u << kWideBits;
+static constexpr size_t kWideTabWords = static_cast<size_t>(kWideWindows) * kWideEntries * 16;
 static std::mutex g_tab_mu;
 static uint32_t* g_tab_k1[64];
 static uint32_t* g_tab_sm2[64];
+static uint32_t* g_wtab_k1[64];
+static uint32_t* g_wtab_sm2[64];
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ void load_be256(fe& r, const uint8_t* p) {
@@ -120,26 +131,47 @@ __device__ __forceinline__ void reduce_once(fe& x, const uint32_t* n) {
 }
 
 // ------------------------------------------------------------------ scalar multiplication
-// acc = k * G via the 8-bit comb table (k plain, < 2^256)
-template <class C>
+template <int BITS>
+__device__ __forceinline__ void shr_bits(fe& k) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) k.v[i] = __builtin_amdgcn_alignbit(k.v[i + 1], k.v[i], BITS);
+    k.v[7] >>= BITS;
+}
+__device__ __forceinline__ void load_aff16(Aff& T, const uint32_t* __restrict__ e32) {
+    const uint4* e = reinterpret_cast<const uint4*>(e32);
+    const uint4 q0 = e[0], q1 = e[1], q2 = e[2], q3 = e[3];
+    T.x.v[0] = q0.x; T.x.v[1] = q0.y; T.x.v[2] = q0.z; T.x.v[3] = q0.w;
+    T.x.v[4] = q1.x; T.x.v[5] = q1.y; T.x.v[6] = q1.z; T.x.v[7] = q1.w;
+    T.y.v[0] = q2.x; T.y.v[1] = q2.y; T.y.v[2] = q2.z; T.y.v[3] = q2.w;
+    T.y.v[4] = q3.x; T.y.v[5] = q3.y; T.y.v[6] = q3.z; T.y.v[7] = q3.w;
+}
+
+// acc = k * G via a BITS-bit comb table (k plain, < 2^256): 256 / BITS mixed additions, no
+// doublings.  The entry of window i + 1 is gathered before the addition of window i.
+template <class C, int BITS = kWideBits>
 __device__ __forceinline__ void comb_mul(Jac& acc, const fe& k_plain, const uint32_t* __restrict__ tab) {
+    constexpr int W = 256 / BITS;
+    constexpr uint32_t E = 1u << BITS, MASK = E - 1u;
     fe k;
     fe_copy(k, k_plain);
     C::set_inf(acc);
+    uint32_t b = k.v[0] & MASK;
+    shr_bits<BITS>(k);
+    Aff T;
+    load_aff16(T, tab + static_cast<size_t>(b) * 16);
 #pragma unroll 1
-    for (int i = 0; i < kCombWindows; ++i) {
-        const uint32_t b = k.v[0] & 255u;
-        shr8(k);
-        const uint4* e = reinterpret_cast<const uint4*>(tab + (static_cast<size_t>(i) * kCombEntries + b) * 16);
-        const uint4 q0 = e[0], q1 = e[1], q2 = e[2], q3 = e[3];
-        Aff T;
-        T.x.v[0] = q0.x; T.x.v[1] = q0.y; T.x.v[2] = q0.z; T.x.v[3] = q0.w;
-        T.x.v[4] = q1.x; T.x.v[5] = q1.y; T.x.v[6] = q1.z; T.x.v[7] = q1.w;
-        T.y.v[0] = q2.x; T.y.v[1] = q2.y; T.y.v[2] = q2.z; T.y.v[3] = q2.w;
-        T.y.v[4] = q3.x; T.y.v[5] = q3.y; T.y.v[6] = q3.z; T.y.v[7] = q3.w;
+    for (int i = 0; i < W; ++i) {
+        const uint32_t bi = b;
+        Aff N;
+        const int in = i + 1 < W ? i + 1 : i;  // last window: a harmless reload
+        b = k.v[0] & MASK;
+        shr_bits<BITS>(k);
+        load_aff16(N, tab + (static_cast<size_t>(in) * E + b) * 16);
         Jac S;
         C::madd(S, acc, T);
-        C::cmov(acc, S, b != 0u);
+        C::cmov(acc, S, bi != 0u);
+        fe_copy(T.x, N.x);
+        fe_copy(T.y, N.y);
     }
 }
 
@@ -511,6 +543,39 @@ __global__ __launch_bounds__(256) void comb_table_kernel(uint32_t* tab, int sm2)
     }
 }
 
+// 16-bit comb entry (i, b) = lo * 2^(16 i) G + hi * 2^(16 i + 8) G (b = lo + 256 hi): one addition of
+// two 8-bit-table entries and one inversion.  The two addends never coincide or cancel
+// (lo - 256 hi != 0 mod n), and the madd is complete anyway.
+template <class C, class F>
+__global__ __launch_bounds__(256) void comb_wide_kernel(uint32_t* __restrict__ wide, const uint32_t* __restrict__ tab8) {
+    const uint64_t idx = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (idx >= static_cast<uint64_t>(kWideWindows) * kWideEntries) return;
+    const int i = static_cast<int>(idx / kWideEntries);
+    uint32_t b = static_cast<uint32_t>(idx % kWideEntries);
+    if (b == 0) b = 1;  // unused slot: a valid point, never selected
+    const uint32_t lo = b & 255u, hi = b >> 8;
+    Aff A, B;
+    load_aff16(A, tab8 + (static_cast<size_t>(2 * i) * kCombEntries + (lo ? lo : 1u)) * 16);
+    load_aff16(B, tab8 + (static_cast<size_t>(2 * i + 1) * kCombEntries + (hi ? hi : 1u)) * 16);
+    Aff R;
+    if (lo && hi) {
+        Jac P, S;
+        C::from_aff(P, A);
+        C::madd(S, P, B);
+        C::to_aff(R, S);
+        F::normalize(R.x);
+        F::normalize(R.y);
+    } else {
+        R = lo ? A : B;
+    }
+    uint32_t* o = wide + idx * 16;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        o[w] = R.x.v[w];
+        o[8 + w] = R.y.v[w];
+    }
+}
+
 int ecc_init_tables(int device) {
     std::lock_guard<std::mutex> g(g_tab_mu);
     if (device < 0 || device >= 64) return BCOSGPU_E_ARG;
@@ -521,16 +586,34 @@ int ecc_init_tables(int device) {
     const int n = kCombWindows * kCombEntries;
     hipLaunchKernelGGL((comb_table_kernel<CurveK1, FieldK1>), dim3((n + 255) / 256), dim3(256), 0, 0, k1, 0);
     hipLaunchKernelGGL((comb_table_kernel<CurveSM2, FieldP2>), dim3((n + 255) / 256), dim3(256), 0, 0, sm2, 1);
+    uint32_t *wk1 = nullptr, *wsm2 = nullptr;
+    if (hipMalloc(&wk1, kWideTabWords * 4) != hipSuccess) return BCOSGPU_E_HIP;
+    if (hipMalloc(&wsm2, kWideTabWords * 4) != hipSuccess) return BCOSGPU_E_HIP;
+    const unsigned gw = static_cast<unsigned>((static_cast<uint64_t>(kWideWindows) * kWideEntries + 255) / 256);
+    hipLaunchKernelGGL((comb_wide_kernel<CurveK1, FieldK1>), dim3(gw), dim3(256), 0, 0, wk1, k1);
+    hipLaunchKernelGGL((comb_wide_kernel<CurveSM2, FieldP2>), dim3(gw), dim3(256), 0, 0, wsm2, sm2);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return BCOSGPU_E_HIP;
     g_tab_k1[device] = k1;
     g_tab_sm2[device] = sm2;
+    g_wtab_k1[device] = wk1;
+    g_wtab_sm2[device] = wsm2;
     return 0;
 }
 
+// 16-bit comb tables (the default for every kernel but the small-batch secp tx_verify ones)
 static int tables(const uint32_t** k1, const uint32_t** sm2) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BCOSGPU_E_NODEV;
-    if (!g_tab_k1[dev]) return BCOSGPU_E_NODEV;  // bcosgpu_init(dev) not called
+    if (!g_wtab_k1[dev]) return BCOSGPU_E_NODEV;  // bcosgpu_init(dev) not called
+    *k1 = g_wtab_k1[dev];
+    *sm2 = g_wtab_sm2[dev];
+    return 0;
+}
+// 8-bit comb tables
+static int tables8(const uint32_t** k1, const uint32_t** sm2) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BCOSGPU_E_NODEV;
+    if (!g_tab_k1[dev]) return BCOSGPU_E_NODEV;
     *k1 = g_tab_k1[dev];
     *sm2 = g_tab_sm2[dev];
     return 0;
@@ -1355,7 +1438,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_split_kernel(const uint8_t* 
             fe u1;
             lds_load_fe(u1, L.u1, lane);
             Jac PG;
-            comb_mul<CurveK1>(PG, u1, tab);
+            comb_mul<CurveK1, 8>(PG, u1, tab);
             lds_store_jac(L.pt[2], PG, lane);
         }
     }
@@ -1993,6 +2076,8 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
     int rc = tables(&k1, &sm2);
     if (rc) return rc;
     if (suite == BCOSGPU_SUITE_SECP256K1 && use_split(n)) {
+        rc = tables8(&k1, &sm2);
+        if (rc) return rc;
         if (use_coop()) {
             hipLaunchKernelGGL(tx_verify_coop_kernel, dim3(static_cast<unsigned>((n + 63) / 64)), dim3(256), 0, st,
                                d_pre, d_pre_off, d_sig, d_sig_off, n, k1, d_txhash, d_sender, d_status);

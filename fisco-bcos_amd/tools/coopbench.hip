@@ -25,7 +25,7 @@ int main() {
     hipMemcpy(dpo, po.data(), 8 * (n + 1), hipMemcpyHostToDevice);
     hipMemcpy(dso, so.data(), 8 * (n + 1), hipMemcpyHostToDevice);
     const uint32_t *k1, *sm2;
-    tables(&k1, &sm2);
+    tables8(&k1, &sm2);
     for (int rep = 0; rep < 3; ++rep) {
         hipLaunchKernelGGL(tx_verify_coop_kernel, dim3((n + 63) / 64), dim3(256), 0, 0, dp, dpo, ds, dso, n, k1, dh, dsn, dst);
         hipDeviceSynchronize();
