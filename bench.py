@@ -38,6 +38,15 @@ sys.path.insert(0, ROOT)
 MAC_PER_F = 136
 F_SECP_RECOVER = 3240
 F_SM2_VERIFY = 3210
+# Field multiplications this implementation actually executes per unit (counted from the kernel
+# schedules; the safegcd inversions are ALU work outside the F count, so these are
+# lower bounds on issued work). GLV halves the doublings (128 x 7 F) with 66 mixed adds (11 F) and
+# 33 phi lookups (1 F), the R table costs ~130 F, u1*G takes 16 mixed adds on the 16-bit comb
+# (32 on the 8-bit comb of the small-batch coop/split kernels), sqrt 270, complete add 16, rest ~10.
+# SM2: 256 a=-3 doublings x 8 F, 65 Booth mixed adds x 11 F, table ~133 F, comb 176 F, rest ~20.
+F_SECP_EXEC_WIDE = 2255
+F_SECP_EXEC_COMB8 = 2431
+F_SM2_EXEC = 3092
 # integer-MAC peak of gfx950 (v_mad_u64_u32 lane-ops/s), measured by fisco-bcos_amd/tools/intbench.hip
 # on MI355X (profiles/r01_intbench.json)
 PEAK_MAC_PER_S = 3.0785e13
@@ -196,6 +205,16 @@ def main():
                     "traffic_source": traffic_src, "kernel": kname, "kernel_ms": kernel_ms,
                     "units_per_launch": n,
                     "work_per_unit": "%d F x %d MAC (SURVEY.md 8d)" % (f_per, MAC_PER_F)}
+        # achieved/frac above use the fixed non-GLV count of SURVEY 8d (useful work per second), which
+        # can exceed 1 because GLV and the 16-bit comb execute fewer multiplications; "executed" is
+        # the issue-bound fraction for the multiplications the kernel really performs
+        if suite == 0:
+            f_exec = F_SECP_EXEC_WIDE if kname.startswith("tx_verify_kernel") else F_SECP_EXEC_COMB8
+        else:
+            f_exec = F_SM2_EXEC
+        ex = n * f_exec * MAC_PER_F / (kernel_ms * 1e-3)
+        roofline["executed"] = {"f_per_unit": f_exec, "achieved": ex / 1e12, "frac": ex / PEAK_MAC_PER_S,
+                                "note": "F counted from the kernel schedule (DESIGN.md 9); inversions excluded"}
         cpu = None
         host_api = None
         if world == 1 and not args.no_cpu_baseline:
