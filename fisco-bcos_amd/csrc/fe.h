@@ -21,32 +21,38 @@ struct fe {
     uint32_t v[8];
 };
 
-// acc(64) + c2(32) += a * b   -- 96-bit column accumulator of the Comba product
+// acc(64) + c2(32) += a * b   -- 96-bit column accumulator of the generic Montgomery product (group
+// orders only; the base-field products are the scheduled blocks of fe_asm.h).  gfx940+ require two
+// wait states between a VALU write of an SGPR and a VALU read of it, and hipcc pads neither inside
+// an asm string nor across its boundary: s_nop 1 after the carry write (read by the v_addc and,
+// after the statement, possibly by hipcc's code) and, in BG_MADC_K, before the SGPR operand read.
 #define BG_MADC(acc, c2, a, b)                                                                 \
     do {                                                                                       \
         uint64_t cc_;                                                                          \
-        asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32_e64 %2, %1, %2, 0, %1"          \
-            : "+v"(acc), "=&s"(cc_), "+v"(c2)                                                  \
-            : "v"(a), "v"(b));                                                                 \
+        asm volatile("v_mad_u64_u32 %0, %1, %3, %4, %0\n\ts_nop 1\n\tv_addc_co_u32_e64 %2, %1, %2, 0, %1\n\ts_nop 1" \
+                     : "+v"(acc), "=&s"(cc_), "+v"(c2)                                         \
+                     : "v"(a), "v"(b));                                                        \
     } while (0)
 // same with a compile-time constant multiplier (lives in an SGPR)
 #define BG_MADC_K(acc, c2, a, k)                                                               \
     do {                                                                                       \
         uint64_t cc_;                                                                          \
-        asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32_e64 %2, %1, %2, 0, %1"          \
-            : "+v"(acc), "=&s"(cc_), "+v"(c2)                                                  \
-            : "v"(a), "s"(k));                                                                 \
+        asm volatile("s_nop 1\n\tv_mad_u64_u32 %0, %1, %3, %4, %0\n\ts_nop 1\n\tv_addc_co_u32_e64 %2, %1, %2, 0, %1\n\ts_nop 1" \
+                     : "+v"(acc), "=&s"(cc_), "+v"(c2)                                         \
+                     : "v"(a), "s"(k));                                                        \
     } while (0)
 
 // 32 x 32 -> 64-bit product in one v_mad_u64_u32 (instead of a v_mul_lo_u32 / v_mul_hi_u32 pair)
+// (the carry-out of these writes is a junk SGPR pair: padded so hipcc's next instructions may reuse
+// it at once)
 __device__ __forceinline__ uint64_t mul_wide(uint32_t a, uint32_t b) {
     uint64_t r, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cc) : "v"(a), "v"(b));
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0\n\ts_nop 1" : "=v"(r), "=s"(cc) : "v"(a), "v"(b));
     return r;
 }
 __device__ __forceinline__ uint64_t mul_wide_k(uint32_t a, uint32_t k) {
     uint64_t r, cc;
-    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cc) : "v"(a), "s"(k));
+    asm("s_nop 1\n\tv_mad_u64_u32 %0, %1, %2, %3, 0\n\ts_nop 1" : "=v"(r), "=s"(cc) : "v"(a), "s"(k));
     return r;
 }
 
@@ -94,9 +100,17 @@ __device__ __forceinline__ uint32_t subc32(uint32_t a, uint32_t b, uint32_t bin,
 }
 // r = lane-in-mask ? a : r, as explicit v_cndmask_b32 (the compiler cannot turn a chain of these
 // into an indexed scratch array access, which it otherwise does for per-lane table selects)
+// (one statement, opened by the two wait states hipcc owes the v_cmp that usually just wrote the mask)
 __device__ __forceinline__ void fe_cmov_mask(fe& r, const fe& a, uint64_t mask) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) asm("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(r.v[i]) : "v"(a.v[i]), "s"(mask));
+    asm volatile("s_nop 1\n\t"
+                 "v_cndmask_b32_e64 %0, %0, %8, %16\n\tv_cndmask_b32_e64 %1, %1, %9, %16\n\t"
+                 "v_cndmask_b32_e64 %2, %2, %10, %16\n\tv_cndmask_b32_e64 %3, %3, %11, %16\n\t"
+                 "v_cndmask_b32_e64 %4, %4, %12, %16\n\tv_cndmask_b32_e64 %5, %5, %13, %16\n\t"
+                 "v_cndmask_b32_e64 %6, %6, %14, %16\n\tv_cndmask_b32_e64 %7, %7, %15, %16"
+                 : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+                   "+v"(r.v[6]), "+v"(r.v[7])
+                 : "v"(a.v[0]), "v"(a.v[1]), "v"(a.v[2]), "v"(a.v[3]), "v"(a.v[4]), "v"(a.v[5]), "v"(a.v[6]),
+                   "v"(a.v[7]), "s"(mask));
 }
 // a < b as 256-bit integers
 __device__ __forceinline__ bool fe_lt(const fe& a, const fe& b) {
@@ -140,57 +154,9 @@ __device__ __forceinline__ uint32_t fe_add_k(fe& r, const fe& a, const uint32_t*
     return c;
 }
 
-// 256 x 256 -> 512-bit product, Comba (column) order.
-__device__ __forceinline__ void mul_512(uint32_t r[16], const fe& a, const fe& b) {
-    uint64_t acc = 0;
-    uint32_t c2 = 0;
-#pragma unroll
-    for (int k = 0; k < 15; ++k) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int j = k - i;
-            if (j >= 0 && j < 8) BG_MADC(acc, c2, a.v[i], b.v[j]);
-        }
-        r[k] = static_cast<uint32_t>(acc);
-        acc = (acc >> 32) | (static_cast<uint64_t>(c2) << 32);
-        c2 = 0;
-    }
-    r[15] = static_cast<uint32_t>(acc);
-}
-
-// 256-bit square: off-diagonal products once, doubled, plus the diagonal.
-__device__ __forceinline__ void sqr_512(uint32_t r[16], const fe& a) {
-    uint64_t acc = 0;
-    uint32_t c2 = 0;
-    uint32_t t[16];
-    t[0] = 0;
-#pragma unroll
-    for (int k = 1; k < 14; ++k) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int j = k - i;
-            if (j > i && j < 8) BG_MADC(acc, c2, a.v[i], a.v[j]);
-        }
-        t[k] = static_cast<uint32_t>(acc);
-        acc = (acc >> 32) | (static_cast<uint64_t>(c2) << 32);
-        c2 = 0;
-    }
-    t[14] = static_cast<uint32_t>(acc);
-    t[15] = static_cast<uint32_t>(acc >> 32);
-    // double: t <<= 1 (t < 2^479 so the shift cannot overflow 512 bits)
-#pragma unroll
-    for (int k = 15; k > 0; --k) t[k] = __builtin_amdgcn_alignbit(t[k], t[k - 1], 31);
-    t[0] = 0;
-    // add diagonal squares a_i^2 at columns 2i, 2i+1
-    uint32_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint64_t sq = mul_wide(a.v[i], a.v[i]);
-        const uint32_t lo = static_cast<uint32_t>(sq), hi = static_cast<uint32_t>(sq >> 32);
-        r[2 * i] = addc32(t[2 * i], lo, c, c);
-        r[2 * i + 1] = addc32(t[2 * i + 1], hi, c, c);
-    }
-}
+// 256 x 256 -> 512-bit product and 256-bit square: the scheduled Comba blocks of fe_asm.h
+__device__ __forceinline__ void mul_512(uint32_t r[16], const fe& a, const fe& b) { mul_512_asm(r, a.v, b.v); }
+__device__ __forceinline__ void sqr_512(uint32_t r[16], const fe& a) { sqr_512_asm(r, a.v); }
 
 // ============================================================================ secp256k1 base field
 struct FieldK1 {
@@ -218,16 +184,7 @@ struct FieldK1 {
     }
 
     // reduce a 512-bit value T = L + H 2^256 to [0, 2^256):  T = L + H*977 + H*2^32 (mod p)
-    __device__ static __forceinline__ void reduce(fe& o, const uint32_t t[16]) {
-        uint32_t lo[8], hi[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint64_t h = mul_wide_k(t[8 + k], 977u);
-            lo[k] = static_cast<uint32_t>(h);
-            hi[k] = static_cast<uint32_t>(h >> 32);
-        }
-        k1_reduce_asm(o.v, t, lo, hi);
-    }
+    __device__ static __forceinline__ void reduce(fe& o, const uint32_t t[16]) { k1_reduce_asm(o.v, t); }
 
     __device__ static __forceinline__ void mul(fe& r, const fe& a, const fe& b) {
         uint32_t t[16];
