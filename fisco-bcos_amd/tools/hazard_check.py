@@ -20,6 +20,7 @@ usage: hazard_check.py [--quiet] FILE...   (exit status 1 when a violation is fo
 """
 import os
 import re
+import struct
 import subprocess
 import sys
 import tempfile
@@ -70,15 +71,33 @@ def valu_defs_uses(mn, ops):
     return (), tuple(r for t in ops[1:] for r in sregs(t))
 
 
-def extract_code_object(path, tmpdir):
-    """The gfx950 code object inside a HIP host object / shared library (its .hip_fatbin bundle)."""
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def extract_code_objects(path, tmpdir):
+    """The gfx950 code objects inside a HIP host object / shared library: its .hip_fatbin section
+    holds one clang offload bundle per linked translation unit."""
     fat = os.path.join(tmpdir, os.path.basename(path) + ".fatbin")
-    co = os.path.join(tmpdir, os.path.basename(path) + ".co")
     subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section=.hip_fatbin=" + fat, path, os.devnull],
                    check=True, capture_output=True)
-    subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", "--targets=" + TARGET,
-                    "--input=" + fat, "--output=" + co], check=True, capture_output=True)
-    return co
+    blob = open(fat, "rb").read()
+    out, pos = [], 0
+    while True:
+        pos = blob.find(MAGIC, pos)
+        if pos < 0:
+            return out
+        n = struct.unpack_from("<Q", blob, pos + len(MAGIC))[0]
+        q = pos + len(MAGIC) + 8
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", blob, q)
+            triple = blob[q + 24:q + 24 + tlen].decode()
+            q += 24 + tlen
+            if triple == TARGET:
+                co = os.path.join(tmpdir, "%d.co" % len(out))
+                with open(co, "wb") as f:
+                    f.write(blob[pos + off:pos + off + size])
+                out.append(co)
+        pos += len(MAGIC)
 
 
 def disassemble(co):
@@ -165,8 +184,10 @@ def check_function(name, start, insts):
 
 
 def check_file(path, quiet=False):
+    funcs = []
     with tempfile.TemporaryDirectory() as td:
-        funcs = disassemble(extract_code_object(path, td))
+        for co in extract_code_objects(path, td):
+            funcs += disassemble(co)
     total = 0
     report = []
     for name, start, insts in funcs:
