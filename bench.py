@@ -1,31 +1,42 @@
 #!/usr/bin/env python3
-"""bench.py -- headline benchmark of the MI355X batch-verification engine.
+"""bench.py -- BASELINE.json's metric on MI355X: "secp256k1 recover & SM2 verify sigs/sec at 1/8 GPUs;
+Merkle root GB/s".  One JSON line (rank 0).
 
-Default workload (BASELINE.json configs[1], "C2"): per GPU, a batch of 10,000 synthetic
+`value` (the headline, BASELINE.json configs[1], "C2"): per GPU a batch of 10,000 synthetic
 secp256k1-signed transactions resident in HBM; one step = one pass of the hot path over the batch:
 Keccak256 tx hash of each preimage (TarsHashable.h:16-41) + ECDSA public-key recovery
 (Secp256k1Crypto.cpp:79-93) + sender = right160(Keccak256(pub)) (Transaction.h:68-82), i.e.
 bcosgpu_tx_verify_batch_dev.  Multi-GPU: one process per GPU, each verifies its own shard (weak
-scaling, no data-path collective); rank 0 prints one JSON line with the whole-job rate.
+scaling, no data-path collective); value = txs of all ranks / max-over-ranks wall time.  Exactly
+--steps steps are timed; the warm-up runs at least --warmup steps AND --warm-seconds of back-to-back
+launches so the clock has settled under load before the timed region starts.
 
-Other BASELINE.json configs (--workload):
-  c3  configs[2]: 1M SM2/SM3 txs per GPU (SM3 tx hash + SM2 verify + sender), weak scaling.
-  c4  configs[3]: 1M secp256k1 txs in TOTAL, sharded by index over the ranks (width^L-aligned shard
-      plan); step = verify the shard + the block tx root (width-2 Keccak Merkle, BlockImpl.h:111-154):
-      per-rank frontier, ONE RCCL all-gather over xGMI, top levels on every rank.  Strong scaling.
-  c5  configs[4]: PBFT block-verify replay, 64 blocks x 20k txs in TOTAL, blocks sharded over the
-      ranks; step = verify every tx of the rank's blocks + each block's tx root
-      (bcosgpu_merkle_roots_batch_dev, one launch per tree level for all blocks).  Strong scaling.
+Sub-legs in the same line (`legs`), each timed for >= --leg-seconds of back-to-back steps:
+  c3  configs[2]: 1M SM2/SM3 txs per GPU: SM3 tx hash + SM2 verify + sender (weak scaling).
+  c4  configs[3]: 1M secp256k1 txs in TOTAL sharded over the ranks + the block tx root (width-2
+      Keccak Merkle, BlockImpl.h:111-154): per-rank frontier, ONE RCCL all-gather, top levels on
+      every rank (strong scaling).
+  c5  configs[4] (with --legs ...,c5): PBFT block-verify replay, 64 blocks x 20k txs sharded by block:
+      recover + each block's tx root (strong scaling).
+Each leg carries its roofline (the tx_verify kernel, HIP events on its launch stream; integer-MAC
+bound) and its HBM traffic from the committed rocprofv3 PMC pass of the same workload (profiles/).
 
-Also reported (same line): the roofline of the dominant kernel (tx_verify) from HIP events on the
-launch stream, its HBM traffic from the committed rocprofv3 PMC pass of the same workload
-(profiles/), the CPU baseline (the oracle restatement, multi-threaded, on a bounded sample, rank 0 at
-N=1 only), and the C1 Merkle rate (merkleBench: width-16 root over 100k 32-byte leaves).
+`merkle` (rank 0, N = 1): configs[0] (merkleBench, width-16 root over 100k 32-byte leaves) and 1M /
+16M-leaf roots, Keccak256 and SM3, widths 2 and 16, device-resident, with the ALU roofline.
+
+`cpu_baseline` (rank 0, N = 1): the same work on the host's cores over bounded samples -- the OpenSSL
+1.1.1 libcrypto EC stand-in (oracle/standin_openssl.c) and the oracle's portable C
+restatement, secp256k1 and SM2 -- plus the Merkle CPU restatement with per-level threads.
+
+--gpus N without torchrun spawns the N ranks itself (torch.distributed.run, 127.0.0.1) before
+touching the GPU; under torchrun WORLD_SIZE must equal --gpus.
 """
 import argparse
+import hashlib
 import json
 import math
 import os
+import subprocess
 import sys
 import time
 
@@ -33,47 +44,54 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "fisco-bcos_amd"))
 sys.path.insert(0, ROOT)
 
-# Algorithmic work per unit, used for roofline.achieved:
-#   1 F = one 256-bit modular multiplication = 136 32x32->64 multiply-accumulates (8-limb CIOS)
+# Algorithmic work per unit: 1 F = one 256-bit modular multiplication = 136 32x32->64
+# multiply-accumulates (8-limb CIOS); secp256k1 recover 3,240 F, SM2 verify 3,210 F (non-GLV counts).
 MAC_PER_F = 136
 F_SECP_RECOVER = 3240
 F_SM2_VERIFY = 3210
-# Field multiplications this implementation actually executes per unit (counted from the kernel
-# schedules; the safegcd inversions are ALU work outside the F count, so these are
-# lower bounds on issued work). GLV halves the doublings (128 x 7 F) with 66 mixed adds (11 F) and
-# 33 phi lookups (1 F), the R table costs ~130 F, u1*G takes 16 mixed adds on the 16-bit comb
-# (32 on the 8-bit comb of the small-batch coop/split kernels), sqrt 270, complete add 16, rest ~10.
-# SM2: 256 a=-3 doublings x 8 F, 65 Booth mixed adds x 11 F, table ~133 F, comb 176 F, rest ~20.
+# Field multiplications the kernels actually execute per unit (counted from their schedules,
+# DESIGN.md §9; the safegcd inversions are ALU work outside the F count): GLV recover with the
+# 16-bit comb (throughput kernels) / the 8-bit comb (small-batch kernels); SM2 radix-16 Booth.
 F_SECP_EXEC_WIDE = 2255
 F_SECP_EXEC_COMB8 = 2431
 F_SM2_EXEC = 3092
-# integer-MAC peak of gfx950 (v_mad_u64_u32 lane-ops/s), measured by fisco-bcos_amd/tools/intbench.hip
-# on MI355X (profiles/r01_intbench.json)
-PEAK_MAC_PER_S = 3.0785e13
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_{}.json")
+# measured gfx950 lane-op peaks (fisco-bcos_amd/tools/intbench.hip on MI355X, profiles/r01_intbench.json)
+PEAK_MAC_PER_S = 3.0785e13      # v_mad_u64_u32
+PEAK_ALU_PER_S = 3.7497e13      # full-rate 32-bit VALU (v_alignbit_b32)
+# SURVEY §8d ALU ops per permutation / compression
+KECCAK_F_OPS = 6240
+SM3_C_OPS = 2100
+PMC_GLOB = "r02_pmc_{}.json"
+KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_kernels.hip", "fisco-bcos_amd/csrc/fe_asm.h", "fisco-bcos_amd/csrc/fe.h",
+              "fisco-bcos_amd/csrc/ec.h", "fisco-bcos_amd/csrc/hash_device.h", "fisco-bcos_amd/csrc/modinv.h"]
 
 WORKLOADS = {
-    "c2": dict(suite=0, n=10_000, scaling="weak", metric="sigs_per_sec",
+    "c2": dict(suite=0, n=10_000, scaling="weak",
                name="C2: 10k synthetic secp256k1 txs / GPU: Keccak256 tx hash + ECDSA recover + sender"),
-    "c3": dict(suite=1, n=1_000_000, scaling="weak", metric="sm2_verify_per_sec",
+    "c3": dict(suite=1, n=1_000_000, scaling="weak",
                name="C3: 1M synthetic SM2/SM3 txs / GPU: SM3 tx hash + SM2 verify + sender"),
-    "c4": dict(suite=0, n=1_000_000, scaling="strong", metric="sigs_per_sec",
+    "c4": dict(suite=0, n=1_000_000, scaling="strong",
                name="C4: 1M synthetic secp256k1 txs sharded over the GPUs: tx hash + recover + sender "
                     "+ width-2 Keccak tx root (per-GPU frontier, RCCL all-gather)"),
-    "c5": dict(suite=0, n=64 * 20_000, blocks=64, scaling="strong", metric="sigs_per_sec",
+    "c5": dict(suite=0, n=64 * 20_000, blocks=64, scaling="strong",
                name="C5: PBFT block-verify replay, 64 blocks x 20k secp256k1 txs sharded by block: "
                     "recover + per-block width-2 Keccak tx root"),
 }
 
 
+def kernel_source_sha():
+    h = hashlib.sha256()
+    for p in KERNEL_SRC:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def _kernel_name(suite, n):
-    """Which tx-verify kernel the library launches for this batch (mirrors ecc_kernels.hip policy)."""
-    split = os.environ.get("BCOSGPU_TXV_SPLIT")
-    if suite == 0 and (split == "1" or (split != "0" and n <= (1 << 15))):
-        return "tx_verify_split_kernel" if os.environ.get("BCOSGPU_TXV_COOP") == "0" else "tx_verify_coop_kernel"
-    occ = os.environ.get("BCOSGPU_TXV_OCC")
-    occ = int(occ) if occ in ("1", "2") else (2 if n >= (1 << 17) else 1)
-    return "tx_verify_kernel<%d,%d>" % (suite, occ)
+    """Which tx-verify kernel the library launches for this batch (mirrors launch_tx_verify)."""
+    if suite == 0 and n <= (1 << 15):
+        return "tx_verify_coop_kernel"
+    return "tx_verify_kernel<%d,%d>" % (suite, 2 if n >= (1 << 17) else 1)
 
 
 def _norm(name):
@@ -82,68 +100,73 @@ def _norm(name):
 
 def _traffic(workload, kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes of this workload
-    (tools/prof_summary.py; FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction)."""
-    path = PMC_FILE.format(workload)
+    (tools/prof_summary.py; FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 correction), and
+    whether they were taken on the kernel sources of this tree."""
+    path = os.path.join(ROOT, "profiles", PMC_GLOB.format(workload))
     try:
         with open(path) as f:
             pmc = json.load(f)
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
     for name, c in pmc.get("kernels", {}).items():
         if _norm(name) == _norm(kernel) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            return (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, ROOT)
-    return None, None
+            same = pmc.get("kernel_source_sha") == kernel_source_sha()
+            return (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, ROOT), same
+    return None, None, None
 
 
 def _block_plan(nblocks, world, rank):
     per = math.ceil(nblocks / world)
-    lo, hi = min(rank * per, nblocks), min((rank + 1) * per, nblocks)
-    return lo, hi
+    return min(rank * per, nblocks), min((rank + 1) * per, nblocks)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-merkle", action="store_true")
-    ap.add_argument("--no-tars", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    args = ap.parse_args()
+def spawn_ranks(args):
+    """--gpus N without a launcher: run this script under torch.distributed.run (one process per GPU,
+    RCCL rendezvous on 127.0.0.1) as a child -- before this process touches the GPU -- and return its
+    exit status."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
+
+class Ctx:
+    def __init__(self, world, rank, dist):
+        self.world, self.rank, self.dist = world, rank, dist
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        dev = "cpu" if self.dist.get_backend() == "gloo" else "cuda"
+        t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+
+def run_leg(ctx, wl_name, steps=None, warmup=3, warm_seconds=0.0, min_seconds=2.0):
+    """One workload on this rank; returns the leg's record (rank 0's view, times max over ranks)."""
     import numpy as np
     import torch
-    import torch.distributed as dist
-
-    import bcos_gpu
     from bcos_gpu import device, parallel, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local)
-    if world > 1:
-        # RCCL over xGMI; BCOSGPU_BENCH_BACKEND=gloo rehearses the multi-rank logic on one GPU
-        backend = os.environ.get("BCOSGPU_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    bcos_gpu.ensure_device(local)
-    wl = WORKLOADS[args.workload]
-    suite = wl["suite"]
+    wl = WORKLOADS[wl_name]
+    suite, world, rank = wl["suite"], ctx.world, ctx.rank
     stream = torch.cuda.current_stream()
-
-    # ---- this rank's share of the work
     txroot = None
     block_off = None
-    if args.workload == "c4":
+    if wl_name == "c4":
         txroot = parallel.gpu_sharded_tx_root(wl["n"], world, rank, device.KECCAK256, 2, "cuda")
         lo, hi = txroot.local_range
         n = hi - lo
-    elif args.workload == "c5":
+    elif wl_name == "c5":
         per_block = wl["n"] // wl["blocks"]
         blo, bhi = _block_plan(wl["blocks"], world, rank)
         n = (bhi - blo) * per_block
@@ -153,115 +176,223 @@ def main():
     else:
         n = wl["n"]
     units_total = wl["n"] if wl["scaling"] == "strong" else wl["n"] * world
-
-    # ---- synthetic, device-resident batch of this rank (distinct keys/txs per rank)
     b = synth.make_batch(suite, max(n, 1), seed=0xF15C0BC5 + 7919 * rank)
     txhash = torch.empty((max(n, 1), 32), dtype=torch.uint8, device="cuda")
     sender = torch.empty((max(n, 1), 20), dtype=torch.uint8, device="cuda")
     status = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    evs = []
 
-    def step(k=None):
-        if k is not None:
-            ev[k][0].record(stream)
+    def step(timed=False):
+        if timed:
+            a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
         if n:
             device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, txhash, sender, status, stream)
-        if k is not None:
-            ev[k][1].record(stream)
+        if timed:
+            c.record(stream)
+            evs.append((a, c))
         if txroot is not None:
             txroot(txhash[:n])
         elif block_off is not None and n:
             device.merkle_roots_batch(device.KECCAK256, 2, txhash, block_off, work, roots, stream)
 
-    for _ in range(args.warmup):
+    # calibrate, then warm up for >= warmup steps and >= warm_seconds of back-to-back launches (the
+    # clock settles under load); step counts are agreed over the ranks (C4 steps hold a collective)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(3):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    per = ctx.max((time.perf_counter() - t1) / 3)
+    for k in range(max(warmup, int(math.ceil(warm_seconds / max(per, 1e-6))))):
+        step()
+        if k % 32 == 31:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    if steps is None:  # time-based leg: enough steps for >= min_seconds
+        steps = max(3, int(math.ceil(min_seconds / max(per, 1e-6))))
+    ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
+    for _ in range(steps):
+        step(timed=True)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    ctx.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = sum(a.elapsed_time(c) for a, c in ev) / args.steps  # tx_verify launch, on its stream
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = ctx.max(time.perf_counter() - t0)
+    kernel_ms = sum(a.elapsed_time(c) for a, c in evs) / len(evs)
     ok_frac = float((status[:n] == 0).float().mean().item()) if n else 1.0
-
-    if rank == 0:
-        value = units_total * args.steps / elapsed
-        f_per = F_SECP_RECOVER if suite == 0 else F_SM2_VERIFY
-        kname = _kernel_name(suite, n)
-        achieved = n * f_per * MAC_PER_F / (kernel_ms * 1e-3)
-        traffic, traffic_src = _traffic(args.workload, kname)
-        roofline = {"bound": "int-valu", "achieved": achieved / 1e12, "peak": PEAK_MAC_PER_S / 1e12,
-                    "unit": "TMAC/s", "frac": achieved / PEAK_MAC_PER_S, "traffic": traffic,
-                    "traffic_source": traffic_src, "kernel": kname, "kernel_ms": kernel_ms,
-                    "units_per_launch": n,
-                    "work_per_unit": "%d F x %d MAC (SURVEY.md 8d)" % (f_per, MAC_PER_F)}
-        # achieved/frac above use the fixed non-GLV count of SURVEY 8d (useful work per second), which
-        # can exceed 1 because GLV and the 16-bit comb execute fewer multiplications; "executed" is
-        # the issue-bound fraction for the multiplications the kernel really performs
-        if suite == 0:
-            f_exec = F_SECP_EXEC_WIDE if kname.startswith("tx_verify_kernel") else F_SECP_EXEC_COMB8
-        else:
-            f_exec = F_SM2_EXEC
-        ex = n * f_exec * MAC_PER_F / (kernel_ms * 1e-3)
-        roofline["executed"] = {"f_per_unit": f_exec, "achieved": ex / 1e12, "frac": ex / PEAK_MAC_PER_S,
-                                "note": "F counted from the kernel schedule (DESIGN.md 9); inversions excluded"}
-        cpu = None
-        host_api = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(b, suite, min(n, 20000), args.cpu_threads)
-            host_api = host_api_rate(b, suite, n)
-        line = {
-            "metric": wl["metric"],
-            "value": value, "unit": "tx/s (hash + recover/verify + sender%s)" % (
-                " + tx root" if args.workload in ("c4", "c5") else ""),
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True, "scaling": wl["scaling"], "vs_baseline": None,
-            "dtype": "u32 (256-bit integer)",
-            "data": "synthetic (distinct key per tx, 1%% bit-flipped s, 0.1%% v=4; valid frac %.4f)" % ok_frac,
-            "config": {"workload": wl["name"], "txs_total": units_total, "txs_rank0": n,
-                       "parallelism": "dp%d (%s)" % (world, "block shards" if args.workload == "c5" else "tx-index shards")},
-            "roofline": roofline, "cpu_baseline": cpu, "pcie_inclusive": host_api,
-        }
-        if not args.no_merkle:
-            line["merkle_c1"] = merkle_c1()
-        if world == 1 and n and not args.no_tars:
-            line["create_transaction"] = create_transaction_leg(b, suite, n, status[:n])
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    kname = _kernel_name(suite, n)
+    f_alg = F_SECP_RECOVER if suite == 0 else F_SM2_VERIFY
+    if suite == 0:
+        f_exec = F_SECP_EXEC_WIDE if kname.startswith("tx_verify_kernel") else F_SECP_EXEC_COMB8
+    else:
+        f_exec = F_SM2_EXEC
+    ex = n * f_exec * MAC_PER_F / (kernel_ms * 1e-3)
+    alg = n * f_alg * MAC_PER_F / (kernel_ms * 1e-3)
+    traffic, traffic_src, same_src = _traffic(wl_name, kname)
+    roofline = {
+        "bound": "int-valu", "achieved": ex / 1e12, "peak": PEAK_MAC_PER_S / 1e12, "unit": "TMAC/s",
+        "frac": ex / PEAK_MAC_PER_S, "traffic": traffic, "traffic_source": traffic_src,
+        "traffic_same_kernel_source": same_src, "kernel": kname, "kernel_ms": kernel_ms, "units_per_launch": n,
+        "work_per_unit": "%d F x %d MAC executed (kernel schedule, DESIGN.md 9)" % (f_exec, MAC_PER_F),
+        "algorithmic": {"work_per_unit": "%d F x %d MAC (SURVEY.md 8d, non-GLV count)" % (f_alg, MAC_PER_F),
+                        "achieved": alg / 1e12, "frac": alg / PEAK_MAC_PER_S,
+                        "note": "useful work per second against the MAC peak; exceeds the executed frac "
+                                "because GLV and the comb execute fewer multiplications than 8d counts"},
+        "algorithmic_bytes_per_unit": 151 + 65 + 53 if suite == 0 else 151 + 128 + 53,
+    }
+    rec = {"workload": wl["name"], "value": units_total * steps / elapsed, "unit": "tx/s",
+           "ms_per_step": elapsed / steps * 1e3, "steps": steps, "timed_s": elapsed, "scaling": wl["scaling"],
+           "txs_total": units_total, "txs_rank0": n, "valid_frac": ok_frac, "roofline": roofline}
+    state = {"batch": b, "status": status[:n], "n": n}
+    return rec, state
 
 
-def cpu_baseline(b, suite, sample, threads, min_seconds=1.0):
-    """The oracle (C restatement, multi-threaded) on `sample` txs of the same batch, host cores,
-    repeated until >= min_seconds of wall time (~16 CPU-seconds at 16 threads)."""
+def merkle_legs(cpu_threads):
+    """configs[0] (merkleBench: width-16 root, 100k leaves) and the 1M / 16M-leaf roofline legs."""
+    import numpy as np
+    import torch
+    from bcos_gpu import device
+    out = {}
+    for n in (100_000, 1_000_000, 16_000_000):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(n)
+        leaves = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
+        for hname, h in (("keccak256", device.KECCAK256), ("sm3", device.SM3)):
+            for width in (16, 2):
+                tree = torch.empty((device.merkle_size(n, width), 32), dtype=torch.uint8, device="cuda")
+                root = torch.empty(32, dtype=torch.uint8, device="cuda")
+                for _ in range(3):
+                    device.merkle_root(h, width, leaves, tree, root)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                device.merkle_root(h, width, leaves, tree, root)
+                torch.cuda.synchronize()
+                reps = max(5, int(0.25 / max(time.perf_counter() - t1, 1e-6)))
+                a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(reps):
+                    device.merkle_root(h, width, leaves, tree, root)
+                c.record()
+                torch.cuda.synchronize()
+                ms = a.elapsed_time(c) / reps
+                units, ops = merkle_work(n, width, h == device.KECCAK256)
+                rec = {"ms": ms, "GB_per_s": n * 32 / (ms * 1e-3) / 1e9, "reps": reps,
+                       "roofline": {"bound": "int-valu", "achieved": ops / (ms * 1e-3) / 1e12,
+                                    "peak": PEAK_ALU_PER_S / 1e12, "unit": "Tops/s",
+                                    "frac": ops / (ms * 1e-3) / PEAK_ALU_PER_S,
+                                    "work": "%d %s x %d ops (SURVEY.md 8d)" % (
+                                        units, "Keccak-f" if h == device.KECCAK256 else "SM3 compressions",
+                                        KECCAK_F_OPS if h == device.KECCAK256 else SM3_C_OPS),
+                                    "hbm_bytes": n * 32 + device.merkle_size(n, width) * 32}}
+                out["%s_w%d_%s" % (hname, width, _count(n))] = rec
+        del leaves
+        torch.cuda.empty_cache()
+    if cpu_threads:
+        out["cpu_baseline"] = merkle_cpu(cpu_threads)
+    return out
+
+
+def _count(n):
+    return "%dk" % (n // 1000) if n < 1_000_000 else "%dM" % (n // 1_000_000)
+
+
+def merkle_work(n, width, keccak):
+    """Exact permutation / compression count of Merkle<H,width> over n leaves (Merkle.h:243-261):
+    per level, groups of <= width children hashed as 32k-byte messages."""
+    units, m = 0, n
+    while m > 1:
+        full, rem = divmod(m, width)
+        for k, cnt in ((width, full), (rem, 1 if rem else 0)):
+            if cnt:
+                ln = 32 * k
+                units += cnt * ((ln // 136 + 1) if keccak else ((ln + 8) // 64 + 1))
+        m = full + (1 if rem else 0)
+    return units, units * (KECCAK_F_OPS if keccak else SM3_C_OPS)
+
+
+def merkle_cpu(threads):
+    """The oracle's Merkle restatement (per-level std::thread parallelism, as TBB Merkle.h:248) on the
+    host over 1M leaves, widths 16 and 2, Keccak256 and SM3."""
     import numpy as np
     from oracle import oracle
-    pre = b.pre.cpu().numpy()
-    pre_off = b.pre_off[: sample + 1].cpu().numpy().astype(np.uint64)
-    sig = b.sig.cpu().numpy()
-    sig_off = b.sig_off[: sample + 1].cpu().numpy().astype(np.uint64)
-    oracle.tx_verify_packed(suite, pre, pre_off[:65], sig, sig_off[:65], nthreads=threads)  # warm-up
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        oracle.tx_verify_packed(suite, pre, pre_off, sig, sig_off, nthreads=threads)
-        reps += 1
-        dt = time.perf_counter() - t0
-        if dt >= min_seconds:
-            break
-    return {"value": reps * sample / dt, "unit": "tx/s", "cores": threads, "kind": "port",
-            "sample": "%d x %d txs of the same batch (%.1f s wall), oracle/ C restatement (4x64-bit Montgomery, "
-                      "4-bit Straus), %d threads" % (reps, sample, dt, threads)}
+    rng = np.random.default_rng(3)
+    leaves = rng.integers(0, 256, size=(1_000_000, 32), dtype=np.uint8)
+    res = {}
+    for hname, h in (("keccak256", oracle.KECCAK256), ("sm3", oracle.SM3)):
+        for width in (16, 2):
+            oracle.merkle(h, width, leaves[:1000], nthreads=threads)
+            reps, t0 = 0, time.perf_counter()
+            while reps < 1 or time.perf_counter() - t0 < 0.5:
+                oracle.merkle(h, width, leaves, nthreads=threads)
+                reps += 1
+            dt = (time.perf_counter() - t0) / reps
+            res["%s_w%d_1M" % (hname, width)] = {"ms": dt * 1e3, "GB_per_s": 32e6 / dt / 1e9}
+    return {"legs": res, "threads": threads, "kind": "port",
+            "impl": "oracle/merkle.c restatement of Merkle.h:170-261, level-parallel pthreads"}
+
+
+def _cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model
+
+
+def cpu_threads():
+    """Threads for the CPU legs: the box's CPU share (OMP_NUM_THREADS is set to it on the GPU box;
+    nproc / the affinity mask show the whole machine there), else the affinity mask."""
+    env = os.environ.get("BCOSGPU_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    aff = len(os.sched_getaffinity(0))
+    return min(int(env), aff) if env and env.isdigit() and int(env) > 0 else aff
+
+
+def cpu_baseline(batches, threads, min_seconds=1.0):
+    """Transaction::verify (Transaction.h:68-82) per tx on the host (TransactionSync.cpp:516-548's
+    parallel_for) over bounded samples of the benchmark batches: the OpenSSL 1.1.1 EC stand-in
+     and the oracle's portable C restatement, secp256k1 and SM2.  value = the faster
+    secp256k1 leg (the headline metric's CPU counterpart)."""
+    import numpy as np
+    from oracle import oracle
+    legs = {}
+    for suite, b, sample in batches:
+        pre = b.pre.cpu().numpy()
+        pre_off = np.ascontiguousarray(b.pre_off[: sample + 1].cpu().numpy().astype(np.uint64))
+        sig = b.sig.cpu().numpy()
+        sig_off = np.ascontiguousarray(b.sig_off[: sample + 1].cpu().numpy().astype(np.uint64))
+        impls = [("port", oracle.tx_verify_packed)]
+        if oracle.standin() is not None:
+            impls.append(("openssl", oracle.standin_tx_verify_packed))
+        for name, fn in impls:
+            fn(suite, pre, pre_off[:65], sig, sig_off[:65], nthreads=threads)  # warm-up
+            reps, t0 = 0, time.perf_counter()
+            while reps < 1 or time.perf_counter() - t0 < min_seconds:
+                fn(suite, pre, pre_off, sig, sig_off, nthreads=threads)
+                reps += 1
+            dt = time.perf_counter() - t0
+            legs["%s_%s" % ("secp256k1" if suite == 0 else "sm2", name)] = {
+                "value": reps * sample / dt, "unit": "tx/s", "per_thread": reps * sample / dt / threads,
+                "sample": "%d x %d txs (%.1f s wall)" % (reps, sample, dt)}
+    best = max((v for k, v in legs.items() if k.startswith("secp256k1")), key=lambda v: v["value"])
+    best_name = [k for k, v in legs.items() if v is best][0]
+    logical = os.cpu_count()
+    return {"value": best["value"], "unit": "tx/s", "cores": threads, "kind": "port",
+            "impl": best_name, "sample": best["sample"],
+            "host": {"cpu_model": _cpu_info(), "nproc": logical, "affinity": len(os.sched_getaffinity(0)),
+                     "threads_used": threads, "libcrypto": oracle.standin_version()},
+            "full_host_estimate": {"value": best["per_thread"] * logical, "unit": "tx/s",
+                                   "note": "per-thread rate x logical CPUs (linear upper bound, SMT counted); "
+                                           "the legs ran on the box's CPU share"},
+            "legs": legs,
+            "note": "stand-ins for the reference's third-party ECC (wedpr libsecp256k1 / TASSL, absent and "
+                    "unbuildable here, BASELINE.md 3): OpenSSL libcrypto EC and the oracle's 4x64 Montgomery port"}
 
 
 def host_api_rate(b, suite, n, reps=5):
@@ -286,8 +417,7 @@ def host_api_rate(b, suite, n, reps=5):
 
 def create_transaction_leg(b, suite, n, want_status, reps=20):
     """The same batch from raw Tars encodings (createTransaction(bytes, checkSig = true, checkHash = true),
-    TransactionFactoryImpl.h:46-85): device decode + pack + verify + hash check, HBM-resident.  Reported
-    beside `value` (which starts from packed preimages); decode_ms is the decode + pack share."""
+    TransactionFactoryImpl.h:46-85): device decode + pack + verify + hash check, HBM-resident."""
     import torch
     from bcos_gpu import device, synth
     enc, off = synth.tars_encodings(b)
@@ -320,30 +450,94 @@ def create_transaction_leg(b, suite, n, want_status, reps=20):
             "path": "bcosgpu_tars_tx_verify_batch_dev (decode + pack + verify + dataHash check)"}
 
 
-def merkle_c1():
-    """C1: merkleBench width-16 Merkle root over 100k leaves (Keccak256 and SM3), device-resident."""
-    import numpy as np
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3500, help="timed steps of the headline (C2) leg")
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warm-seconds", type=float, default=2.0, help="minimum warm-up before the timed region")
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS), help="the headline leg")
+    ap.add_argument("--legs", default="c3,c4", help="comma-separated sub-legs ('' for none)")
+    ap.add_argument("--leg-seconds", type=float, default=2.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-merkle", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the PCIe and createTransaction legs")
+    args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+
     import torch
-    from bcos_gpu import device
-    n = 100_000
-    rng = np.random.default_rng(1)
-    leaves = torch.from_numpy(rng.integers(0, 256, size=(n, 32), dtype=np.uint8)).cuda()
-    out = {}
-    for hname, h in (("keccak256", device.KECCAK256), ("sm3", device.SM3)):
-        tree = torch.empty((device.merkle_size(n, 16), 32), dtype=torch.uint8, device="cuda")
-        root = torch.empty(32, dtype=torch.uint8, device="cuda")
-        for _ in range(3):
-            device.merkle_root(h, 16, leaves, tree, root)
-        torch.cuda.synchronize()
-        reps = 20
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            device.merkle_root(h, 16, leaves, tree, root)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / reps
-        out[hname] = {"ms": dt * 1e3, "GB_per_s": n * 32 / dt / 1e9}
-    return out
+    import torch.distributed as dist
+    import bcos_gpu
+
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local)
+    if world > 1:
+        # RCCL over xGMI; BCOSGPU_BENCH_BACKEND=gloo rehearses the multi-rank logic on one GPU
+        backend = os.environ.get("BCOSGPU_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    bcos_gpu.ensure_device(local)
+    ctx = Ctx(world, rank, dist)
+
+    head, head_state = run_leg(ctx, args.workload, steps=args.steps, warmup=args.warmup,
+                               warm_seconds=args.warm_seconds)
+    legs = {}
+    states = {}
+    for wl in [x for x in args.legs.split(",") if x and x != args.workload]:
+        legs[wl], states[wl] = run_leg(ctx, wl, steps=None, warmup=3, warm_seconds=0.5,
+                                       min_seconds=args.leg_seconds)
+        if wl not in ("c3",):
+            states.pop(wl)
+        torch.cuda.empty_cache()
+
+    line = None
+    if rank == 0:
+        wl = WORKLOADS[args.workload]
+        line = {
+            "metric": "sigs_per_sec", "value": head["value"], "unit": "tx/s (hash + recover/verify + sender%s)" % (
+                " + tx root" if args.workload in ("c4", "c5") else ""),
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
+            "higher_is_better": True, "scaling": wl["scaling"], "vs_baseline": None,
+            "dtype": "u32 (256-bit integer)",
+            "data": "synthetic (distinct key per tx, 1%% bit-flipped s, 0.1%% v=4; valid frac %.4f)" % head["valid_frac"],
+            "config": {"workload": wl["name"], "txs_total": head["txs_total"], "txs_rank0": head["txs_rank0"],
+                       "parallelism": "dp%d (%s)" % (world, "block shards" if args.workload == "c5" else "tx-index shards"),
+                       "timed_s": head["timed_s"], "warm_seconds": args.warm_seconds},
+            "roofline": head["roofline"], "cpu_baseline": None, "legs": legs,
+            "kernel_source_sha": kernel_source_sha(),
+        }
+    if rank == 0 and world == 1:
+        threads = cpu_threads()
+        if not args.no_extras:
+            b = head_state["batch"]
+            line["pcie_inclusive"] = host_api_rate(b, b.suite, head_state["n"])
+            line["create_transaction"] = create_transaction_leg(b, b.suite, head_state["n"], head_state["status"])
+        if not args.no_merkle:
+            line["merkle"] = merkle_legs(0 if args.no_cpu_baseline else threads)
+            line["merkle_c1"] = {h: line["merkle"]["%s_w16_100k" % h] for h in ("keccak256", "sm3")}
+        if not args.no_cpu_baseline:
+            from bcos_gpu import synth
+            batches = [(0, head_state["batch"], min(head_state["n"], 20000))]
+            sm2 = states.get("c3", {}).get("batch") or synth.make_batch(1, 20000, seed=0x5A2)
+            batches.append((1, sm2, 20000))
+            line["cpu_baseline"] = cpu_baseline(batches, threads)
+            line["cpu_baseline"]["merkle"] = line.get("merkle", {}).pop("cpu_baseline", None)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -34,6 +34,8 @@ _SIGS = {
     "bcosgpu_version": (_I, []),
     "bcosgpu_device_count": (_I, []),
     "bcosgpu_init": (_I, [_I]),
+    "bcosgpu_init_ex": (_I, [_I, _I]),
+    "bcosgpu_set_tx_kernel_policy": (_I, [_I, _I, _I]),
     "bcosgpu_last_error": (ctypes.c_char_p, []),
     "bcosgpu_merkle_size": (ctypes.c_uint64, [ctypes.c_uint64, _I]),
     "bcosgpu_hash_batch": (_I, [_I, _P, _P, _SZ, _P]),

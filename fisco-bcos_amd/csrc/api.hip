@@ -97,7 +97,9 @@ uint64_t bcosgpu_merkle_size(uint64_t n, int width) {
     return n == 1 ? 1 : merkle_size(n, width);
 }
 
-int bcosgpu_init(int device) {
+int bcosgpu_init(int device) { return bcosgpu_init_ex(device, 0); }
+
+int bcosgpu_init_ex(int device, int flags) {
     int n = bcosgpu_device_count();
     if (n <= 0) return set_err(BCOSGPU_E_NODEV, "no HIP device visible");
     if (device < 0 || device >= n) return set_err(BCOSGPU_E_ARG, "device index out of range");
@@ -112,10 +114,15 @@ int bcosgpu_init(int device) {
         if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
             return set_err(BCOSGPU_E_NODEV, std::string("device is ") + prop.gcnArchName + ", built for gfx950");
         HIP_OK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
-        int rc = ecc_init_tables(device);
+        int rc = ecc_init_tables(device, (flags & BCOSGPU_INIT_SMALL_TABLES) != 0);
         if (rc) return set_err(rc, "ecc table setup failed");
         w->ready = true;
     }
+    return 0;
+}
+
+int bcosgpu_set_tx_kernel_policy(int split, int occupancy, int coop) {
+    set_tx_kernel_policy(split, occupancy, coop);
     return 0;
 }
 

@@ -15,6 +15,7 @@
 //   variable base: radix-16 Booth recoding (digits in [-8, 8]) over a register-resident table of
 //                  1P..8P; every lane runs the same 65-window schedule (no divergence).
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <type_traits>
 #include "ec.h"
@@ -173,6 +174,19 @@ __device__ __forceinline__ void comb_mul(Jac& acc, const fe& k_plain, const uint
         fe_copy(T.x, N.x);
         fe_copy(T.y, N.y);
     }
+}
+
+struct CombTab {
+    const uint32_t* p;
+    int bits;
+};
+
+// comb_mul over whichever table the device holds: the 16-bit one, or the 8-bit one when the 64 MiB
+// tables were not allocated (bcosgpu_init_ex flag / allocation failure); tbits is launch-uniform
+template <class C>
+__device__ __forceinline__ void comb_mul_rt(Jac& acc, const fe& k, const uint32_t* __restrict__ tab, int tbits) {
+    if (tbits == kWideBits) comb_mul<C, kWideBits>(acc, k, tab);
+    else comb_mul<C, 8>(acc, k, tab);
 }
 
 // acc = k * P, radix-16 Booth recoding over the table 1P..8P (k plain, < 2^256)
@@ -576,23 +590,72 @@ __global__ __launch_bounds__(256) void comb_wide_kernel(uint32_t* __restrict__ w
     }
 }
 
-int ecc_init_tables(int device) {
+// Kernel-selection policy, read from the environment once (at the first bcosgpu_init) and settable
+// through bcosgpu_set_tx_kernel_policy (tests, tuning); never read per launch.
+struct TxKernelPolicy {
+    int split = -1;  // small-batch secp kernels: -1 by size (n <= 2^15), 0 never, 1 always
+    int occ = 0;     // tx_verify_kernel occupancy: 0 by size (2 for n >= 2^17), 1 or 2 forced
+    int coop = 1;    // small-batch secp kernel: 1 cooperative-pair, 0 4-wave split
+};
+static TxKernelPolicy g_policy;
+static bool g_policy_read = false;
+
+static void read_policy_env() {
+    if (g_policy_read) return;
+    g_policy_read = true;
+    if (const char* e = getenv("BCOSGPU_TXV_SPLIT")) g_policy.split = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
+    if (const char* e = getenv("BCOSGPU_TXV_OCC")) g_policy.occ = (atoi(e) == 1 || atoi(e) == 2) ? atoi(e) : 0;
+    if (const char* e = getenv("BCOSGPU_TXV_COOP")) g_policy.coop = atoi(e) != 0;
+}
+
+void set_tx_kernel_policy(int split, int occ, int coop) {
     std::lock_guard<std::mutex> g(g_tab_mu);
+    read_policy_env();
+    g_policy.split = (split == 0 || split == 1) ? split : -1;
+    g_policy.occ = (occ == 1 || occ == 2) ? occ : 0;
+    g_policy.coop = coop != 0;
+}
+
+static void free_tables(uint32_t*& a, uint32_t*& b, uint32_t*& c, uint32_t*& d) {
+    for (uint32_t** p : {&a, &b, &c, &d}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
+}
+
+// Builds the device's comb tables: the 8-bit ones (512 KiB per curve) always; the 16-bit ones (64 MiB
+// per curve) unless `small` or their allocation fails -- the kernels then run the 8-bit comb.
+int ecc_init_tables(int device, int small) {
+    std::lock_guard<std::mutex> g(g_tab_mu);
+    read_policy_env();
     if (device < 0 || device >= 64) return BCOSGPU_E_ARG;
     if (g_tab_k1[device] && g_tab_sm2[device]) return 0;
-    uint32_t *k1 = nullptr, *sm2 = nullptr;
-    if (hipMalloc(&k1, kTabWords * 4) != hipSuccess) return BCOSGPU_E_HIP;
-    if (hipMalloc(&sm2, kTabWords * 4) != hipSuccess) return BCOSGPU_E_HIP;
+    if (const char* e = getenv("BCOSGPU_TABLES")) small = small || std::strcmp(e, "small") == 0;
+    uint32_t *k1 = nullptr, *sm2 = nullptr, *wk1 = nullptr, *wsm2 = nullptr;
+    if (hipMalloc(&k1, kTabWords * 4) != hipSuccess || hipMalloc(&sm2, kTabWords * 4) != hipSuccess) {
+        (void)hipGetLastError();
+        free_tables(k1, sm2, wk1, wsm2);
+        return BCOSGPU_E_HIP;
+    }
     const int n = kCombWindows * kCombEntries;
     hipLaunchKernelGGL((comb_table_kernel<CurveK1, FieldK1>), dim3((n + 255) / 256), dim3(256), 0, 0, k1, 0);
     hipLaunchKernelGGL((comb_table_kernel<CurveSM2, FieldP2>), dim3((n + 255) / 256), dim3(256), 0, 0, sm2, 1);
-    uint32_t *wk1 = nullptr, *wsm2 = nullptr;
-    if (hipMalloc(&wk1, kWideTabWords * 4) != hipSuccess) return BCOSGPU_E_HIP;
-    if (hipMalloc(&wsm2, kWideTabWords * 4) != hipSuccess) return BCOSGPU_E_HIP;
-    const unsigned gw = static_cast<unsigned>((static_cast<uint64_t>(kWideWindows) * kWideEntries + 255) / 256);
-    hipLaunchKernelGGL((comb_wide_kernel<CurveK1, FieldK1>), dim3(gw), dim3(256), 0, 0, wk1, k1);
-    hipLaunchKernelGGL((comb_wide_kernel<CurveSM2, FieldP2>), dim3(gw), dim3(256), 0, 0, wsm2, sm2);
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return BCOSGPU_E_HIP;
+    if (!small && (hipMalloc(&wk1, kWideTabWords * 4) != hipSuccess ||
+                   hipMalloc(&wsm2, kWideTabWords * 4) != hipSuccess)) {
+        (void)hipGetLastError();  // not enough memory for the wide tables: run on the 8-bit ones
+        if (wk1) (void)hipFree(wk1);
+        if (wsm2) (void)hipFree(wsm2);
+        wk1 = wsm2 = nullptr;
+    }
+    if (wk1) {
+        const unsigned gw = static_cast<unsigned>((static_cast<uint64_t>(kWideWindows) * kWideEntries + 255) / 256);
+        hipLaunchKernelGGL((comb_wide_kernel<CurveK1, FieldK1>), dim3(gw), dim3(256), 0, 0, wk1, k1);
+        hipLaunchKernelGGL((comb_wide_kernel<CurveSM2, FieldP2>), dim3(gw), dim3(256), 0, 0, wsm2, sm2);
+    }
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        free_tables(k1, sm2, wk1, wsm2);
+        return BCOSGPU_E_HIP;
+    }
     g_tab_k1[device] = k1;
     g_tab_sm2[device] = sm2;
     g_wtab_k1[device] = wk1;
@@ -600,13 +663,16 @@ int ecc_init_tables(int device) {
     return 0;
 }
 
-// 16-bit comb tables (the default for every kernel but the small-batch secp tx_verify ones)
-static int tables(const uint32_t** k1, const uint32_t** sm2) {
+// The comb tables of the current device: the 16-bit ones when present (*bits = 16), else the 8-bit
+// ones (*bits = 8).
+static int tables(const uint32_t** k1, const uint32_t** sm2, int* bits) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BCOSGPU_E_NODEV;
-    if (!g_wtab_k1[dev]) return BCOSGPU_E_NODEV;  // bcosgpu_init(dev) not called
-    *k1 = g_wtab_k1[dev];
-    *sm2 = g_wtab_sm2[dev];
+    if (!g_tab_k1[dev]) return BCOSGPU_E_NODEV;  // bcosgpu_init(dev) not called
+    const bool wide = g_wtab_k1[dev] != nullptr;
+    *k1 = wide ? g_wtab_k1[dev] : g_tab_k1[dev];
+    *sm2 = wide ? g_wtab_sm2[dev] : g_tab_sm2[dev];
+    *bits = wide ? kWideBits : 8;
     return 0;
 }
 // 8-bit comb tables
@@ -624,7 +690,7 @@ static int tables8(const uint32_t** k1, const uint32_t** sm2) {
 // (v & 2) with r >= p - n, x not on the curve, Q = infinity.  pub = (x, y) canonical, plain.
 template <bool LDS = false>
 __device__ __forceinline__ bool secp256k1_recover_rsv(const fe& hash_be, const fe& r, const fe& s, uint32_t v,
-                                                      const uint32_t* tab, fe& px, fe& py, uint32_t* ldsx = nullptr) {
+                                                      CombTab tab, fe& px, fe& py, uint32_t* ldsx = nullptr) {
     bool ok = v <= 3u;
     ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, ParamN1::M);
     fe x;
@@ -671,7 +737,7 @@ __device__ __forceinline__ bool secp256k1_recover_rsv(const fe& hash_be, const f
     fe_copy(R.y, y);
     Jac QG, QR, Q;
     glv_mul_k1<LDS>(QR, u2, R, ldsx);
-    comb_mul<CurveK1>(QG, u1, tab);
+    comb_mul_rt<CurveK1>(QG, u1, tab.p, tab.bits);
     CurveK1::add(Q, QG, QR);
     ok = ok && !Q.inf;
     Aff A;
@@ -685,7 +751,7 @@ __device__ __forceinline__ bool secp256k1_recover_rsv(const fe& hash_be, const f
 
 template <bool LDS = false>
 __device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const uint8_t* sig, uint32_t siglen,
-                                                       const uint32_t* tab, fe& px, fe& py, uint32_t* ldsx = nullptr) {
+                                                       CombTab tab, fe& px, fe& py, uint32_t* ldsx = nullptr) {
     if (siglen != 65u) return false;
     ByteReader rd(sig, 65);
     uint32_t w[8];
@@ -767,7 +833,7 @@ __device__ __forceinline__ void sm2_e(uint32_t e[8], const uint32_t X[8], const 
 // The comparison is done projectively (X == (r - e mod n [+ n]) * Z^2), so no inversion.
 template <bool LDS = false>
 __device__ __forceinline__ bool sm2_verify_rs(const fe& hash_be, const fe& r, const fe& s, const uint32_t X[8],
-                                              const uint32_t Y[8], const uint32_t* tab, fe& px, fe& py,
+                                              const uint32_t Y[8], CombTab tab, fe& px, fe& py,
                                               uint32_t* ldsx = nullptr) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -793,7 +859,7 @@ __device__ __forceinline__ bool sm2_verify_rs(const fe& hash_be, const fe& r, co
     reduce_once(e, ParamN2::M);
     Jac QG, QP, Q;
     booth_mul_sm2<LDS>(QP, t, P, ldsx);
-    comb_mul<CurveSM2>(QG, s, tab);
+    comb_mul_rt<CurveSM2>(QG, s, tab.p, tab.bits);
     CurveSM2::add(Q, QG, QP);
     ok = ok && !Q.inf;
     // x1 = X / Z^2 must be congruent to r - e (mod n): x1 = c or c + n (when c + n < p)
@@ -815,7 +881,7 @@ __device__ __forceinline__ bool sm2_verify_rs(const fe& hash_be, const fe& r, co
 
 template <bool LDS = false>
 __device__ __forceinline__ bool sm2_verify_lane(const fe& hash_be, const uint8_t* sig, uint32_t siglen,
-                                                const uint32_t* tab, fe& px, fe& py, uint32_t* ldsx = nullptr) {
+                                                CombTab tab, fe& px, fe& py, uint32_t* ldsx = nullptr) {
     if (siglen != 128u) return false;
     ByteReader rd(sig, 128);
     uint32_t w[8], X[8], Y[8];
@@ -842,7 +908,7 @@ __device__ __forceinline__ bool sm2_verify_lane(const fe& hash_be, const uint8_t
 __device__ __constant__ static const uint32_t kN1HalfPlus[8] = {0x681b20a1u, 0xdfe92f46u, 0x57a4501du, 0x5d576e73u,
                                                             0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu};
 __device__ __forceinline__ bool secp256k1_verify_lane(const fe& hash_be, const uint8_t* sig, const uint8_t* pub,
-                                                      const uint32_t* tab) {
+                                                      CombTab tab) {
     ByteReader rs(sig, 64), rp(pub, 64);
     uint32_t w[8];
     fe r, s, x, y;
@@ -892,7 +958,7 @@ __device__ __forceinline__ bool secp256k1_verify_lane(const fe& hash_be, const u
     }
     Jac QG, QP, Q;
     glv_mul_k1(QP, u2, P);
-    comb_mul<CurveK1>(QG, u1, tab);
+    comb_mul_rt<CurveK1>(QG, u1, tab.p, tab.bits);
     CurveK1::add(Q, QG, QP);
     ok = ok && !Q.inf;
     fe z2, rhs, r2;
@@ -910,14 +976,14 @@ __device__ __forceinline__ bool secp256k1_verify_lane(const fe& hash_be, const u
 // ------------------------------------------------------------------ kernels
 __global__ __launch_bounds__(256) void secp256k1_recover_kernel(const uint8_t* __restrict__ hash,
                                                                 const uint8_t* __restrict__ sig, uint32_t stride,
-                                                                uint64_t n, const uint32_t* __restrict__ tab,
+                                                                uint64_t n, const uint32_t* __restrict__ tab, int tbits,
                                                                 uint8_t* __restrict__ pub, uint8_t* __restrict__ addr,
                                                                 uint8_t* __restrict__ okout) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     fe h, x, y;
     load_be256_aligned(h, hash + 32 * i);
-    const bool ok = secp256k1_recover_lane(h, sig + static_cast<uint64_t>(stride) * i, 65u, tab, x, y);
+    const bool ok = secp256k1_recover_lane(h, sig + static_cast<uint64_t>(stride) * i, 65u, CombTab{tab, tbits}, x, y);
     if (!ok) {
         fe_zero(x);
         fe_zero(y);
@@ -938,13 +1004,13 @@ __global__ __launch_bounds__(256) void secp256k1_recover_kernel(const uint8_t* _
 
 __global__ __launch_bounds__(256) void sm2_verify_kernel(const uint8_t* __restrict__ hash,
                                                          const uint8_t* __restrict__ sig, uint32_t stride,
-                                                         uint64_t n, const uint32_t* __restrict__ tab,
+                                                         uint64_t n, const uint32_t* __restrict__ tab, int tbits,
                                                          uint8_t* __restrict__ addr, uint8_t* __restrict__ okout) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
     fe h, x, y;
     load_be256_aligned(h, hash + 32 * i);
-    const bool ok = sm2_verify_lane(h, sig + static_cast<uint64_t>(stride) * i, 128u, tab, x, y);
+    const bool ok = sm2_verify_lane(h, sig + static_cast<uint64_t>(stride) * i, 128u, CombTab{tab, tbits}, x, y);
     if (addr) {
         uint32_t a[5] = {0, 0, 0, 0, 0};
         if (ok) sm3_address(a, x, y);
@@ -962,7 +1028,7 @@ template <int SUITE>
 __global__ __launch_bounds__(256) void sig_verify_kernel(const uint8_t* __restrict__ pub,
                                                          const uint8_t* __restrict__ hash,
                                                          const uint8_t* __restrict__ sig, uint32_t stride,
-                                                         uint64_t n, const uint32_t* __restrict__ tab,
+                                                         uint64_t n, const uint32_t* __restrict__ tab, int tbits,
                                                          uint8_t* __restrict__ okout) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -985,9 +1051,9 @@ __global__ __launch_bounds__(256) void sig_verify_kernel(const uint8_t* __restri
             X[k] = bswap32(rp.word(k));
             Y[k] = bswap32(rp.word(8 + k));
         }
-        ok = sm2_verify_rs(h, r, s, X, Y, tab, x, y);
+        ok = sm2_verify_rs(h, r, s, X, Y, CombTab{tab, tbits}, x, y);
     } else {
-        ok = secp256k1_verify_lane(h, sg, pub + 64 * i, tab);
+        ok = secp256k1_verify_lane(h, sg, pub + 64 * i, CombTab{tab, tbits});
     }
     okout[i] = ok ? 1 : 0;
 }
@@ -997,7 +1063,7 @@ __global__ __launch_bounds__(256) void sig_verify_kernel(const uint8_t* __restri
 // read); on success out = 12 zero bytes || right160(Keccak256(pub)), ok = 1; on failure the
 // precompile returns an empty output: out = zeros, ok = 0.
 __global__ __launch_bounds__(256) void ecrecover_kernel(const uint8_t* __restrict__ in, uint64_t n,
-                                                        const uint32_t* __restrict__ tab,
+                                                        const uint32_t* __restrict__ tab, int tbits,
                                                         uint8_t* __restrict__ out, uint8_t* __restrict__ okout) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1007,7 +1073,7 @@ __global__ __launch_bounds__(256) void ecrecover_kernel(const uint8_t* __restric
     load_be256_aligned(r, p + 64);
     load_be256_aligned(s, p + 96);
     const uint32_t v = (reinterpret_cast<const uint32_t*>(p)[15] >> 24) - 27u;
-    const bool ok = secp256k1_recover_rsv(h, r, s, v & 0xffu, tab, x, y);
+    const bool ok = secp256k1_recover_rsv(h, r, s, v & 0xffu, CombTab{tab, tbits}, x, y);
     uint32_t a[5] = {0, 0, 0, 0, 0};
     if (ok) keccak_address(a, x, y);
     uint32_t* o = reinterpret_cast<uint32_t*>(out + 32 * i);
@@ -1026,7 +1092,7 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(const uint8_t* __re
                                                         const uint64_t* __restrict__ pre_off,
                                                         const uint8_t* __restrict__ sig,
                                                         const uint64_t* __restrict__ sig_off, uint64_t n,
-                                                        const uint32_t* __restrict__ tab,
+                                                        const uint32_t* __restrict__ tab, int tbits,
                                                         uint8_t* __restrict__ txhash, uint8_t* __restrict__ sender,
                                                         uint8_t* __restrict__ status) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -1057,10 +1123,10 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(const uint8_t* __re
     __shared__ uint32_t ldsx_all[kLds ? 4 * 4096 : 1];
     uint32_t* ldsx = kLds ? ldsx_all + (threadIdx.x >> 6) * 4096 + (threadIdx.x & 63) : nullptr;
     if (SUITE == BCOSGPU_SUITE_SM2) {
-        ok = sm2_verify_lane<kLds>(h, sig + sa, slen, tab, x, y, ldsx);
+        ok = sm2_verify_lane<kLds>(h, sig + sa, slen, CombTab{tab, tbits}, x, y, ldsx);
         if (ok) sm3_address(ad, x, y);
     } else {
-        ok = secp256k1_recover_lane<kLds>(h, sig + sa, slen, tab, x, y, ldsx);
+        ok = secp256k1_recover_lane<kLds>(h, sig + sa, slen, CombTab{tab, tbits}, x, y, ldsx);
         if (ok) keccak_address(ad, x, y);
     }
     uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
@@ -1073,7 +1139,7 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(const uint8_t* __re
 // k = Keccak256(sk || hash) mod n.
 __global__ __launch_bounds__(256) void secp256k1_sign_kernel(const uint8_t* __restrict__ sk32,
                                                              const uint8_t* __restrict__ hash32, uint64_t n,
-                                                             const uint32_t* __restrict__ tab,
+                                                             const uint32_t* __restrict__ tab, int tbits,
                                                              uint8_t* __restrict__ pub, uint8_t* __restrict__ sigout,
                                                              uint8_t* __restrict__ okout) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -1094,8 +1160,8 @@ __global__ __launch_bounds__(256) void secp256k1_sign_kernel(const uint8_t* __re
     bool ok = !fe_is_zero_raw(d) && fe_lt_k(d, ParamN1::M) && !fe_is_zero_raw(k);
     Jac P, R;
     Aff PA, RA;
-    comb_mul<CurveK1>(P, d, tab);
-    comb_mul<CurveK1>(R, k, tab);
+    comb_mul_rt<CurveK1>(P, d, tab, tbits);
+    comb_mul_rt<CurveK1>(R, k, tab, tbits);
     CurveK1::to_aff(PA, P);
     CurveK1::to_aff(RA, R);
     FieldK1::normalize(PA.x);
@@ -1143,7 +1209,7 @@ __global__ __launch_bounds__(256) void secp256k1_sign_kernel(const uint8_t* __re
 // SM2 key derivation + signing (GB/T 32918.2), k = SM3(sk || hash) mod n; sig = r || s || pub.
 __global__ __launch_bounds__(256) void sm2_sign_kernel(const uint8_t* __restrict__ sk32,
                                                        const uint8_t* __restrict__ hash32, uint64_t n,
-                                                       const uint32_t* __restrict__ tab,
+                                                       const uint32_t* __restrict__ tab, int tbits,
                                                        uint8_t* __restrict__ sigout, uint8_t* __restrict__ okout) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1174,8 +1240,8 @@ __global__ __launch_bounds__(256) void sm2_sign_kernel(const uint8_t* __restrict
     bool ok = !fe_is_zero_raw(d) && fe_lt(d, nm1) && !fe_is_zero_raw(k);
     Jac P, K;
     Aff PA, KA;
-    comb_mul<CurveSM2>(P, d, tab);
-    comb_mul<CurveSM2>(K, k, tab);
+    comb_mul_rt<CurveSM2>(P, d, tab, tbits);
+    comb_mul_rt<CurveSM2>(K, k, tab, tbits);
     CurveSM2::to_aff(PA, P);
     CurveSM2::to_aff(KA, K);
     fe px, py, x1;
@@ -1982,10 +2048,11 @@ int launch_secp256k1_recover(const uint8_t* d_hash, const uint8_t* d_sig, uint32
                              uint8_t* d_pub, uint8_t* d_addr, uint8_t* d_ok, hipStream_t st) {
     if (n == 0) return 0;
     const uint32_t *k1, *sm2;
-    int rc = tables(&k1, &sm2);
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
     hipLaunchKernelGGL(secp256k1_recover_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, k1,
-                       d_pub, d_addr, d_ok);
+                       bits, d_pub, d_addr, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
@@ -1993,22 +2060,26 @@ int launch_sm2_verify(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stri
                       uint8_t* d_ok, hipStream_t st) {
     if (n == 0) return 0;
     const uint32_t *k1, *sm2;
-    int rc = tables(&k1, &sm2);
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    hipLaunchKernelGGL(sm2_verify_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, sm2, d_addr,
-                       d_ok);
+    hipLaunchKernelGGL(sm2_verify_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, sm2, bits,
+                       d_addr, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
+// Signing exists to build the synthetic benchmark / test batches on the device.  It is NOT
+// constant-time (the comb gather address depends on secret key and nonce bits): test use only.
 int launch_secp256k1_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint8_t* d_pub, uint8_t* d_sig,
                           uint8_t* d_ok, hipStream_t st) {
     if (n == 0) return 0;
     const uint32_t *k1, *sm2;
-    int rc = tables(&k1, &sm2);
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
     if (!d_pub) return BCOSGPU_E_ARG;
-    hipLaunchKernelGGL(secp256k1_sign_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_sk, d_hash, n, k1, d_pub, d_sig,
-                       d_ok);
+    hipLaunchKernelGGL(secp256k1_sign_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_sk, d_hash, n, k1, bits, d_pub,
+                       d_sig, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
@@ -2016,9 +2087,10 @@ int launch_sm2_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint
                     hipStream_t st) {
     if (n == 0) return 0;
     const uint32_t *k1, *sm2;
-    int rc = tables(&k1, &sm2);
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    hipLaunchKernelGGL(sm2_sign_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_sk, d_hash, n, sm2, d_sig, d_ok);
+    hipLaunchKernelGGL(sm2_sign_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_sk, d_hash, n, sm2, bits, d_sig, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
@@ -2026,46 +2098,26 @@ int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, co
                       uint64_t n, uint8_t* d_ok, hipStream_t st) {
     if (n == 0) return 0;
     const uint32_t *k1, *sm2;
-    int rc = tables(&k1, &sm2);
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
     if (suite == BCOSGPU_SUITE_SM2)
         hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SM2>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash, d_sig,
-                           stride, n, sm2, d_ok);
+                           stride, n, sm2, bits, d_ok);
     else
         hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SECP256K1>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash,
-                           d_sig, stride, n, k1, d_ok);
+                           d_sig, stride, n, k1, bits, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
 int launch_ecrecover(const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint8_t* d_ok, hipStream_t st) {
     if (n == 0) return 0;
     const uint32_t *k1, *sm2;
-    int rc = tables(&k1, &sm2);
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    hipLaunchKernelGGL(ecrecover_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_in, n, k1, d_out, d_ok);
+    hipLaunchKernelGGL(ecrecover_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_in, n, k1, bits, d_out, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
-}
-
-static int tx_verify_occupancy(uint64_t n) {
-    const char* e = getenv("BCOSGPU_TXV_OCC");  // read per launch so tests can A/B both variants
-    const int forced = e ? atoi(e) : 0;
-    if (forced == 1 || forced == 2) return forced;
-    return n >= (1ull << 17) ? 2 : 1;  // >= 2 waves per SIMD of work on 256 CUs
-}
-
-// Split kernel (4 waves per 64 txs) while the batch leaves SIMDs idle; BCOSGPU_TXV_SPLIT=0/1 forces it.
-static bool use_split(uint64_t n) {
-    const char* e = getenv("BCOSGPU_TXV_SPLIT");
-    const int forced = e ? atoi(e) : -1;
-    if (forced == 0 || forced == 1) return forced == 1;
-    return n <= (1ull << 15);
-}
-
-// Small secp256k1 batches run the cooperative-pair kernel (C2: 0.74 ms vs 0.87 ms for the 4-wave
-// split kernel); BCOSGPU_TXV_COOP=0 selects the split kernel (A/B tests).
-static bool use_coop() {
-    const char* e = getenv("BCOSGPU_TXV_COOP");
-    return e ? atoi(e) != 0 : true;
 }
 
 int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off, const uint8_t* d_sig,
@@ -2073,23 +2125,28 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
                      hipStream_t st) {
     if (n == 0) return 0;
     const uint32_t *k1, *sm2;
-    int rc = tables(&k1, &sm2);
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    if (suite == BCOSGPU_SUITE_SECP256K1 && use_split(n)) {
+    const TxKernelPolicy pol = g_policy;
+    // small secp256k1 batches (SIMDs left idle by one tx per lane): the cooperative-pair kernel
+    // (C2), or the 4-wave split kernel; both on the L2-resident 8-bit comb tables
+    const bool small = pol.split >= 0 ? pol.split == 1 : n <= (1ull << 15);
+    if (suite == BCOSGPU_SUITE_SECP256K1 && small) {
         rc = tables8(&k1, &sm2);
         if (rc) return rc;
-        if (use_coop()) {
-            hipLaunchKernelGGL(tx_verify_coop_kernel, dim3(static_cast<unsigned>((n + 63) / 64)), dim3(256), 0, st,
-                               d_pre, d_pre_off, d_sig, d_sig_off, n, k1, d_txhash, d_sender, d_status);
-            return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
-        }
-        hipLaunchKernelGGL(tx_verify_split_kernel, dim3(static_cast<unsigned>((n + 63) / 64)), dim3(256), 0, st, d_pre,
-                           d_pre_off, d_sig, d_sig_off, n, k1, d_txhash, d_sender, d_status);
+        const dim3 grid(static_cast<unsigned>((n + 63) / 64));
+        if (pol.coop)
+            hipLaunchKernelGGL(tx_verify_coop_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n, k1,
+                               d_txhash, d_sender, d_status);
+        else
+            hipLaunchKernelGGL(tx_verify_split_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n,
+                               k1, d_txhash, d_sender, d_status);
         return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
     }
-    const int occ = tx_verify_occupancy(n);
+    const int occ = pol.occ ? pol.occ : (n >= (1ull << 17) ? 2 : 1);  // >= 2 waves per SIMD of work
 #define TXV(S, O, T) hipLaunchKernelGGL((tx_verify_kernel<S, O>), dim3(grid_of(n)), dim3(256), 0, st, d_pre, d_pre_off, \
-                                        d_sig, d_sig_off, n, T, d_txhash, d_sender, d_status)
+                                        d_sig, d_sig_off, n, T, bits, d_txhash, d_sender, d_status)
     if (suite == BCOSGPU_SUITE_SM2) {
         if (occ == 2) TXV(BCOSGPU_SUITE_SM2, 2, sm2); else TXV(BCOSGPU_SUITE_SM2, 1, sm2);
     } else {

@@ -244,8 +244,12 @@ int launch_merkle_levelwise(int hasher, int width, const uint8_t* d_leaves, uint
 int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
                   uint8_t* d_root, hipStream_t st) {
     if (n == 0 || width < 2 || width > 64) return BCOSGPU_E_ARG;
-    const char* lw = getenv("BCOSGPU_MERKLE_LEVELWISE");  // A/B switch to the one-launch-per-level path
-    if (lw && atoi(lw) == 1) return launch_merkle_levelwise(hasher, width, d_leaves, n, d_tree, d_root, st);
+    // A/B switch to the one-launch-per-level path, read once per process
+    static const bool levelwise = [] {
+        const char* lw = getenv("BCOSGPU_MERKLE_LEVELWISE");
+        return lw && atoi(lw) == 1;
+    }();
+    if (levelwise) return launch_merkle_levelwise(hasher, width, d_leaves, n, d_tree, d_root, st);
     if (n == 1) {  // Merkle.h:177-182
         hipLaunchKernelGGL(copy32_kernel, dim3(1), dim3(64), 0, st, d_leaves, d_tree);
         if (d_root) hipLaunchKernelGGL(copy32_kernel, dim3(1), dim3(64), 0, st, d_leaves, d_root);

@@ -62,6 +62,16 @@ int bcosgpu_version(void);
 int bcosgpu_device_count(void);
 /* Select the calling thread's device and build its constant tables (idempotent). */
 int bcosgpu_init(int device);
+/* Same, with flags: BCOSGPU_INIT_SMALL_TABLES skips the two 64 MiB 16-bit comb tables (the kernels
+ * then use the 512 KiB 8-bit ones, as they also do when the 64 MiB allocation fails).  Flags only
+ * matter at a device's first initialisation. */
+#define BCOSGPU_INIT_SMALL_TABLES 1
+int bcosgpu_init_ex(int device, int flags);
+/* Kernel selection for the tx-verify batch (tuning / tests; the default is chosen by batch size and
+ * read once from BCOSGPU_TXV_SPLIT / _OCC / _COOP at the first init, never per launch):
+ * split -1 by size (secp256k1 batches <= 2^15 run the small-batch kernels), 0 never, 1 always;
+ * occupancy 0 by size (2 waves/SIMD for n >= 2^17), 1 or 2 forced; coop 1 cooperative-pair, 0 split. */
+int bcosgpu_set_tx_kernel_policy(int split, int occupancy, int coop);
 /* Last error message of the calling thread. */
 const char* bcosgpu_last_error(void);
 /* Bytes of the reference's Merkle output vector, in 32-byte entries (Merkle.h:224-236 getMerkleSize). */
@@ -143,7 +153,8 @@ int bcosgpu_sm2_verify_batch(const uint8_t* hash32, const uint8_t* sig128, size_
 int bcosgpu_sm2_verify_batch_dev(const uint8_t* d_hash32, const uint8_t* d_sig128, size_t n,
                                  uint8_t* d_addr20, uint8_t* d_ok, void* stream);
 /* Key derivation + deterministic signing (SignatureCrypto::createKeyPair / sign), used to build
- * synthetic signed batches on the device.  Nonce k = H(sk || hash) mod n (H = Keccak256 for
+ * synthetic signed batches on the device.  TEST / BENCHMARK USE ONLY: not constant-time (the comb
+ * gather addresses depend on key and nonce bits) -- the reference signs on the host.  Nonce k = H(sk || hash) mod n (H = Keccak256 for
  * secp256k1, SM3 for SM2); sig65 = r||s||v (low-S, libsecp256k1 convention), sig128 = r||s||pub.
  * ok[i] = 0 when sk is out of range or the nonce is degenerate. */
 int bcosgpu_secp256k1_sign_batch_dev(const uint8_t* d_sk32, const uint8_t* d_hash32, size_t n,

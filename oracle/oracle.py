@@ -251,3 +251,44 @@ def tx_preimage(version, chain_id, group_id, block_limit, nonce, to, input_, abi
     return ((version & 0xFFFFFFFF).to_bytes(4, "big") + chain_id.encode() + group_id.encode()
             + (block_limit & 0xFFFFFFFFFFFFFFFF).to_bytes(8, "big") + nonce.encode() + to.encode() + bytes(input_)
             + abi.encode())
+
+
+# ---------------------------------------------------------------- OpenSSL stand-in (CPU baseline)
+STANDIN = os.path.join(HERE, "libstandin.so")
+_standin = None
+
+
+def standin():
+    """oracle/libstandin.so (standin_openssl.c): the reference's per-tx path over OpenSSL 1.1.1's
+    libcrypto EC, the declared CPU stand-in of BASELINE.md §3.  None when it is not built (no
+    OpenSSL headers) or its libcrypto does not load."""
+    global _standin
+    if _standin is None:
+        if not os.path.exists(STANDIN):
+            subprocess.run(["make", "-s", "-C", HERE, "standin"], check=False)
+        try:
+            L = ctypes.CDLL(STANDIN)
+        except OSError:
+            return None
+        P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.standin_version.restype = ctypes.c_char_p
+        L.standin_version.argtypes = []
+        L.standin_tx_verify_batch.restype = None
+        L.standin_tx_verify_batch.argtypes = [I, P, P, P, P, S, P, P, P, I]
+        _standin = L
+    return _standin
+
+
+def standin_version():
+    L = standin()
+    return L.standin_version().decode() if L else None
+
+
+def standin_tx_verify_packed(suite, pre, pre_off, sig, sig_off, nthreads=1):
+    n = len(pre_off) - 1
+    txhash = np.zeros((n, 32), dtype=np.uint8)
+    sender = np.zeros((n, 20), dtype=np.uint8)
+    status = np.zeros(n, dtype=np.uint8)
+    standin().standin_tx_verify_batch(suite, _p(pre), _p(pre_off), _p(sig), _p(sig_off), n, _p(txhash),
+                                      _p(sender), _p(status), nthreads)
+    return txhash, sender, status

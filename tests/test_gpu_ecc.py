@@ -253,26 +253,65 @@ def test_synthetic_batch_device_path(gpu, oracle, suite):
 
 
 @pytest.mark.parametrize("suite", [0, 1])
-def test_tx_verify_kernel_variants_agree(gpu, oracle, suite, monkeypatch):
+def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
     """Every launch variant (cooperative-pair and 4-wave split kernels, occupancy 1 and 2) gives
-    identical outputs."""
+    identical outputs (bcosgpu_set_tx_kernel_policy forces each one)."""
     import torch
     from bcos_gpu import device, synth
     n = 3000 + 17  # ragged last workgroup
     b = synth.make_batch(suite, n, seed=91, flip_frac=0.02, bad_v_frac=0.01)
     pre, po, sg, so = (x.cpu().numpy() for x in (b.pre, b.pre_off, b.sig, b.sig_off))
     wh, ws, wst = oracle.tx_verify_packed(suite, pre, po.astype(np.uint64), sg, so.astype(np.uint64), nthreads=16)
-    variants = [("1", "1", "1"), ("1", "1", "0"), ("0", "1", "0"), ("0", "2", "0")] if suite == 0 else \
-        [("0", "1", "0"), ("0", "2", "0")]
-    for split, occ, coop in variants:
-        monkeypatch.setenv("BCOSGPU_TXV_SPLIT", split)
-        monkeypatch.setenv("BCOSGPU_TXV_OCC", occ)
-        monkeypatch.setenv("BCOSGPU_TXV_COOP", coop)
-        th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
-        snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
-        st = torch.empty(n, dtype=torch.uint8, device="cuda")
-        device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
-        torch.cuda.synchronize()
-        assert np.array_equal(th.cpu().numpy(), wh), (split, occ)
-        assert np.array_equal(st.cpu().numpy(), wst), (split, occ)
-        assert np.array_equal(snd.cpu().numpy(), ws), (split, occ)
+    variants = [(1, 1, 1), (1, 1, 0), (0, 1, 0), (0, 2, 0)] if suite == 0 else [(0, 1, 0), (0, 2, 0)]
+    try:
+        for split, occ, coop in variants:
+            gpu.check(gpu.lib().bcosgpu_set_tx_kernel_policy(split, occ, coop))
+            th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+            snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
+            st = torch.empty(n, dtype=torch.uint8, device="cuda")
+            device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
+            torch.cuda.synchronize()
+            assert np.array_equal(th.cpu().numpy(), wh), (split, occ)
+            assert np.array_equal(st.cpu().numpy(), wst), (split, occ)
+            assert np.array_equal(snd.cpu().numpy(), ws), (split, occ)
+    finally:
+        gpu.lib().bcosgpu_set_tx_kernel_policy(-1, 0, 1)
+
+
+_SMALL_TABLES_SCRIPT = """
+import sys
+import numpy as np
+import torch
+sys.path[:0] = [{pkg!r}, {root!r}]
+import bcos_gpu
+from bcos_gpu import device, synth
+from oracle import oracle
+bcos_gpu.check(bcos_gpu.lib().bcosgpu_init_ex(0, 1))  # BCOSGPU_INIT_SMALL_TABLES
+for suite in (0, 1):
+    n = 3000
+    b = synth.make_batch(suite, n, seed=5 + suite, flip_frac=0.02, bad_v_frac=0.01)
+    th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    bcos_gpu.check(bcos_gpu.lib().bcosgpu_set_tx_kernel_policy(0, 2, 1))  # the throughput kernel
+    device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
+    torch.cuda.synchronize()
+    pre, po, sg, so = (x.cpu().numpy() for x in (b.pre, b.pre_off, b.sig, b.sig_off))
+    wh, ws, wst = oracle.tx_verify_packed(suite, pre, po.astype(np.uint64), sg, so.astype(np.uint64), nthreads=16)
+    assert np.array_equal(th.cpu().numpy(), wh) and np.array_equal(st.cpu().numpy(), wst)
+    assert np.array_equal(snd.cpu().numpy(), ws)
+print("small-tables ok")
+"""
+
+
+def test_small_comb_tables_path(gpu):
+    """bcosgpu_init_ex(dev, BCOSGPU_INIT_SMALL_TABLES) (also the fallback when the 64 MiB tables do not
+    fit): the throughput kernels run the 8-bit comb and stay bit-exact.  Own process: the flag only
+    matters at a device's first initialisation."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _SMALL_TABLES_SCRIPT.format(pkg=os.path.join(root, "fisco-bcos_amd"), root=root)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "small-tables ok" in r.stdout, r.stderr[-2000:]
