@@ -74,6 +74,7 @@ _SIGS = {
                                               _P, _P]),
     "bcosgpu_wedpr_secp256k1_recover_public_key": (ctypes.c_int8, [_P, _P, _P]),
     "bcosgpu_wedpr_sm2_verify": (ctypes.c_int8, [_P, _P, _P]),
+    "bcosgpu_wedpr_secp256k1_verify": (ctypes.c_int8, [_P, _P, _P]),
 }
 
 
@@ -120,3 +121,9 @@ def ensure_device(device=0):
     if device not in _inited:
         check(lib().bcosgpu_init(device))
         _inited.add(device)
+
+
+def set_tx_kernel_policy(split=-1, occupancy=0, coop=1):
+    """bcosgpu_set_tx_kernel_policy: force a tx-verify kernel variant (tests / tuning); the defaults
+    restore the size-based choice."""
+    check(lib().bcosgpu_set_tx_kernel_policy(split, occupancy, coop))

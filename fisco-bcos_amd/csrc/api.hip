@@ -652,4 +652,15 @@ int8_t bcosgpu_wedpr_sm2_verify(const bcosgpu_CInputBuffer* pub, const bcosgpu_C
     return ok ? 0 : -1;
 }
 
+int8_t bcosgpu_wedpr_secp256k1_verify(const bcosgpu_CInputBuffer* pub, const bcosgpu_CInputBuffer* hash,
+                                      const bcosgpu_CInputBuffer* sig) {
+    if (!pub || !hash || !sig || hash->len != 32 || pub->len != 64 || sig->len < 64) return -1;
+    uint8_t ok = 0;
+    if (bcosgpu_verify_batch(BCOSGPU_SUITE_SECP256K1, reinterpret_cast<const uint8_t*>(pub->data),
+                             reinterpret_cast<const uint8_t*>(hash->data), reinterpret_cast<const uint8_t*>(sig->data),
+                             64, 1, &ok))
+        return -1;
+    return ok ? 0 : -1;
+}
+
 }  // extern "C"

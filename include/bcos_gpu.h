@@ -243,9 +243,13 @@ int bcosgpu_pack_tx_preimages(const bcosgpu_TransactionData* txs, size_t n, uint
                               uint64_t* offsets);
 
 /* ---------------------------------------------------------------- wedpr-ABI single-call shims */
-/* Same layout as wedpr-crypto's CInputBuffer / COutputBuffer; return 0 (WEDPR_SUCCESS) or -1. */
+/* Same layout as wedpr-crypto's CInputBuffer / COutputBuffer; return 0 (WEDPR_SUCCESS) or -1.
+ * A reference translation unit that already has wedpr's types (<wedpr-crypto/WedprCrypto.h>) includes
+ * bcos_gpu_wedpr.h instead, which declares these two symbols over CInputBuffer / COutputBuffer so they
+ * bind to SM2Crypto::m_verifier (SM2Crypto.h:64-65) and to wedpr's call sites unchanged. */
 typedef struct { const char* data; uintptr_t len; } bcosgpu_CInputBuffer;
 typedef struct { char* data; uintptr_t len; } bcosgpu_COutputBuffer;
+#ifndef BCOSGPU_WEDPR_TYPES
 /* wedpr_secp256k1_recover_public_key (Secp256k1Crypto.cpp:79-93) */
 int8_t bcosgpu_wedpr_secp256k1_recover_public_key(const bcosgpu_CInputBuffer* hash,
                                                    const bcosgpu_CInputBuffer* sig,
@@ -253,6 +257,10 @@ int8_t bcosgpu_wedpr_secp256k1_recover_public_key(const bcosgpu_CInputBuffer* ha
 /* fast_sm2_verify / wedpr_sm2_verify (fast_sm2.cpp:139-227): sig = r||s (64 B), pub = 64 B */
 int8_t bcosgpu_wedpr_sm2_verify(const bcosgpu_CInputBuffer* pub, const bcosgpu_CInputBuffer* hash,
                                  const bcosgpu_CInputBuffer* sig);
+/* wedpr_secp256k1_verify (Secp256k1Crypto.cpp:51-63): libsecp256k1 verify semantics (low-S) */
+int8_t bcosgpu_wedpr_secp256k1_verify(const bcosgpu_CInputBuffer* pub, const bcosgpu_CInputBuffer* hash,
+                                      const bcosgpu_CInputBuffer* sig);
+#endif
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,65 @@
+// mirror of the SM2Crypto class shape (test infrastructure, ../../../README.md): verify / recover
+// go through m_verifier as SM2Crypto.cpp:66-92 does; the host-side members only throw
+#pragma once
+#include <bcos-crypto/signature/Exceptions.h>
+#include <bcos-crypto/signature/key/KeyImpl.h>
+#include <wedpr-crypto/WedprCrypto.h>
+#include <functional>
+namespace bcos
+{
+namespace crypto
+{
+const int SM2_SIGNATURE_LEN = 64;
+class SM2Crypto : public SignatureCrypto
+{
+public:
+    SM2Crypto() = default;
+    ~SM2Crypto() override = default;
+    std::shared_ptr<bytes> sign(const KeyPairInterface&, const HashType&, bool) const override
+    {
+        throw SignException() << errinfo_comment("host-side (wedpr) in the reference");
+    }
+    bool verify(PublicPtr _pubKey, const HashType& _hash, bytesConstRef _signatureData) const override
+    {
+        CInputBuffer publicKey{_pubKey->constData(), _pubKey->size()};
+        CInputBuffer messageHash{(const char*)_hash.data(), HashType::SIZE};
+        CInputBuffer signature{(const char*)_signatureData.data(), SM2_SIGNATURE_LEN};
+        return m_verifier(&publicKey, &messageHash, &signature) == WEDPR_SUCCESS;
+    }
+    bool verify(std::shared_ptr<const bytes> _pubKeyBytes, const HashType& _hash,
+        bytesConstRef _signatureData) const override
+    {
+        return verify(std::make_shared<KeyImpl>(64, _pubKeyBytes), _hash, _signatureData);
+    }
+    PublicPtr recover(const HashType& _hash, bytesConstRef _signData) const override
+    {
+        if (_signData.size() < 128)
+        {
+            BOOST_THROW_EXCEPTION(InvalidSignature() << errinfo_comment("invalid signature data"));
+        }
+        auto pub = std::make_shared<KeyImpl>(
+            64, std::make_shared<const bytes>(_signData.data() + 64, _signData.data() + 128));
+        if (verify(pub, _hash, _signData))
+        {
+            return pub;
+        }
+        BOOST_THROW_EXCEPTION(InvalidSignature() << errinfo_comment(
+                                  "invalid signature: sm2 recover public key failed, msgHash : " + _hash.hex()));
+    }
+    KeyPairInterface::UniquePtr generateKeyPair() const override
+    {
+        throw SignException() << errinfo_comment("host-side (wedpr) in the reference");
+    }
+    std::pair<bool, bytes> recoverAddress(Hash::Ptr, bytesConstRef) const override { return {false, {}}; }
+    KeyPairInterface::UniquePtr createKeyPair(SecretPtr) const override
+    {
+        throw SignException() << errinfo_comment("host-side (wedpr) in the reference");
+    }
+
+protected:
+    std::function<int8_t(const CInputBuffer* public_key, const CInputBuffer* message_hash,
+        const CInputBuffer* signature)>
+        m_verifier;
+};
+}  // namespace crypto
+}  // namespace bcos

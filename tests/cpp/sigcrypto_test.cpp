@@ -1,0 +1,105 @@
+// sigcrypto_test.cpp -- the drop-in SignatureCrypto subclasses of include/bcos_gpu_crypto.hpp, used
+// through the reference's polymorphic interface (SignatureCrypto&), written like
+// bcos-crypto/test/unittests/SignatureTest.cpp.  Compiled against tests/cpp/mirror/ (the interface
+// shapes); exit 0 = pass, 77 = compiled and linked but no gfx950 device here.
+#include <bcos_gpu_crypto.hpp>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+using namespace bcos;
+using namespace bcos::crypto;
+
+static int fails = 0;
+#define CHECK(c)                                                      \
+    do {                                                              \
+        if (!(c)) {                                                   \
+            printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c);        \
+            ++fails;                                                  \
+        }                                                             \
+    } while (0)
+
+static bytes unhex(const char* h) {
+    bytes b(strlen(h) / 2);
+    for (size_t i = 0; i < b.size(); ++i) sscanf(h + 2 * i, "%2hhx", &b[i]);
+    return b;
+}
+static HashType hash_of(const char* hex) {
+    HashType h;
+    bytes b = unhex(hex);
+    std::memcpy(h.data(), b.data(), 32);
+    return h;
+}
+template <class F>
+static bool throws_invalid(F&& f) {
+    try {
+        f();
+    } catch (const InvalidSignature&) {
+        return true;
+    }
+    return false;
+}
+
+int main() {
+    if (bcosgpu_device_count() <= 0) {
+        printf("no gfx950 device\n");
+        return 77;
+    }
+    bcosgpu::ref::GpuSecp256k1Crypto secp;
+    bcosgpu::ref::GpuSM2Crypto sm2;
+    SignatureCrypto& k1 = secp;
+    SignatureCrypto& s2 = sm2;
+
+    // ecrecover vector (EVMPrecompiledTest.cpp:58-72): recid 0, address ceaccac6...
+    const char* H = "38d18acb67d25c8bb9942764b62f18e17054f66a817bd4295423adf9ed98873e";
+    bytes sig = unhex(H);
+    bytes s = unhex("789d1dd423d25f0772d2748d60f7e4b81bb14d086eba8e8e8efb6dcff8a4ae02");
+    sig.insert(sig.end(), s.begin(), s.end());
+    sig.push_back(0);
+    HashType mh = hash_of(H);
+    PublicPtr pub = k1.recover(mh, bytesConstRef(sig));
+    CHECK(pub && pub->size() == 64);
+    uint8_t d[32];
+    uint64_t off[2] = {0, 64};
+    CHECK(bcosgpu_keccak256_batch((const uint8_t*)pub->constData(), off, 1, d) == 0);
+    static const uint8_t want[20] = {0xce, 0xac, 0xca, 0xc6, 0x40, 0xad, 0xf5, 0x5b, 0x20, 0x28,
+                                     0x46, 0x9b, 0xd3, 0x6b, 0xa5, 0x01, 0xf2, 0x8b, 0x69, 0x9d};
+    CHECK(std::memcmp(d + 12, want, 20) == 0);
+    CHECK(k1.verify(pub, mh, bytesConstRef(sig)));  // known-key verify (Secp256k1Crypto.cpp:51-63)
+    CHECK(k1.verify(std::make_shared<const bytes>(pub->data()), mh, bytesConstRef(sig)));
+    // v = 4 must throw InvalidSignature (SignatureTest.cpp:156-162); a wrong length too
+    bytes bad = sig;
+    bad[64] = 4;
+    CHECK(throws_invalid([&] { k1.recover(mh, bytesConstRef(bad)); }));
+    CHECK(throws_invalid([&] { k1.recover(mh, bytesConstRef(sig.data(), 64)); }));
+    // a different hash recovers a different key (TxPoolTest.cpp:469-489): accepted
+    HashType mh2 = hash_of("48bed44d1bcd124a28c27f343a817e5f5243190d3c52bf347daf876de1dbbf77");
+    PublicPtr pub2 = k1.recover(mh2, bytesConstRef(sig));
+    CHECK(pub2 && pub2->data() != pub->data());
+    CHECK(!k1.verify(pub, mh2, bytesConstRef(sig)));
+    // batch hook: entries of SignatureCrypto::recover, nullptr where it throws
+    auto batch = secp.recoverBatch({mh, mh, mh2}, {bytesConstRef(sig), bytesConstRef(bad), bytesConstRef(sig)});
+    CHECK(batch.size() == 3 && batch[0] && !batch[1] && batch[2]);
+    CHECK(batch[0]->data() == pub->data() && batch[2]->data() == pub2->data());
+
+    // SM2 KAT (SignatureTest.cpp:238-251): r || s || pub over SM3("abcd"), through m_verifier
+    bytes sm2sig = unhex(
+        "cd39bf939d999ca710576a629c962edfc28608701a3a7b61c971daeac5a1399c"
+        "f4a7272fa80783e171c7fd5b038a3af4521f681ebe9fd44db3b60e750c438293"
+        "f7dee65e76603ed7cd4c598d53cabe875c459e0fae4c6fd7b858189fd4741081"
+        "e970bca0d5cb571a7ac30586aec71b23187d4b25e59143812f74a2744604d42b");
+    HashType sm3abcd = hash_of("82ec580fe6d36ae4f81cae3c73f4a5b3b5a09c943172dc9053c69fd8e18dca1e");
+    PublicPtr sp = s2.recover(sm3abcd, bytesConstRef(sm2sig));
+    CHECK(sp && std::memcmp(sp->constData(), sm2sig.data() + 64, 64) == 0);
+    CHECK(s2.verify(sp, sm3abcd, bytesConstRef(sm2sig)));
+    bytes sm2bad = sm2sig;
+    sm2bad[5] ^= 1;
+    CHECK(throws_invalid([&] { s2.recover(sm3abcd, bytesConstRef(sm2bad)); }));
+    CHECK(throws_invalid([&] { s2.recover(mh, bytesConstRef(sm2sig)); }));  // wrong hash: SM2 rejects
+    auto sb = sm2.recoverBatch({sm3abcd, sm3abcd}, {bytesConstRef(sm2sig), bytesConstRef(sm2bad)});
+    CHECK(sb.size() == 2 && sb[0] && !sb[1]);
+
+    printf(fails ? "sigcrypto_test: %d failures\n" : "sigcrypto_test: ok\n", fails);
+    return fails ? 1 : 0;
+}

@@ -29,3 +29,29 @@ def test_adapter_kats_on_gpu(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "adapter_test: ok" in r.stdout
+
+
+def _build_sigcrypto(tmp_path):
+    """include/bcos_gpu_crypto.hpp (GpuSecp256k1Crypto / GpuSM2Crypto : the reference's SignatureCrypto
+    classes) compiled against the interface mirror in tests/cpp/mirror/ -- including
+    `m_verifier = bcosgpu_wedpr_sm2_verify` over wedpr's CInputBuffer type (SM2Crypto.h:64-65)."""
+    exe = str(tmp_path / "sigcrypto_test")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "tests", "cpp", "mirror"),
+                    "-I" + os.path.join(ROOT, "include"), "-o", exe,
+                    os.path.join(ROOT, "tests", "cpp", "sigcrypto_test.cpp"), "-L" + LIBDIR, "-lbcosgpu",
+                    "-Wl,-rpath," + LIBDIR], check=True)
+    return exe
+
+
+def test_signaturecrypto_subclasses_compile_and_link(tmp_path):
+    exe = _build_sigcrypto(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode in (0, 77), r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_signaturecrypto_subclasses_on_gpu(tmp_path):
+    exe = _build_sigcrypto(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sigcrypto_test: ok" in r.stdout

@@ -265,7 +265,7 @@ def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
     variants = [(1, 1, 1), (1, 1, 0), (0, 1, 0), (0, 2, 0)] if suite == 0 else [(0, 1, 0), (0, 2, 0)]
     try:
         for split, occ, coop in variants:
-            gpu.check(gpu.lib().bcosgpu_set_tx_kernel_policy(split, occ, coop))
+            gpu.set_tx_kernel_policy(split, occ, coop)
             th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
             snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
             st = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -275,7 +275,7 @@ def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
             assert np.array_equal(st.cpu().numpy(), wst), (split, occ)
             assert np.array_equal(snd.cpu().numpy(), ws), (split, occ)
     finally:
-        gpu.lib().bcosgpu_set_tx_kernel_policy(-1, 0, 1)
+        gpu.set_tx_kernel_policy()
 
 
 _SMALL_TABLES_SCRIPT = """
