@@ -12,6 +12,7 @@ scaling, no data-path collective); value = txs of all ranks / max-over-ranks wal
 launches so the clock has settled under load before the timed region starts.
 
 Sub-legs in the same line (`legs`), each timed for >= --leg-seconds of back-to-back steps:
+  c2sm2  C2's size on the guomi suite: 10k SM2/SM3 txs per GPU (the SM2 pair kernel; weak scaling).
   c3  configs[2]: 1M SM2/SM3 txs per GPU: SM3 tx hash + SM2 verify + sender (weak scaling).
   c4  configs[3]: 1M secp256k1 txs in TOTAL sharded over the ranks + the block tx root (width-2
       Keccak Merkle, BlockImpl.h:111-154): per-rank frontier, ONE RCCL all-gather, top levels on
@@ -55,6 +56,7 @@ F_SM2_VERIFY = 3210
 F_SECP_EXEC_WIDE = 2255
 F_SECP_EXEC_COMB8 = 2431
 F_SM2_EXEC = 3092
+F_SM2_EXEC_COMB8 = 3268
 # measured gfx950 lane-op peaks (fisco-bcos_amd/tools/intbench.hip on MI355X, profiles/r01_intbench.json)
 PEAK_MAC_PER_S = 3.0785e13      # v_mad_u64_u32
 PEAK_ALU_PER_S = 3.7497e13      # full-rate 32-bit VALU (v_alignbit_b32)
@@ -68,6 +70,9 @@ KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_kernels.hip", "fisco-bcos_amd/csrc/fe_asm
 WORKLOADS = {
     "c2": dict(suite=0, n=10_000, scaling="weak",
                name="C2: 10k synthetic secp256k1 txs / GPU: Keccak256 tx hash + ECDSA recover + sender"),
+    "c2sm2": dict(suite=1, n=10_000, scaling="weak",
+                  name="C2-SM2: 10k synthetic SM2/SM3 txs / GPU (C2's size, guomi suite): SM3 tx hash + SM2 verify "
+                       "+ sender"),
     "c3": dict(suite=1, n=1_000_000, scaling="weak",
                name="C3: 1M synthetic SM2/SM3 txs / GPU: SM3 tx hash + SM2 verify + sender"),
     "c4": dict(suite=0, n=1_000_000, scaling="strong",
@@ -91,6 +96,8 @@ def _kernel_name(suite, n):
     """Which tx-verify kernel the library launches for this batch (mirrors launch_tx_verify)."""
     if suite == 0 and n <= (1 << 15):
         return "tx_verify_coop_kernel"
+    if suite == 1 and n <= (1 << 15):
+        return "tx_verify_sm2_pair_kernel"
     return "tx_verify_kernel<%d,%d>" % (suite, 2 if n >= (1 << 17) else 1)
 
 
@@ -227,7 +234,7 @@ def run_leg(ctx, wl_name, steps=None, warmup=3, warm_seconds=0.0, min_seconds=2.
     if suite == 0:
         f_exec = F_SECP_EXEC_WIDE if kname.startswith("tx_verify_kernel") else F_SECP_EXEC_COMB8
     else:
-        f_exec = F_SM2_EXEC
+        f_exec = F_SM2_EXEC if kname.startswith("tx_verify_kernel") else F_SM2_EXEC_COMB8
     ex = n * f_exec * MAC_PER_F / (kernel_ms * 1e-3)
     alg = n * f_alg * MAC_PER_F / (kernel_ms * 1e-3)
     traffic, traffic_src, same_src = _traffic(wl_name, kname)
@@ -457,7 +464,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--warm-seconds", type=float, default=2.0, help="minimum warm-up before the timed region")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS), help="the headline leg")
-    ap.add_argument("--legs", default="c3,c4", help="comma-separated sub-legs ('' for none)")
+    ap.add_argument("--legs", default="c2sm2,c3,c4", help="comma-separated sub-legs ('' for none)")
     ap.add_argument("--leg-seconds", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")

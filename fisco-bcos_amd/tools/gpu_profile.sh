@@ -11,7 +11,8 @@ B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --no-cpu-baseline -
 timeout -k 10 $LIM rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 && \
 timeout -s KILL $LIM rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B > $OUT/fetch.log 2>&1 && \
 timeout -s KILL $LIM rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B > $OUT/write.log 2>&1 && \
-timeout -s KILL $LIM rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS --output-format csv -d $OUT/sq -o run -- $B > $OUT/sq.log 2>&1
+timeout -s KILL $LIM rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS --output-format csv -d $OUT/sq -o run -- $B > $OUT/sq.log 2>&1 && \
+timeout -s KILL $LIM rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/valu -o run -- $B > $OUT/valu.log 2>&1
 rc=$?
 echo "profile $WL rc=$rc"
 exit $rc
