@@ -7,7 +7,7 @@ WL=${1:-c2}; STEPS=${2:-10}; LIM=${3:-180}
 OUT=gpurun_out/prof/$WL
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --no-cpu-baseline --no-merkle --no-tars"
+B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --warm-seconds 0 --legs= --no-cpu-baseline --no-merkle --no-extras"
 timeout -k 10 $LIM rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 && \
 timeout -s KILL $LIM rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B > $OUT/fetch.log 2>&1 && \
 timeout -s KILL $LIM rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B > $OUT/write.log 2>&1 && \

@@ -60,9 +60,17 @@ def main():
     for k, c in ks.items():
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             c["hbm_bytes_per_dispatch"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+    for k, c in ks.items():
+        if "SQ_ACTIVE_INST_VALU" in c and c.get("GRBM_GUI_ACTIVE"):
+            # SQ_ACTIVE_INST_VALU: quad-cycles summed over all SIMDs; GRBM_GUI_ACTIVE: GPU-busy cycles summed
+            # over the 8 XCDs -> busy fraction of the 1,024 SIMDs while the kernel runs
+            c["valu_busy"] = 4.0 * c["SQ_ACTIVE_INST_VALU"] / 1024.0 / (c["GRBM_GUI_ACTIVE"] / 8.0)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+    import bench
     with open(out, "w") as f:
         json.dump({"source": "rocprofv3 --kernel-trace --stats + separate --pmc passes", "trace_dir": trace,
-                   "pmc_dirs": pmcs, "kernels": ks}, f, indent=1, sort_keys=True)
+                   "pmc_dirs": pmcs, "kernel_source_sha": bench.kernel_source_sha(), "kernels": ks}, f,
+                  indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
