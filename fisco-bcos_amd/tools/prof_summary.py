@@ -61,10 +61,15 @@ def main():
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             c["hbm_bytes_per_dispatch"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
     for k, c in ks.items():
-        if "SQ_ACTIVE_INST_VALU" in c and c.get("GRBM_GUI_ACTIVE"):
-            # SQ_ACTIVE_INST_VALU: quad-cycles summed over all SIMDs; GRBM_GUI_ACTIVE: GPU-busy cycles summed
-            # over the 8 XCDs -> busy fraction of the 1,024 SIMDs while the kernel runs
-            c["valu_busy"] = 4.0 * c["SQ_ACTIVE_INST_VALU"] / 1024.0 / (c["GRBM_GUI_ACTIVE"] / 8.0)
+        if c.get("GRBM_GUI_ACTIVE") and c.get("avg_ns"):
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back)
+            cyc = c["GRBM_GUI_ACTIVE"] / 8.0
+            c["eff_clock_ghz"] = cyc / c["avg_ns"]
+            if c.get("SQ_INSTS_VALU"):
+                # On gfx950 SQ_ACTIVE_INST_VALU reads equal to SQ_INSTS_VALU (an instruction count, not
+                # quad-cycles), so VALU pressure is stated as kernel cycles per wave-instruction per SIMD:
+                # 4.0 = one wave64 VALU instruction every 4 cycles on every one of the 1,024 SIMDs.
+                c["valu_cycles_per_instr_per_simd"] = cyc * 1024.0 / c["SQ_INSTS_VALU"]
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
     import bench
     with open(out, "w") as f:
