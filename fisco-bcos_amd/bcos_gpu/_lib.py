@@ -35,7 +35,7 @@ _SIGS = {
     "bcosgpu_device_count": (_I, []),
     "bcosgpu_init": (_I, [_I]),
     "bcosgpu_init_ex": (_I, [_I, _I]),
-    "bcosgpu_set_tx_kernel_policy": (_I, [_I, _I, _I]),
+    "bcosgpu_set_tx_kernel_policy": (_I, [_I, _I, _I, _I]),
     "bcosgpu_last_error": (ctypes.c_char_p, []),
     "bcosgpu_merkle_size": (ctypes.c_uint64, [ctypes.c_uint64, _I]),
     "bcosgpu_hash_batch": (_I, [_I, _P, _P, _SZ, _P]),
@@ -123,7 +123,7 @@ def ensure_device(device=0):
         _inited.add(device)
 
 
-def set_tx_kernel_policy(split=-1, occupancy=0, coop=1):
+def set_tx_kernel_policy(split=-1, occupancy=0, coop=1, field=1):
     """bcosgpu_set_tx_kernel_policy: force a tx-verify kernel variant (tests / tuning); the defaults
-    restore the size-based choice."""
-    check(lib().bcosgpu_set_tx_kernel_policy(split, occupancy, coop))
+    restore the size-based choice (field 1: the 10 x 26-bit secp256k1 point arithmetic)."""
+    check(lib().bcosgpu_set_tx_kernel_policy(split, occupancy, coop, field))

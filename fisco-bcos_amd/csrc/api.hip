@@ -121,8 +121,8 @@ int bcosgpu_init_ex(int device, int flags) {
     return 0;
 }
 
-int bcosgpu_set_tx_kernel_policy(int split, int occupancy, int coop) {
-    set_tx_kernel_policy(split, occupancy, coop);
+int bcosgpu_set_tx_kernel_policy(int split, int occupancy, int coop, int field) {
+    set_tx_kernel_policy(split, occupancy, coop, field);
     return 0;
 }
 

@@ -600,6 +600,7 @@ struct TxKernelPolicy {
     int split = -1;  // small-batch secp kernels: -1 by size (n <= 2^15), 0 never, 1 always
     int occ = 0;     // tx_verify_kernel occupancy: 0 by size (2 for n >= 2^17), 1 or 2 forced
     int coop = 1;    // small-batch secp kernel: 1 cooperative-pair, 0 4-wave split
+    int f26 = 1;     // throughput secp kernels: 1 point arithmetic on the 10 x 26-bit field, 0 on FieldK1
 };
 static TxKernelPolicy g_policy;
 static bool g_policy_read = false;
@@ -610,14 +611,16 @@ static void read_policy_env() {
     if (const char* e = getenv("BCOSGPU_TXV_SPLIT")) g_policy.split = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char* e = getenv("BCOSGPU_TXV_OCC")) g_policy.occ = (atoi(e) == 1 || atoi(e) == 2) ? atoi(e) : 0;
     if (const char* e = getenv("BCOSGPU_TXV_COOP")) g_policy.coop = atoi(e) != 0;
+    if (const char* e = getenv("BCOSGPU_K1_F26")) g_policy.f26 = atoi(e) != 0;
 }
 
-void set_tx_kernel_policy(int split, int occ, int coop) {
+void set_tx_kernel_policy(int split, int occ, int coop, int f26) {
     std::lock_guard<std::mutex> g(g_tab_mu);
     read_policy_env();
     g_policy.split = (split == 0 || split == 1) ? split : -1;
     g_policy.occ = (occ == 1 || occ == 2) ? occ : 0;
     g_policy.coop = coop != 0;
+    if (f26 == 0 || f26 == 1) g_policy.f26 = f26;
 }
 
 static void free_tables(uint32_t*& a, uint32_t*& b, uint32_t*& c, uint32_t*& d) {
@@ -768,6 +771,10 @@ __device__ __forceinline__ bool secp256k1_recover_lane(const fe& hash_be, const 
     fe_from_be_words(s, w);
     return secp256k1_recover_rsv<LDS>(hash_be, r, s, rd.word(16) & 0xffu, tab, px, py, ldsx);
 }
+
+}  // namespace bcosgpu
+#include "recover26.h"
+namespace bcosgpu {
 
 // pub -> right160(Keccak256(pub)) as 5 little-endian memory words
 __device__ __forceinline__ void keccak_address(uint32_t a[5], const fe& x, const fe& y) {
@@ -1091,7 +1098,7 @@ __global__ __launch_bounds__(256) void ecrecover_kernel(const uint8_t* __restric
 // Transaction::verify for a batch: tx hash of the preimage, recover / verify, sender address.
 // OCC = waves per SIMD the register allocation must allow: 1 (no spills, lowest per-tx latency:
 // small batches) or 2 (spills ~120 VGPRs to scratch but doubles the resident waves: large batches).
-template <int SUITE, int OCC>
+template <int SUITE, int OCC, bool F26 = false>
 __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(const uint8_t* __restrict__ pre,
                                                         const uint64_t* __restrict__ pre_off,
                                                         const uint8_t* __restrict__ sig,
@@ -1130,7 +1137,8 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(const uint8_t* __re
         ok = sm2_verify_lane<kLds>(h, sig + sa, slen, CombTab{tab, tbits}, x, y, ldsx);
         if (ok) sm3_address(ad, x, y);
     } else {
-        ok = secp256k1_recover_lane<kLds>(h, sig + sa, slen, CombTab{tab, tbits}, x, y, ldsx);
+        if constexpr (F26) ok = secp256k1_recover_lane26<kLds>(h, sig + sa, slen, CombTab{tab, tbits}, x, y, ldsx);
+        else ok = secp256k1_recover_lane<kLds>(h, sig + sa, slen, CombTab{tab, tbits}, x, y, ldsx);
         if (ok) keccak_address(ad, x, y);
     }
     uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
@@ -2562,12 +2570,14 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
         return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
     }
     const int occ = pol.occ ? pol.occ : (n >= (1ull << 17) ? 2 : 1);  // >= 2 waves per SIMD of work
-#define TXV(S, O, T) hipLaunchKernelGGL((tx_verify_kernel<S, O>), dim3(grid_of(n)), dim3(256), 0, st, d_pre, d_pre_off, \
-                                        d_sig, d_sig_off, n, T, bits, d_txhash, d_sender, d_status)
+#define TXV(S, O, F, T) hipLaunchKernelGGL((tx_verify_kernel<S, O, F>), dim3(grid_of(n)), dim3(256), 0, st, d_pre, \
+                                           d_pre_off, d_sig, d_sig_off, n, T, bits, d_txhash, d_sender, d_status)
     if (suite == BCOSGPU_SUITE_SM2) {
-        if (occ == 2) TXV(BCOSGPU_SUITE_SM2, 2, sm2); else TXV(BCOSGPU_SUITE_SM2, 1, sm2);
+        if (occ == 2) TXV(BCOSGPU_SUITE_SM2, 2, false, sm2); else TXV(BCOSGPU_SUITE_SM2, 1, false, sm2);
+    } else if (pol.f26) {
+        if (occ == 2) TXV(BCOSGPU_SUITE_SECP256K1, 2, true, k1); else TXV(BCOSGPU_SUITE_SECP256K1, 1, true, k1);
     } else {
-        if (occ == 2) TXV(BCOSGPU_SUITE_SECP256K1, 2, k1); else TXV(BCOSGPU_SUITE_SECP256K1, 1, k1);
+        if (occ == 2) TXV(BCOSGPU_SUITE_SECP256K1, 2, false, k1); else TXV(BCOSGPU_SUITE_SECP256K1, 1, false, k1);
     }
 #undef TXV
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;

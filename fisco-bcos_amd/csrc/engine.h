@@ -28,7 +28,7 @@ int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* 
 
 // ecc_kernels.hip
 int ecc_init_tables(int device, int small_tables);
-void set_tx_kernel_policy(int split, int occ, int coop);
+void set_tx_kernel_policy(int split, int occ, int coop, int f26);
 int launch_secp256k1_recover(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t sig_stride,
                              uint64_t n, uint8_t* d_pub, uint8_t* d_addr, uint8_t* d_ok,
                              hipStream_t st);

@@ -45,12 +45,15 @@ def keys(x):
 
 
 class Op:
-    def __init__(self, text, vd=(), vu=(), sd=(), su=(), valu=True, cost=1, barrier=False):
+    def __init__(self, text, vd=(), vu=(), sd=(), su=(), valu=True, cost=1, barrier=False, sjunk=()):
         self.text, self.valu, self.cost, self.barrier = text, valu, cost, barrier
         self.vd = [k for x in vd for k in keys(x)]
         self.vu = [k for x in vu for k in keys(x)]
         self.sd = [k for x in sd for k in keys(x)]
         self.su = [k for x in su for k in keys(x)]
+        # SGPRs written but never read in the block (a discarded carry-out): no ordering constraint,
+        # but their write time still counts for the exit pad
+        self.sj = [k for x in sjunk for k in keys(x)]
 
 
 def isv(x):
@@ -91,6 +94,11 @@ def subbrev(d, x, y, ci, co):  # d = y - x - ci
 def mad(dp, co, x, y, acc):
     """dp (pair) = x * y + acc (pair or 0); co = carry-out of the 64-bit addition."""
     return Op(f"v_mad_u64_u32 {dp}, {co}, {x}, {y}, {acc}", [dp], [x, y, acc], [co], cost=2)
+
+
+def madj(dp, junk, x, y, acc):
+    """dp (pair) = x * y + acc with the carry-out discarded into `junk` (never read)."""
+    return Op(f"v_mad_u64_u32 {dp}, {junk}, {x}, {y}, {acc}", [dp], [x, y, acc], cost=2, sjunk=[junk])
 
 
 def mov(d, x):
@@ -173,7 +181,7 @@ def schedule_segment(ops, wtime, t0):
         o = ops[i]
         lines.append(o.text)
         if o.valu:
-            for k in o.sd:
+            for k in o.sd + o.sj:
                 wtime[k] = t
         else:
             for k in o.sd:
@@ -619,6 +627,88 @@ def gen_mod_sub():
     return blk
 
 
+# ------------------------------------------------------------------ 10 x 26-bit secp256k1 field
+def gen_fe26(square):
+    """fe26_mul / fe26_sqr (fe26.h): 19 product columns as two v_mad_u64_u32 chains the scheduler
+    interleaves -- the high chain (columns 10..18, pair v[0:1]) carries into 26-bit limbs H0..H8 and
+    H9; the low chain (columns 0..9, pair v[2:3]) adds H_j * R0 and H_(j-1) * 2^10 (2^260 = 2^36 + R0)
+    to column j before cutting limb j -- then the carry x out of bit 256 and the H9 terms fold into
+    limbs 0..3.  Carries enter each column as the accumulator the first product adds to, so a column
+    costs its products plus one v_and and one 64-bit shift."""
+    name = "fe26_sqr_asm(uint32_t r[10], const uint32_t a[10])" if square else \
+        "fe26_mul_asm(uint32_t r[10], const uint32_t a[10], const uint32_t b[10])"
+    blk = Blk(name, "r = a^2 mod p (fe26, inputs m <= 16, output m = 1)" if square else
+              "r = a * b mod p (fe26, inputs m <= 16, output m = 1)",
+              "uint32_t h[10], d[9]; uint64_t jh, jl; uint32_t kR0 = 0x3d10u, k1024 = 1024u, "
+              "kR0x = 0x3d10u << 10, k20 = 1u << 20, k977 = 977u;" if square else
+              "uint32_t h[10]; uint64_t jh, jl; uint32_t kR0 = 0x3d10u, k1024 = 1024u, "
+              "kR0x = 0x3d10u << 10, k20 = 1u << 20, k977 = 977u;")
+    R = blk.vout("r", 10)
+    H = blk.vout("h", 10)
+    D = blk.vout("d", 9) if square else None
+    JH, JL = blk.sout("jh"), blk.sout("jl")
+    A = blk.vin("a", 10)
+    B = A if square else blk.vin("b", 10)
+    kR0, k1024, kR0x, k20, k977 = (blk.sin(x) for x in ("kR0", "k1024", "kR0x", "k20", "k977"))
+    blk.clobbers = ["v0", "v1", "v2", "v3"]
+    HP, LP = ("v[0:1]", "v0", "v1"), ("v[2:3]", "v2", "v3")
+    M26, M22 = "0x3ffffff", "0x3fffff"
+    if square:
+        for i in range(9):
+            blk.emit(valu(f"v_lshlrev_b32_e32 {D[i]}, 1, {A[i]}", D[i], A[i]))
+
+    def prods(k):
+        if not square:
+            return [(A[i], B[k - i]) for i in range(10) if 0 <= k - i < 10]
+        out = [(D[i], A[k - i]) for i in range(10) if i < k - i < 10]
+        if k % 2 == 0:
+            out.append((A[k // 2], A[k // 2]))
+        return out
+
+    def column(P, junk, k, first):
+        ps = prods(k)
+        for idx, (x, y) in enumerate(ps):
+            blk.emit(madj(P[0], junk, x, y, "0" if (first and idx == 0) else P[0]))
+
+    # both chains in one stream; the scheduler interleaves them
+    for j in range(10):
+        if j < 9:  # high column 10 + j -> H_j
+            column(HP, JH, 10 + j, j == 0)
+            blk.emit(valu(f"v_and_b32_e32 {H[j]}, {M26}, {HP[1]}", H[j], HP[1]))
+            blk.emit(valu(f"v_lshrrev_b64 {HP[0]}, 26, {HP[0]}", HP[0], HP[0]))
+            if j == 8:
+                blk.emit(mov(H[9], HP[1]))  # H9 < 2^27
+        column(LP, JL, j, j == 0)
+        blk.emit(madj(LP[0], JL, H[j], kR0, LP[0]))
+        if j >= 1:
+            blk.emit(madj(LP[0], JL, H[j - 1], k1024, LP[0]))
+        if j < 9:
+            blk.emit(valu(f"v_and_b32_e32 {R[j]}, {M26}, {LP[1]}", R[j], LP[1]))
+            blk.emit(valu(f"v_lshrrev_b64 {LP[0]}, 26, {LP[0]}", LP[0], LP[0]))
+        else:
+            blk.emit(valu(f"v_and_b32_e32 {R[9]}, {M22}, {LP[1]}", R[9], LP[1]))
+            blk.emit(valu(f"v_lshrrev_b64 {LP[0]}, 22, {LP[0]}", LP[0], LP[0]))  # x < 2^42
+    # limb 0 += x 977 + H9 R0 2^10;  limb 1 += x 2^6 + H9 2^20;  carries through limb 3
+    blk.emit(madj(HP[0], JH, H[9], kR0x, "0"))
+    blk.emit(madj(HP[0], JH, LP[1], k977, HP[0]))
+    blk.emit(valu(f"v_mad_u32_u24 {HP[2]}, {LP[2]}, {k977}, {HP[2]}", HP[2], LP[2], k977, HP[2]))
+    blk.emit(madj(HP[0], JH, R[0], "1", HP[0]))
+    blk.emit(valu(f"v_and_b32_e32 {R[0]}, {M26}, {HP[1]}", R[0], HP[1]))
+    blk.emit(valu(f"v_lshrrev_b64 {HP[0]}, 26, {HP[0]}", HP[0], HP[0]))
+    # (v_lshl_add_u64 takes shift amounts 0..4 only: shift x first)
+    blk.emit(valu(f"v_lshlrev_b64 {LP[0]}, 6, {LP[0]}", LP[0], LP[0]))
+    blk.emit(valu(f"v_lshl_add_u64 {HP[0]}, {LP[0]}, 0, {HP[0]}", HP[0], LP[0], HP[0]))
+    blk.emit(madj(HP[0], JH, H[9], k20, HP[0]))
+    blk.emit(madj(HP[0], JH, R[1], "1", HP[0]))
+    blk.emit(valu(f"v_and_b32_e32 {R[1]}, {M26}, {HP[1]}", R[1], HP[1]))
+    blk.emit(valu(f"v_alignbit_b32 {HP[1]}, {HP[2]}, {HP[1]}, 26", HP[1], HP[2], HP[1]))  # < 2^23
+    blk.emit(valu(f"v_add_u32_e32 {HP[1]}, {R[2]}, {HP[1]}", HP[1], R[2], HP[1]))
+    blk.emit(valu(f"v_and_b32_e32 {R[2]}, {M26}, {HP[1]}", R[2], HP[1]))
+    blk.emit(valu(f"v_lshrrev_b32_e32 {HP[1]}, 26, {HP[1]}", HP[1], HP[1]))
+    blk.emit(valu(f"v_add_u32_e32 {R[3]}, {R[3]}, {HP[1]}", R[3], R[3], HP[1]))
+    return blk
+
+
 def main():
     parts = ["// fe_asm.h -- GENERATED by tools/gen_fe_asm.py; do not edit by hand.",
              "// 256-bit field primitives as single inline-asm blocks, scheduled so that every VALU read of",
@@ -629,7 +719,7 @@ def main():
     stats = []
     for g in (gen_mul512, gen_sqr512, gen_k1_reduce, lambda: gen_k1_addsub(False), lambda: gen_k1_addsub(True),
               lambda: gen_k1_shl(1), lambda: gen_k1_shl(2), lambda: gen_k1_shl(3), lambda: gen_k1_add_shl(1),
-              gen_k1_normalize, gen_mod_add, gen_mod_sub):
+              gen_k1_normalize, gen_mod_add, gen_mod_sub, lambda: gen_fe26(False), lambda: gen_fe26(True)):
         blk = g()
         text, ninst, nops = blk.render()
         name = blk.sig.split("(")[0]

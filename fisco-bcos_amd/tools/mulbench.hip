@@ -3,9 +3,11 @@
 // wave (the C2 / small-batch regime) issue-bound or dependency-latency-bound in FieldK1::mul?
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include "../csrc/fe.h"
 #include "../csrc/ec.h"
+#include "../csrc/ec26.h"
 
 using namespace bcosgpu;
 #define ITERS 2000
@@ -193,6 +195,90 @@ __global__ __launch_bounds__(256) void k_mulpair(uint64_t* cyc, uint32_t* out, u
     if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+
+__device__ __forceinline__ void seed_fe26(fe26& x, uint32_t s) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) x.v[i] = (s * 2654435761u + i * 40503u + 1u) & 0x3ffffffu;
+    x.v[9] &= 0x3fffffu;
+}
+template <int CHAINS>
+__global__ __launch_bounds__(256) void k_f26mul(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    fe26 x[CHAINS], y;
+    seed_fe26(y, s + 99);
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) seed_fe26(x[c], s + threadIdx.x + c);
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) fe26_mul(x[c], x[c], y);
+    }
+    const uint64_t t1 = clock64();
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) r ^= x[c].v[0] ^ x[c].v[7];
+    if (r == 0x00345678u) out[0] = r;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+template <int CHAINS>
+__global__ __launch_bounds__(256) void k_f26sqr(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    fe26 x[CHAINS];
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) seed_fe26(x[c], s + threadIdx.x + c);
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) fe26_sqr(x[c], x[c]);
+    }
+    const uint64_t t1 = clock64();
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) r ^= x[c].v[0] ^ x[c].v[7];
+    if (r == 0x00345678u) out[0] = r;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+__global__ __launch_bounds__(256) void k_f26dbl(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    Jac26 P;
+    seed_fe26(P.X, s + threadIdx.x);
+    seed_fe26(P.Y, s + threadIdx.x + 7);
+    seed_fe26(P.Z, s + threadIdx.x + 9);
+    P.inf = false;
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS / 8; ++it) CurveK1x::dbl(P, P);
+    const uint64_t t1 = clock64();
+    if ((P.X.v[0] ^ P.Y.v[3]) == 0x00345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+__global__ __launch_bounds__(256) void k_madd(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    Jac P;
+    Aff Q;
+    seed_fe(P.X, s + threadIdx.x);
+    seed_fe(P.Y, s + threadIdx.x + 7);
+    seed_fe(P.Z, s + threadIdx.x + 9);
+    seed_fe(Q.x, s + 3);
+    seed_fe(Q.y, s + 5);
+    P.inf = false;
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS / 8; ++it) CurveK1::madd(P, P, Q);
+    const uint64_t t1 = clock64();
+    if ((P.X.v[0] ^ P.Y.v[3]) == 0x00345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+__global__ __launch_bounds__(256) void k_f26madd(uint64_t* cyc, uint32_t* out, uint32_t s) {
+    Jac26 P;
+    Aff26 Q;
+    seed_fe26(P.X, s + threadIdx.x);
+    seed_fe26(P.Y, s + threadIdx.x + 7);
+    seed_fe26(P.Z, s + threadIdx.x + 9);
+    seed_fe26(Q.x, s + 3);
+    seed_fe26(Q.y, s + 5);
+    P.inf = false;
+    const uint64_t t0 = clock64();
+    for (int it = 0; it < ITERS / 8; ++it) CurveK1x::madd(P, P, Q);
+    const uint64_t t1 = clock64();
+    if ((P.X.v[0] ^ P.Y.v[3]) == 0x00345678u) out[0] = 1;
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 template <class K>
 static void run(const char* name, K kern, int waves_per_simd, double ops_per_iter, int iters, uint64_t* d_cyc, uint32_t* d_out,
                 bool last) {
@@ -227,26 +313,36 @@ int main() {
     hipDeviceProp_t p;
     hipGetDeviceProperties(&p, 0);
     printf("{\"device\": \"%s\", \"clock_khz\": %d,\n", p.gcnArchName, p.clockRate);
-    for (int occ = 1; occ <= 2; ++occ) {
-        run("madnc_chain1", k_madnc<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
-        run("madnc_chain4", k_madnc<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
-        run("lshladd_chain1", k_lshladd<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
-        run("lshladd_chain4", k_lshladd<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
-        run("add_chain1", k_add<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
-        run("add_chain4", k_add<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
-        run("mulpair_chain4", k_mulpair<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
-        run("madc_chain1", k_madchain<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
-        run("madc_chain2", k_madchain<2>, occ, 2, ITERS * 8, d_cyc, d_out, false);
-        run("madc_chain4", k_madchain<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
+    const bool quick = getenv("MULBENCH_QUICK") != nullptr;
+    for (int occ = 1; occ <= 4; occ *= 2) {
+        if (!quick) {
+            run("madnc_chain1", k_madnc<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
+            run("madnc_chain4", k_madnc<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
+            run("lshladd_chain1", k_lshladd<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
+            run("lshladd_chain4", k_lshladd<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
+            run("add_chain1", k_add<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
+            run("add_chain4", k_add<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
+            run("mulpair_chain4", k_mulpair<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
+            run("madc_chain1", k_madchain<1>, occ, 1, ITERS * 8, d_cyc, d_out, false);
+            run("madc_chain2", k_madchain<2>, occ, 2, ITERS * 8, d_cyc, d_out, false);
+            run("madc_chain4", k_madchain<4>, occ, 4, ITERS * 8, d_cyc, d_out, false);
+            run("p2_mul", k_fmul<FieldP2>, occ, 1, ITERS, d_cyc, d_out, false);
+            run("p2_sqr", k_fsqr<FieldP2>, occ, 1, ITERS, d_cyc, d_out, false);
+            run("n2_mul_generic", k_fmul<FieldN2>, occ, 1, ITERS, d_cyc, d_out, false);
+            run("n2_sqr_generic", k_fsqr<FieldN2>, occ, 1, ITERS, d_cyc, d_out, false);
+        }
         run("fk1_mul_chain1", k_mul<1>, occ, 1, ITERS, d_cyc, d_out, false);
         run("fk1_mul_chain2", k_mul<2>, occ, 2, ITERS, d_cyc, d_out, false);
         run("fk1_sqr_chain1", k_sqr<1>, occ, 1, ITERS, d_cyc, d_out, false);
         run("fk1_sqr_chain2", k_sqr<2>, occ, 2, ITERS, d_cyc, d_out, false);
-        run("p2_mul", k_fmul<FieldP2>, occ, 1, ITERS, d_cyc, d_out, false);
-        run("p2_sqr", k_fsqr<FieldP2>, occ, 1, ITERS, d_cyc, d_out, false);
-        run("n2_mul_generic", k_fmul<FieldN2>, occ, 1, ITERS, d_cyc, d_out, false);
-        run("n2_sqr_generic", k_fsqr<FieldN2>, occ, 1, ITERS, d_cyc, d_out, false);
-        run("k1_dbl", k_dbl, occ, 1, ITERS / 8, d_cyc, d_out, occ == 2);
+        run("f26_mul_chain1", k_f26mul<1>, occ, 1, ITERS, d_cyc, d_out, false);
+        run("f26_mul_chain2", k_f26mul<2>, occ, 2, ITERS, d_cyc, d_out, false);
+        run("f26_sqr_chain1", k_f26sqr<1>, occ, 1, ITERS, d_cyc, d_out, false);
+        run("f26_sqr_chain2", k_f26sqr<2>, occ, 2, ITERS, d_cyc, d_out, false);
+        run("k1_dbl", k_dbl, occ, 1, ITERS / 8, d_cyc, d_out, false);
+        run("f26_dbl", k_f26dbl, occ, 1, ITERS / 8, d_cyc, d_out, false);
+        run("k1_madd", k_madd, occ, 1, ITERS / 8, d_cyc, d_out, false);
+        run("f26_madd", k_f26madd, occ, 1, ITERS / 8, d_cyc, d_out, occ == 4);
     }
     printf("}\n");
     return 0;

@@ -68,10 +68,12 @@ int bcosgpu_init(int device);
 #define BCOSGPU_INIT_SMALL_TABLES 1
 int bcosgpu_init_ex(int device, int flags);
 /* Kernel selection for the tx-verify batch (tuning / tests; the default is chosen by batch size and
- * read once from BCOSGPU_TXV_SPLIT / _OCC / _COOP at the first init, never per launch):
+ * read once from BCOSGPU_TXV_SPLIT / _OCC / _COOP and BCOSGPU_K1_F26 at the first init, never per launch):
  * split -1 by size (secp256k1 batches <= 2^15 run the small-batch kernels), 0 never, 1 always;
- * occupancy 0 by size (2 waves/SIMD for n >= 2^17), 1 or 2 forced; coop 1 cooperative-pair, 0 split. */
-int bcosgpu_set_tx_kernel_policy(int split, int occupancy, int coop);
+ * occupancy 0 by size (2 waves/SIMD for n >= 2^17), 1 or 2 forced; coop 1 cooperative-pair, 0 split;
+ * field (secp256k1 throughput kernels) 1 the 10 x 26-bit point arithmetic (default), 0 the 8 x 32-bit
+ * one, -1 unchanged.  Every variant returns identical results. */
+int bcosgpu_set_tx_kernel_policy(int split, int occupancy, int coop, int field);
 /* Last error message of the calling thread. */
 const char* bcosgpu_last_error(void);
 /* Bytes of the reference's Merkle output vector, in 32-byte entries (Merkle.h:224-236 getMerkleSize). */

@@ -263,19 +263,21 @@ def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
     b = synth.make_batch(suite, n, seed=91, flip_frac=0.02, bad_v_frac=0.01)
     pre, po, sg, so = (x.cpu().numpy() for x in (b.pre, b.pre_off, b.sig, b.sig_off))
     wh, ws, wst = oracle.tx_verify_packed(suite, pre, po.astype(np.uint64), sg, so.astype(np.uint64), nthreads=16)
-    # secp256k1: cooperative-pair, 4-wave split, one-lane occ 1 / 2; SM2: pair kernel, one-lane occ 1 / 2
-    variants = [(1, 1, 1), (1, 1, 0), (0, 1, 0), (0, 2, 0)] if suite == 0 else [(1, 1, 1), (0, 1, 0), (0, 2, 0)]
+    # secp256k1: cooperative-pair, 4-wave split, one-lane occ 1 / 2 on the 10 x 26-bit and on the
+    # 8 x 32-bit point arithmetic; SM2: pair kernel, one-lane occ 1 / 2
+    variants = ([(1, 1, 1, 1), (1, 1, 0, 1), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)] if suite == 0
+                else [(1, 1, 1, 1), (0, 1, 0, 1), (0, 2, 0, 1)])
     try:
-        for split, occ, coop in variants:
-            gpu.set_tx_kernel_policy(split, occ, coop)
+        for split, occ, coop, field in variants:
+            gpu.set_tx_kernel_policy(split, occ, coop, field)
             th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
             snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
             st = torch.empty(n, dtype=torch.uint8, device="cuda")
             device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
             torch.cuda.synchronize()
-            assert np.array_equal(th.cpu().numpy(), wh), (split, occ)
-            assert np.array_equal(st.cpu().numpy(), wst), (split, occ)
-            assert np.array_equal(snd.cpu().numpy(), ws), (split, occ)
+            assert np.array_equal(th.cpu().numpy(), wh), (split, occ, field)
+            assert np.array_equal(st.cpu().numpy(), wst), (split, occ, field)
+            assert np.array_equal(snd.cpu().numpy(), ws), (split, occ, field)
     finally:
         gpu.set_tx_kernel_policy()
 
@@ -295,7 +297,7 @@ for suite in (0, 1):
     th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
     snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
     st = torch.empty(n, dtype=torch.uint8, device="cuda")
-    bcos_gpu.check(bcos_gpu.lib().bcosgpu_set_tx_kernel_policy(0, 2, 1))  # the throughput kernel
+    bcos_gpu.check(bcos_gpu.lib().bcosgpu_set_tx_kernel_policy(0, 2, 1, -1))  # the throughput kernel
     device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
     torch.cuda.synchronize()
     pre, po, sg, so = (x.cpu().numpy() for x in (b.pre, b.pre_off, b.sig, b.sig_off))
