@@ -2053,6 +2053,431 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* _
     COOP_T(3);
 }
 
+// ------------------------------------------------------------------ cooperative kernel on fe26
+// tx_verify_coop_kernel with the curve work of phases A and C on the 10 x 26-bit field (fe26.h): the
+// same schedule, the same wave roles and the same pair split of every doubling and mixed addition, but
+// a lone wave (one per SIMD here) no longer waits on carry chains: its field additions are independent
+// limb adds and its multiplies are two interleaved mad chains.  Field elements cross between the two
+// waves of a pair as their raw limbs (magnitudes travel with them, as the formulas state); the tables
+// and phase results in LDS stay canonical 8-word values, so phase D is tx_verify_coop_kernel's.
+// Bit-identical to tx_verify_kernel<0, *>.
+struct Coop26Lds {
+    uint32_t tab[8][16][64];          // co-Z table on E', canonical words: [entry][x0..7, y0..7][lane]
+    uint32_t zc[8][64];
+    uint32_t k[2][4][64];             // GLV halves
+    uint32_t flags[64];               // bit0 scalars ok, bit1 R ok, bit2 neg1, bit3 neg2
+    uint2 ex[2][2][6][5][64];         // [chain][writer role][slot][limb pair][lane]: one fe26 = 5 ds_write_b64
+    uint32_t tabphx[8][8][64];        // beta * x of the table entries
+    uint32_t pt[5][25][64];           // chain results 0/1, G partials 2..4 (canonical X, Y, Z, inf)
+    uint32_t xe[8][64];
+    uint32_t xrinv[8][64];
+    uint32_t ys[8][64];
+    uint32_t rflag[64];
+    uint32_t post[2];
+};
+
+struct Coop26Ctx {
+    Coop26Lds* L;
+    int chain, role, lane;
+    __device__ __forceinline__ void puts(int s, const fe26& a) const {
+        uint2* p = &L->ex[chain][role][s][0][0] + lane;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) p[q * 64] = make_uint2(a.v[2 * q], a.v[2 * q + 1]);
+    }
+    __device__ __forceinline__ void gets(int s, fe26& a) const {
+        const uint2* p = &L->ex[chain][role ^ 1][s][0][0] + lane;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const uint2 w = p[q * 64];
+            a.v[2 * q] = w.x;
+            a.v[2 * q + 1] = w.y;
+        }
+    }
+};
+
+// as coop_dbl (slot buffers 0-2 / 3-5 alternate the same way); magnitudes as CurveK1x::dbl:
+//   a: A = X^2, E = 3A (3), F = E^2, Z3 = 2 Y Z (2) | b: B = Y^2, D = 4 X B (4), C8 = 8 B^2 (8)
+//   -> both: X3 = F - 2D (10), Y3 = E (D - X3) - C8 (10)
+template <int S0>
+__device__ __forceinline__ void coop26_dbl(Jac26& P, const Coop26Ctx& c) {
+    fe26 E, F, D, C8, Z3, X3, Y3, t;
+    if (c.role == 0) {
+        fe26 A;
+        fe26_sqr(A, P.X);
+        fe26_mul_int<3>(E, A);
+        fe26_sqr(F, E);
+        c.puts(S0, E);
+        c.puts(S0 + 1, F);
+        fe26_mul(Z3, P.Y, P.Z);
+        fe26_mul_int<2>(Z3, Z3);
+        c.puts(S0 + 2, Z3);
+    } else {
+        fe26 B, C;
+        fe26_sqr(B, P.Y);
+        fe26_mul(D, P.X, B);
+        fe26_mul_int<4>(D, D);
+        c.puts(S0, D);
+        fe26_sqr(C, B);
+        fe26_mul_int<8>(C8, C);
+        c.puts(S0 + 1, C8);
+    }
+    __syncthreads();
+    if (c.role == 0) {
+        c.gets(S0, D);
+        c.gets(S0 + 1, C8);
+    } else {
+        c.gets(S0, E);
+        c.gets(S0 + 1, F);
+        c.gets(S0 + 2, Z3);
+    }
+    fe26_mul_int<2>(t, D);
+    fe26_sub<9>(X3, F, t);
+    fe26_sub<11>(t, D, X3);
+    fe26_mul(Y3, E, t);
+    fe26_sub<9>(Y3, Y3, C8);
+    fe26_copy(P.X, X3);
+    fe26_copy(P.Y, Y3);
+    fe26_copy(P.Z, Z3);
+}
+
+// as coop_madd, with CurveK1x::madd's arrangement (r = 2 rr, Z3 = 2 Z1 H):
+//   both: Z1Z1 | a: U2, H (12), HH, Z3 (2) | b: S2, rr (12), R2 = 4 rr^2 (4)
+//   -> a: J = H I | b: V = X1 I        (I = 4 HH)
+//   -> a: rr (V - X3) | b: Y1 J        -> Y3 = 2 (a - b) (6);  X3 = R2 - J - 2V (9)
+__device__ __forceinline__ void coop26_madd(Jac26& R, const Jac26& P, const Aff26& Q, const Coop26Ctx& c) {
+    fe26 Z1Z1, H, HH, Z3, rr, R2, I, J, V, X3, Y3, t, u;
+    fe26_sqr(Z1Z1, P.Z);
+    if (c.role == 0) {
+        fe26_mul(u, Q.x, Z1Z1);
+        fe26_sub<11>(H, u, P.X);
+        fe26_sqr(HH, H);
+        fe26_mul(Z3, P.Z, H);
+        fe26_mul_int<2>(Z3, Z3);
+        c.puts(0, H);
+        c.puts(1, HH);
+        c.puts(2, Z3);
+    } else {
+        fe26_mul(u, Q.y, P.Z);
+        fe26_mul(u, u, Z1Z1);
+        fe26_sub<11>(rr, u, P.Y);
+        fe26_sqr(R2, rr);
+        fe26_mul_int<4>(R2, R2);
+        c.puts(0, rr);
+        c.puts(1, R2);
+    }
+    __syncthreads();
+    if (c.role == 0) {
+        c.gets(0, rr);
+        c.gets(1, R2);
+    } else {
+        c.gets(0, H);
+        c.gets(1, HH);
+        c.gets(2, Z3);
+    }
+    fe26_mul_int<4>(I, HH);
+    if (c.role == 0) {
+        fe26_mul(J, H, I);
+        c.puts(3, J);
+    } else {
+        fe26_mul(V, P.X, I);
+        c.puts(3, V);
+    }
+    __syncthreads();
+    if (c.role == 0) c.gets(3, V);
+    else c.gets(3, J);
+    fe26_sub<2>(X3, R2, J);
+    fe26_mul_int<2>(t, V);
+    fe26_sub<3>(X3, X3, t);
+    if (c.role == 0) {
+        fe26_sub<10>(t, V, X3);
+        fe26_mul(u, rr, t);
+        c.puts(4, u);
+    } else {
+        fe26_mul(u, P.Y, J);
+        c.puts(4, u);
+    }
+    __syncthreads();
+    c.gets(4, t);
+    if (c.role == 0) fe26_sub<2>(Y3, u, t);
+    else fe26_sub<2>(Y3, t, u);
+    fe26_mul_int<2>(Y3, Y3);
+    const bool hz = fe26_is_zero(H) && !P.inf;
+    const bool rz = fe26_is_zero(rr);
+    Jac26 D;
+    if (hz && rz) CurveK1x::dbl(D, P);  // P == Q (rare)
+    const bool pinf = P.inf;
+    fe26_copy(R.X, X3);
+    fe26_copy(R.Y, Y3);
+    fe26_copy(R.Z, Z3);
+    R.inf = false;
+    if (hz) {
+        if (rz) CurveK1x::cmov(R, D, true);
+        else R.inf = true;
+    }
+    if (pinf) {
+        fe26_copy(R.X, Q.x);
+        fe26_copy(R.Y, Q.y);
+        fe26_one(R.Z);
+        R.inf = false;
+    }
+}
+
+__device__ __forceinline__ void coop26_add_digit(Jac26& acc, const Coop26Ctx& c, int d, bool neg, bool phi) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &c.L->tab[0][0][0] + m * (16 * 64) + c.lane;
+    const uint32_t* bx = phi ? &c.L->tabphx[0][0][0] + m * (8 * 64) + c.lane : base;
+    Aff26 S;
+    {
+        uint32_t x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            x[k] = bx[k * 64];
+            y[k] = base[(8 + k) * 64];
+        }
+        fe26_from_words(S.x, x);
+        fe26_from_words(S.y, y);
+    }
+    fe26 ny;
+    fe26_neg<2>(ny, S.y);
+    fe26_cmov(S.y, ny, (d < 0) != neg);
+    Jac26 R;
+    coop26_madd(R, acc, S, c);
+    CurveK1x::cmov(acc, R, d != 0);
+}
+
+// acc = u1 * G restricted to 8-bit comb windows [lo, hi)
+__device__ __forceinline__ void comb_range26(Jac26& acc, const fe& k_plain, const uint32_t* __restrict__ tab, int lo,
+                                             int hi) {
+    fe k;
+    fe_copy(k, k_plain);
+    for (int i = 0; i < lo; ++i) shr8(k);
+    CurveK1x::set_inf(acc);
+#pragma unroll 1
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t b = k.v[0] & 255u;
+        shr8(k);
+        Aff26 T;
+        load_aff26(T, tab + (static_cast<size_t>(i) * kCombEntries + b) * 16);
+        Jac26 S;
+        CurveK1x::madd(S, acc, T);
+        CurveK1x::cmov(acc, S, b != 0u);
+    }
+}
+
+// canonical 8-word coordinates into a phase-result slot (the layout coop_load_jac reads)
+__device__ __forceinline__ void coop26_store_jac(uint32_t (*dst)[64], const Jac26& P, int lane) {
+    fe X, Y, Z;
+    fe26_to_fe(X, P.X);
+    fe26_to_fe(Y, P.Y);
+    fe26_to_fe(Z, P.Z);
+    Jac J;
+    fe_copy(J.X, X);
+    fe_copy(J.Y, Y);
+    fe_copy(J.Z, Z);
+    J.inf = P.inf;
+    coop_store_jac(dst, J, lane);
+}
+__device__ __forceinline__ void lds_store_fe26(uint32_t (*dst)[64], const fe26& a, int lane) {
+    fe w;
+    fe26_to_fe(w, a);
+    lds_store_fe(dst, w, lane);
+}
+
+__global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t* __restrict__ pre,
+                                                                  const uint64_t* __restrict__ pre_off,
+                                                                  const uint8_t* __restrict__ sig,
+                                                                  const uint64_t* __restrict__ sig_off, uint64_t n,
+                                                                  const uint32_t* __restrict__ tab,
+                                                                  uint8_t* __restrict__ txhash,
+                                                                  uint8_t* __restrict__ sender,
+                                                                  uint8_t* __restrict__ status) {
+    __shared__ Coop26Lds L;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
+    const bool active = i < n;
+    uint64_t sa = 0, sb = 0, pa = 0, pb = 0;
+    if (active) {
+        sa = sig_off[i];
+        sb = sig_off[i + 1];
+        pa = pre_off[i];
+        pb = pre_off[i + 1];
+    }
+    const uint32_t slen = (sb - sa) > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(sb - sa);
+    if (threadIdx.x == 0) {
+        L.post[0] = 0u;
+        L.post[1] = 0u;
+    }
+    __syncthreads();
+    // ---------------------------------------------------------------- phase A (as tx_verify_coop_kernel)
+    fe r, s;
+    uint32_t v = 0;
+    bool ok = false;
+    if (active) ok = parse_sig65(sig + sa, slen, r, s, v);
+    else { fe_zero(r); fe_zero(s); }
+    if (wave == 1 || wave == 2) {
+        fe x;
+        fe_copy(x, r);
+        bool okr = ok;
+        if (v & 2u) {
+            okr = okr && fe_lt_k(r, kK1PminusN);
+            fe_add_k(x, r, ParamN1::M);
+        }
+        fe26 X, rhs, t, seven;
+        fe26_from_fe(X, x);
+        fe26_sqr(t, X);
+        fe26_mul(rhs, t, X);
+        fe26_set_small(seven, 7u);
+        fe26_add(rhs, rhs, seven);  // w (m 2)
+        if (wave == 2) {
+            fe26 y, ny;
+            fe26_sqrt_cand(y, rhs);
+            fe26_sqr(t, y);
+            fe26_sub<3>(t, t, rhs);
+            okr = okr && fe26_is_zero(t);
+            fe26_normalize(y);
+            fe26_neg<2>(ny, y);
+            fe26_normalize(ny);
+            fe26_cmov(y, ny, (y.v[0] & 1u) != (v & 1u));
+            lds_store_fe26(L.ys, y, lane);
+            L.rflag[lane] = okr ? 2u : 0u;
+        } else {
+            Aff26 R, A[8];
+            fe26_mul(R.x, rhs, X);  // w x
+            fe26_sqr(R.y, rhs);     // w^2
+            fe26 Zc, beta;
+            {
+                Jac26 T[8];
+                multiples8_26(T, R);
+                coz_table26(A, Zc, T);
+            }
+            fe26_const(beta, kGlvBeta);
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                lds_store_fe26(L.tab[j], A[j].x, lane);
+                lds_store_fe26(L.tab[j] + 8, A[j].y, lane);
+                fe26 bx;
+                fe26_mul(bx, A[j].x, beta);
+                lds_store_fe26(L.tabphx[j], bx, lane);
+            });
+            lds_store_fe26(L.zc, Zc, lane);
+        }
+    }
+    if (!ok) {
+        fe_zero(r);
+        r.v[0] = 1;
+        fe_zero(s);
+    }
+    if (wave == 3) {
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (active) {
+            const uint32_t len = static_cast<uint32_t>(pb - pa);
+            ByteReader rd(pre + pa, len);
+            keccak256_msg(rd, len, d);
+            store_digest(KECCAK256, txhash + 32 * i, d);
+        }
+        fe e;
+        fe_from_be_words(e, d);
+        reduce_once(e, ParamN1::M);
+        lds_store_fe(L.xe, e, lane);
+        coop_post(&L.post[1]);
+    } else if (wave == 0) {
+        fe rm, rinv;
+        FieldN1::from_plain(rm, r);
+        FieldInv<FieldN1>::inv(rinv, rm);
+        lds_store_fe(L.xrinv, rinv, lane);
+        coop_post(&L.post[0]);
+    }
+    if (wave != 2) {
+        coop_wait(&L.post[0]);
+        coop_wait(&L.post[1]);
+        fe e, rinv, u1;
+        lds_load_fe(e, L.xe, lane);
+        lds_load_fe(rinv, L.xrinv, lane);
+        FieldN1::mul(u1, e, rinv);
+        FieldN1::neg(u1, u1);
+        if (wave == 1) {
+            fe u2, k1, k2;
+            FieldN1::mul(u2, s, rinv);
+            bool neg1, neg2;
+            glv_split(k1, neg1, k2, neg2, u2);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                L.k[0][q][lane] = k1.v[q];
+                L.k[1][q][lane] = k2.v[q];
+            }
+            L.flags[lane] = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
+        }
+        constexpr int kCombW0 = 12, kCombW1 = 24;
+        Jac26 G;
+        const int lo = wave == 0 ? 0 : wave == 3 ? kCombW0 : kCombW1;
+        const int hi = wave == 0 ? kCombW0 : wave == 3 ? kCombW1 : 32;
+        comb_range26(G, u1, tab, lo, hi);
+        coop26_store_jac(L.pt[wave == 0 ? 2 : wave == 3 ? 3 : 4], G, lane);
+    }
+    __syncthreads();
+    // ---------------------------------------------------------------- phase C: two cooperative GLV chains
+    const uint32_t flags = L.flags[lane] | L.rflag[lane];
+    Coop26Ctx c{&L, wave >> 1, wave & 1, lane};
+    fe k;
+    fe_zero(k);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) k.v[q] = L.k[c.chain][q][lane];
+    const bool neg = c.chain == 0 ? (flags & 4u) != 0 : (flags & 8u) != 0;
+    const bool phi = c.chain == 1;
+    Jac26 acc;
+    CurveK1x::set_inf(acc);
+    coop26_add_digit(acc, c, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
+#pragma unroll 1
+    for (int w = 31; w >= 0; --w) {
+        coop26_dbl<0>(acc, c);
+        coop26_dbl<3>(acc, c);
+        coop26_dbl<0>(acc, c);
+        coop26_dbl<3>(acc, c);
+        coop26_add_digit(acc, c, booth_digit128(k), neg, phi);
+    }
+    if (c.role == 0) coop26_store_jac(L.pt[c.chain], acc, lane);
+    __syncthreads();
+    // ---------------------------------------------------------------- phase D (tx_verify_coop_kernel's)
+    if (wave == 1) {
+        Jac G0, G1, T, U;
+        coop_load_jac(G0, L.pt[2], lane);
+        coop_load_jac(G1, L.pt[3], lane);
+        CurveK1::add(T, G0, G1);
+        coop_load_jac(G0, L.pt[4], lane);
+        CurveK1::add(U, T, G0);
+        coop_store_jac(L.pt[2], U, lane);
+    } else if (wave == 0) {
+        Jac P0, P1, Q;
+        coop_load_jac(P0, L.pt[0], lane);
+        coop_load_jac(P1, L.pt[1], lane);
+        fe Zc, y;
+        lds_load_fe(Zc, L.zc, lane);
+        lds_load_fe(y, L.ys, lane);
+        CurveK1::add(Q, P0, P1);
+        FieldK1::mul(Zc, Zc, y);
+        FieldK1::mul(Q.Z, Q.Z, Zc);
+        coop_store_jac(L.pt[0], Q, lane);
+    }
+    __syncthreads();
+    if (wave == 0 && active) {
+        Jac Q, G, R;
+        coop_load_jac(Q, L.pt[0], lane);
+        coop_load_jac(G, L.pt[2], lane);
+        CurveK1::add(R, Q, G);
+        const bool ok2 = (flags & 3u) == 3u && !R.inf;
+        Aff A;
+        CurveK1::to_aff(A, R);
+        FieldK1::normalize(A.x);
+        FieldK1::normalize(A.y);
+        uint32_t ad[5] = {0, 0, 0, 0, 0};
+        if (ok2) keccak_address(ad, A.x, A.y);
+        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) o[q] = ad[q];
+        status[i] = ok2 ? 0 : 1;
+    }
+}
+
 // ------------------------------------------------------------------ SM2 small-batch (pair) tx verify
 // Guomi chains verify blocks of C2 size (FastSM2Crypto, FastSM2Crypto.h:33-44).  SM2 has no efficient
 // endomorphism, so t*P is ONE chain of 256 doublings and 65 mixed additions.  A 256-thread workgroup
@@ -2554,7 +2979,10 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
         rc = tables8(&k1, &sm2);
         if (rc) return rc;
         const dim3 grid(static_cast<unsigned>((n + 63) / 64));
-        if (pol.coop)
+        if (pol.coop && pol.f26)
+            hipLaunchKernelGGL(tx_verify_coop26_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n,
+                               k1, d_txhash, d_sender, d_status);
+        else if (pol.coop)
             hipLaunchKernelGGL(tx_verify_coop_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n, k1,
                                d_txhash, d_sender, d_status);
         else
