@@ -65,7 +65,8 @@ KECCAK_F_OPS = 6240
 SM3_C_OPS = 2100
 PMC_GLOB = "r02_pmc_{}.json"
 KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_kernels.hip", "fisco-bcos_amd/csrc/fe_asm.h", "fisco-bcos_amd/csrc/fe.h",
-              "fisco-bcos_amd/csrc/ec.h", "fisco-bcos_amd/csrc/hash_device.h", "fisco-bcos_amd/csrc/modinv.h"]
+              "fisco-bcos_amd/csrc/ec.h", "fisco-bcos_amd/csrc/hash_device.h", "fisco-bcos_amd/csrc/modinv.h",
+              "fisco-bcos_amd/csrc/fe26.h", "fisco-bcos_amd/csrc/ec26.h", "fisco-bcos_amd/csrc/recover26.h"]
 
 WORKLOADS = {
     "c2": dict(suite=0, n=10_000, scaling="weak",
@@ -93,12 +94,21 @@ def kernel_source_sha():
 
 
 def _kernel_name(suite, n):
-    """Which tx-verify kernel the library launches for this batch (mirrors launch_tx_verify)."""
-    if suite == 0 and n <= (1 << 15):
-        return "tx_verify_coop_kernel"
-    if suite == 1 and n <= (1 << 15):
+    """Which tx-verify kernel the library launches for this batch (mirrors launch_tx_verify and its
+    policy: BCOSGPU_TXV_* and BCOSGPU_K1_F26, read once by the library)."""
+    f26 = os.environ.get("BCOSGPU_K1_F26", "1") != "0"
+    split = os.environ.get("BCOSGPU_TXV_SPLIT")
+    small = (split == "1") if split in ("0", "1") else n <= (1 << 15)
+    coop = os.environ.get("BCOSGPU_TXV_COOP", "1") != "0"
+    if suite == 0 and small:
+        if not coop:
+            return "tx_verify_split_kernel"
+        return "tx_verify_coop26_kernel" if f26 else "tx_verify_coop_kernel"
+    if suite == 1 and small and coop:
         return "tx_verify_sm2_pair_kernel"
-    return "tx_verify_kernel<%d,%d>" % (suite, 2 if n >= (1 << 17) else 1)
+    occ = os.environ.get("BCOSGPU_TXV_OCC")
+    occ = int(occ) if occ in ("1", "2") else (2 if n >= (1 << 17) else 1)
+    return "tx_verify_kernel<%d,%d,%s>" % (suite, occ, "true" if (suite == 0 and f26) else "false")
 
 
 def _norm(name):

@@ -984,7 +984,80 @@ __device__ __forceinline__ bool secp256k1_verify_lane(const fe& hash_be, const u
     return ok && match;
 }
 
+// secp256k1_verify_lane with the point arithmetic on fe26 (same decisions and result)
+__device__ __forceinline__ bool secp256k1_verify_lane26(const fe& hash_be, const uint8_t* sig, const uint8_t* pub,
+                                                        CombTab tab) {
+    ByteReader rs(sig, 64), rp(pub, 64);
+    uint32_t w[8];
+    fe r, s, x, y;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rs.word(i);
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rs.word(8 + i);
+    fe_from_be_words(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rp.word(i);
+    fe_from_be_words(x, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rp.word(8 + i);
+    fe_from_be_words(y, w);
+    bool ok = fe_lt_k(x, FieldK1::P) && fe_lt_k(y, FieldK1::P);
+    Aff26 P;
+    fe26_from_fe(P.x, x);
+    fe26_from_fe(P.y, y);
+    {
+        fe26 l, rr, t, seven;
+        fe26_sqr(l, P.y);
+        fe26_sqr(t, P.x);
+        fe26_mul(rr, t, P.x);
+        fe26_set_small(seven, 7u);
+        fe26_add(rr, rr, seven);
+        fe26_sub<3>(l, l, rr);
+        ok = ok && fe26_is_zero(l);
+    }
+    ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, kN1HalfPlus);
+    fe e;
+    fe_copy(e, hash_be);
+    reduce_once(e, ParamN1::M);
+    fe ss = s;
+    if (!ok) {
+        fe_zero(ss);
+        ss.v[0] = 1;
+    }
+    fe sm, sinv, u1, u2;
+    FieldN1::from_plain(sm, ss);
+    FieldInv<FieldN1>::inv(sinv, sm);
+    FieldN1::mul(u1, e, sinv);
+    FieldN1::mul(u2, r, sinv);
+    if (!ok) {
+        fe26_const(P.x, kK1Gx);
+        fe26_const(P.y, kK1Gy);
+    }
+    Jac26 QG, QP, Q;
+    glv_mul_k1_26<false>(QP, u2, P, nullptr);
+    comb_mul26_rt(QG, u1, tab);
+    CurveK1x::add(Q, QG, QP);  // X m 6
+    ok = ok && !Q.inf;
+    fe26 z2, rhs, R, d;
+    fe26_sqr(z2, Q.Z);
+    fe26_from_fe(R, r);
+    fe26_mul(rhs, R, z2);
+    fe26_sub<7>(d, rhs, Q.X);
+    bool match = fe26_is_zero(d);
+    fe r2;
+    const uint32_t carry = fe_add_k(r2, r, ParamN1::M);
+    if (carry == 0u && fe_lt_k(r2, FieldK1::P)) {
+        fe26_from_fe(R, r2);
+        fe26_mul(rhs, R, z2);
+        fe26_sub<7>(d, rhs, Q.X);
+        match = match || fe26_is_zero(d);
+    }
+    return ok && match;
+}
+
 // ------------------------------------------------------------------ kernels
+template <bool F26>
 __global__ __launch_bounds__(256) void secp256k1_recover_kernel(const uint8_t* __restrict__ hash,
                                                                 const uint8_t* __restrict__ sig, uint32_t stride,
                                                                 uint64_t n, const uint32_t* __restrict__ tab, int tbits,
@@ -994,7 +1067,8 @@ __global__ __launch_bounds__(256) void secp256k1_recover_kernel(const uint8_t* _
     if (i >= n) return;
     fe h, x, y;
     load_be256_aligned(h, hash + 32 * i);
-    const bool ok = secp256k1_recover_lane(h, sig + static_cast<uint64_t>(stride) * i, 65u, CombTab{tab, tbits}, x, y);
+    const bool ok = F26 ? secp256k1_recover_lane26(h, sig + static_cast<uint64_t>(stride) * i, 65u, CombTab{tab, tbits}, x, y)
+                        : secp256k1_recover_lane(h, sig + static_cast<uint64_t>(stride) * i, 65u, CombTab{tab, tbits}, x, y);
     if (!ok) {
         fe_zero(x);
         fe_zero(y);
@@ -1035,7 +1109,7 @@ __global__ __launch_bounds__(256) void sm2_verify_kernel(const uint8_t* __restri
 // SignatureCrypto::verify(pub, hash, sig) for a batch (sealer signatures: BlockValidator.cpp:141-182,
 // PBFTCacheProcessor.cpp:795-821).  SM2: SM2Crypto::verify reads the first 64 signature bytes (r || s)
 // and verifies against the GIVEN key (SM2Crypto.cpp:66-79); secp256k1: secp256k1_verify_lane.
-template <int SUITE>
+template <int SUITE, bool F26 = false>
 __global__ __launch_bounds__(256) void sig_verify_kernel(const uint8_t* __restrict__ pub,
                                                          const uint8_t* __restrict__ hash,
                                                          const uint8_t* __restrict__ sig, uint32_t stride,
@@ -1064,7 +1138,8 @@ __global__ __launch_bounds__(256) void sig_verify_kernel(const uint8_t* __restri
         }
         ok = sm2_verify_rs(h, r, s, X, Y, CombTab{tab, tbits}, x, y);
     } else {
-        ok = secp256k1_verify_lane(h, sg, pub + 64 * i, CombTab{tab, tbits});
+        if constexpr (F26) ok = secp256k1_verify_lane26(h, sg, pub + 64 * i, CombTab{tab, tbits});
+        else ok = secp256k1_verify_lane(h, sg, pub + 64 * i, CombTab{tab, tbits});
     }
     okout[i] = ok ? 1 : 0;
 }
@@ -1073,6 +1148,7 @@ __global__ __launch_bounds__(256) void sig_verify_kernel(const uint8_t* __restri
 // hash(32) || v(32) || r(32) || s(32); recid = (byte)(in[63] - 27) (the other 31 bytes of v are not
 // read); on success out = 12 zero bytes || right160(Keccak256(pub)), ok = 1; on failure the
 // precompile returns an empty output: out = zeros, ok = 0.
+template <bool F26>
 __global__ __launch_bounds__(256) void ecrecover_kernel(const uint8_t* __restrict__ in, uint64_t n,
                                                         const uint32_t* __restrict__ tab, int tbits,
                                                         uint8_t* __restrict__ out, uint8_t* __restrict__ okout) {
@@ -1084,7 +1160,8 @@ __global__ __launch_bounds__(256) void ecrecover_kernel(const uint8_t* __restric
     load_be256_aligned(r, p + 64);
     load_be256_aligned(s, p + 96);
     const uint32_t v = (reinterpret_cast<const uint32_t*>(p)[15] >> 24) - 27u;
-    const bool ok = secp256k1_recover_rsv(h, r, s, v & 0xffu, CombTab{tab, tbits}, x, y);
+    const bool ok = F26 ? secp256k1_recover_rsv26(h, r, s, v & 0xffu, CombTab{tab, tbits}, x, y)
+                        : secp256k1_recover_rsv(h, r, s, v & 0xffu, CombTab{tab, tbits}, x, y);
     uint32_t a[5] = {0, 0, 0, 0, 0};
     if (ok) keccak_address(a, x, y);
     uint32_t* o = reinterpret_cast<uint32_t*>(out + 32 * i);
@@ -2079,6 +2156,7 @@ struct Coop26Lds {
 struct Coop26Ctx {
     Coop26Lds* L;
     int chain, role, lane;
+    bool probe;  // BCOSGPU_COOP_TIMING
     __device__ __forceinline__ void puts(int s, const fe26& a) const {
         uint2* p = &L->ex[chain][role][s][0][0] + lane;
 #pragma unroll
@@ -2101,6 +2179,7 @@ struct Coop26Ctx {
 template <int S0>
 __device__ __forceinline__ void coop26_dbl(Jac26& P, const Coop26Ctx& c) {
     fe26 E, F, D, C8, Z3, X3, Y3, t;
+    DBL_T(0);
     if (c.role == 0) {
         fe26 A;
         fe26_sqr(A, P.X);
@@ -2121,7 +2200,9 @@ __device__ __forceinline__ void coop26_dbl(Jac26& P, const Coop26Ctx& c) {
         fe26_mul_int<8>(C8, C);
         c.puts(S0 + 1, C8);
     }
+    DBL_T(1);
     __syncthreads();
+    DBL_T(2);
     if (c.role == 0) {
         c.gets(S0, D);
         c.gets(S0 + 1, C8);
@@ -2135,9 +2216,11 @@ __device__ __forceinline__ void coop26_dbl(Jac26& P, const Coop26Ctx& c) {
     fe26_sub<11>(t, D, X3);
     fe26_mul(Y3, E, t);
     fe26_sub<9>(Y3, Y3, C8);
+    DBL_T(3);
     fe26_copy(P.X, X3);
     fe26_copy(P.Y, Y3);
     fe26_copy(P.Z, Z3);
+    DBL_T(4);
 }
 
 // as coop_madd, with CurveK1x::madd's arrangement (r = 2 rr, Z3 = 2 Z1 H):
@@ -2277,6 +2360,19 @@ __device__ __forceinline__ void coop26_store_jac(uint32_t (*dst)[64], const Jac2
     J.inf = P.inf;
     coop_store_jac(dst, J, lane);
 }
+__device__ __forceinline__ void coop26_load_jac(Jac26& P, const uint32_t (*src)[64], int lane) {
+    Jac J;
+    coop_load_jac(J, src, lane);
+    fe26_from_fe(P.X, J.X);
+    fe26_from_fe(P.Y, J.Y);
+    fe26_from_fe(P.Z, J.Z);
+    P.inf = J.inf;
+}
+__device__ __forceinline__ void lds_load_fe26(fe26& a, const uint32_t (*src)[64], int lane) {
+    fe w;
+    lds_load_fe(w, src, lane);
+    fe26_from_fe(a, w);
+}
 __device__ __forceinline__ void lds_store_fe26(uint32_t (*dst)[64], const fe26& a, int lane) {
     fe w;
     fe26_to_fe(w, a);
@@ -2295,6 +2391,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t*
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
     const bool active = i < n;
+    COOP_T(0);
     uint64_t sa = 0, sb = 0, pa = 0, pb = 0;
     if (active) {
         sa = sig_off[i];
@@ -2340,6 +2437,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t*
             fe26_cmov(y, ny, (y.v[0] & 1u) != (v & 1u));
             lds_store_fe26(L.ys, y, lane);
             L.rflag[lane] = okr ? 2u : 0u;
+            COOP_T(6);
         } else {
             Aff26 R, A[8];
             fe26_mul(R.x, rhs, X);  // w x
@@ -2360,6 +2458,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t*
                 lds_store_fe26(L.tabphx[j], bx, lane);
             });
             lds_store_fe26(L.zc, Zc, lane);
+            COOP_T(6);
         }
     }
     if (!ok) {
@@ -2380,12 +2479,14 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t*
         reduce_once(e, ParamN1::M);
         lds_store_fe(L.xe, e, lane);
         coop_post(&L.post[1]);
+        COOP_T(7);
     } else if (wave == 0) {
         fe rm, rinv;
         FieldN1::from_plain(rm, r);
         FieldInv<FieldN1>::inv(rinv, rm);
         lds_store_fe(L.xrinv, rinv, lane);
         coop_post(&L.post[0]);
+        COOP_T(7);
     }
     if (wave != 2) {
         coop_wait(&L.post[0]);
@@ -2414,10 +2515,11 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t*
         comb_range26(G, u1, tab, lo, hi);
         coop26_store_jac(L.pt[wave == 0 ? 2 : wave == 3 ? 3 : 4], G, lane);
     }
+    COOP_T(1);
     __syncthreads();
     // ---------------------------------------------------------------- phase C: two cooperative GLV chains
     const uint32_t flags = L.flags[lane] | L.rflag[lane];
-    Coop26Ctx c{&L, wave >> 1, wave & 1, lane};
+    Coop26Ctx c{&L, wave >> 1, wave & 1, lane, false};
     fe k;
     fe_zero(k);
 #pragma unroll
@@ -2430,52 +2532,76 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t*
 #pragma unroll 1
     for (int w = 31; w >= 0; --w) {
         coop26_dbl<0>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+        c.probe = blockIdx.x == 0 && w == 20;
+#endif
         coop26_dbl<3>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+        c.probe = false;
+        if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][5] = clock64();
+#endif
         coop26_dbl<0>(acc, c);
         coop26_dbl<3>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+        if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][6] = clock64();
+#endif
         coop26_add_digit(acc, c, booth_digit128(k), neg, phi);
+#ifdef BCOSGPU_COOP_TIMING
+        if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][7] = clock64();
+#endif
     }
+    COOP_T(2);
     if (c.role == 0) coop26_store_jac(L.pt[c.chain], acc, lane);
     __syncthreads();
-    // ---------------------------------------------------------------- phase D (tx_verify_coop_kernel's)
-    if (wave == 1) {
-        Jac G0, G1, T, U;
-        coop_load_jac(G0, L.pt[2], lane);
-        coop_load_jac(G1, L.pt[3], lane);
-        CurveK1::add(T, G0, G1);
-        coop_load_jac(G0, L.pt[4], lane);
-        CurveK1::add(U, T, G0);
-        coop_store_jac(L.pt[2], U, lane);
-    } else if (wave == 0) {
-        Jac P0, P1, Q;
-        coop_load_jac(P0, L.pt[0], lane);
-        coop_load_jac(P1, L.pt[1], lane);
-        fe Zc, y;
-        lds_load_fe(Zc, L.zc, lane);
-        lds_load_fe(y, L.ys, lane);
-        CurveK1::add(Q, P0, P1);
-        FieldK1::mul(Zc, Zc, y);
-        FieldK1::mul(Q.Z, Q.Z, Zc);
-        coop_store_jac(L.pt[0], Q, lane);
+    // ---------------------------------------------------------------- phase D (on fe26 as well)
+    if (wave == 1) {  // G part: partials 0 + 1 + 2
+        Jac26 G0, G1, T, U;
+        coop26_load_jac(G0, L.pt[2], lane);
+        coop26_load_jac(G1, L.pt[3], lane);
+        CurveK1x::add(T, G0, G1);
+        coop26_load_jac(G0, L.pt[4], lane);
+        CurveK1x::add(U, T, G0);
+        coop26_store_jac(L.pt[2], U, lane);
+    } else if (wave == 0) {  // R part: co-Z curve -> E_w (Z * Zc) -> E (Z * y)
+        Jac26 P0, P1, Q;
+        coop26_load_jac(P0, L.pt[0], lane);
+        coop26_load_jac(P1, L.pt[1], lane);
+        fe26 Zc, y;
+        lds_load_fe26(Zc, L.zc, lane);
+        lds_load_fe26(y, L.ys, lane);
+        CurveK1x::add(Q, P0, P1);
+        fe26_mul(Zc, Zc, y);
+        fe26_mul(Q.Z, Q.Z, Zc);
+        coop26_store_jac(L.pt[0], Q, lane);
     }
     __syncthreads();
     if (wave == 0 && active) {
-        Jac Q, G, R;
-        coop_load_jac(Q, L.pt[0], lane);
-        coop_load_jac(G, L.pt[2], lane);
-        CurveK1::add(R, Q, G);
+        Jac26 Q, G, R;
+        coop26_load_jac(Q, L.pt[0], lane);
+        coop26_load_jac(G, L.pt[2], lane);
+        CurveK1x::add(R, Q, G);
         const bool ok2 = (flags & 3u) == 3u && !R.inf;
-        Aff A;
-        CurveK1::to_aff(A, R);
-        FieldK1::normalize(A.x);
-        FieldK1::normalize(A.y);
+        COOP_T(4);
+        fe z, zi, ax, ay;
+        fe26_to_fe(z, R.Z);
+        FieldInv<FieldK1>::inv(zi, z);
+        COOP_T(5);
+        fe26 zi26, zi2, zi3, X, Y;
+        fe26_from_fe(zi26, zi);
+        fe26_sqr(zi2, zi26);
+        fe26_mul(X, R.X, zi2);
+        fe26_mul(zi3, zi2, zi26);
+        fe26_mul(Y, R.Y, zi3);
+        fe26_to_fe(ax, X);
+        fe26_to_fe(ay, Y);
         uint32_t ad[5] = {0, 0, 0, 0, 0};
-        if (ok2) keccak_address(ad, A.x, A.y);
+        if (ok2) keccak_address(ad, ax, ay);
         uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
 #pragma unroll
         for (int q = 0; q < 5; ++q) o[q] = ad[q];
         status[i] = ok2 ? 0 : 1;
     }
+    COOP_T(3);
 }
 
 // ------------------------------------------------------------------ SM2 small-batch (pair) tx verify
@@ -2894,8 +3020,12 @@ int launch_secp256k1_recover(const uint8_t* d_hash, const uint8_t* d_sig, uint32
     int bits;
     int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    hipLaunchKernelGGL(secp256k1_recover_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, k1,
-                       bits, d_pub, d_addr, d_ok);
+    if (g_policy.f26)
+        hipLaunchKernelGGL(secp256k1_recover_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n,
+                           k1, bits, d_pub, d_addr, d_ok);
+    else
+        hipLaunchKernelGGL(secp256k1_recover_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n,
+                           k1, bits, d_pub, d_addr, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
@@ -2947,6 +3077,9 @@ int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, co
     if (suite == BCOSGPU_SUITE_SM2)
         hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SM2>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash, d_sig,
                            stride, n, sm2, bits, d_ok);
+    else if (g_policy.f26)
+        hipLaunchKernelGGL((sig_verify_kernel<BCOSGPU_SUITE_SECP256K1, true>), dim3(grid_of(n)), dim3(256), 0, st, d_pub,
+                           d_hash, d_sig, stride, n, k1, bits, d_ok);
     else
         hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SECP256K1>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash,
                            d_sig, stride, n, k1, bits, d_ok);
@@ -2959,7 +3092,10 @@ int launch_ecrecover(const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint8_t* d
     int bits;
     int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    hipLaunchKernelGGL(ecrecover_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_in, n, k1, bits, d_out, d_ok);
+    if (g_policy.f26)
+        hipLaunchKernelGGL(ecrecover_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, d_in, n, k1, bits, d_out, d_ok);
+    else
+        hipLaunchKernelGGL(ecrecover_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, d_in, n, k1, bits, d_out, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 

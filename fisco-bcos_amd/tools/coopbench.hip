@@ -1,13 +1,15 @@
-// coopbench.hip -- phase timestamps (s_memtime cycles) of tx_verify_coop_kernel's workgroup 0 on a
+// coopbench.hip -- phase timestamps (s_memtime cycles) of tx_verify_coop_kernel's (argv[1] = 26:
+// tx_verify_coop26_kernel's) workgroup 0 on a
 // 10k-tx batch of random inputs (the schedule is input-independent), to see where C2's latency goes.
 #define BCOSGPU_COOP_TIMING 1
 #include "../csrc/ecc_kernels.hip"
 #include <cstdio>
 #include <vector>
 
-int main() {
+int main(int argc, char** argv) {
     using namespace bcosgpu;
-    if (ecc_init_tables(0)) { printf("no device\n"); return 77; }
+    const bool f26 = argc > 1 && argv[1][0] == '2';  // "26": tx_verify_coop26_kernel
+    if (ecc_init_tables(0, 1)) { printf("no device\n"); return 77; }
     const uint64_t n = 10000;
     std::vector<uint8_t> pre(n * 151), sig(n * 65);
     std::vector<uint64_t> po(n + 1), so(n + 1);
@@ -27,7 +29,12 @@ int main() {
     const uint32_t *k1, *sm2;
     tables8(&k1, &sm2);
     for (int rep = 0; rep < 3; ++rep) {
-        hipLaunchKernelGGL(tx_verify_coop_kernel, dim3((n + 63) / 64), dim3(256), 0, 0, dp, dpo, ds, dso, n, k1, dh, dsn, dst);
+        if (f26)
+            hipLaunchKernelGGL(tx_verify_coop26_kernel, dim3((n + 63) / 64), dim3(256), 0, 0, dp, dpo, ds, dso, n, k1, dh,
+                               dsn, dst);
+        else
+            hipLaunchKernelGGL(tx_verify_coop_kernel, dim3((n + 63) / 64), dim3(256), 0, 0, dp, dpo, ds, dso, n, k1, dh,
+                               dsn, dst);
         hipDeviceSynchronize();
     }
     uint64_t t[4][8];
@@ -43,9 +50,10 @@ int main() {
     hipMemcpyFromSymbol(dt, HIP_SYMBOL(g_dbl_t), sizeof(dt));
     printf("], \"dbl\": [");
     for (int w = 0; w < 4; ++w)
-        printf("%s[%llu, %llu, %llu, %llu]", w ? ", " : "", (unsigned long long)(dt[w][1] - dt[w][0]),
+        printf("%s[%llu, %llu, %llu, %llu, %llu, %llu, %llu]", w ? ", " : "", (unsigned long long)(dt[w][1] - dt[w][0]),
                (unsigned long long)(dt[w][2] - dt[w][0]), (unsigned long long)(dt[w][3] - dt[w][0]),
-               (unsigned long long)(dt[w][4] - dt[w][0]));
+               (unsigned long long)(dt[w][4] - dt[w][0]), (unsigned long long)(dt[w][5] - dt[w][0]),
+               (unsigned long long)(dt[w][6] - dt[w][0]), (unsigned long long)(dt[w][7] - dt[w][0]));
     printf("], \"wave0_phase_d\": [%llu, %llu], \"probes\": \"end of phase A work, end of phase C loop, end of kernel; wave 0: before / after the affine inversion\"}\n",
            (unsigned long long)(t[0][4] - t[0][0]), (unsigned long long)(t[0][5] - t[0][0]));
     return 0;

@@ -135,7 +135,7 @@ def _mutate(rng, sig, kind):
     return bytes(s)
 
 
-def test_secp256k1_recover_random_and_edge(gpu, oracle):
+def test_secp256k1_recover_random_and_edge(gpu, oracle, k1_field):
     rng = np.random.default_rng(23)
     n = 4000
     sk = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)

@@ -48,7 +48,7 @@ def _edit(rng, pub, h, sig, i, kind, order, other_pub):
 
 
 @pytest.mark.parametrize("suite", [0, 1])
-def test_verify_known_key_vs_oracle(gpu, oracle, suite):
+def test_verify_known_key_vs_oracle(gpu, oracle, suite, k1_field):
     rng = np.random.default_rng(31 + suite)
     n = 2000
     sk = _keys(rng, n)
@@ -78,7 +78,7 @@ def test_verify_known_key_vs_oracle(gpu, oracle, suite):
     assert not crypto.verify(pub[2].tobytes(), h[2].tobytes(), sig[2].tobytes())
 
 
-def test_ecrecover_precompile_vs_oracle(gpu, oracle):
+def test_ecrecover_precompile_vs_oracle(gpu, oracle, k1_field):
     from bcos_gpu.precompiled import ec_recover, ec_recover_batch
     rng = np.random.default_rng(41)
     n = 1500
