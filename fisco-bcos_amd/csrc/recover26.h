@@ -92,22 +92,21 @@ __device__ __forceinline__ void multiples8_26(Jac26 T[8], const Aff26& P) {
 // co-Z rescale of T[0..7] (T[0].Z == 1) to Zc = Z1 ... Z7, as coz_table_k1: the entries are affine on
 // the isomorphic curve y^2 = x^3 + 7 Zc^6 (a = 0 kept), results are (X, Y, Z Zc) on the real curve
 __device__ __forceinline__ void coz_table26(Aff26 A[8], fe26& Zc, const Jac26 T[8]) {
-    fe26 pre[8], suf[8];
+    // s_j = Zc / Z_j = (Z_1 ... Z_(j-1)) (Z_(j+1) ... Z_7): prefix products kept, the suffix as a running
+    // product while the entries are emitted from the top down (T[7] is released first)
+    fe26 pre[7], suf;
     fe26_one(pre[0]);
     fe26_copy(pre[1], T[1].Z);
-    Unroll<2, 8>::run([&](auto J) { fe26_mul(pre[J], pre[J - 1], T[J].Z); });
-    fe26_one(suf[7]);
-    Unroll<0, 7>::run([&](auto J) {
-        constexpr int j = 6 - decltype(J)::value;
-        fe26_mul(suf[j], suf[j + 1], T[j + 1].Z);
-    });
-    fe26_copy(Zc, pre[7]);
+    Unroll<2, 7>::run([&](auto J) { fe26_mul(pre[J], pre[J - 1], T[J].Z); });
+    fe26_mul(Zc, pre[6], T[7].Z);
     Unroll<0, 8>::run([&](auto J) {
-        constexpr int j = decltype(J)::value;
+        constexpr int j = 7 - decltype(J)::value;
         fe26 sj, s2, s3;
-        if constexpr (j == 0) fe26_copy(sj, suf[0]);
-        else if constexpr (j == 7) fe26_copy(sj, pre[6]);
-        else fe26_mul(sj, pre[j - 1], suf[j]);
+        if constexpr (j == 7) fe26_copy(sj, pre[6]);
+        else if constexpr (j <= 1) fe26_copy(sj, suf);
+        else fe26_mul(sj, pre[j - 1], suf);
+        if constexpr (j == 7) fe26_copy(suf, T[7].Z);
+        else if constexpr (j >= 1) fe26_mul(suf, suf, T[j].Z);
         fe26_sqr(s2, sj);
         fe26_mul(s3, s2, sj);
         fe26_mul(A[j].x, T[j].X, s2);
@@ -116,8 +115,9 @@ __device__ __forceinline__ void coz_table26(Aff26 A[8], fe26& Zc, const Jac26 T[
 }
 
 // acc += (sign d) (phi ? lambda : 1) P from the table: x-coordinates as canonical words in the wave's
-// LDS slice ([entry][word][lane], ldsx offset by the lane), y-coordinates in registers
-__device__ __forceinline__ void add_digit26(Jac26& acc, const uint32_t* ldsx, const fe26 Y[8], const fe26& beta,
+// LDS slice ([entry][word][lane], ldsx offset by the lane), y-coordinates as canonical words in
+// registers (8 per entry instead of 10: the window loop of the occupancy-2 kernel is register-bound)
+__device__ __forceinline__ void add_digit26(Jac26& acc, const uint32_t* ldsx, const fe Y[8], const fe26& beta,
                                             int d, bool neg, bool phi) {
     const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
     Aff26 S;
@@ -128,9 +128,13 @@ __device__ __forceinline__ void add_digit26(Jac26& acc, const uint32_t* ldsx, co
         for (int k = 0; k < 8; ++k) w[k] = b[k * 64];
         fe26_from_words(S.x, w);
     }
-    fe26_copy(S.y, Y[0]);
+    {
+        fe y;
+        fe_copy(y, Y[0]);
 #pragma unroll
-    for (int q = 1; q < 8; ++q) fe26_cmov(S.y, Y[q], m == static_cast<uint32_t>(q));
+        for (int q = 1; q < 8; ++q) fe_cmov(y, Y[q], m == static_cast<uint32_t>(q));
+        fe26_from_fe(S.y, y);
+    }
     if (phi) fe26_mul(S.x, S.x, beta);
     fe26 ny;
     fe26_neg<2>(ny, S.y);
@@ -178,14 +182,14 @@ __device__ __forceinline__ void glv_mul_k1_26(Jac26& acc, const fe& k, const Aff
     fe26_const(beta, kGlvBeta);
     CurveK1x::set_inf(acc);
     if constexpr (LDS) {
-        fe26 Y[8];
+        fe Y[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             fe x;
             fe26_to_fe(x, A[j].x);
 #pragma unroll
             for (int w = 0; w < 8; ++w) ldsx[(j * 8 + w) * 64] = x.v[w];
-            fe26_copy(Y[j], A[j].y);
+            fe26_to_fe(Y[j], A[j].y);
         }
         add_digit26(acc, ldsx, Y, beta, static_cast<int>(k1.v[3] >> 31), neg1, false);
         add_digit26(acc, ldsx, Y, beta, static_cast<int>(k2.v[3] >> 31), neg2, true);
