@@ -470,7 +470,7 @@ def create_transaction_leg(b, suite, n, want_status, reps=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3500, help="timed steps of the headline (C2) leg")
+    ap.add_argument("--steps", type=int, default=4500, help="timed steps of the headline (C2) leg")
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--warm-seconds", type=float, default=2.0, help="minimum warm-up before the timed region")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS), help="the headline leg")
