@@ -479,6 +479,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the PCIe and createTransaction legs")
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="CPU test of the --gpus launcher path only: spawn, rendezvous (gloo), max over ranks; no GPU work")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -491,6 +493,17 @@ def main():
 
     import torch
     import torch.distributed as dist
+    if args.launcher_selftest:
+        if world > 1:
+            dist.init_process_group("gloo")
+        ctx = Ctx(world, rank, dist)
+        slowest = ctx.max(rank)
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "max_over_ranks": slowest, "launcher_selftest": True}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return 0
     import bcos_gpu
 
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
