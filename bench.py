@@ -108,7 +108,7 @@ def _kernel_name(suite, n):
         return "tx_verify_sm2_pair_kernel"
     occ = os.environ.get("BCOSGPU_TXV_OCC")
     occ = int(occ) if occ in ("1", "2") else (2 if n >= (1 << 17) else 1)
-    return "tx_verify_kernel<%d,%d,%s>" % (suite, occ, "true" if (suite == 0 and f26) else "false")
+    return "tx_verify_kernel<%d,%d,%s>" % (suite, occ, "true" if f26 else "false")
 
 
 def _norm(name):

@@ -80,6 +80,8 @@ static uint32_t* g_tab_k1[64];
 static uint32_t* g_tab_sm2[64];
 static uint32_t* g_wtab_k1[64];
 static uint32_t* g_wtab_sm2[64];
+static uint32_t* g_tab_sm2_26[64];   // the SM2 tables re-expressed in fp26's Montgomery domain (R = 2^286)
+static uint32_t* g_wtab_sm2_26[64];
 
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ void load_be256(fe& r, const uint8_t* p) {
@@ -630,6 +632,30 @@ static void free_tables(uint32_t*& a, uint32_t*& b, uint32_t*& c, uint32_t*& d) 
     }
 }
 
+// init: SM2 comb table entries (x || y, R = 2^256 Montgomery domain, canonical) -> fp26's R' = 2^286
+// domain: the Montgomery product (R domain) with 2^286 mod p
+__device__ __constant__ static const uint32_t kSm2RtoR26[8] = {0x40000000u, 0x0u, 0xc0000000u, 0x3fffffffu,
+                                                               0x0u,        0x0u, 0x0u,        0x40000000u};
+__global__ __launch_bounds__(256) void sm2_table_to_r26_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                                                               uint64_t entries) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= entries) return;
+    fe c, x, y;
+    fe_set(c, kSm2RtoR26);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        x.v[w] = src[i * 16 + w];
+        y.v[w] = src[i * 16 + 8 + w];
+    }
+    FieldP2::mul(x, x, c);
+    FieldP2::mul(y, y, c);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        dst[i * 16 + w] = x.v[w];
+        dst[i * 16 + 8 + w] = y.v[w];
+    }
+}
+
 // Builds the device's comb tables: the 8-bit ones (512 KiB per curve) always; the 16-bit ones (64 MiB
 // per curve) unless `small` or their allocation fails -- the kernels then run the 8-bit comb.
 int ecc_init_tables(int device, int small) {
@@ -659,10 +685,35 @@ int ecc_init_tables(int device, int small) {
         hipLaunchKernelGGL((comb_wide_kernel<CurveK1, FieldK1>), dim3(gw), dim3(256), 0, 0, wk1, k1);
         hipLaunchKernelGGL((comb_wide_kernel<CurveSM2, FieldP2>), dim3(gw), dim3(256), 0, 0, wsm2, sm2);
     }
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    uint32_t *sm2r = nullptr, *wsm2r = nullptr;
+    if (hipMalloc(&sm2r, kTabWords * 4) != hipSuccess) {
+        (void)hipGetLastError();
         free_tables(k1, sm2, wk1, wsm2);
         return BCOSGPU_E_HIP;
     }
+    {
+        const uint64_t ent = kTabWords / 16;
+        hipLaunchKernelGGL(sm2_table_to_r26_kernel, dim3(static_cast<unsigned>((ent + 255) / 256)), dim3(256), 0, 0,
+                           sm2r, sm2, ent);
+    }
+    if (wsm2) {
+        if (hipMalloc(&wsm2r, kWideTabWords * 4) == hipSuccess) {
+            const uint64_t ent = kWideTabWords / 16;
+            hipLaunchKernelGGL(sm2_table_to_r26_kernel, dim3(static_cast<unsigned>((ent + 255) / 256)), dim3(256), 0,
+                               0, wsm2r, wsm2, ent);
+        } else {  // no room for the R'-domain copy of the wide SM2 table: every SM2 kernel on the 8-bit ones
+            (void)hipGetLastError();
+            wsm2r = nullptr;
+        }
+    }
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        free_tables(k1, sm2, wk1, wsm2);
+        if (sm2r) (void)hipFree(sm2r);
+        if (wsm2r) (void)hipFree(wsm2r);
+        return BCOSGPU_E_HIP;
+    }
+    g_tab_sm2_26[device] = sm2r;
+    g_wtab_sm2_26[device] = wsm2r;
     g_tab_k1[device] = k1;
     g_tab_sm2[device] = sm2;
     g_wtab_k1[device] = wk1;
@@ -679,6 +730,16 @@ static int tables(const uint32_t** k1, const uint32_t** sm2, int* bits) {
     const bool wide = g_wtab_k1[dev] != nullptr;
     *k1 = wide ? g_wtab_k1[dev] : g_tab_k1[dev];
     *sm2 = wide ? g_wtab_sm2[dev] : g_tab_sm2[dev];
+    *bits = wide ? kWideBits : 8;
+    return 0;
+}
+// the SM2 comb table in fp26's R' domain: the 16-bit one when present, else the 8-bit one
+static int tables_sm2_26(const uint32_t** tab, int* bits) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BCOSGPU_E_NODEV;
+    if (!g_tab_sm2_26[dev]) return BCOSGPU_E_NODEV;
+    const bool wide = g_wtab_sm2_26[dev] != nullptr;
+    *tab = wide ? g_wtab_sm2_26[dev] : g_tab_sm2_26[dev];
     *bits = wide ? kWideBits : 8;
     return 0;
 }
@@ -911,6 +972,10 @@ __device__ __forceinline__ bool sm2_verify_lane(const fe& hash_be, const uint8_t
     return sm2_verify_rs<LDS>(hash_be, r, s, X, Y, tab, px, py, ldsx);
 }
 
+}  // namespace bcosgpu
+#include "verify_sm2_26.h"
+namespace bcosgpu {
+
 // ------------------------------------------------------------------ secp256k1 verify (known key)
 // libsecp256k1 secp256k1_ecdsa_verify as wedpr_secp256k1_verify calls it (Secp256k1Crypto.cpp:51-63):
 // pub (x, y) < p on the curve, r, s in [1, n-1], low-S (s <= n/2), e = hash mod n,
@@ -1087,6 +1152,7 @@ __global__ __launch_bounds__(256) void secp256k1_recover_kernel(const uint8_t* _
     okout[i] = ok ? 1 : 0;
 }
 
+template <bool F26>
 __global__ __launch_bounds__(256) void sm2_verify_kernel(const uint8_t* __restrict__ hash,
                                                          const uint8_t* __restrict__ sig, uint32_t stride,
                                                          uint64_t n, const uint32_t* __restrict__ tab, int tbits,
@@ -1095,7 +1161,8 @@ __global__ __launch_bounds__(256) void sm2_verify_kernel(const uint8_t* __restri
     if (i >= n) return;
     fe h, x, y;
     load_be256_aligned(h, hash + 32 * i);
-    const bool ok = sm2_verify_lane(h, sig + static_cast<uint64_t>(stride) * i, 128u, CombTab{tab, tbits}, x, y);
+    const bool ok = F26 ? sm2_verify_lane26(h, sig + static_cast<uint64_t>(stride) * i, 128u, CombTab{tab, tbits}, x, y)
+                        : sm2_verify_lane(h, sig + static_cast<uint64_t>(stride) * i, 128u, CombTab{tab, tbits}, x, y);
     if (addr) {
         uint32_t a[5] = {0, 0, 0, 0, 0};
         if (ok) sm3_address(a, x, y);
@@ -1136,7 +1203,8 @@ __global__ __launch_bounds__(256) void sig_verify_kernel(const uint8_t* __restri
             X[k] = bswap32(rp.word(k));
             Y[k] = bswap32(rp.word(8 + k));
         }
-        ok = sm2_verify_rs(h, r, s, X, Y, CombTab{tab, tbits}, x, y);
+        if constexpr (F26) ok = sm2_verify_rs26(h, r, s, X, Y, CombTab{tab, tbits}, x, y);
+        else ok = sm2_verify_rs(h, r, s, X, Y, CombTab{tab, tbits}, x, y);
     } else {
         if constexpr (F26) ok = secp256k1_verify_lane26(h, sg, pub + 64 * i, CombTab{tab, tbits});
         else ok = secp256k1_verify_lane(h, sg, pub + 64 * i, CombTab{tab, tbits});
@@ -1211,7 +1279,8 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(const uint8_t* __re
     __shared__ uint32_t ldsx_all[kLds ? 4 * 4096 : 1];
     uint32_t* ldsx = kLds ? ldsx_all + (threadIdx.x >> 6) * 4096 + (threadIdx.x & 63) : nullptr;
     if (SUITE == BCOSGPU_SUITE_SM2) {
-        ok = sm2_verify_lane<kLds>(h, sig + sa, slen, CombTab{tab, tbits}, x, y, ldsx);
+        if constexpr (F26) ok = sm2_verify_lane26<kLds>(h, sig + sa, slen, CombTab{tab, tbits}, x, y, ldsx);
+        else ok = sm2_verify_lane<kLds>(h, sig + sa, slen, CombTab{tab, tbits}, x, y, ldsx);
         if (ok) sm3_address(ad, x, y);
     } else {
         if constexpr (F26) ok = secp256k1_recover_lane26<kLds>(h, sig + sa, slen, CombTab{tab, tbits}, x, y, ldsx);
@@ -3036,8 +3105,17 @@ int launch_sm2_verify(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stri
     int bits;
     int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    hipLaunchKernelGGL(sm2_verify_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, sm2, bits,
-                       d_addr, d_ok);
+    if (g_policy.f26) {
+        const uint32_t* t26;
+        int b26;
+        rc = tables_sm2_26(&t26, &b26);
+        if (rc) return rc;
+        hipLaunchKernelGGL(sm2_verify_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, t26,
+                           b26, d_addr, d_ok);
+    } else {
+        hipLaunchKernelGGL(sm2_verify_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, sm2,
+                           bits, d_addr, d_ok);
+    }
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
@@ -3074,7 +3152,14 @@ int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, co
     int bits;
     int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    if (suite == BCOSGPU_SUITE_SM2)
+    if (suite == BCOSGPU_SUITE_SM2 && g_policy.f26) {
+        const uint32_t* t26;
+        int b26;
+        rc = tables_sm2_26(&t26, &b26);
+        if (rc) return rc;
+        hipLaunchKernelGGL((sig_verify_kernel<BCOSGPU_SUITE_SM2, true>), dim3(grid_of(n)), dim3(256), 0, st, d_pub,
+                           d_hash, d_sig, stride, n, t26, b26, d_ok);
+    } else if (suite == BCOSGPU_SUITE_SM2)
         hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SM2>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash, d_sig,
                            stride, n, sm2, bits, d_ok);
     else if (g_policy.f26)
@@ -3136,7 +3221,12 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
     const int occ = pol.occ ? pol.occ : (n >= (1ull << 17) ? 2 : 1);  // >= 2 waves per SIMD of work
 #define TXV(S, O, F, T) hipLaunchKernelGGL((tx_verify_kernel<S, O, F>), dim3(grid_of(n)), dim3(256), 0, st, d_pre, \
                                            d_pre_off, d_sig, d_sig_off, n, T, bits, d_txhash, d_sender, d_status)
-    if (suite == BCOSGPU_SUITE_SM2) {
+    if (suite == BCOSGPU_SUITE_SM2 && pol.f26) {
+        const uint32_t* t26;
+        rc = tables_sm2_26(&t26, &bits);
+        if (rc) return rc;
+        if (occ == 2) TXV(BCOSGPU_SUITE_SM2, 2, true, t26); else TXV(BCOSGPU_SUITE_SM2, 1, true, t26);
+    } else if (suite == BCOSGPU_SUITE_SM2) {
         if (occ == 2) TXV(BCOSGPU_SUITE_SM2, 2, false, sm2); else TXV(BCOSGPU_SUITE_SM2, 1, false, sm2);
     } else if (pol.f26) {
         if (occ == 2) TXV(BCOSGPU_SUITE_SECP256K1, 2, true, k1); else TXV(BCOSGPU_SUITE_SECP256K1, 1, true, k1);

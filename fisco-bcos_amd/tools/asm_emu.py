@@ -66,7 +66,18 @@ class Lane:
                 continue
             if op == "v_mad_u64_u32":
                 acc = self.get(a[4])
-                self.set(a[0], (self.get(a[2]) & M32) * (self.get(a[3]) & M32) + acc)
+                self.set(a[0], ((self.get(a[2]) & M32) * (self.get(a[3]) & M32) + acc) & M64)
+            elif op == "v_mad_i64_i32":
+                def s32(v):
+                    v &= M32
+                    return v - (1 << 32) if v >> 31 else v
+                acc = self.get(a[4]) & M64
+                acc = acc - (1 << 64) if acc >> 63 else acc
+                self.set(a[0], (s32(self.get(a[2])) * s32(self.get(a[3])) + acc) & M64)
+            elif op == "v_ashrrev_i64":
+                v = self.get(a[2]) & M64
+                v = v - (1 << 64) if v >> 63 else v
+                self.set(a[0], (v >> int(a[1], 0)) & M64)
             elif op == "v_mad_u32_u24":
                 self.set(a[0], ((self.get(a[1]) & 0xFFFFFF) * (self.get(a[2]) & 0xFFFFFF) + self.get(a[3])) & M32)
             elif op == "v_and_b32_e32":

@@ -709,6 +709,74 @@ def gen_fe26(square):
     return blk
 
 
+def gen_fp26(square):
+    """fp26_mul / fp26_sqr (fp26.h, SM2, Montgomery R = 2^286): the 19 product columns in the fixed
+    pairs v[2k:2k+1] (column k), then eleven Montgomery digits, each m = low 26 bits of its column, the
+    column's floor-carry (64-bit arithmetic shift) into the next, and m's four shifted multiply-adds
+    (+2^12 at k+2, -2^18 at k+3, -2^16 at k+8, +2^22 at k+9) as signed / unsigned v_mad; the result is
+    columns 11..20 carried into 26-bit limbs.  Physical registers because inline asm cannot name half of a
+    64-bit operand; v0..v47 are declared clobbered."""
+    name = "fp26_sqr_asm(uint32_t r[10], const uint32_t a[10])" if square else \
+        "fp26_mul_asm(uint32_t r[10], const uint32_t a[10], const uint32_t b[10])"
+    blk = Blk(name, "r = a^2 R^-1 mod p (SM2, fp26: inputs m <= 8, output m = 1)" if square else
+              "r = a b R^-1 mod p (SM2, fp26: inputs m <= 8, output m = 1)",
+              ("uint32_t d[9]; " if square else "") + "uint64_t jp, jr; uint32_t k12 = 1u << 12, kn18 = 0xfffc0000u, "
+              "kn16 = 0xffff0000u, k22 = 1u << 22;")
+    R = blk.vout("r", 10)
+    D = blk.vout("d", 9) if square else None
+    JP, JR = blk.sout("jp"), blk.sout("jr")
+    A = blk.vin("a", 10)
+    B = A if square else blk.vin("b", 10)
+    k12, kn18, kn16, k22 = (blk.sin(x) for x in ("k12", "kn18", "kn16", "k22"))
+    blk.clobbers = ["v%d" % i for i in range(48)]
+    C = [("v[%d:%d]" % (2 * k, 2 * k + 1), "v%d" % (2 * k), "v%d" % (2 * k + 1)) for k in range(21)]
+    MT = ["v42", "v43"]
+    TT = ["v[44:45]", "v[46:47]"]
+    M26, M22 = "0x3ffffff", "0x3fffff"
+    if square:
+        for i in range(9):
+            blk.emit(valu(f"v_lshlrev_b32_e32 {D[i]}, 1, {A[i]}", D[i], A[i]))
+
+    def prods(k):
+        if not square:
+            return [(A[i], B[k - i]) for i in range(10) if 0 <= k - i < 10]
+        out = [(D[i], A[k - i]) for i in range(10) if i < k - i < 10]
+        if k % 2 == 0:
+            out.append((A[k // 2], A[k // 2]))
+        return out
+
+    for k in range(19):
+        for idx, (x, y) in enumerate(prods(k)):
+            blk.emit(madj(C[k][0], JP, x, y, "0" if idx == 0 else C[k][0]))
+    started = set(range(19))
+
+    def acc_into(k, x, const, signed):
+        op = "v_mad_i64_i32" if signed else "v_mad_u64_u32"
+        src = C[k][0] if k in started else "0"
+        started.add(k)
+        blk.emit(Op(f"{op} {C[k][0]}, {JR}, {x}, {const}, {src}", [C[k][0]], [x, const] + ([] if src == "0" else [src]),
+                    cost=2, sjunk=[JR]))
+
+    for i in range(11):
+        m, t = MT[i % 2], TT[i % 2]
+        blk.emit(valu(f"v_and_b32_e32 {m}, {M26}, {C[i][1]}", m, C[i][1]))
+        blk.emit(valu(f"v_ashrrev_i64 {t}, 26, {C[i][0]}", t, C[i][0]))
+        blk.emit(valu(f"v_lshl_add_u64 {C[i + 1][0]}, {t}, 0, {C[i + 1][0]}", C[i + 1][0], t, C[i + 1][0]))
+        acc_into(i + 2, m, k12, False)
+        acc_into(i + 3, m, kn18, True)
+        acc_into(i + 8, m, kn16, True)
+        acc_into(i + 9, m, k22, False)
+    for j in range(11, 20):
+        t = TT[j % 2]
+        blk.emit(valu(f"v_and_b32_e32 {R[j - 11]}, {M26}, {C[j][1]}", R[j - 11], C[j][1]))
+        blk.emit(valu(f"v_ashrrev_i64 {t}, 26, {C[j][0]}", t, C[j][0]))
+        if j < 19:
+            blk.emit(valu(f"v_lshl_add_u64 {C[j + 1][0]}, {t}, 0, {C[j + 1][0]}", C[j + 1][0], t, C[j + 1][0]))
+        else:
+            blk.emit(mov(R[9], t.replace("v[44:45]", "v44").replace("v[46:47]", "v46")))  # c20 = the carry, < 2^23
+    return blk
+
+
 def main():
     parts = ["// fe_asm.h -- GENERATED by tools/gen_fe_asm.py; do not edit by hand.",
              "// 256-bit field primitives as single inline-asm blocks, scheduled so that every VALU read of",
@@ -719,7 +787,7 @@ def main():
     stats = []
     for g in (gen_mul512, gen_sqr512, gen_k1_reduce, lambda: gen_k1_addsub(False), lambda: gen_k1_addsub(True),
               lambda: gen_k1_shl(1), lambda: gen_k1_shl(2), lambda: gen_k1_shl(3), lambda: gen_k1_add_shl(1),
-              gen_k1_normalize, gen_mod_add, gen_mod_sub, lambda: gen_fe26(False), lambda: gen_fe26(True)):
+              gen_k1_normalize, gen_mod_add, gen_mod_sub, lambda: gen_fe26(False), lambda: gen_fe26(True), lambda: gen_fp26(False), lambda: gen_fp26(True)):
         blk = g()
         text, ninst, nops = blk.render()
         name = blk.sig.split("(")[0]

@@ -1,0 +1,9 @@
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_ecc.py tests/test_gpu_verify.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_sm2.log 2>&1
+rc=$?; tail -2 gpurun_out/pytest_sm2.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" gpurun_out/pytest_sm2.log | head -20; exit $rc; }
+for cfg in "1 2" "0 2" "1 1" "0 1"; do
+  set -- $cfg
+  BCOSGPU_K1_F26=$1 BCOSGPU_TXV_OCC=$2 timeout -k 10 200 python3 bench.py --workload c3 --steps 20 --warmup 3 --warm-seconds 1 --legs= --no-cpu-baseline --no-merkle --no-extras > gpurun_out/sm2_c3.json 2> gpurun_out/sm2_c3.err || { tail -20 gpurun_out/sm2_c3.err; exit 1; }
+  python3 -c "import json;d=json.load(open('gpurun_out/sm2_c3.json'));print('c3 f26=$1 occ=$2', round(d['value']/1e6,3), round(d['roofline']['kernel_ms'],3))"
+done

@@ -51,8 +51,9 @@ def gpu():
 
 @pytest.fixture(params=[1, 0], ids=["fe26", "fe32"])
 def k1_field(request, gpu):
-    """Runs a secp256k1 test on both point-arithmetic variants of the kernels (the 10 x 26-bit default and
-    the 8 x 32-bit one, bcosgpu_set_tx_kernel_policy's field) and restores the default."""
+    """Runs an ECC test on both point-arithmetic variants of the kernels (the 10 x 26-bit fields -- fe26 for
+    secp256k1, fp26 for SM2 -- by default, and the 8 x 32-bit ones; bcosgpu_set_tx_kernel_policy's field)
+    and restores the default."""
     gpu.set_tx_kernel_policy(field=request.param)
     yield request.param
     gpu.set_tx_kernel_policy()

@@ -156,7 +156,7 @@ def test_secp256k1_recover_random_and_edge(gpu, oracle, k1_field):
     assert want_ok.sum() > n // 3 and (~want_ok).sum() > n // 10
 
 
-def test_sm2_verify_random_and_edge(gpu, oracle):
+def test_sm2_verify_random_and_edge(gpu, oracle, k1_field):
     rng = np.random.default_rng(24)
     n = 4000
     sk = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
@@ -266,7 +266,7 @@ def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
     # secp256k1: cooperative-pair, 4-wave split, one-lane occ 1 / 2 on the 10 x 26-bit and on the
     # 8 x 32-bit point arithmetic; SM2: pair kernel, one-lane occ 1 / 2
     variants = ([(1, 1, 1, 1), (1, 1, 0, 1), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)] if suite == 0
-                else [(1, 1, 1, 1), (0, 1, 0, 1), (0, 2, 0, 1)])
+                else [(1, 1, 1, 1), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)])
     try:
         for split, occ, coop, field in variants:
             gpu.set_tx_kernel_policy(split, occ, coop, field)
