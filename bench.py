@@ -66,7 +66,8 @@ SM3_C_OPS = 2100
 PMC_GLOB = "r02_pmc_{}.json"
 KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_kernels.hip", "fisco-bcos_amd/csrc/fe_asm.h", "fisco-bcos_amd/csrc/fe.h",
               "fisco-bcos_amd/csrc/ec.h", "fisco-bcos_amd/csrc/hash_device.h", "fisco-bcos_amd/csrc/modinv.h",
-              "fisco-bcos_amd/csrc/fe26.h", "fisco-bcos_amd/csrc/ec26.h", "fisco-bcos_amd/csrc/recover26.h"]
+              "fisco-bcos_amd/csrc/fe26.h", "fisco-bcos_amd/csrc/ec26.h", "fisco-bcos_amd/csrc/recover26.h",
+              "fisco-bcos_amd/csrc/fp26.h", "fisco-bcos_amd/csrc/ecp26.h", "fisco-bcos_amd/csrc/verify_sm2_26.h"]
 
 WORKLOADS = {
     "c2": dict(suite=0, n=10_000, scaling="weak",
@@ -105,7 +106,7 @@ def _kernel_name(suite, n):
             return "tx_verify_split_kernel"
         return "tx_verify_coop26_kernel" if f26 else "tx_verify_coop_kernel"
     if suite == 1 and small and coop:
-        return "tx_verify_sm2_pair_kernel"
+        return "tx_verify_sm2_pair26_kernel" if f26 else "tx_verify_sm2_pair_kernel"
     occ = os.environ.get("BCOSGPU_TXV_OCC")
     occ = int(occ) if occ in ("1", "2") else (2 if n >= (1 << 17) else 1)
     return "tx_verify_kernel<%d,%d,%s>" % (suite, occ, "true" if f26 else "false")

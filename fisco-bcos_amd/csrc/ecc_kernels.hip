@@ -3079,6 +3079,429 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair_kernel(const uint8_
     }
 }
 
+// ------------------------------------------------------------------ SM2 pair kernel on fp26
+// tx_verify_sm2_pair_kernel with the t*P chain, the comb halves and the final check on fp26 (R' =
+// 2^286, ecp26.h); the split of each doubling / mixed addition between the pair is the same, with the
+// magnitude plan of CurveSM2x (each wave of the pair normalises the same operands, so both hold
+// identical limbs).  Exchanged elements are 5 x uint2 (raw limbs, no canonicalisation).
+struct Sm2Pair26Lds {
+    uint32_t tab[8][16][64];         // affine 1P..8P in the R' domain, canonical words
+    uint2 ex[2][2][3][5][64];        // [parity][writer role][slot][limb pair][lane]
+    uint32_t g[25][64];
+    uint32_t gh[25][64];
+    uint32_t c[8][64];
+    uint32_t addr[5][64];
+    uint32_t ok2[64];
+    uint32_t seq[4];
+};
+
+struct Pair26Ctx {
+    Sm2Pair26Lds* L;
+    int role, lane;
+    uint32_t seq;
+    int par;
+    __device__ __forceinline__ void put(int s, const fp26& a) const {
+        uint2* p = &L->ex[par][role][s][0][0] + lane;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) p[q * 64] = make_uint2(a.v[2 * q], a.v[2 * q + 1]);
+    }
+    __device__ __forceinline__ void get(int s, fp26& a) const {
+        const uint2* p = &L->ex[par][role ^ 1][s][0][0] + lane;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const uint2 w = p[q * 64];
+            a.v[2 * q] = w.x;
+            a.v[2 * q + 1] = w.y;
+        }
+    }
+    __device__ __forceinline__ void sync() {
+        ++seq;
+        __hip_atomic_store(&L->seq[role], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(&L->seq[role ^ 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < seq) {
+        }
+    }
+    __device__ __forceinline__ void next() { par ^= 1; }
+};
+
+// as pair_dbl_am3 with CurveSM2x::dbl's magnitudes (X <= 5, Y, Z <= 8 -> (2, 2, 2)):
+//   a: alpha = 3 (X - d)(X + d) (3), alpha^2 (1) | b: 4 beta (4), 8 gamma^2 (8)
+//   -> both: X3 = alpha^2 - 8 beta (2) -> a: Y3 (2) | b: Z3 = 2 Y Z (2)
+__device__ __forceinline__ void pair26_dbl(JacP26& P, Pair26Ctx& c) {
+    fp26 alpha, A2, b4, g8, X3, Y3, Z3, t, u;
+    if (c.role == 0) {
+        fp26 d;
+        fp26_sqr(d, P.Z);
+        fp26_sub<2>(t, P.X, d);
+        fp26_add(u, P.X, d);
+        fp26_mul(alpha, t, u);
+        fp26_mul_int<3>(alpha, alpha);
+        fp26_sqr(A2, alpha);
+        c.put(0, alpha);
+        c.put(1, A2);
+    } else {
+        fp26 g;
+        fp26_sqr(g, P.Y);
+        fp26_mul(b4, P.X, g);
+        fp26_mul_int<4>(b4, b4);
+        fp26_sqr(g8, g);
+        fp26_mul_int<8>(g8, g8);
+        c.put(0, b4);
+        c.put(1, g8);
+    }
+    c.sync();
+    if (c.role == 0) {
+        c.get(0, b4);
+        c.get(1, g8);
+    } else {
+        c.get(0, alpha);
+        c.get(1, A2);
+    }
+    c.next();
+    F26_SETM(alpha, 3);
+    F26_SETM(A2, 1);
+    F26_SETM(b4, 4);
+    F26_SETM(g8, 8);
+    fp26_mul_int<2>(t, b4);
+    fp26_sub<9>(X3, A2, t);
+    fp26_normalize_weak(X3);
+    if (c.role == 0) {
+        fp26_sub<3>(t, b4, X3);
+        fp26_mul(Y3, alpha, t);
+        fp26_sub<9>(Y3, Y3, g8);
+        fp26_normalize_weak(Y3);
+        c.put(0, Y3);
+    } else {
+        fp26_mul(Z3, P.Y, P.Z);
+        fp26_mul_int<2>(Z3, Z3);
+        c.put(0, Z3);
+    }
+    c.sync();
+    if (c.role == 0) c.get(0, Z3);
+    else c.get(0, Y3);
+    c.next();
+    F26_SETM(Y3, 2);
+    F26_SETM(Z3, 2);
+    fp26_copy(P.X, X3);
+    fp26_copy(P.Y, Y3);
+    fp26_copy(P.Z, Z3);
+}
+
+// as pair_madd with CurveSM2x::madd's arrangement (r = 2 rr, Z3 = 2 Z1 H): P (2, 2, <= 8), Q <= 2
+//   a: H (5), HH, Z3 (2) | b: rr (5), R2 = 4 rr^2 (4) -> a: J | b: V -> a: rr (V - X3) | b: Y1 J
+__device__ __forceinline__ void pair26_madd(JacP26& R, const JacP26& P, const AffP26& Q, Pair26Ctx& c) {
+    fp26 Z1Z1, H, HH, Z3, rr, R2, I, J, V, X3, Y3, t, u;
+    fp26_sqr(Z1Z1, P.Z);
+    if (c.role == 0) {
+        fp26_mul(u, Q.x, Z1Z1);
+        fp26_sub<3>(H, u, P.X);
+        fp26_sqr(HH, H);
+        fp26_mul(Z3, P.Z, H);
+        fp26_mul_int<2>(Z3, Z3);
+        c.put(0, H);
+        c.put(1, HH);
+        c.put(2, Z3);
+    } else {
+        fp26_mul(u, Q.y, P.Z);
+        fp26_mul(u, u, Z1Z1);
+        fp26_sub<3>(rr, u, P.Y);
+        fp26_sqr(R2, rr);
+        fp26_mul_int<4>(R2, R2);
+        c.put(0, rr);
+        c.put(1, R2);
+    }
+    c.sync();
+    if (c.role == 0) {
+        c.get(0, rr);
+        c.get(1, R2);
+    } else {
+        c.get(0, H);
+        c.get(1, HH);
+        c.get(2, Z3);
+    }
+    c.next();
+    F26_SETM(rr, 5);
+    F26_SETM(R2, 4);
+    F26_SETM(H, 5);
+    F26_SETM(HH, 1);
+    F26_SETM(Z3, 2);
+    fp26_mul_int<4>(I, HH);
+    if (c.role == 0) {
+        fp26_mul(J, H, I);
+        c.put(0, J);
+    } else {
+        fp26_mul(V, P.X, I);
+        c.put(0, V);
+    }
+    c.sync();
+    if (c.role == 0) c.get(0, V);
+    else c.get(0, J);
+    c.next();
+    F26_SETM(V, 1);
+    F26_SETM(J, 1);
+    fp26_sub<2>(X3, R2, J);
+    fp26_mul_int<2>(t, V);
+    fp26_sub<3>(X3, X3, t);
+    fp26_normalize_weak(X3);
+    if (c.role == 0) {
+        fp26_sub<3>(t, V, X3);
+        fp26_mul(u, rr, t);
+    } else {
+        fp26_mul(u, P.Y, J);
+    }
+    c.put(0, u);
+    c.sync();
+    c.get(0, t);
+    c.next();
+    F26_SETM(t, 1);
+    if (c.role == 0) fp26_sub<2>(Y3, u, t);
+    else fp26_sub<2>(Y3, t, u);
+    fp26_mul_int<2>(Y3, Y3);
+    fp26_normalize_weak(Y3);
+    const bool hz = fp26_is_zero(H) && !P.inf;
+    const bool rz = fp26_is_zero(rr);
+    JacP26 D;
+    if (hz && rz) CurveSM2x::dbl(D, P);  // P == Q (rare)
+    const bool pinf = P.inf;
+    fp26_copy(R.X, X3);
+    fp26_copy(R.Y, Y3);
+    fp26_copy(R.Z, Z3);
+    R.inf = false;
+    if (hz) {
+        if (rz) CurveSM2x::cmov(R, D, true);
+        else R.inf = true;
+    }
+    if (pinf) {
+        fp26_copy(R.X, Q.x);
+        fp26_copy(R.Y, Q.y);
+        fp26_set(R.Z, p26::ONE_R);
+        R.inf = false;
+    }
+}
+
+__device__ __forceinline__ void pair26_add_digit(JacP26& acc, Pair26Ctx& c, int d) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &c.L->tab[0][0][0] + m * (16 * 64) + c.lane;
+    AffP26 S;
+    {
+        uint32_t x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            x[k] = base[k * 64];
+            y[k] = base[(8 + k) * 64];
+        }
+        fp26_from_words(S.x, x);
+        fp26_from_words(S.y, y);
+    }
+    fp26 ny;
+    fp26_neg<2>(ny, S.y);
+    fp26_cmov(S.y, ny, d < 0);
+    fp26_normalize_weak(S.y);
+    JacP26 R;
+    pair26_madd(R, acc, S, c);
+    CurveSM2x::cmov(acc, R, d != 0);
+}
+
+// acc = k * G restricted to the 8-bit comb windows [lo, hi) of the R'-domain table
+__device__ __forceinline__ void comb_range_sm2_26(JacP26& acc, const fe& k_plain, const uint32_t* __restrict__ tab,
+                                                  int lo, int hi) {
+    fe k;
+    fe_copy(k, k_plain);
+    for (int i = 0; i < lo; ++i) shr8(k);
+    CurveSM2x::set_inf(acc);
+#pragma unroll 1
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t b = k.v[0] & 255u;
+        shr8(k);
+        AffP26 T;
+        load_affp26(T, tab + (static_cast<size_t>(i) * kCombEntries + b) * 16);
+        JacP26 S;
+        CurveSM2x::madd(S, acc, T);
+        CurveSM2x::cmov(acc, S, b != 0u);
+    }
+}
+
+__device__ __forceinline__ void pair26_store_jac(uint32_t (*dst)[64], const JacP26& P, int lane) {
+    fe X, Y, Z;
+    fp26_to_fe(X, P.X);
+    fp26_to_fe(Y, P.Y);
+    fp26_to_fe(Z, P.Z);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        dst[k][lane] = X.v[k];
+        dst[8 + k][lane] = Y.v[k];
+        dst[16 + k][lane] = Z.v[k];
+    }
+    dst[24][lane] = P.inf ? 1u : 0u;
+}
+__device__ __forceinline__ void pair26_load_jac(JacP26& P, const uint32_t (*src)[64], int lane) {
+    uint32_t x[8], y[8], z[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        x[k] = src[k][lane];
+        y[k] = src[8 + k][lane];
+        z[k] = src[16 + k][lane];
+    }
+    fp26_from_words(P.X, x);
+    fp26_from_words(P.Y, y);
+    fp26_from_words(P.Z, z);
+    P.inf = src[24][lane] != 0u;
+}
+
+__global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(const uint8_t* __restrict__ pre,
+                                                                      const uint64_t* __restrict__ pre_off,
+                                                                      const uint8_t* __restrict__ sig,
+                                                                      const uint64_t* __restrict__ sig_off,
+                                                                      uint64_t n, const uint32_t* __restrict__ tab,
+                                                                      uint8_t* __restrict__ txhash,
+                                                                      uint8_t* __restrict__ sender,
+                                                                      uint8_t* __restrict__ status) {
+    __shared__ Sm2Pair26Lds L;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
+    const bool active = i < n;
+    if (threadIdx.x < 4) L.seq[threadIdx.x] = 0u;
+    __syncthreads();
+    uint64_t sa = 0, sb = 0;
+    if (active) {
+        sa = sig_off[i];
+        sb = sig_off[i + 1];
+    }
+    const bool len_ok = active && sb - sa == 128u;
+    fe r, s, px, py;
+    uint32_t X[8], Y[8];
+    if (len_ok) {
+        ByteReader rd(sig + sa, 128);
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rd.word(k);
+        fe_from_be_words(r, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rd.word(8 + k);
+        fe_from_be_words(s, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            X[k] = bswap32(rd.word(16 + k));
+            Y[k] = bswap32(rd.word(24 + k));
+        }
+    } else {
+        fe_zero(r);
+        fe_zero(s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) X[k] = Y[k] = 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        px.v[k] = X[7 - k];
+        py.v[k] = Y[7 - k];
+    }
+    bool ok = len_ok && fe_lt_k(px, ParamP2::M) && fe_lt_k(py, ParamP2::M);
+    ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN2::M) && fe_lt_k(s, ParamN2::M);
+    fe t;
+    FieldN2::add(t, r, s);
+    ok = ok && !fe_is_zero_raw(t);
+    AffP26 P;
+    fp26_from_plain(P.x, px);
+    fp26_from_plain(P.y, py);
+    JacP26 acc;
+    if (wave <= 1) {
+        Pair26Ctx c{&L, wave, lane, 0u, 0};
+        if (wave == 0) {
+            AffP26 A[8];
+            sm2_affine_table26(A, P);
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                fe x, y;
+                fp26_to_fe(x, A[j].x);
+                fp26_to_fe(y, A[j].y);
+                lds_store_fe(L.tab[j], x, lane);
+                lds_store_fe(L.tab[j] + 8, y, lane);
+            });
+        }
+        c.sync();  // the table is in LDS
+        fe k;
+        fe_copy(k, t);
+        CurveSM2x::set_inf(acc);
+        pair26_add_digit(acc, c, static_cast<int>(k.v[7] >> 31));  // digit 64 = bit 255
+#pragma unroll 1
+        for (int w = 63; w >= 0; --w) {
+            pair26_dbl(acc, c);
+            pair26_dbl(acc, c);
+            pair26_dbl(acc, c);
+            pair26_dbl(acc, c);
+            const uint32_t top = k.v[7];
+            const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
+            const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
+            shl4(k);
+            pair26_add_digit(acc, c, d);
+        }
+    } else if (wave == 2) {
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (active) {
+            const uint64_t pa = pre_off[i], pb = pre_off[i + 1];
+            const uint32_t len = static_cast<uint32_t>(pb - pa);
+            ByteReader rd(pre + pa, len);
+            sm3_msg(rd, len, d);
+            store_digest(SM3, txhash + 32 * i, d);
+        }
+        fe h;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h.v[k] = d[7 - k];
+        uint32_t eb[8];
+        sm2_e(eb, X, Y, h);
+        fe e, cc;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e.v[k] = eb[7 - k];
+        reduce_once(e, ParamN2::M);
+        FieldN2::sub(cc, r, e);
+        lds_store_fe(L.c, cc, lane);
+        L.ok2[lane] = sm2_on_curve26(P) ? 1u : 0u;
+        uint32_t ad[5];
+        sm3_address(ad, px, py);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) L.addr[k][lane] = ad[k];
+        JacP26 G0, G1, G;
+        comb_range_sm2_26(G0, s, tab, 0, 16);
+        while (__hip_atomic_load(&L.seq[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+            __builtin_amdgcn_s_sleep(1);
+        }
+        pair26_load_jac(G1, L.gh, lane);
+        CurveSM2x::add(G, G0, G1);
+        pair26_store_jac(L.g, G, lane);
+    } else {
+        JacP26 G1;
+        comb_range_sm2_26(G1, s, tab, 16, 32);
+        pair26_store_jac(L.gh, G1, lane);
+        __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    if (wave == 0 && active) {
+        JacP26 G, Q;
+        pair26_load_jac(G, L.g, lane);
+        CurveSM2x::add(Q, G, acc);
+        ok = ok && L.ok2[lane] != 0u && !Q.inf;
+        fe cc, c2;
+        lds_load_fe(cc, L.c, lane);
+        fp26 z2, cm, rhs, dlt;
+        fp26_sqr(z2, Q.Z);
+        fp26_from_plain(cm, cc);
+        fp26_mul(rhs, cm, z2);
+        fp26_sub<3>(dlt, rhs, Q.X);
+        bool match = fp26_is_zero(dlt);
+        const uint32_t carry = fe_add_k(c2, cc, ParamN2::M);
+        if (carry == 0u && fe_lt_k(c2, ParamP2::M)) {
+            fp26_from_plain(cm, c2);
+            fp26_mul(rhs, cm, z2);
+            fp26_sub<3>(dlt, rhs, Q.X);
+            match = match || fp26_is_zero(dlt);
+        }
+        ok = ok && match;
+        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = ok ? L.addr[k][lane] : 0u;
+        status[i] = ok ? 0 : 1;
+    }
+}
+
 // ------------------------------------------------------------------ launchers
 static inline unsigned grid_of(uint64_t n) { return static_cast<unsigned>((n + 255) / 256); }
 
@@ -3209,6 +3632,13 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
         else
             hipLaunchKernelGGL(tx_verify_split_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n,
                                k1, d_txhash, d_sender, d_status);
+        return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+    }
+    if (suite == BCOSGPU_SUITE_SM2 && small && pol.coop && pol.f26) {  // the SM2 pair kernel on fp26
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || !g_tab_sm2_26[dev]) return BCOSGPU_E_NODEV;
+        hipLaunchKernelGGL(tx_verify_sm2_pair26_kernel, dim3(static_cast<unsigned>((n + 63) / 64)), dim3(256), 0, st,
+                           d_pre, d_pre_off, d_sig, d_sig_off, n, g_tab_sm2_26[dev], d_txhash, d_sender, d_status);
         return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
     }
     if (suite == BCOSGPU_SUITE_SM2 && small && pol.coop) {  // the SM2 pair kernel (8-bit comb)

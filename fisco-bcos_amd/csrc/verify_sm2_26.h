@@ -42,6 +42,20 @@ __device__ __forceinline__ void load_affp26(AffP26& T, const uint32_t* __restric
     fp26_from_words(T.y, y);
 }
 
+// y^2 == x^3 - 3x + b for P in the R' domain (P.x, P.y <= 2)
+__device__ __forceinline__ bool sm2_on_curve26(const AffP26& P) {
+    fp26 l, rr, t, b;
+    fp26_sqr(l, P.y);
+    fp26_sqr(t, P.x);
+    fp26_mul(rr, t, P.x);
+    fp26_mul_int<3>(t, P.x);
+    fp26_sub<4>(rr, rr, t);  // m 6
+    fp26_set(b, p26::B_R);
+    fp26_add(rr, rr, b);     // m 7
+    fp26_sub<8>(l, l, rr);
+    return fp26_is_zero(l);
+}
+
 // acc = k * G over a BITS-bit comb table in the R' domain
 template <int BITS>
 __device__ __forceinline__ void comb_mul_sm2_26(JacP26& acc, const fe& k_plain, const uint32_t* __restrict__ tab) {
@@ -177,18 +191,7 @@ __device__ __forceinline__ bool sm2_verify_rs26(const fe& hash_be, const fe& r, 
     AffP26 P;
     fp26_from_plain(P.x, px);
     fp26_from_plain(P.y, py);
-    {  // y^2 == x^3 - 3x + b
-        fp26 l, rr, t, b;
-        fp26_sqr(l, P.y);
-        fp26_sqr(t, P.x);
-        fp26_mul(rr, t, P.x);
-        fp26_mul_int<3>(t, P.x);
-        fp26_sub<4>(rr, rr, t);  // m 6
-        fp26_set(b, p26::B_R);
-        fp26_add(rr, rr, b);     // m 7
-        fp26_sub<8>(l, l, rr);
-        ok = ok && fp26_is_zero(l);
-    }
+    ok = ok && sm2_on_curve26(P);
     fe t;
     FieldN2::add(t, r, s);
     ok = ok && !fe_is_zero_raw(t);
