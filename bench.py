@@ -64,7 +64,9 @@ PEAK_ALU_PER_S = 3.7497e13      # full-rate 32-bit VALU (v_alignbit_b32)
 KECCAK_F_OPS = 6240
 SM3_C_OPS = 2100
 PMC_GLOB = "r02_pmc_{}.json"
-KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_kernels.hip", "fisco-bcos_amd/csrc/fe_asm.h", "fisco-bcos_amd/csrc/fe.h",
+KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_device.h", "fisco-bcos_amd/csrc/ecc_tables.hip", "fisco-bcos_amd/csrc/ecc_sig.hip",
+              "fisco-bcos_amd/csrc/ecc_txv.hip", "fisco-bcos_amd/csrc/ecc_coop.hip", "fisco-bcos_amd/csrc/ecc_pair.hip",
+              "fisco-bcos_amd/csrc/fe_asm.h", "fisco-bcos_amd/csrc/fe.h",
               "fisco-bcos_amd/csrc/ec.h", "fisco-bcos_amd/csrc/hash_device.h", "fisco-bcos_amd/csrc/modinv.h",
               "fisco-bcos_amd/csrc/fe26.h", "fisco-bcos_amd/csrc/ec26.h", "fisco-bcos_amd/csrc/recover26.h",
               "fisco-bcos_amd/csrc/fp26.h", "fisco-bcos_amd/csrc/ecp26.h", "fisco-bcos_amd/csrc/verify_sm2_26.h"]

@@ -1,0 +1,1242 @@
+// ecc_coop.hip -- small-batch secp256k1 tx verify: the 4-wave split kernel and the cooperative-pair kernels
+// (8 x 32 and fe26 point arithmetic).
+#include "ecc_device.h"
+
+namespace bcosgpu {
+
+// ------------------------------------------------------------------ split (latency) secp256k1 tx verify
+// Small batches are latency-bound: 10k txs fill 157 waves on 1,024 SIMDs, so one recovery per lane
+// leaves most of the chip idle.  Here a 256-thread workgroup owns 64 txs and its 4 waves (on the
+// CU's 4 SIMDs) run independent parts of every recovery concurrently, exchanging through LDS:
+//   phase A  wave 1: tx hash, r^-1 (safegcd), u1 = -e/r, u2 = s/r, GLV split of u2
+//            wave 2: y = sqrt(x^3 + 7), table 1R..8R, co-Z rescale -> LDS (affine on E')
+//   phase C  wave 0: k1 * R      wave 1: k2 * phi(R)   (32 radix-16 windows each, table in LDS)
+//            wave 2: u1 * G (comb)
+//   phase D  wave 0: sum on E', map to E, add the G part, affine, Keccak address, store
+// Results are bit-identical to tx_verify_kernel<0, *>.
+struct SplitLds {
+    uint32_t tab[8][16][64];  // [entry][x0..7, y0..7][lane]: conflict-free per-lane gathers
+    uint32_t zc[8][64];
+    uint32_t u1[8][64];
+    uint32_t k1[4][64];
+    uint32_t k2[4][64];
+    uint32_t flags[64];       // bit0 wave-1 checks ok, bit1 wave-2 checks ok, bit2 neg1, bit3 neg2
+    uint32_t pt[3][25][64];   // partial results: X, Y, Z, inf
+};
+
+__device__ __forceinline__ void lds_store_jac(uint32_t (*dst)[64], const Jac& P, int lane) {
+    lds_store_fe(dst, P.X, lane);
+    lds_store_fe(dst + 8, P.Y, lane);
+    lds_store_fe(dst + 16, P.Z, lane);
+    dst[24][lane] = P.inf ? 1u : 0u;
+}
+__device__ __forceinline__ void lds_load_jac(Jac& P, const uint32_t (*src)[64], int lane) {
+    lds_load_fe(P.X, src, lane);
+    lds_load_fe(P.Y, src + 8, lane);
+    lds_load_fe(P.Z, src + 16, lane);
+    P.inf = src[24][lane] != 0u;
+}
+
+// acc += (+-d) (phi ? lambda : 1) T[|d| - 1], T gathered per lane from the LDS table (on E')
+__device__ __forceinline__ void add_digit_lds(Jac& acc, const SplitLds& L, int lane, int d, bool neg, bool phi) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &L.tab[0][0][0] + m * (16 * 64) + lane;
+    Aff S;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        S.x.v[k] = base[k * 64];
+        S.y.v[k] = base[(8 + k) * 64];
+    }
+    if (phi) {
+        fe b;
+        fe_set(b, kGlvBeta);
+        FieldK1::mul(S.x, S.x, b);
+    }
+    fe ny;
+    FieldK1::neg(ny, S.y);
+    fe_cmov(S.y, ny, (d < 0) != neg);
+    Jac R;
+    CurveK1::madd(R, acc, S);
+    CurveK1::cmov(acc, R, d != 0);
+}
+
+__device__ __forceinline__ void glv_half_lds(Jac& acc, fe& k, bool neg, bool phi, const SplitLds& L, int lane) {
+    CurveK1::set_inf(acc);
+    add_digit_lds(acc, L, lane, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
+#pragma unroll 1
+    for (int i = 31; i >= 0; --i) {
+        CurveK1::dbl(acc, acc);
+        CurveK1::dbl(acc, acc);
+        CurveK1::dbl(acc, acc);
+        CurveK1::dbl(acc, acc);
+        add_digit_lds(acc, L, lane, booth_digit128(k), neg, phi);
+    }
+}
+
+// parse r, s, v of a 65-byte signature; ok = libsecp256k1 parse_compact + r, s != 0
+__device__ __forceinline__ bool parse_sig65(const uint8_t* sig, uint32_t siglen, fe& r, fe& s, uint32_t& v) {
+    if (siglen != 65u) {
+        fe_zero(r);
+        fe_zero(s);
+        v = 0;
+        return false;
+    }
+    ByteReader rd(sig, 65);
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
+    fe_from_be_words(s, w);
+    v = rd.word(16) & 0xffu;
+    return v <= 3u && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, ParamN1::M);
+}
+
+__global__ __launch_bounds__(256, 1) void tx_verify_split_kernel(const uint8_t* __restrict__ pre,
+                                                                 const uint64_t* __restrict__ pre_off,
+                                                                 const uint8_t* __restrict__ sig,
+                                                                 const uint64_t* __restrict__ sig_off, uint64_t n,
+                                                                 const uint32_t* __restrict__ tab,
+                                                                 uint8_t* __restrict__ txhash,
+                                                                 uint8_t* __restrict__ sender,
+                                                                 uint8_t* __restrict__ status) {
+    __shared__ SplitLds L;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
+    const bool active = i < n;
+    uint64_t sa = 0, sb = 0;
+    if (active) {
+        sa = sig_off[i];
+        sb = sig_off[i + 1];
+    }
+    const uint32_t slen = (sb - sa) > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(sb - sa);
+    // ---------------------------------------------------------------- phase A
+    if (wave == 1) {
+        if (active) {
+            const uint64_t a = pre_off[i], b = pre_off[i + 1];
+            const uint32_t len = static_cast<uint32_t>(b - a);
+            ByteReader rd(pre + a, len);
+            uint32_t d[8];
+            keccak256_msg(rd, len, d);
+            store_digest(KECCAK256, txhash + 32 * i, d);
+            fe e, r, s;
+            uint32_t v;
+            fe_from_be_words(e, d);
+            reduce_once(e, ParamN1::M);
+            const bool ok = parse_sig65(sig + sa, slen, r, s, v);
+            if (!ok) {
+                fe_zero(r);
+                r.v[0] = 1;
+                fe_zero(s);
+            }
+            fe rm, rinv, u1, u2, k1, k2;
+            FieldN1::from_plain(rm, r);
+            FieldInv<FieldN1>::inv(rinv, rm);
+            FieldN1::mul(u1, e, rinv);
+            FieldN1::neg(u1, u1);
+            FieldN1::mul(u2, s, rinv);
+            bool neg1, neg2;
+            glv_split(k1, neg1, k2, neg2, u2);
+            lds_store_fe(L.u1, u1, lane);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                L.k1[k][lane] = k1.v[k];
+                L.k2[k][lane] = k2.v[k];
+            }
+            L.flags[lane] = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
+        }
+    } else if (wave == 2) {
+        if (active) {
+            fe r, s;
+            uint32_t v;
+            bool ok = parse_sig65(sig + sa, slen, r, s, v);
+            fe x;
+            fe_copy(x, r);
+            if (v & 2u) {
+                ok = ok && fe_lt_k(r, kK1PminusN);
+                fe_add_k(x, r, ParamN1::M);
+            }
+            fe rhs, y, t, seven;
+            FieldK1::sqr(t, x);
+            FieldK1::mul(rhs, t, x);
+            fe_zero(seven);
+            seven.v[0] = 7;
+            FieldK1::add(rhs, rhs, seven);
+            FieldK1::sqrt_cand(y, rhs);
+            FieldK1::sqr(t, y);
+            ok = ok && FieldK1::eq(t, rhs);
+            FieldK1::normalize(y);
+            fe ny;
+            FieldK1::neg(ny, y);
+            FieldK1::normalize(ny);
+            fe_cmov(y, ny, (y.v[0] & 1u) != (v & 1u));
+            Aff R, A[8];
+            fe_copy(R.x, x);
+            fe_copy(R.y, y);
+            fe Zc;
+            {
+                Jac T[8];
+                multiples8<CurveK1>(T, R);
+                coz_table_k1(A, Zc, T);
+            }
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                lds_store_fe(L.tab[j], A[j].x, lane);
+                lds_store_fe(L.tab[j] + 8, A[j].y, lane);
+            });
+            lds_store_fe(L.zc, Zc, lane);
+            L.pt[2][24][lane] = ok ? 2u : 0u;  // wave-2 verdict travels in a scratch slot until phase C
+        }
+    }
+    __syncthreads();
+    // ---------------------------------------------------------------- phase C
+    uint32_t flags = 0;
+    if (active) flags = L.flags[lane] | L.pt[2][24][lane];
+    __syncthreads();
+    if (wave <= 1) {
+        if (active) {
+            fe k;
+            fe_zero(k);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) k.v[q] = wave == 0 ? L.k1[q][lane] : L.k2[q][lane];
+            const bool neg = wave == 0 ? (flags & 4u) != 0 : (flags & 8u) != 0;
+            Jac P;
+            glv_half_lds(P, k, neg, wave == 1, L, lane);
+            lds_store_jac(L.pt[wave], P, lane);
+        }
+    } else if (wave == 2) {
+        if (active) {
+            fe u1;
+            lds_load_fe(u1, L.u1, lane);
+            Jac PG;
+            comb_mul<CurveK1, 8>(PG, u1, tab);
+            lds_store_jac(L.pt[2], PG, lane);
+        }
+    }
+    __syncthreads();
+    // ---------------------------------------------------------------- phase D
+    if (wave == 0 && active) {
+        Jac P0, P1, PG, Q, R;
+        lds_load_jac(P0, L.pt[0], lane);
+        lds_load_jac(P1, L.pt[1], lane);
+        lds_load_jac(PG, L.pt[2], lane);
+        fe Zc;
+        lds_load_fe(Zc, L.zc, lane);
+        CurveK1::add(Q, P0, P1);  // on E'
+        FieldK1::mul(Q.Z, Q.Z, Zc);  // -> E
+        CurveK1::add(R, Q, PG);
+        const bool ok = (flags & 3u) == 3u && !R.inf;
+        Aff A;
+        CurveK1::to_aff(A, R);
+        FieldK1::normalize(A.x);
+        FieldK1::normalize(A.y);
+        uint32_t ad[5] = {0, 0, 0, 0, 0};
+        if (ok) keccak_address(ad, A.x, A.y);
+        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = ad[k];
+        status[i] = ok ? 0 : 1;
+    }
+}
+
+// ------------------------------------------------------------------ cooperative (latency) secp256k1 tx verify
+// A lone wave on a SIMD issues a Comba step only every ~15 cycles and a 64-bit-result op every ~10
+// (profiles/r01_mulbench.json), so C2's one-wave-per-SIMD batches are bound by the length of the
+// serial point-operation chain, not by the SIMD.  Here the two GLV halves each run on a PAIR of
+// waves that split every doubling and mixed addition by dependency level and trade intermediate
+// field elements through LDS:
+//   dbl  (3M + 4S, depth 2): a: A = X^2, F = (3A)^2, Z3 = 2 Y Z | b: B = Y^2, D = 4 X B, 8 B^2
+//                            -> both: X3, Y3 = E (D - X3) - 8C        4 instead of 7, one barrier
+//   madd (7M + 4S):          a: Z1Z1, U2, HH, Z3 | b: Z1Z1, S2', S2, rr^2 -> a: J | b: V
+//                            -> a: rr (V - X3) | b: Y J        6 instead of 11
+// Both waves of a pair hold the whole point after every operation (they compute bit-identical
+// values), so the four waves run the same barrier schedule.  Phase A needs no square root before
+// the table (the R chain runs on an isomorphic curve, see phase A), so the hash, r^-1, the R table,
+// the square root and the comb windows of u1*G run side by side on the four waves, and phase C is
+// the two cooperative GLV chains only.  Bit-identical to tx_verify_kernel<0, *>.
+#ifdef BCOSGPU_COOP_TIMING  // tools/coopbench.hip: phase timestamps of workgroup 0
+__device__ uint64_t g_coop_t[4][8];
+__device__ uint64_t g_dbl_t[4][8];
+#define DBL_T(k) \
+    if (c.probe && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][k] = clock64()
+#define COOP_T(k) \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_coop_t[threadIdx.x >> 6][k] = clock64()
+#else
+#define COOP_T(k) \
+    do {          \
+    } while (0)
+#define DBL_T(k) \
+    do {         \
+    } while (0)
+#endif
+struct CoopLds {
+    uint32_t tab[8][16][64];          // co-Z table on E': [entry][x0..7, y0..7][lane]
+    uint32_t zc[8][64];
+    uint32_t k[2][4][64];             // GLV halves
+    uint32_t flags[64];               // bit0 scalars ok, bit1 R ok, bit2 neg1, bit3 neg2
+    uint4 ex[2][2][6][2][64];         // [chain][writer role][slot][word quad][lane]; madd: 0-2 exchange 0, 3: 1, 4: 2; dbl: 0-2 | 3-5
+    uint32_t tabphx[8][8][64];        // beta * x of the table entries (chain 1's phi(R) table)
+    uint32_t pt[5][25][64];           // chain results 0/1, G partials 2..4 (X, Y, Z, inf)
+    uint32_t xe[8][64];               // e = H(m) mod n (wave 3 -> waves 0, 1)
+    uint32_t xrinv[8][64];            // r^-1, Montgomery form (wave 0 -> waves 1, 3)
+    uint32_t ys[8][64];               // y of R with v's parity (wave 2 -> phase D)
+    uint32_t rflag[64];               // R verdict (wave 2)
+    uint32_t post[2];                 // phase-A hand-off flags: 0 r^-1 ready, 1 e ready
+};
+
+// One-way hand-offs between waves inside phase A: the producer writes its per-lane values, then
+// releases the flag; the consumer acquires it.  Workgroup scope, so these are LDS-only fences.
+__device__ __forceinline__ void coop_post(uint32_t* f) {
+    __hip_atomic_store(f, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void coop_wait(uint32_t* f) {
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(1);
+}
+
+struct CoopCtx {
+    CoopLds* L;
+    int chain, role, lane;
+    bool probe;  // BCOSGPU_COOP_TIMING: stamp the doubling phases (workgroup 0, one doubling)
+    // An exchange slot is rewritten only after the barrier that follows the partner's read of it,
+    // so one slot per (exchange, field element) suffices across consecutive operations.
+    // Layout [quad][lane] of uint4: one fe is two conflict-free ds_write_b128 / ds_read_b128.
+    __device__ __forceinline__ uint4* slot(int x, int r, int f) const {
+        return &L->ex[chain][r][x == 0 ? f : 2 + x][0][0] + lane;
+    }
+    __device__ __forceinline__ void put(int x, int f, const fe& a) const {
+        uint4* p = slot(x, role, f);
+        p[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+        p[64] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+    }
+    __device__ __forceinline__ void puts(int s, const fe& a) const {  // raw slot index 0..5
+        uint4* p = &L->ex[chain][role][s][0][0] + lane;
+        p[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+        p[64] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+    }
+    __device__ __forceinline__ void gets(int s, fe& a) const {
+        const uint4* p = &L->ex[chain][role ^ 1][s][0][0] + lane;
+        const uint4 q0 = p[0], q1 = p[64];
+        a.v[0] = q0.x; a.v[1] = q0.y; a.v[2] = q0.z; a.v[3] = q0.w;
+        a.v[4] = q1.x; a.v[5] = q1.y; a.v[6] = q1.z; a.v[7] = q1.w;
+    }
+    __device__ __forceinline__ void get(int x, int f, fe& a) const {  // the partner's value
+        const uint4* p = slot(x, role ^ 1, f);
+        const uint4 q0 = p[0], q1 = p[64];
+        a.v[0] = q0.x; a.v[1] = q0.y; a.v[2] = q0.z; a.v[3] = q0.w;
+        a.v[4] = q1.x; a.v[5] = q1.y; a.v[6] = q1.z; a.v[7] = q1.w;
+    }
+};
+
+// P = 2 P (a = 0, dbl-2009-l with D = 4 X B), P replicated on both waves of the pair; ONE exchange:
+//   a: A = X^2, E = 3A, F = E^2, Z3 = 2 Y Z | b: B = Y^2, D = 4 X B, C = B^2, C8 = 8 C
+//   -> both: X3 = F - 2D, Y3 = E (D - X3) - C8
+// The shifted passes (shl<k>, mul3) replace ten field additions.  S0 is the exchange buffer: slots
+// 0-2 (shared with coop_madd's exchange 0) or 3-5 (3, 4 shared with its exchanges 1, 2).  The four
+// doublings of a window use 0, 3, 0, 3, so a slot is rewritten only after the barrier that follows
+// the partner's last read of it (the madd rewrites 0-2 before its first barrier, two doublings after
+// the last read of buffer 0, and 3/4 only after its first/second barrier).
+template <int S0>
+__device__ __forceinline__ void coop_dbl(Jac& P, const CoopCtx& c) {
+    fe E, F, D, C8, Z3, X3, Y3, t;
+    DBL_T(0);
+    if (c.role == 0) {
+        fe A;
+        FieldK1::sqr(A, P.X);
+        FieldK1::mul3(E, A);
+        FieldK1::sqr(F, E);
+        c.puts(S0, E);
+        c.puts(S0 + 1, F);
+        FieldK1::mul(Z3, P.Y, P.Z);
+        FieldK1::template shl<1>(Z3, Z3);
+        c.puts(S0 + 2, Z3);
+    } else {
+        fe B, C;
+        FieldK1::sqr(B, P.Y);
+        FieldK1::mul(D, P.X, B);
+        FieldK1::template shl<2>(D, D);
+        c.puts(S0, D);
+        FieldK1::sqr(C, B);
+        FieldK1::template shl<3>(C8, C);
+        c.puts(S0 + 1, C8);
+    }
+    DBL_T(1);
+    __syncthreads();
+    DBL_T(2);
+    if (c.role == 0) {
+        c.gets(S0, D);
+        c.gets(S0 + 1, C8);
+    } else {
+        c.gets(S0, E);
+        c.gets(S0 + 1, F);
+        c.gets(S0 + 2, Z3);
+    }
+    FieldK1::template shl<1>(t, D);
+    FieldK1::sub(X3, F, t);
+    FieldK1::sub(t, D, X3);
+    FieldK1::mul(Y3, E, t);
+    FieldK1::sub(Y3, Y3, C8);
+    DBL_T(3);
+    fe_copy(P.X, X3);
+    fe_copy(P.Y, Y3);
+    fe_copy(P.Z, Z3);
+    DBL_T(4);
+}
+
+// P = P + Q (madd-2007-bl with the complete-addition special cases of CurveK1::madd), Q affine.
+__device__ __forceinline__ void coop_madd(Jac& R, const Jac& P, const Aff& Q, const CoopCtx& c) {
+    fe Z1Z1, H, HH, Z3, rr, R2, I, J, V, X3, Y3, t, u;
+    FieldK1::sqr(Z1Z1, P.Z);
+    if (c.role == 0) {
+        FieldK1::mul(u, Q.x, Z1Z1);       // U2
+        FieldK1::sub(H, u, P.X);
+        FieldK1::sqr(HH, H);
+        FieldK1::add(t, P.Z, H);
+        FieldK1::sqr(Z3, t);
+        FieldK1::sub(Z3, Z3, Z1Z1);
+        FieldK1::sub(Z3, Z3, HH);
+        c.put(0, 0, H);
+        c.put(0, 1, HH);
+        c.put(0, 2, Z3);
+    } else {
+        FieldK1::mul(u, Q.y, P.Z);
+        FieldK1::mul(u, u, Z1Z1);         // S2
+        FieldK1::sub(rr, u, P.Y);
+        FieldK1::template shl<1>(rr, rr);
+        FieldK1::sqr(R2, rr);
+        c.put(0, 0, rr);
+        c.put(0, 1, R2);
+    }
+    __syncthreads();
+    if (c.role == 0) {
+        c.get(0, 0, rr);
+        c.get(0, 1, R2);
+    } else {
+        c.get(0, 0, H);
+        c.get(0, 1, HH);
+        c.get(0, 2, Z3);
+    }
+    FieldK1::template shl<2>(I, HH);
+    if (c.role == 0) {
+        FieldK1::mul(J, H, I);
+        c.put(1, 0, J);
+    } else {
+        FieldK1::mul(V, P.X, I);
+        c.put(1, 0, V);
+    }
+    __syncthreads();
+    if (c.role == 0) c.get(1, 0, V);
+    else c.get(1, 0, J);
+    FieldK1::sub(X3, R2, J);
+    FieldK1::template shl<1>(t, V);
+    FieldK1::sub(X3, X3, t);
+    if (c.role == 0) {
+        FieldK1::sub(t, V, X3);
+        FieldK1::mul(u, rr, t);           // rr (V - X3)
+        c.put(2, 0, u);
+    } else {
+        FieldK1::mul(u, P.Y, J);
+        FieldK1::template shl<1>(u, u);   // 2 Y J
+        c.put(2, 0, u);
+    }
+    __syncthreads();
+    if (c.role == 0) {
+        c.get(2, 0, t);
+        FieldK1::sub(Y3, u, t);
+    } else {
+        c.get(2, 0, t);
+        FieldK1::sub(Y3, t, u);
+    }
+    // special cases, as CurveK1::madd (computed identically on both waves, no barriers)
+    const bool hz = FieldK1::is_zero(H) && !P.inf;
+    const bool rz = FieldK1::is_zero(rr);
+    Jac D;
+    if (hz && rz) CurveK1::dbl(D, P);  // P == Q (rare)
+    const bool pinf = P.inf;
+    fe_copy(R.X, X3);
+    fe_copy(R.Y, Y3);
+    fe_copy(R.Z, Z3);
+    R.inf = false;
+    if (hz) {
+        if (rz) CurveK1::cmov(R, D, true);
+        else R.inf = true;
+    }
+    if (pinf) {
+        fe_copy(R.X, Q.x);
+        fe_copy(R.Y, Q.y);
+        FieldK1::set_one(R.Z);
+        R.inf = false;
+    }
+}
+
+__device__ __forceinline__ void coop_add_digit(Jac& acc, const CoopCtx& c, int d, bool neg, bool phi) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &c.L->tab[0][0][0] + m * (16 * 64) + c.lane;
+    const uint32_t* bx = phi ? &c.L->tabphx[0][0][0] + m * (8 * 64) + c.lane : base;
+    Aff S;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        S.x.v[k] = bx[k * 64];
+        S.y.v[k] = base[(8 + k) * 64];
+    }
+    fe ny;
+    FieldK1::neg(ny, S.y);
+    fe_cmov(S.y, ny, (d < 0) != neg);
+    Jac R;
+    coop_madd(R, acc, S, c);
+    CurveK1::cmov(acc, R, d != 0);
+}
+
+// acc = u1 * G restricted to comb windows [lo, hi)
+__device__ __forceinline__ void comb_range_k1(Jac& acc, const fe& k_plain, const uint32_t* __restrict__ tab, int lo, int hi) {
+    fe k;
+    fe_copy(k, k_plain);
+    for (int i = 0; i < lo; ++i) shr8(k);
+    CurveK1::set_inf(acc);
+#pragma unroll 1
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t b = k.v[0] & 255u;
+        shr8(k);
+        const uint4* e = reinterpret_cast<const uint4*>(tab + (static_cast<size_t>(i) * kCombEntries + b) * 16);
+        const uint4 q0 = e[0], q1 = e[1], q2 = e[2], q3 = e[3];
+        Aff T;
+        T.x.v[0] = q0.x; T.x.v[1] = q0.y; T.x.v[2] = q0.z; T.x.v[3] = q0.w;
+        T.x.v[4] = q1.x; T.x.v[5] = q1.y; T.x.v[6] = q1.z; T.x.v[7] = q1.w;
+        T.y.v[0] = q2.x; T.y.v[1] = q2.y; T.y.v[2] = q2.z; T.y.v[3] = q2.w;
+        T.y.v[4] = q3.x; T.y.v[5] = q3.y; T.y.v[6] = q3.z; T.y.v[7] = q3.w;
+        Jac S;
+        CurveK1::madd(S, acc, T);
+        CurveK1::cmov(acc, S, b != 0u);
+    }
+}
+
+__device__ __forceinline__ void coop_store_jac(uint32_t (*dst)[64], const Jac& P, int lane) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        dst[k][lane] = P.X.v[k];
+        dst[8 + k][lane] = P.Y.v[k];
+        dst[16 + k][lane] = P.Z.v[k];
+    }
+    dst[24][lane] = P.inf ? 1u : 0u;
+}
+__device__ __forceinline__ void coop_load_jac(Jac& P, const uint32_t (*src)[64], int lane) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        P.X.v[k] = src[k][lane];
+        P.Y.v[k] = src[8 + k][lane];
+        P.Z.v[k] = src[16 + k][lane];
+    }
+    P.inf = src[24][lane] != 0u;
+}
+
+__global__ __launch_bounds__(256, 1) void tx_verify_coop_kernel(const uint8_t* __restrict__ pre,
+                                                                const uint64_t* __restrict__ pre_off,
+                                                                const uint8_t* __restrict__ sig,
+                                                                const uint64_t* __restrict__ sig_off, uint64_t n,
+                                                                const uint32_t* __restrict__ tab,
+                                                                uint8_t* __restrict__ txhash,
+                                                                uint8_t* __restrict__ sender,
+                                                                uint8_t* __restrict__ status) {
+    __shared__ CoopLds L;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
+    const bool active = i < n;
+    COOP_T(0);
+    uint64_t sa = 0, sb = 0, pa = 0, pb = 0;
+    if (active) {
+        sa = sig_off[i];
+        sb = sig_off[i + 1];
+        pa = pre_off[i];
+        pb = pre_off[i + 1];
+    }
+    const uint32_t slen = (sb - sa) > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(sb - sa);
+    if (threadIdx.x == 0) {
+        L.post[0] = 0u;
+        L.post[1] = 0u;
+    }
+    __syncthreads();
+    // ---------------------------------------------------------------- phase A
+    // R = (x, y) is needed through y only at the very end: the R chain runs on the isomorphic curve
+    // E_w: Y^2 = X^3 + 7 w^3 (w = x^3 + 7), where R' = (w x, w^2) needs no square root, and a point
+    // (X, Y, Z) of E_w is (X, Y, Z y) on E.  So the square root runs beside the table instead of
+    // before it.  Schedule: wave 0 inverts r, wave 3 hashes (they swap r^-1 and e through LDS flags),
+    // wave 1 builds the R' table and then the GLV split, wave 2 takes the square root; the comb
+    // windows of u1 * G go to waves 0 and 3 and the tail of wave 1.
+    fe r, s;
+    uint32_t v = 0;
+    bool ok = false;
+    if (active) ok = parse_sig65(sig + sa, slen, r, s, v);
+    else { fe_zero(r); fe_zero(s); }
+    if (wave == 1 || wave == 2) {
+        fe x, rhs, t, seven;
+        fe_copy(x, r);
+        bool okr = ok;
+        if (v & 2u) {
+            okr = okr && fe_lt_k(r, kK1PminusN);
+            fe_add_k(x, r, ParamN1::M);
+        }
+        FieldK1::sqr(t, x);
+        FieldK1::mul(rhs, t, x);
+        fe_zero(seven);
+        seven.v[0] = 7;
+        FieldK1::add(rhs, rhs, seven);  // w
+        if (wave == 2) {
+            fe y;
+            FieldK1::sqrt_cand(y, rhs);
+            FieldK1::sqr(t, y);
+            okr = okr && FieldK1::eq(t, rhs);
+            FieldK1::normalize(y);
+            fe ny;
+            FieldK1::neg(ny, y);
+            FieldK1::normalize(ny);
+            fe_cmov(y, ny, (y.v[0] & 1u) != (v & 1u));
+            lds_store_fe(L.ys, y, lane);
+            L.rflag[lane] = okr ? 2u : 0u;
+            COOP_T(6);
+        } else {
+            Aff R, A[8];
+            FieldK1::mul(R.x, rhs, x);  // w x
+            FieldK1::sqr(R.y, rhs);     // w^2
+            fe Zc;
+            {
+                Jac T[8];
+                multiples8<CurveK1>(T, R);
+                coz_table_k1(A, Zc, T);
+            }
+            fe beta;
+            fe_set(beta, kGlvBeta);
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                lds_store_fe(L.tab[j], A[j].x, lane);
+                lds_store_fe(L.tab[j] + 8, A[j].y, lane);
+                fe bx;
+                FieldK1::mul(bx, A[j].x, beta);
+                lds_store_fe(L.tabphx[j], bx, lane);
+            });
+            lds_store_fe(L.zc, Zc, lane);
+            COOP_T(6);
+        }
+    }
+    if (!ok) {  // scalars of a rejected signature: any well-defined values (the verdict is already 1)
+        fe_zero(r);
+        r.v[0] = 1;
+        fe_zero(s);
+    }
+    if (wave == 3) {
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (active) {
+            const uint32_t len = static_cast<uint32_t>(pb - pa);
+            ByteReader rd(pre + pa, len);
+            keccak256_msg(rd, len, d);
+            store_digest(KECCAK256, txhash + 32 * i, d);
+        }
+        fe e;
+        fe_from_be_words(e, d);
+        reduce_once(e, ParamN1::M);
+        lds_store_fe(L.xe, e, lane);
+        coop_post(&L.post[1]);
+        COOP_T(7);
+    } else if (wave == 0) {
+        fe rm, rinv;
+        FieldN1::from_plain(rm, r);
+        FieldInv<FieldN1>::inv(rinv, rm);
+        lds_store_fe(L.xrinv, rinv, lane);
+        coop_post(&L.post[0]);
+        COOP_T(7);
+    }
+    if (wave != 2) {
+        coop_wait(&L.post[0]);
+        coop_wait(&L.post[1]);
+        fe e, rinv, u1;
+        lds_load_fe(e, L.xe, lane);
+        lds_load_fe(rinv, L.xrinv, lane);
+        FieldN1::mul(u1, e, rinv);
+        FieldN1::neg(u1, u1);
+        if (wave == 1) {
+            fe u2, k1, k2;
+            FieldN1::mul(u2, s, rinv);
+            bool neg1, neg2;
+            glv_split(k1, neg1, k2, neg2, u2);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                L.k[0][q][lane] = k1.v[q];
+                L.k[1][q][lane] = k2.v[q];
+            }
+            L.flags[lane] = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
+        }
+        // comb windows of u1 * G: wave 0 [0, kCombW0), wave 3 [kCombW0, kCombW1), wave 1 [kCombW1, 32)
+        constexpr int kCombW0 = 12, kCombW1 = 24;
+        Jac G;
+        const int lo = wave == 0 ? 0 : wave == 3 ? kCombW0 : kCombW1;
+        const int hi = wave == 0 ? kCombW0 : wave == 3 ? kCombW1 : 32;
+        comb_range_k1(G, u1, tab, lo, hi);
+        coop_store_jac(L.pt[wave == 0 ? 2 : wave == 3 ? 3 : 4], G, lane);
+    }
+    COOP_T(1);
+    __syncthreads();
+    // ---------------------------------------------------------------- phase C: two cooperative GLV chains
+    const uint32_t flags = L.flags[lane] | L.rflag[lane];
+    CoopCtx c{&L, wave >> 1, wave & 1, lane, false};
+    fe k;
+    fe_zero(k);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) k.v[q] = L.k[c.chain][q][lane];
+    const bool neg = c.chain == 0 ? (flags & 4u) != 0 : (flags & 8u) != 0;
+    const bool phi = c.chain == 1;
+    Jac acc;
+    CurveK1::set_inf(acc);
+    coop_add_digit(acc, c, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
+#pragma unroll 1
+    for (int w = 31; w >= 0; --w) {
+        coop_dbl<0>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+        c.probe = blockIdx.x == 0 && w == 20;
+#endif
+        coop_dbl<3>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+        c.probe = false;
+#endif
+        coop_dbl<0>(acc, c);
+        coop_dbl<3>(acc, c);
+        coop_add_digit(acc, c, booth_digit128(k), neg, phi);
+    }
+    COOP_T(2);
+    if (c.role == 0) coop_store_jac(L.pt[c.chain], acc, lane);
+    __syncthreads();
+    // ---------------------------------------------------------------- phase D
+    if (wave == 1) {  // G part: partials 0 + 1 + 2
+        Jac G0, G1, T, U;
+        coop_load_jac(G0, L.pt[2], lane);
+        coop_load_jac(G1, L.pt[3], lane);
+        CurveK1::add(T, G0, G1);
+        coop_load_jac(G0, L.pt[4], lane);
+        CurveK1::add(U, T, G0);
+        coop_store_jac(L.pt[2], U, lane);
+    } else if (wave == 0) {  // R part: co-Z curve -> E_w (Z * Zc) -> E (Z * y)
+        Jac P0, P1, Q;
+        coop_load_jac(P0, L.pt[0], lane);
+        coop_load_jac(P1, L.pt[1], lane);
+        fe Zc, y;
+        lds_load_fe(Zc, L.zc, lane);
+        lds_load_fe(y, L.ys, lane);
+        CurveK1::add(Q, P0, P1);
+        FieldK1::mul(Zc, Zc, y);
+        FieldK1::mul(Q.Z, Q.Z, Zc);
+        coop_store_jac(L.pt[0], Q, lane);
+    }
+    __syncthreads();
+    if (wave == 0 && active) {
+        Jac Q, G, R;
+        coop_load_jac(Q, L.pt[0], lane);
+        coop_load_jac(G, L.pt[2], lane);
+        CurveK1::add(R, Q, G);
+        const bool ok = (flags & 3u) == 3u && !R.inf;
+        Aff A;
+        COOP_T(4);
+        CurveK1::to_aff(A, R);
+        COOP_T(5);
+        FieldK1::normalize(A.x);
+        FieldK1::normalize(A.y);
+        uint32_t ad[5] = {0, 0, 0, 0, 0};
+        if (ok) keccak_address(ad, A.x, A.y);
+        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) o[q] = ad[q];
+        status[i] = ok ? 0 : 1;
+    }
+    COOP_T(3);
+}
+
+// ------------------------------------------------------------------ cooperative kernel on fe26
+// tx_verify_coop_kernel with the curve work of phases A and C on the 10 x 26-bit field (fe26.h): the
+// same schedule, the same wave roles and the same pair split of every doubling and mixed addition, but
+// a lone wave (one per SIMD here) no longer waits on carry chains: its field additions are independent
+// limb adds and its multiplies are two interleaved mad chains.  Field elements cross between the two
+// waves of a pair as their raw limbs (magnitudes travel with them, as the formulas state); the tables
+// and phase results in LDS stay canonical 8-word values, so phase D is tx_verify_coop_kernel's.
+// Bit-identical to tx_verify_kernel<0, *>.
+struct Coop26Lds {
+    uint32_t tab[8][16][64];          // co-Z table on E', canonical words: [entry][x0..7, y0..7][lane]
+    uint32_t zc[8][64];
+    uint32_t k[2][4][64];             // GLV halves
+    uint32_t flags[64];               // bit0 scalars ok, bit1 R ok, bit2 neg1, bit3 neg2
+    uint2 ex[2][2][6][5][64];         // [chain][writer role][slot][limb pair][lane]: one fe26 = 5 ds_write_b64
+    uint32_t tabphx[8][8][64];        // beta * x of the table entries
+    uint32_t pt[5][25][64];           // chain results 0/1, G partials 2..4 (canonical X, Y, Z, inf)
+    uint32_t xe[8][64];
+    uint32_t xrinv[8][64];
+    uint32_t ys[8][64];
+    uint32_t rflag[64];
+    uint32_t post[2];
+};
+
+struct Coop26Ctx {
+    Coop26Lds* L;
+    int chain, role, lane;
+    bool probe;  // BCOSGPU_COOP_TIMING
+    __device__ __forceinline__ void puts(int s, const fe26& a) const {
+        uint2* p = &L->ex[chain][role][s][0][0] + lane;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) p[q * 64] = make_uint2(a.v[2 * q], a.v[2 * q + 1]);
+    }
+    __device__ __forceinline__ void gets(int s, fe26& a) const {
+        const uint2* p = &L->ex[chain][role ^ 1][s][0][0] + lane;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const uint2 w = p[q * 64];
+            a.v[2 * q] = w.x;
+            a.v[2 * q + 1] = w.y;
+        }
+    }
+};
+
+// as coop_dbl (slot buffers 0-2 / 3-5 alternate the same way); magnitudes as CurveK1x::dbl:
+//   a: A = X^2, E = 3A (3), F = E^2, Z3 = 2 Y Z (2) | b: B = Y^2, D = 4 X B (4), C8 = 8 B^2 (8)
+//   -> both: X3 = F - 2D (10), Y3 = E (D - X3) - C8 (10)
+template <int S0>
+__device__ __forceinline__ void coop26_dbl(Jac26& P, const Coop26Ctx& c) {
+    fe26 E, F, D, C8, Z3, X3, Y3, t;
+    DBL_T(0);
+    if (c.role == 0) {
+        fe26 A;
+        fe26_sqr(A, P.X);
+        fe26_mul_int<3>(E, A);
+        fe26_sqr(F, E);
+        c.puts(S0, E);
+        c.puts(S0 + 1, F);
+        fe26_mul(Z3, P.Y, P.Z);
+        fe26_mul_int<2>(Z3, Z3);
+        c.puts(S0 + 2, Z3);
+    } else {
+        fe26 B, C;
+        fe26_sqr(B, P.Y);
+        fe26_mul(D, P.X, B);
+        fe26_mul_int<4>(D, D);
+        c.puts(S0, D);
+        fe26_sqr(C, B);
+        fe26_mul_int<8>(C8, C);
+        c.puts(S0 + 1, C8);
+    }
+    DBL_T(1);
+    __syncthreads();
+    DBL_T(2);
+    if (c.role == 0) {
+        c.gets(S0, D);
+        c.gets(S0 + 1, C8);
+    } else {
+        c.gets(S0, E);
+        c.gets(S0 + 1, F);
+        c.gets(S0 + 2, Z3);
+    }
+    fe26_mul_int<2>(t, D);
+    fe26_sub<9>(X3, F, t);
+    fe26_sub<11>(t, D, X3);
+    fe26_mul(Y3, E, t);
+    fe26_sub<9>(Y3, Y3, C8);
+    DBL_T(3);
+    fe26_copy(P.X, X3);
+    fe26_copy(P.Y, Y3);
+    fe26_copy(P.Z, Z3);
+    DBL_T(4);
+}
+
+// as coop_madd, with CurveK1x::madd's arrangement (r = 2 rr, Z3 = 2 Z1 H):
+//   both: Z1Z1 | a: U2, H (12), HH, Z3 (2) | b: S2, rr (12), R2 = 4 rr^2 (4)
+//   -> a: J = H I | b: V = X1 I        (I = 4 HH)
+//   -> a: rr (V - X3) | b: Y1 J        -> Y3 = 2 (a - b) (6);  X3 = R2 - J - 2V (9)
+__device__ __forceinline__ void coop26_madd(Jac26& R, const Jac26& P, const Aff26& Q, const Coop26Ctx& c) {
+    fe26 Z1Z1, H, HH, Z3, rr, R2, I, J, V, X3, Y3, t, u;
+    fe26_sqr(Z1Z1, P.Z);
+    if (c.role == 0) {
+        fe26_mul(u, Q.x, Z1Z1);
+        fe26_sub<11>(H, u, P.X);
+        fe26_sqr(HH, H);
+        fe26_mul(Z3, P.Z, H);
+        fe26_mul_int<2>(Z3, Z3);
+        c.puts(0, H);
+        c.puts(1, HH);
+        c.puts(2, Z3);
+    } else {
+        fe26_mul(u, Q.y, P.Z);
+        fe26_mul(u, u, Z1Z1);
+        fe26_sub<11>(rr, u, P.Y);
+        fe26_sqr(R2, rr);
+        fe26_mul_int<4>(R2, R2);
+        c.puts(0, rr);
+        c.puts(1, R2);
+    }
+    __syncthreads();
+    if (c.role == 0) {
+        c.gets(0, rr);
+        c.gets(1, R2);
+    } else {
+        c.gets(0, H);
+        c.gets(1, HH);
+        c.gets(2, Z3);
+    }
+    fe26_mul_int<4>(I, HH);
+    if (c.role == 0) {
+        fe26_mul(J, H, I);
+        c.puts(3, J);
+    } else {
+        fe26_mul(V, P.X, I);
+        c.puts(3, V);
+    }
+    __syncthreads();
+    if (c.role == 0) c.gets(3, V);
+    else c.gets(3, J);
+    fe26_sub<2>(X3, R2, J);
+    fe26_mul_int<2>(t, V);
+    fe26_sub<3>(X3, X3, t);
+    if (c.role == 0) {
+        fe26_sub<10>(t, V, X3);
+        fe26_mul(u, rr, t);
+        c.puts(4, u);
+    } else {
+        fe26_mul(u, P.Y, J);
+        c.puts(4, u);
+    }
+    __syncthreads();
+    c.gets(4, t);
+    if (c.role == 0) fe26_sub<2>(Y3, u, t);
+    else fe26_sub<2>(Y3, t, u);
+    fe26_mul_int<2>(Y3, Y3);
+    const bool hz = fe26_is_zero(H) && !P.inf;
+    const bool rz = fe26_is_zero(rr);
+    Jac26 D;
+    if (hz && rz) CurveK1x::dbl(D, P);  // P == Q (rare)
+    const bool pinf = P.inf;
+    fe26_copy(R.X, X3);
+    fe26_copy(R.Y, Y3);
+    fe26_copy(R.Z, Z3);
+    R.inf = false;
+    if (hz) {
+        if (rz) CurveK1x::cmov(R, D, true);
+        else R.inf = true;
+    }
+    if (pinf) {
+        fe26_copy(R.X, Q.x);
+        fe26_copy(R.Y, Q.y);
+        fe26_one(R.Z);
+        R.inf = false;
+    }
+}
+
+__device__ __forceinline__ void coop26_add_digit(Jac26& acc, const Coop26Ctx& c, int d, bool neg, bool phi) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &c.L->tab[0][0][0] + m * (16 * 64) + c.lane;
+    const uint32_t* bx = phi ? &c.L->tabphx[0][0][0] + m * (8 * 64) + c.lane : base;
+    Aff26 S;
+    {
+        uint32_t x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            x[k] = bx[k * 64];
+            y[k] = base[(8 + k) * 64];
+        }
+        fe26_from_words(S.x, x);
+        fe26_from_words(S.y, y);
+    }
+    fe26 ny;
+    fe26_neg<2>(ny, S.y);
+    fe26_cmov(S.y, ny, (d < 0) != neg);
+    Jac26 R;
+    coop26_madd(R, acc, S, c);
+    CurveK1x::cmov(acc, R, d != 0);
+}
+
+// acc = u1 * G restricted to 8-bit comb windows [lo, hi)
+__device__ __forceinline__ void comb_range26(Jac26& acc, const fe& k_plain, const uint32_t* __restrict__ tab, int lo,
+                                             int hi) {
+    fe k;
+    fe_copy(k, k_plain);
+    for (int i = 0; i < lo; ++i) shr8(k);
+    CurveK1x::set_inf(acc);
+#pragma unroll 1
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t b = k.v[0] & 255u;
+        shr8(k);
+        Aff26 T;
+        load_aff26(T, tab + (static_cast<size_t>(i) * kCombEntries + b) * 16);
+        Jac26 S;
+        CurveK1x::madd(S, acc, T);
+        CurveK1x::cmov(acc, S, b != 0u);
+    }
+}
+
+// canonical 8-word coordinates into a phase-result slot (the layout coop_load_jac reads)
+__device__ __forceinline__ void coop26_store_jac(uint32_t (*dst)[64], const Jac26& P, int lane) {
+    fe X, Y, Z;
+    fe26_to_fe(X, P.X);
+    fe26_to_fe(Y, P.Y);
+    fe26_to_fe(Z, P.Z);
+    Jac J;
+    fe_copy(J.X, X);
+    fe_copy(J.Y, Y);
+    fe_copy(J.Z, Z);
+    J.inf = P.inf;
+    coop_store_jac(dst, J, lane);
+}
+__device__ __forceinline__ void coop26_load_jac(Jac26& P, const uint32_t (*src)[64], int lane) {
+    Jac J;
+    coop_load_jac(J, src, lane);
+    fe26_from_fe(P.X, J.X);
+    fe26_from_fe(P.Y, J.Y);
+    fe26_from_fe(P.Z, J.Z);
+    P.inf = J.inf;
+}
+__device__ __forceinline__ void lds_load_fe26(fe26& a, const uint32_t (*src)[64], int lane) {
+    fe w;
+    lds_load_fe(w, src, lane);
+    fe26_from_fe(a, w);
+}
+__device__ __forceinline__ void lds_store_fe26(uint32_t (*dst)[64], const fe26& a, int lane) {
+    fe w;
+    fe26_to_fe(w, a);
+    lds_store_fe(dst, w, lane);
+}
+
+__global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t* __restrict__ pre,
+                                                                  const uint64_t* __restrict__ pre_off,
+                                                                  const uint8_t* __restrict__ sig,
+                                                                  const uint64_t* __restrict__ sig_off, uint64_t n,
+                                                                  const uint32_t* __restrict__ tab,
+                                                                  uint8_t* __restrict__ txhash,
+                                                                  uint8_t* __restrict__ sender,
+                                                                  uint8_t* __restrict__ status) {
+    __shared__ Coop26Lds L;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
+    const bool active = i < n;
+    COOP_T(0);
+    uint64_t sa = 0, sb = 0, pa = 0, pb = 0;
+    if (active) {
+        sa = sig_off[i];
+        sb = sig_off[i + 1];
+        pa = pre_off[i];
+        pb = pre_off[i + 1];
+    }
+    const uint32_t slen = (sb - sa) > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(sb - sa);
+    if (threadIdx.x == 0) {
+        L.post[0] = 0u;
+        L.post[1] = 0u;
+    }
+    __syncthreads();
+    // ---------------------------------------------------------------- phase A (as tx_verify_coop_kernel)
+    fe r, s;
+    uint32_t v = 0;
+    bool ok = false;
+    if (active) ok = parse_sig65(sig + sa, slen, r, s, v);
+    else { fe_zero(r); fe_zero(s); }
+    if (wave == 1 || wave == 2) {
+        fe x;
+        fe_copy(x, r);
+        bool okr = ok;
+        if (v & 2u) {
+            okr = okr && fe_lt_k(r, kK1PminusN);
+            fe_add_k(x, r, ParamN1::M);
+        }
+        fe26 X, rhs, t, seven;
+        fe26_from_fe(X, x);
+        fe26_sqr(t, X);
+        fe26_mul(rhs, t, X);
+        fe26_set_small(seven, 7u);
+        fe26_add(rhs, rhs, seven);  // w (m 2)
+        if (wave == 2) {
+            fe26 y, ny;
+            fe26_sqrt_cand(y, rhs);
+            fe26_sqr(t, y);
+            fe26_sub<3>(t, t, rhs);
+            okr = okr && fe26_is_zero(t);
+            fe26_normalize(y);
+            fe26_neg<2>(ny, y);
+            fe26_normalize(ny);
+            fe26_cmov(y, ny, (y.v[0] & 1u) != (v & 1u));
+            lds_store_fe26(L.ys, y, lane);
+            L.rflag[lane] = okr ? 2u : 0u;
+            COOP_T(6);
+        } else {
+            Aff26 R, A[8];
+            fe26_mul(R.x, rhs, X);  // w x
+            fe26_sqr(R.y, rhs);     // w^2
+            fe26 Zc, beta;
+            {
+                Jac26 T[8];
+                multiples8_26(T, R);
+                coz_table26(A, Zc, T);
+            }
+            fe26_const(beta, kGlvBeta);
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                lds_store_fe26(L.tab[j], A[j].x, lane);
+                lds_store_fe26(L.tab[j] + 8, A[j].y, lane);
+                fe26 bx;
+                fe26_mul(bx, A[j].x, beta);
+                lds_store_fe26(L.tabphx[j], bx, lane);
+            });
+            lds_store_fe26(L.zc, Zc, lane);
+            COOP_T(6);
+        }
+    }
+    if (!ok) {
+        fe_zero(r);
+        r.v[0] = 1;
+        fe_zero(s);
+    }
+    if (wave == 3) {
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (active) {
+            const uint32_t len = static_cast<uint32_t>(pb - pa);
+            ByteReader rd(pre + pa, len);
+            keccak256_msg(rd, len, d);
+            store_digest(KECCAK256, txhash + 32 * i, d);
+        }
+        fe e;
+        fe_from_be_words(e, d);
+        reduce_once(e, ParamN1::M);
+        lds_store_fe(L.xe, e, lane);
+        coop_post(&L.post[1]);
+        COOP_T(7);
+    } else if (wave == 0) {
+        fe rm, rinv;
+        FieldN1::from_plain(rm, r);
+        FieldInv<FieldN1>::inv(rinv, rm);
+        lds_store_fe(L.xrinv, rinv, lane);
+        coop_post(&L.post[0]);
+        COOP_T(7);
+    }
+    if (wave != 2) {
+        coop_wait(&L.post[0]);
+        coop_wait(&L.post[1]);
+        fe e, rinv, u1;
+        lds_load_fe(e, L.xe, lane);
+        lds_load_fe(rinv, L.xrinv, lane);
+        FieldN1::mul(u1, e, rinv);
+        FieldN1::neg(u1, u1);
+        if (wave == 1) {
+            fe u2, k1, k2;
+            FieldN1::mul(u2, s, rinv);
+            bool neg1, neg2;
+            glv_split(k1, neg1, k2, neg2, u2);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                L.k[0][q][lane] = k1.v[q];
+                L.k[1][q][lane] = k2.v[q];
+            }
+            L.flags[lane] = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
+        }
+        constexpr int kCombW0 = 12, kCombW1 = 24;
+        Jac26 G;
+        const int lo = wave == 0 ? 0 : wave == 3 ? kCombW0 : kCombW1;
+        const int hi = wave == 0 ? kCombW0 : wave == 3 ? kCombW1 : 32;
+        comb_range26(G, u1, tab, lo, hi);
+        coop26_store_jac(L.pt[wave == 0 ? 2 : wave == 3 ? 3 : 4], G, lane);
+    }
+    COOP_T(1);
+    __syncthreads();
+    // ---------------------------------------------------------------- phase C: two cooperative GLV chains
+    const uint32_t flags = L.flags[lane] | L.rflag[lane];
+    Coop26Ctx c{&L, wave >> 1, wave & 1, lane, false};
+    fe k;
+    fe_zero(k);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) k.v[q] = L.k[c.chain][q][lane];
+    const bool neg = c.chain == 0 ? (flags & 4u) != 0 : (flags & 8u) != 0;
+    const bool phi = c.chain == 1;
+    Jac26 acc;
+    CurveK1x::set_inf(acc);
+    coop26_add_digit(acc, c, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
+#pragma unroll 1
+    for (int w = 31; w >= 0; --w) {
+        coop26_dbl<0>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+        c.probe = blockIdx.x == 0 && w == 20;
+#endif
+        coop26_dbl<3>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+        c.probe = false;
+        if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][5] = clock64();
+#endif
+        coop26_dbl<0>(acc, c);
+        coop26_dbl<3>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+        if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][6] = clock64();
+#endif
+        coop26_add_digit(acc, c, booth_digit128(k), neg, phi);
+#ifdef BCOSGPU_COOP_TIMING
+        if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][7] = clock64();
+#endif
+    }
+    COOP_T(2);
+    if (c.role == 0) coop26_store_jac(L.pt[c.chain], acc, lane);
+    __syncthreads();
+    // ---------------------------------------------------------------- phase D (on fe26 as well)
+    if (wave == 1) {  // G part: partials 0 + 1 + 2
+        Jac26 G0, G1, T, U;
+        coop26_load_jac(G0, L.pt[2], lane);
+        coop26_load_jac(G1, L.pt[3], lane);
+        CurveK1x::add(T, G0, G1);
+        coop26_load_jac(G0, L.pt[4], lane);
+        CurveK1x::add(U, T, G0);
+        coop26_store_jac(L.pt[2], U, lane);
+    } else if (wave == 0) {  // R part: co-Z curve -> E_w (Z * Zc) -> E (Z * y)
+        Jac26 P0, P1, Q;
+        coop26_load_jac(P0, L.pt[0], lane);
+        coop26_load_jac(P1, L.pt[1], lane);
+        fe26 Zc, y;
+        lds_load_fe26(Zc, L.zc, lane);
+        lds_load_fe26(y, L.ys, lane);
+        CurveK1x::add(Q, P0, P1);
+        fe26_mul(Zc, Zc, y);
+        fe26_mul(Q.Z, Q.Z, Zc);
+        coop26_store_jac(L.pt[0], Q, lane);
+    }
+    __syncthreads();
+    if (wave == 0 && active) {
+        Jac26 Q, G, R;
+        coop26_load_jac(Q, L.pt[0], lane);
+        coop26_load_jac(G, L.pt[2], lane);
+        CurveK1x::add(R, Q, G);
+        const bool ok2 = (flags & 3u) == 3u && !R.inf;
+        COOP_T(4);
+        fe z, zi, ax, ay;
+        fe26_to_fe(z, R.Z);
+        FieldInv<FieldK1>::inv(zi, z);
+        COOP_T(5);
+        fe26 zi26, zi2, zi3, X, Y;
+        fe26_from_fe(zi26, zi);
+        fe26_sqr(zi2, zi26);
+        fe26_mul(X, R.X, zi2);
+        fe26_mul(zi3, zi2, zi26);
+        fe26_mul(Y, R.Y, zi3);
+        fe26_to_fe(ax, X);
+        fe26_to_fe(ay, Y);
+        uint32_t ad[5] = {0, 0, 0, 0, 0};
+        if (ok2) keccak_address(ad, ax, ay);
+        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) o[q] = ad[q];
+        status[i] = ok2 ? 0 : 1;
+    }
+    COOP_T(3);
+}
+int launch_tx_verify_small_secp(const TxKernelPolicy& pol, const uint8_t* d_pre, const uint64_t* d_pre_off,
+                                const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash,
+                                uint8_t* d_sender, uint8_t* d_status, hipStream_t st) {
+    const uint32_t *k1, *sm2;
+    const int rc = tables8(&k1, &sm2);
+    if (rc) return rc;
+    const dim3 grid(static_cast<unsigned>((n + 63) / 64));
+    if (pol.coop && pol.f26)
+        hipLaunchKernelGGL(tx_verify_coop26_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n, k1,
+                           d_txhash, d_sender, d_status);
+    else if (pol.coop)
+        hipLaunchKernelGGL(tx_verify_coop_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n, k1,
+                           d_txhash, d_sender, d_status);
+    else
+        hipLaunchKernelGGL(tx_verify_split_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n, k1,
+                           d_txhash, d_sender, d_status);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+}  // namespace bcosgpu

@@ -1,0 +1,854 @@
+// ecc_pair.hip -- small-batch SM2 tx verify: the pair kernels (8 x 32 and fp26 point arithmetic).
+#include "ecc_device.h"
+
+namespace bcosgpu {
+
+// ------------------------------------------------------------------ SM2 small-batch (pair) tx verify
+// Guomi chains verify blocks of C2 size (FastSM2Crypto, FastSM2Crypto.h:33-44).  SM2 has no efficient
+// endomorphism, so t*P is ONE chain of 256 doublings and 65 mixed additions.  A 256-thread workgroup
+// owns 64 txs:
+//   waves 0, 1  build the affine table 1P..8P (wave 0), then run the t*P chain as a PAIR that splits
+//               every a = -3 doubling and mixed addition by dependency level and trades field elements
+//               through LDS, synchronised by per-wave LDS counters (not workgroup barriers, so the other
+//               two waves are never held up):
+//                 dbl  (3M + 5S):  a: delta = Z^2, alpha = 3(X - delta)(X + delta), alpha^2
+//                                  b: gamma = Y^2, 4 beta = 4 X gamma, 8 gamma^2
+//                                  -> a: Y3 = alpha (4 beta - X3) - 8 gamma^2 | b: Z3 = 2 Y Z  (4 of 8 M/S)
+//                 madd (7M + 4S):  as tx_verify_coop_kernel's                                   (6 of 11)
+//   wave 2      tx hash, e = SM3(Z_A || h), the on-curve check, the address SM3(pub), comb windows
+//               0..15 of s*G, then the sum of both comb halves;
+//   wave 3      comb windows 16..31 of s*G.
+// Waves 2 and 3 finish long before the chain; one final barrier, then wave 0 adds s*G, compares
+// projectively and writes the verdict.  Bit-identical to tx_verify_kernel<1, *>.
+struct Sm2PairLds {
+    uint32_t tab[8][16][64];   // affine 1P..8P (Montgomery): [entry][x0..7, y0..7][lane]
+    uint4 ex[2][2][3][2][64];  // [parity][writer role][slot][quad][lane]
+    uint32_t g[25][64];        // s*G, Jacobian + inf (wave 2)
+    uint32_t gh[25][64];       // comb windows 16..31 (wave 3)
+    uint32_t c[8][64];         // (r - e) mod n, plain (wave 2)
+    uint32_t addr[5][64];      // right160(SM3(pub)) (wave 2)
+    uint32_t ok2[64];          // wave 2's checks: pub on the curve
+    uint32_t seq[4];           // pair counters of waves 0, 1; wave 3 done
+};
+
+// One pair of waves: each exchange writes the caller's slots of the current parity, publishes its
+// sequence number, waits for the partner's, reads the partner's slots and flips parity.  A parity's
+// slots are rewritten only after the partner has published the NEXT exchange, i.e. after it has read
+// them.
+struct PairCtx {
+    Sm2PairLds* L;
+    int role, lane;
+    uint32_t seq;
+    int par;
+    __device__ __forceinline__ void put(int s, const fe& a) const {
+        uint4* p = &L->ex[par][role][s][0][0] + lane;
+        p[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+        p[64] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+    }
+    __device__ __forceinline__ void get(int s, fe& a) const {
+        const uint4* p = &L->ex[par][role ^ 1][s][0][0] + lane;
+        const uint4 q0 = p[0], q1 = p[64];
+        a.v[0] = q0.x; a.v[1] = q0.y; a.v[2] = q0.z; a.v[3] = q0.w;
+        a.v[4] = q1.x; a.v[5] = q1.y; a.v[6] = q1.z; a.v[7] = q1.w;
+    }
+    __device__ __forceinline__ void sync() {
+        ++seq;
+        __hip_atomic_store(&L->seq[role], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(&L->seq[role ^ 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < seq) {
+        }
+    }
+    __device__ __forceinline__ void next() { par ^= 1; }
+};
+
+// P = 2 P on SM2 (a = -3, dbl-2001-b with Z3 = 2 Y Z), P replicated on both waves of the pair
+__device__ __forceinline__ void pair_dbl_am3(Jac& P, PairCtx& c) {
+    using F = FieldP2;
+    fe alpha, A2, b4, g8, X3, Y3, Z3, t, u;
+    if (c.role == 0) {
+        fe d;
+        F::sqr(d, P.Z);
+        F::sub(t, P.X, d);
+        F::add(u, P.X, d);
+        F::mul(alpha, t, u);
+        F::mul3(alpha, alpha);
+        F::sqr(A2, alpha);
+        c.put(0, alpha);
+        c.put(1, A2);
+    } else {
+        fe g;
+        F::sqr(g, P.Y);
+        F::mul(b4, P.X, g);
+        F::template shl<2>(b4, b4);
+        F::sqr(g8, g);
+        F::template shl<3>(g8, g8);
+        c.put(0, b4);
+        c.put(1, g8);
+    }
+    c.sync();
+    if (c.role == 0) {
+        c.get(0, b4);
+        c.get(1, g8);
+    } else {
+        c.get(0, alpha);
+        c.get(1, A2);
+    }
+    c.next();
+    F::template shl<1>(t, b4);
+    F::sub(X3, A2, t);  // alpha^2 - 8 beta
+    if (c.role == 0) {
+        F::sub(t, b4, X3);
+        F::mul(Y3, alpha, t);
+        F::sub(Y3, Y3, g8);
+        c.put(0, Y3);
+    } else {
+        F::mul(Z3, P.Y, P.Z);
+        F::template shl<1>(Z3, Z3);
+        c.put(0, Z3);
+    }
+    c.sync();
+    if (c.role == 0) c.get(0, Z3);
+    else c.get(0, Y3);
+    c.next();
+    fe_copy(P.X, X3);
+    fe_copy(P.Y, Y3);
+    fe_copy(P.Z, Z3);
+}
+
+// R = P + Q (madd-2007-bl with the complete-addition special cases of Curve::madd), Q affine
+template <class F, class C>
+__device__ __forceinline__ void pair_madd(Jac& R, const Jac& P, const Aff& Q, PairCtx& c) {
+    fe Z1Z1, H, HH, Z3, rr, R2, I, J, V, X3, Y3, t, u;
+    F::sqr(Z1Z1, P.Z);
+    if (c.role == 0) {
+        F::mul(u, Q.x, Z1Z1);  // U2
+        F::sub(H, u, P.X);
+        F::sqr(HH, H);
+        F::add(t, P.Z, H);
+        F::sqr(Z3, t);
+        F::sub(Z3, Z3, Z1Z1);
+        F::sub(Z3, Z3, HH);
+        c.put(0, H);
+        c.put(1, HH);
+        c.put(2, Z3);
+    } else {
+        F::mul(u, Q.y, P.Z);
+        F::mul(u, u, Z1Z1);  // S2
+        F::sub(rr, u, P.Y);
+        F::template shl<1>(rr, rr);
+        F::sqr(R2, rr);
+        c.put(0, rr);
+        c.put(1, R2);
+    }
+    c.sync();
+    if (c.role == 0) {
+        c.get(0, rr);
+        c.get(1, R2);
+    } else {
+        c.get(0, H);
+        c.get(1, HH);
+        c.get(2, Z3);
+    }
+    c.next();
+    F::template shl<2>(I, HH);
+    if (c.role == 0) {
+        F::mul(J, H, I);
+        c.put(0, J);
+    } else {
+        F::mul(V, P.X, I);
+        c.put(0, V);
+    }
+    c.sync();
+    if (c.role == 0) c.get(0, V);
+    else c.get(0, J);
+    c.next();
+    F::sub(X3, R2, J);
+    F::template shl<1>(t, V);
+    F::sub(X3, X3, t);
+    if (c.role == 0) {
+        F::sub(t, V, X3);
+        F::mul(u, rr, t);  // rr (V - X3)
+    } else {
+        F::mul(u, P.Y, J);
+        F::template shl<1>(u, u);  // 2 Y J
+    }
+    c.put(0, u);
+    c.sync();
+    c.get(0, t);
+    c.next();
+    if (c.role == 0) F::sub(Y3, u, t);
+    else F::sub(Y3, t, u);
+    // special cases, as Curve::madd (computed identically on both waves, no exchanges)
+    const bool hz = F::is_zero(H) && !P.inf;
+    const bool rz = F::is_zero(rr);
+    Jac D;
+    if (hz && rz) C::dbl(D, P);  // P == Q (rare)
+    const bool pinf = P.inf;
+    fe_copy(R.X, X3);
+    fe_copy(R.Y, Y3);
+    fe_copy(R.Z, Z3);
+    R.inf = false;
+    if (hz) {
+        if (rz) C::cmov(R, D, true);
+        else R.inf = true;
+    }
+    if (pinf) {
+        fe_copy(R.X, Q.x);
+        fe_copy(R.Y, Q.y);
+        F::set_one(R.Z);
+        R.inf = false;
+    }
+}
+
+__device__ __forceinline__ void pair_add_digit_sm2(Jac& acc, PairCtx& c, int d) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &c.L->tab[0][0][0] + m * (16 * 64) + c.lane;
+    Aff S;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        S.x.v[k] = base[k * 64];
+        S.y.v[k] = base[(8 + k) * 64];
+    }
+    fe ny;
+    FieldP2::neg(ny, S.y);
+    fe_cmov(S.y, ny, d < 0);
+    Jac R;
+    pair_madd<FieldP2, CurveSM2>(R, acc, S, c);
+    CurveSM2::cmov(acc, R, d != 0);
+}
+
+// acc = k * G restricted to the 8-bit comb windows [lo, hi)
+template <class C>
+__device__ __forceinline__ void comb_range8(Jac& acc, const fe& k_plain, const uint32_t* __restrict__ tab, int lo,
+                                            int hi) {
+    fe k;
+    fe_copy(k, k_plain);
+    for (int i = 0; i < lo; ++i) shr8(k);
+    C::set_inf(acc);
+#pragma unroll 1
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t b = k.v[0] & 255u;
+        shr8(k);
+        Aff T;
+        load_aff16(T, tab + (static_cast<size_t>(i) * kCombEntries + b) * 16);
+        Jac S;
+        C::madd(S, acc, T);
+        C::cmov(acc, S, b != 0u);
+    }
+}
+
+__device__ __forceinline__ void pair_store_jac(uint32_t (*dst)[64], const Jac& P, int lane) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        dst[k][lane] = P.X.v[k];
+        dst[8 + k][lane] = P.Y.v[k];
+        dst[16 + k][lane] = P.Z.v[k];
+    }
+    dst[24][lane] = P.inf ? 1u : 0u;
+}
+__device__ __forceinline__ void pair_load_jac(Jac& P, const uint32_t (*src)[64], int lane) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        P.X.v[k] = src[k][lane];
+        P.Y.v[k] = src[8 + k][lane];
+        P.Z.v[k] = src[16 + k][lane];
+    }
+    P.inf = src[24][lane] != 0u;
+}
+
+__global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair_kernel(const uint8_t* __restrict__ pre,
+                                                                    const uint64_t* __restrict__ pre_off,
+                                                                    const uint8_t* __restrict__ sig,
+                                                                    const uint64_t* __restrict__ sig_off, uint64_t n,
+                                                                    const uint32_t* __restrict__ tab,
+                                                                    uint8_t* __restrict__ txhash,
+                                                                    uint8_t* __restrict__ sender,
+                                                                    uint8_t* __restrict__ status) {
+    __shared__ Sm2PairLds L;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
+    const bool active = i < n;
+    if (threadIdx.x < 4) L.seq[threadIdx.x] = 0u;
+    __syncthreads();
+    // signature r || s || pub (SM2Crypto::recover, SignatureDataWithPub.h:55-64); sm2_do_verify checks
+    uint64_t sa = 0, sb = 0;
+    if (active) {
+        sa = sig_off[i];
+        sb = sig_off[i + 1];
+    }
+    const bool len_ok = active && sb - sa == 128u;
+    fe r, s, px, py;
+    uint32_t X[8], Y[8];
+    if (len_ok) {
+        ByteReader rd(sig + sa, 128);
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rd.word(k);
+        fe_from_be_words(r, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rd.word(8 + k);
+        fe_from_be_words(s, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            X[k] = bswap32(rd.word(16 + k));
+            Y[k] = bswap32(rd.word(24 + k));
+        }
+    } else {
+        fe_zero(r);
+        fe_zero(s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) X[k] = Y[k] = 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        px.v[k] = X[7 - k];
+        py.v[k] = Y[7 - k];
+    }
+    bool ok = len_ok && fe_lt_k(px, ParamP2::M) && fe_lt_k(py, ParamP2::M);
+    ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN2::M) && fe_lt_k(s, ParamN2::M);
+    fe t;
+    FieldN2::add(t, r, s);
+    ok = ok && !fe_is_zero_raw(t);
+    Aff P;
+    FieldP2::from_plain(P.x, px);
+    FieldP2::from_plain(P.y, py);
+    Jac acc;
+    if (wave <= 1) {
+        PairCtx c{&L, wave, lane, 0u, 0};
+        if (wave == 0) {
+            Aff A[8];
+            sm2_affine_table(A, P);
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                lds_store_fe(L.tab[j], A[j].x, lane);
+                lds_store_fe(L.tab[j] + 8, A[j].y, lane);
+            });
+        }
+        c.sync();  // the table is in LDS
+        fe k;
+        fe_copy(k, t);
+        CurveSM2::set_inf(acc);
+        pair_add_digit_sm2(acc, c, static_cast<int>(k.v[7] >> 31));  // digit 64 = bit 255
+#pragma unroll 1
+        for (int w = 63; w >= 0; --w) {
+            pair_dbl_am3(acc, c);
+            pair_dbl_am3(acc, c);
+            pair_dbl_am3(acc, c);
+            pair_dbl_am3(acc, c);
+            const uint32_t top = k.v[7];
+            const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
+            const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
+            shl4(k);
+            pair_add_digit_sm2(acc, c, d);
+        }
+    } else if (wave == 2) {
+        // tx hash (TarsHashable.h:16-41), e = SM3(Z_A || h) (fast_sm2.cpp:34,203), c = (r - e) mod n
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (active) {
+            const uint64_t pa = pre_off[i], pb = pre_off[i + 1];
+            const uint32_t len = static_cast<uint32_t>(pb - pa);
+            ByteReader rd(pre + pa, len);
+            sm3_msg(rd, len, d);
+            store_digest(SM3, txhash + 32 * i, d);
+        }
+        fe h;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h.v[k] = d[7 - k];
+        uint32_t eb[8];
+        sm2_e(eb, X, Y, h);
+        fe e, cc;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e.v[k] = eb[7 - k];
+        reduce_once(e, ParamN2::M);
+        FieldN2::sub(cc, r, e);
+        lds_store_fe(L.c, cc, lane);
+        fe b;
+        fe_set(b, kSM2B);
+        L.ok2[lane] = CurveSM2::on_curve(P, b) ? 1u : 0u;
+        uint32_t ad[5];
+        sm3_address(ad, px, py);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) L.addr[k][lane] = ad[k];
+        Jac G0, G1, G;
+        comb_range8<CurveSM2>(G0, s, tab, 0, 16);
+        while (__hip_atomic_load(&L.seq[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+            __builtin_amdgcn_s_sleep(1);
+        }
+        pair_load_jac(G1, L.gh, lane);
+        CurveSM2::add(G, G0, G1);
+        pair_store_jac(L.g, G, lane);
+    } else {
+        Jac G1;
+        comb_range8<CurveSM2>(G1, s, tab, 16, 32);
+        pair_store_jac(L.gh, G1, lane);
+        __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    if (wave == 0 && active) {
+        Jac G, Q;
+        pair_load_jac(G, L.g, lane);
+        CurveSM2::add(Q, G, acc);
+        ok = ok && L.ok2[lane] != 0u && !Q.inf;
+        // x1 = X / Z^2 must be congruent to r - e (mod n): x1 = c or c + n (when c + n < p)
+        fe cc, c2, cm, z2, rhs;
+        lds_load_fe(cc, L.c, lane);
+        FieldP2::sqr(z2, Q.Z);
+        FieldP2::from_plain(cm, cc);
+        FieldP2::mul(rhs, cm, z2);
+        bool match = FieldP2::eq(rhs, Q.X);
+        const uint32_t carry = fe_add_k(c2, cc, ParamN2::M);
+        if (carry == 0u && fe_lt_k(c2, ParamP2::M)) {
+            FieldP2::from_plain(cm, c2);
+            FieldP2::mul(rhs, cm, z2);
+            match = match || FieldP2::eq(rhs, Q.X);
+        }
+        ok = ok && match;
+        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = ok ? L.addr[k][lane] : 0u;
+        status[i] = ok ? 0 : 1;
+    }
+}
+
+// ------------------------------------------------------------------ SM2 pair kernel on fp26
+// tx_verify_sm2_pair_kernel with the t*P chain, the comb halves and the final check on fp26 (R' =
+// 2^286, ecp26.h); the split of each doubling / mixed addition between the pair is the same, with the
+// magnitude plan of CurveSM2x (each wave of the pair normalises the same operands, so both hold
+// identical limbs).  Exchanged elements are 5 x uint2 (raw limbs, no canonicalisation).
+struct Sm2Pair26Lds {
+    uint32_t tab[8][16][64];         // affine 1P..8P in the R' domain, canonical words
+    uint2 ex[2][2][3][5][64];        // [parity][writer role][slot][limb pair][lane]
+    uint32_t g[25][64];
+    uint32_t gh[25][64];
+    uint32_t c[8][64];
+    uint32_t addr[5][64];
+    uint32_t ok2[64];
+    uint32_t seq[4];
+};
+
+struct Pair26Ctx {
+    Sm2Pair26Lds* L;
+    int role, lane;
+    uint32_t seq;
+    int par;
+    __device__ __forceinline__ void put(int s, const fp26& a) const {
+        uint2* p = &L->ex[par][role][s][0][0] + lane;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) p[q * 64] = make_uint2(a.v[2 * q], a.v[2 * q + 1]);
+    }
+    __device__ __forceinline__ void get(int s, fp26& a) const {
+        const uint2* p = &L->ex[par][role ^ 1][s][0][0] + lane;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            const uint2 w = p[q * 64];
+            a.v[2 * q] = w.x;
+            a.v[2 * q + 1] = w.y;
+        }
+    }
+    __device__ __forceinline__ void sync() {
+        ++seq;
+        __hip_atomic_store(&L->seq[role], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__hip_atomic_load(&L->seq[role ^ 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < seq) {
+        }
+    }
+    __device__ __forceinline__ void next() { par ^= 1; }
+};
+
+// as pair_dbl_am3 with CurveSM2x::dbl's magnitudes (X <= 5, Y, Z <= 8 -> (2, 2, 2)):
+//   a: alpha = 3 (X - d)(X + d) (3), alpha^2 (1) | b: 4 beta (4), 8 gamma^2 (8)
+//   -> both: X3 = alpha^2 - 8 beta (2) -> a: Y3 (2) | b: Z3 = 2 Y Z (2)
+__device__ __forceinline__ void pair26_dbl(JacP26& P, Pair26Ctx& c) {
+    fp26 alpha, A2, b4, g8, X3, Y3, Z3, t, u;
+    if (c.role == 0) {
+        fp26 d;
+        fp26_sqr(d, P.Z);
+        fp26_sub<2>(t, P.X, d);
+        fp26_add(u, P.X, d);
+        fp26_mul(alpha, t, u);
+        fp26_mul_int<3>(alpha, alpha);
+        fp26_sqr(A2, alpha);
+        c.put(0, alpha);
+        c.put(1, A2);
+    } else {
+        fp26 g;
+        fp26_sqr(g, P.Y);
+        fp26_mul(b4, P.X, g);
+        fp26_mul_int<4>(b4, b4);
+        fp26_sqr(g8, g);
+        fp26_mul_int<8>(g8, g8);
+        c.put(0, b4);
+        c.put(1, g8);
+    }
+    c.sync();
+    if (c.role == 0) {
+        c.get(0, b4);
+        c.get(1, g8);
+    } else {
+        c.get(0, alpha);
+        c.get(1, A2);
+    }
+    c.next();
+    F26_SETM(alpha, 3);
+    F26_SETM(A2, 1);
+    F26_SETM(b4, 4);
+    F26_SETM(g8, 8);
+    fp26_mul_int<2>(t, b4);
+    fp26_sub<9>(X3, A2, t);
+    fp26_normalize_weak(X3);
+    if (c.role == 0) {
+        fp26_sub<3>(t, b4, X3);
+        fp26_mul(Y3, alpha, t);
+        fp26_sub<9>(Y3, Y3, g8);
+        fp26_normalize_weak(Y3);
+        c.put(0, Y3);
+    } else {
+        fp26_mul(Z3, P.Y, P.Z);
+        fp26_mul_int<2>(Z3, Z3);
+        c.put(0, Z3);
+    }
+    c.sync();
+    if (c.role == 0) c.get(0, Z3);
+    else c.get(0, Y3);
+    c.next();
+    F26_SETM(Y3, 2);
+    F26_SETM(Z3, 2);
+    fp26_copy(P.X, X3);
+    fp26_copy(P.Y, Y3);
+    fp26_copy(P.Z, Z3);
+}
+
+// as pair_madd with CurveSM2x::madd's arrangement (r = 2 rr, Z3 = 2 Z1 H): P (2, 2, <= 8), Q <= 2
+//   a: H (5), HH, Z3 (2) | b: rr (5), R2 = 4 rr^2 (4) -> a: J | b: V -> a: rr (V - X3) | b: Y1 J
+__device__ __forceinline__ void pair26_madd(JacP26& R, const JacP26& P, const AffP26& Q, Pair26Ctx& c) {
+    fp26 Z1Z1, H, HH, Z3, rr, R2, I, J, V, X3, Y3, t, u;
+    fp26_sqr(Z1Z1, P.Z);
+    if (c.role == 0) {
+        fp26_mul(u, Q.x, Z1Z1);
+        fp26_sub<3>(H, u, P.X);
+        fp26_sqr(HH, H);
+        fp26_mul(Z3, P.Z, H);
+        fp26_mul_int<2>(Z3, Z3);
+        c.put(0, H);
+        c.put(1, HH);
+        c.put(2, Z3);
+    } else {
+        fp26_mul(u, Q.y, P.Z);
+        fp26_mul(u, u, Z1Z1);
+        fp26_sub<3>(rr, u, P.Y);
+        fp26_sqr(R2, rr);
+        fp26_mul_int<4>(R2, R2);
+        c.put(0, rr);
+        c.put(1, R2);
+    }
+    c.sync();
+    if (c.role == 0) {
+        c.get(0, rr);
+        c.get(1, R2);
+    } else {
+        c.get(0, H);
+        c.get(1, HH);
+        c.get(2, Z3);
+    }
+    c.next();
+    F26_SETM(rr, 5);
+    F26_SETM(R2, 4);
+    F26_SETM(H, 5);
+    F26_SETM(HH, 1);
+    F26_SETM(Z3, 2);
+    fp26_mul_int<4>(I, HH);
+    if (c.role == 0) {
+        fp26_mul(J, H, I);
+        c.put(0, J);
+    } else {
+        fp26_mul(V, P.X, I);
+        c.put(0, V);
+    }
+    c.sync();
+    if (c.role == 0) c.get(0, V);
+    else c.get(0, J);
+    c.next();
+    F26_SETM(V, 1);
+    F26_SETM(J, 1);
+    fp26_sub<2>(X3, R2, J);
+    fp26_mul_int<2>(t, V);
+    fp26_sub<3>(X3, X3, t);
+    fp26_normalize_weak(X3);
+    if (c.role == 0) {
+        fp26_sub<3>(t, V, X3);
+        fp26_mul(u, rr, t);
+    } else {
+        fp26_mul(u, P.Y, J);
+    }
+    c.put(0, u);
+    c.sync();
+    c.get(0, t);
+    c.next();
+    F26_SETM(t, 1);
+    if (c.role == 0) fp26_sub<2>(Y3, u, t);
+    else fp26_sub<2>(Y3, t, u);
+    fp26_mul_int<2>(Y3, Y3);
+    fp26_normalize_weak(Y3);
+    const bool hz = fp26_is_zero(H) && !P.inf;
+    const bool rz = fp26_is_zero(rr);
+    JacP26 D;
+    if (hz && rz) CurveSM2x::dbl(D, P);  // P == Q (rare)
+    const bool pinf = P.inf;
+    fp26_copy(R.X, X3);
+    fp26_copy(R.Y, Y3);
+    fp26_copy(R.Z, Z3);
+    R.inf = false;
+    if (hz) {
+        if (rz) CurveSM2x::cmov(R, D, true);
+        else R.inf = true;
+    }
+    if (pinf) {
+        fp26_copy(R.X, Q.x);
+        fp26_copy(R.Y, Q.y);
+        fp26_set(R.Z, p26::ONE_R);
+        R.inf = false;
+    }
+}
+
+__device__ __forceinline__ void pair26_add_digit(JacP26& acc, Pair26Ctx& c, int d) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &c.L->tab[0][0][0] + m * (16 * 64) + c.lane;
+    AffP26 S;
+    {
+        uint32_t x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            x[k] = base[k * 64];
+            y[k] = base[(8 + k) * 64];
+        }
+        fp26_from_words(S.x, x);
+        fp26_from_words(S.y, y);
+    }
+    fp26 ny;
+    fp26_neg<2>(ny, S.y);
+    fp26_cmov(S.y, ny, d < 0);
+    fp26_normalize_weak(S.y);
+    JacP26 R;
+    pair26_madd(R, acc, S, c);
+    CurveSM2x::cmov(acc, R, d != 0);
+}
+
+// acc = k * G restricted to the 8-bit comb windows [lo, hi) of the R'-domain table
+__device__ __forceinline__ void comb_range_sm2_26(JacP26& acc, const fe& k_plain, const uint32_t* __restrict__ tab,
+                                                  int lo, int hi) {
+    fe k;
+    fe_copy(k, k_plain);
+    for (int i = 0; i < lo; ++i) shr8(k);
+    CurveSM2x::set_inf(acc);
+#pragma unroll 1
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t b = k.v[0] & 255u;
+        shr8(k);
+        AffP26 T;
+        load_affp26(T, tab + (static_cast<size_t>(i) * kCombEntries + b) * 16);
+        JacP26 S;
+        CurveSM2x::madd(S, acc, T);
+        CurveSM2x::cmov(acc, S, b != 0u);
+    }
+}
+
+__device__ __forceinline__ void pair26_store_jac(uint32_t (*dst)[64], const JacP26& P, int lane) {
+    fe X, Y, Z;
+    fp26_to_fe(X, P.X);
+    fp26_to_fe(Y, P.Y);
+    fp26_to_fe(Z, P.Z);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        dst[k][lane] = X.v[k];
+        dst[8 + k][lane] = Y.v[k];
+        dst[16 + k][lane] = Z.v[k];
+    }
+    dst[24][lane] = P.inf ? 1u : 0u;
+}
+__device__ __forceinline__ void pair26_load_jac(JacP26& P, const uint32_t (*src)[64], int lane) {
+    uint32_t x[8], y[8], z[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        x[k] = src[k][lane];
+        y[k] = src[8 + k][lane];
+        z[k] = src[16 + k][lane];
+    }
+    fp26_from_words(P.X, x);
+    fp26_from_words(P.Y, y);
+    fp26_from_words(P.Z, z);
+    P.inf = src[24][lane] != 0u;
+}
+
+__global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(const uint8_t* __restrict__ pre,
+                                                                      const uint64_t* __restrict__ pre_off,
+                                                                      const uint8_t* __restrict__ sig,
+                                                                      const uint64_t* __restrict__ sig_off,
+                                                                      uint64_t n, const uint32_t* __restrict__ tab,
+                                                                      uint8_t* __restrict__ txhash,
+                                                                      uint8_t* __restrict__ sender,
+                                                                      uint8_t* __restrict__ status) {
+    __shared__ Sm2Pair26Lds L;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
+    const bool active = i < n;
+    if (threadIdx.x < 4) L.seq[threadIdx.x] = 0u;
+    __syncthreads();
+    uint64_t sa = 0, sb = 0;
+    if (active) {
+        sa = sig_off[i];
+        sb = sig_off[i + 1];
+    }
+    const bool len_ok = active && sb - sa == 128u;
+    fe r, s, px, py;
+    uint32_t X[8], Y[8];
+    if (len_ok) {
+        ByteReader rd(sig + sa, 128);
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rd.word(k);
+        fe_from_be_words(r, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rd.word(8 + k);
+        fe_from_be_words(s, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            X[k] = bswap32(rd.word(16 + k));
+            Y[k] = bswap32(rd.word(24 + k));
+        }
+    } else {
+        fe_zero(r);
+        fe_zero(s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) X[k] = Y[k] = 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        px.v[k] = X[7 - k];
+        py.v[k] = Y[7 - k];
+    }
+    bool ok = len_ok && fe_lt_k(px, ParamP2::M) && fe_lt_k(py, ParamP2::M);
+    ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN2::M) && fe_lt_k(s, ParamN2::M);
+    fe t;
+    FieldN2::add(t, r, s);
+    ok = ok && !fe_is_zero_raw(t);
+    AffP26 P;
+    fp26_from_plain(P.x, px);
+    fp26_from_plain(P.y, py);
+    JacP26 acc;
+    if (wave <= 1) {
+        Pair26Ctx c{&L, wave, lane, 0u, 0};
+        if (wave == 0) {
+            AffP26 A[8];
+            sm2_affine_table26(A, P);
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                fe x, y;
+                fp26_to_fe(x, A[j].x);
+                fp26_to_fe(y, A[j].y);
+                lds_store_fe(L.tab[j], x, lane);
+                lds_store_fe(L.tab[j] + 8, y, lane);
+            });
+        }
+        c.sync();  // the table is in LDS
+        fe k;
+        fe_copy(k, t);
+        CurveSM2x::set_inf(acc);
+        pair26_add_digit(acc, c, static_cast<int>(k.v[7] >> 31));  // digit 64 = bit 255
+#pragma unroll 1
+        for (int w = 63; w >= 0; --w) {
+            pair26_dbl(acc, c);
+            pair26_dbl(acc, c);
+            pair26_dbl(acc, c);
+            pair26_dbl(acc, c);
+            const uint32_t top = k.v[7];
+            const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
+            const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
+            shl4(k);
+            pair26_add_digit(acc, c, d);
+        }
+    } else if (wave == 2) {
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (active) {
+            const uint64_t pa = pre_off[i], pb = pre_off[i + 1];
+            const uint32_t len = static_cast<uint32_t>(pb - pa);
+            ByteReader rd(pre + pa, len);
+            sm3_msg(rd, len, d);
+            store_digest(SM3, txhash + 32 * i, d);
+        }
+        fe h;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h.v[k] = d[7 - k];
+        uint32_t eb[8];
+        sm2_e(eb, X, Y, h);
+        fe e, cc;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e.v[k] = eb[7 - k];
+        reduce_once(e, ParamN2::M);
+        FieldN2::sub(cc, r, e);
+        lds_store_fe(L.c, cc, lane);
+        L.ok2[lane] = sm2_on_curve26(P) ? 1u : 0u;
+        uint32_t ad[5];
+        sm3_address(ad, px, py);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) L.addr[k][lane] = ad[k];
+        JacP26 G0, G1, G;
+        comb_range_sm2_26(G0, s, tab, 0, 16);
+        while (__hip_atomic_load(&L.seq[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+            __builtin_amdgcn_s_sleep(1);
+        }
+        pair26_load_jac(G1, L.gh, lane);
+        CurveSM2x::add(G, G0, G1);
+        pair26_store_jac(L.g, G, lane);
+    } else {
+        JacP26 G1;
+        comb_range_sm2_26(G1, s, tab, 16, 32);
+        pair26_store_jac(L.gh, G1, lane);
+        __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    if (wave == 0 && active) {
+        JacP26 G, Q;
+        pair26_load_jac(G, L.g, lane);
+        CurveSM2x::add(Q, G, acc);
+        ok = ok && L.ok2[lane] != 0u && !Q.inf;
+        fe cc, c2;
+        lds_load_fe(cc, L.c, lane);
+        fp26 z2, cm, rhs, dlt;
+        fp26_sqr(z2, Q.Z);
+        fp26_from_plain(cm, cc);
+        fp26_mul(rhs, cm, z2);
+        fp26_sub<3>(dlt, rhs, Q.X);
+        bool match = fp26_is_zero(dlt);
+        const uint32_t carry = fe_add_k(c2, cc, ParamN2::M);
+        if (carry == 0u && fe_lt_k(c2, ParamP2::M)) {
+            fp26_from_plain(cm, c2);
+            fp26_mul(rhs, cm, z2);
+            fp26_sub<3>(dlt, rhs, Q.X);
+            match = match || fp26_is_zero(dlt);
+        }
+        ok = ok && match;
+        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = ok ? L.addr[k][lane] : 0u;
+        status[i] = ok ? 0 : 1;
+    }
+}
+int launch_tx_verify_small_sm2(const TxKernelPolicy& pol, const uint8_t* d_pre, const uint64_t* d_pre_off,
+                               const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash,
+                               uint8_t* d_sender, uint8_t* d_status, hipStream_t st) {
+    const dim3 grid(static_cast<unsigned>((n + 63) / 64));
+    if (pol.f26) {  // fp26 point arithmetic over the R'-domain 8-bit table
+        const uint32_t* t26;
+        const int rc = tables8_sm2_26(&t26);
+        if (rc) return rc;
+        hipLaunchKernelGGL(tx_verify_sm2_pair26_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n,
+                           t26, d_txhash, d_sender, d_status);
+    } else {
+        const uint32_t *k1, *sm2;
+        const int rc = tables8(&k1, &sm2);
+        if (rc) return rc;
+        hipLaunchKernelGGL(tx_verify_sm2_pair_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n,
+                           sm2, d_txhash, d_sender, d_status);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+}  // namespace bcosgpu

@@ -1,0 +1,383 @@
+// ecc_sig.hip -- one-lane signature kernels: secp256k1 recover, SM2 verify, known-key verify, the ecRecover
+// precompile, and the deterministic signing used to build synthetic batches; their launchers.
+#include "ecc_device.h"
+
+namespace bcosgpu {
+
+// ------------------------------------------------------------------ kernels
+template <bool F26>
+__global__ __launch_bounds__(256) void secp256k1_recover_kernel(const uint8_t* __restrict__ hash,
+                                                                const uint8_t* __restrict__ sig, uint32_t stride,
+                                                                uint64_t n, const uint32_t* __restrict__ tab, int tbits,
+                                                                uint8_t* __restrict__ pub, uint8_t* __restrict__ addr,
+                                                                uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe h, x, y;
+    load_be256_aligned(h, hash + 32 * i);
+    const bool ok = F26 ? secp256k1_recover_lane26(h, sig + static_cast<uint64_t>(stride) * i, 65u, CombTab{tab, tbits}, x, y)
+                        : secp256k1_recover_lane(h, sig + static_cast<uint64_t>(stride) * i, 65u, CombTab{tab, tbits}, x, y);
+    if (!ok) {
+        fe_zero(x);
+        fe_zero(y);
+    }
+    if (pub) {
+        store_be256(pub + 64 * i, x);
+        store_be256(pub + 64 * i + 32, y);
+    }
+    if (addr) {
+        uint32_t a[5] = {0, 0, 0, 0, 0};
+        if (ok) keccak_address(a, x, y);
+        uint32_t* o = reinterpret_cast<uint32_t*>(addr + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = a[k];
+    }
+    okout[i] = ok ? 1 : 0;
+}
+
+template <bool F26>
+__global__ __launch_bounds__(256) void sm2_verify_kernel(const uint8_t* __restrict__ hash,
+                                                         const uint8_t* __restrict__ sig, uint32_t stride,
+                                                         uint64_t n, const uint32_t* __restrict__ tab, int tbits,
+                                                         uint8_t* __restrict__ addr, uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe h, x, y;
+    load_be256_aligned(h, hash + 32 * i);
+    const bool ok = F26 ? sm2_verify_lane26(h, sig + static_cast<uint64_t>(stride) * i, 128u, CombTab{tab, tbits}, x, y)
+                        : sm2_verify_lane(h, sig + static_cast<uint64_t>(stride) * i, 128u, CombTab{tab, tbits}, x, y);
+    if (addr) {
+        uint32_t a[5] = {0, 0, 0, 0, 0};
+        if (ok) sm3_address(a, x, y);
+        uint32_t* o = reinterpret_cast<uint32_t*>(addr + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = a[k];
+    }
+    okout[i] = ok ? 1 : 0;
+}
+
+// SignatureCrypto::verify(pub, hash, sig) for a batch (sealer signatures: BlockValidator.cpp:141-182,
+// PBFTCacheProcessor.cpp:795-821).  SM2: SM2Crypto::verify reads the first 64 signature bytes (r || s)
+// and verifies against the GIVEN key (SM2Crypto.cpp:66-79); secp256k1: secp256k1_verify_lane.
+template <int SUITE, bool F26 = false>
+__global__ __launch_bounds__(256) void sig_verify_kernel(const uint8_t* __restrict__ pub,
+                                                         const uint8_t* __restrict__ hash,
+                                                         const uint8_t* __restrict__ sig, uint32_t stride,
+                                                         uint64_t n, const uint32_t* __restrict__ tab, int tbits,
+                                                         uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe h;
+    load_be256_aligned(h, hash + 32 * i);
+    const uint8_t* sg = sig + static_cast<uint64_t>(stride) * i;
+    bool ok;
+    if (SUITE == BCOSGPU_SUITE_SM2) {
+        ByteReader rs(sg, 64), rp(pub + 64 * i, 64);
+        uint32_t w[8], X[8], Y[8];
+        fe r, s, x, y;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rs.word(k);
+        fe_from_be_words(r, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rs.word(8 + k);
+        fe_from_be_words(s, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            X[k] = bswap32(rp.word(k));
+            Y[k] = bswap32(rp.word(8 + k));
+        }
+        if constexpr (F26) ok = sm2_verify_rs26(h, r, s, X, Y, CombTab{tab, tbits}, x, y);
+        else ok = sm2_verify_rs(h, r, s, X, Y, CombTab{tab, tbits}, x, y);
+    } else {
+        if constexpr (F26) ok = secp256k1_verify_lane26(h, sg, pub + 64 * i, CombTab{tab, tbits});
+        else ok = secp256k1_verify_lane(h, sg, pub + 64 * i, CombTab{tab, tbits});
+    }
+    okout[i] = ok ? 1 : 0;
+}
+
+// EVM ecRecover precompile (bcos-executor/src/vm/Precompiled.cpp:443-482) for a batch: input =
+// hash(32) || v(32) || r(32) || s(32); recid = (byte)(in[63] - 27) (the other 31 bytes of v are not
+// read); on success out = 12 zero bytes || right160(Keccak256(pub)), ok = 1; on failure the
+// precompile returns an empty output: out = zeros, ok = 0.
+template <bool F26>
+__global__ __launch_bounds__(256) void ecrecover_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                        const uint32_t* __restrict__ tab, int tbits,
+                                                        uint8_t* __restrict__ out, uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* p = in + 128 * i;
+    fe h, r, s, x, y;
+    load_be256_aligned(h, p);
+    load_be256_aligned(r, p + 64);
+    load_be256_aligned(s, p + 96);
+    const uint32_t v = (reinterpret_cast<const uint32_t*>(p)[15] >> 24) - 27u;
+    const bool ok = F26 ? secp256k1_recover_rsv26(h, r, s, v & 0xffu, CombTab{tab, tbits}, x, y)
+                        : secp256k1_recover_rsv(h, r, s, v & 0xffu, CombTab{tab, tbits}, x, y);
+    uint32_t a[5] = {0, 0, 0, 0, 0};
+    if (ok) keccak_address(a, x, y);
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + 32 * i);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o[k] = 0u;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[3 + k] = a[k];
+    okout[i] = ok ? 1 : 0;
+}
+
+// Key derivation + deterministic ECDSA signing, libsecp256k1 conventions (low-S, recid).
+// k = Keccak256(sk || hash) mod n.
+__global__ __launch_bounds__(256) void secp256k1_sign_kernel(const uint8_t* __restrict__ sk32,
+                                                             const uint8_t* __restrict__ hash32, uint64_t n,
+                                                             const uint32_t* __restrict__ tab, int tbits,
+                                                             uint8_t* __restrict__ pub, uint8_t* __restrict__ sigout,
+                                                             uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4* skw = reinterpret_cast<const uint4*>(sk32 + 32 * i);
+    const uint4* hw = reinterpret_cast<const uint4*>(hash32 + 32 * i);
+    const uint4 s0 = skw[0], s1 = skw[1], h0 = hw[0], h1 = hw[1];
+    const uint32_t m[16] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w,
+                            h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    fe d, e, k;
+    fe_from_be_words(d, m);
+    fe_from_be_words(e, m + 8);
+    uint32_t kd[8];
+    keccak256_64(m, kd);
+    fe_from_be_words(k, kd);
+    reduce_once(k, ParamN1::M);
+    reduce_once(e, ParamN1::M);
+    bool ok = !fe_is_zero_raw(d) && fe_lt_k(d, ParamN1::M) && !fe_is_zero_raw(k);
+    Jac P, R;
+    Aff PA, RA;
+    comb_mul_rt<CurveK1>(P, d, tab, tbits);
+    comb_mul_rt<CurveK1>(R, k, tab, tbits);
+    CurveK1::to_aff(PA, P);
+    CurveK1::to_aff(RA, R);
+    FieldK1::normalize(PA.x);
+    FieldK1::normalize(PA.y);
+    FieldK1::normalize(RA.x);
+    FieldK1::normalize(RA.y);
+    uint32_t recid = RA.y.v[0] & 1u;
+    fe r;
+    fe_copy(r, RA.x);
+    if (!fe_lt_k(r, ParamN1::M)) recid |= 2u;
+    reduce_once(r, ParamN1::M);
+    ok = ok && !fe_is_zero_raw(r);
+    // s = k^-1 (e + r d) mod n
+    fe km, kinv, dm, rd, t, s;
+    fe kk = k;
+    if (fe_is_zero_raw(kk)) kk.v[0] = 1;
+    FieldN1::from_plain(km, kk);
+    FieldInv<FieldN1>::inv(kinv, km);
+    FieldN1::from_plain(dm, d);
+    FieldN1::mul(rd, r, dm);
+    FieldN1::add(t, e, rd);
+    FieldN1::mul(s, t, kinv);
+    ok = ok && !fe_is_zero_raw(s);
+    fe half;
+    fe_set(half, kN1Half);
+    if (fe_lt(half, s)) {
+        FieldN1::neg(s, s);
+        recid ^= 1u;
+    }
+    store_be256(pub + 64 * i, PA.x);
+    store_be256(pub + 64 * i + 32, PA.y);
+    uint8_t* so = sigout + 65 * i;
+    uint32_t rw[8], sw[8];
+    fe_to_be_words(rw, r);
+    fe_to_be_words(sw, s);
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+        so[q] = static_cast<uint8_t>(rw[q >> 2] >> ((q & 3) * 8));
+        so[32 + q] = static_cast<uint8_t>(sw[q >> 2] >> ((q & 3) * 8));
+    }
+    so[64] = static_cast<uint8_t>(recid);
+    okout[i] = ok ? 1 : 0;
+}
+
+// SM2 key derivation + signing (GB/T 32918.2), k = SM3(sk || hash) mod n; sig = r || s || pub.
+__global__ __launch_bounds__(256) void sm2_sign_kernel(const uint8_t* __restrict__ sk32,
+                                                       const uint8_t* __restrict__ hash32, uint64_t n,
+                                                       const uint32_t* __restrict__ tab, int tbits,
+                                                       uint8_t* __restrict__ sigout, uint8_t* __restrict__ okout) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe d, h;
+    load_be256_aligned(d, sk32 + 32 * i);
+    load_be256_aligned(h, hash32 + 32 * i);
+    // k = SM3(sk || hash)
+    uint32_t W[16], V[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        W[j] = d.v[7 - j];
+        W[8 + j] = h.v[7 - j];
+    }
+    sm3_init(V);
+    sm3_compress(V, W);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) W[j] = 0;
+    W[0] = 0x80000000u;
+    W[15] = 512u;
+    sm3_compress(V, W);
+    fe k;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) k.v[j] = V[7 - j];
+    reduce_once(k, ParamN2::M);
+    fe nm1;
+    fe_set(nm1, ParamN2::M);
+    nm1.v[0] -= 1;  // n - 1 (low limb of n is odd and > 0)
+    bool ok = !fe_is_zero_raw(d) && fe_lt(d, nm1) && !fe_is_zero_raw(k);
+    Jac P, K;
+    Aff PA, KA;
+    comb_mul_rt<CurveSM2>(P, d, tab, tbits);
+    comb_mul_rt<CurveSM2>(K, k, tab, tbits);
+    CurveSM2::to_aff(PA, P);
+    CurveSM2::to_aff(KA, K);
+    fe px, py, x1;
+    FieldP2::to_plain(px, PA.x);
+    FieldP2::to_plain(py, PA.y);
+    FieldP2::to_plain(x1, KA.x);
+    uint32_t X[8], Y[8], eb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        X[j] = px.v[7 - j];
+        Y[j] = py.v[7 - j];
+    }
+    sm2_e(eb, X, Y, h);
+    fe e;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e.v[j] = eb[7 - j];
+    reduce_once(e, ParamN2::M);
+    reduce_once(x1, ParamN2::M);
+    fe r, t, s;
+    FieldN2::add(r, e, x1);
+    ok = ok && !fe_is_zero_raw(r);
+    FieldN2::add(t, r, k);
+    ok = ok && !fe_is_zero_raw(t);
+    fe one, dp1, dm, inv, rd;
+    fe_zero(one);
+    one.v[0] = 1;
+    FieldN2::add(dp1, d, one);
+    if (fe_is_zero_raw(dp1)) dp1.v[0] = 1;
+    FieldN2::from_plain(dm, dp1);
+    FieldInv<FieldN2>::inv(inv, dm);
+    fe dmm;
+    FieldN2::from_plain(dmm, d);
+    FieldN2::mul(rd, r, dmm);
+    FieldN2::sub(t, k, rd);
+    FieldN2::mul(s, t, inv);
+    ok = ok && !fe_is_zero_raw(s);
+    uint8_t* so = sigout + 128 * i;
+    uint32_t w[8];
+    const fe* parts[4] = {&r, &s, &px, &py};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        fe_to_be_words(w, *parts[p]);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) reinterpret_cast<uint32_t*>(so + 32 * p)[q] = w[q];
+    }
+    okout[i] = ok ? 1 : 0;
+}
+
+int launch_secp256k1_recover(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride, uint64_t n,
+                             uint8_t* d_pub, uint8_t* d_addr, uint8_t* d_ok, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
+    if (rc) return rc;
+    if (tx_policy().f26)
+        hipLaunchKernelGGL(secp256k1_recover_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n,
+                           k1, bits, d_pub, d_addr, d_ok);
+    else
+        hipLaunchKernelGGL(secp256k1_recover_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n,
+                           k1, bits, d_pub, d_addr, d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_sm2_verify(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride, uint64_t n, uint8_t* d_addr,
+                      uint8_t* d_ok, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
+    if (rc) return rc;
+    if (tx_policy().f26) {
+        const uint32_t* t26;
+        int b26;
+        rc = tables_sm2_26(&t26, &b26);
+        if (rc) return rc;
+        hipLaunchKernelGGL(sm2_verify_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, t26,
+                           b26, d_addr, d_ok);
+    } else {
+        hipLaunchKernelGGL(sm2_verify_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, sm2,
+                           bits, d_addr, d_ok);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+// Signing exists to build the synthetic benchmark / test batches on the device.  It is NOT
+// constant-time (the comb gather address depends on secret key and nonce bits): test use only.
+int launch_secp256k1_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint8_t* d_pub, uint8_t* d_sig,
+                          uint8_t* d_ok, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
+    if (rc) return rc;
+    if (!d_pub) return BCOSGPU_E_ARG;
+    hipLaunchKernelGGL(secp256k1_sign_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_sk, d_hash, n, k1, bits, d_pub,
+                       d_sig, d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_sm2_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint8_t* d_sig, uint8_t* d_ok,
+                    hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
+    if (rc) return rc;
+    hipLaunchKernelGGL(sm2_sign_kernel, dim3(grid_of(n)), dim3(256), 0, st, d_sk, d_hash, n, sm2, bits, d_sig, d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
+                      uint64_t n, uint8_t* d_ok, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
+    if (rc) return rc;
+    if (suite == BCOSGPU_SUITE_SM2 && tx_policy().f26) {
+        const uint32_t* t26;
+        int b26;
+        rc = tables_sm2_26(&t26, &b26);
+        if (rc) return rc;
+        hipLaunchKernelGGL((sig_verify_kernel<BCOSGPU_SUITE_SM2, true>), dim3(grid_of(n)), dim3(256), 0, st, d_pub,
+                           d_hash, d_sig, stride, n, t26, b26, d_ok);
+    } else if (suite == BCOSGPU_SUITE_SM2)
+        hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SM2>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash, d_sig,
+                           stride, n, sm2, bits, d_ok);
+    else if (tx_policy().f26)
+        hipLaunchKernelGGL((sig_verify_kernel<BCOSGPU_SUITE_SECP256K1, true>), dim3(grid_of(n)), dim3(256), 0, st, d_pub,
+                           d_hash, d_sig, stride, n, k1, bits, d_ok);
+    else
+        hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SECP256K1>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash,
+                           d_sig, stride, n, k1, bits, d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int launch_ecrecover(const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint8_t* d_ok, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int bits;
+    int rc = tables(&k1, &sm2, &bits);
+    if (rc) return rc;
+    if (tx_policy().f26)
+        hipLaunchKernelGGL(ecrecover_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, d_in, n, k1, bits, d_out, d_ok);
+    else
+        hipLaunchKernelGGL(ecrecover_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, d_in, n, k1, bits, d_out, d_ok);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+}  // namespace bcosgpu

@@ -2,7 +2,8 @@
 // tx_verify_coop26_kernel's) workgroup 0 on a
 // 10k-tx batch of random inputs (the schedule is input-independent), to see where C2's latency goes.
 #define BCOSGPU_COOP_TIMING 1
-#include "../csrc/ecc_kernels.hip"
+#include "../csrc/ecc_tables.hip"
+#include "../csrc/ecc_coop.hip"
 #include <cstdio>
 #include <vector>
 
