@@ -102,10 +102,12 @@ def _kernel_name(suite, n):
     f26 = os.environ.get("BCOSGPU_K1_F26", "1") != "0"
     split = os.environ.get("BCOSGPU_TXV_SPLIT")
     small = (split == "1") if split in ("0", "1") else n <= (1 << 15)
-    coop = os.environ.get("BCOSGPU_TXV_COOP", "1") != "0"
+    coop = {"0": 0, "1": 1}.get(os.environ.get("BCOSGPU_TXV_COOP", "2"), 2)
     if suite == 0 and small:
         if not coop:
             return "tx_verify_split_kernel"
+        if coop == 2 and f26:
+            return "tx_verify_trio26_kernel"
         return "tx_verify_coop26_kernel" if f26 else "tx_verify_coop_kernel"
     if suite == 1 and small and coop:
         return "tx_verify_sm2_pair26_kernel" if f26 else "tx_verify_sm2_pair_kernel"

@@ -123,7 +123,7 @@ def ensure_device(device=0):
         _inited.add(device)
 
 
-def set_tx_kernel_policy(split=-1, occupancy=0, coop=1, field=1):
+def set_tx_kernel_policy(split=-1, occupancy=0, coop=2, field=1):
     """bcosgpu_set_tx_kernel_policy: force a tx-verify kernel variant (tests / tuning); the defaults
     restore the size-based choice (field 1: the 10 x 26-bit secp256k1 point arithmetic)."""
     check(lib().bcosgpu_set_tx_kernel_policy(split, occupancy, coop, field))

@@ -1,0 +1,288 @@
+// ec26_trio.h -- secp256k1 point doubling and mixed addition split over a lane TRIO: three adjacent
+// lanes of one wave (positions 3t, 3t + 1, 3t + 2 of a 16-lane DPP row; position 15 is a phantom
+// role-0 lane whose results are never used) cooperate on ONE point, each lane computing one of the
+// independent field multiplications of a dependency level.  Operands are routed between the lanes of
+// a trio by DPP row shifts (row_shr / row_shl by 1 or 2) and per-role selects, so a level costs one
+// multiplication of latency and no barrier and no LDS round trip -- the wave-pair split of
+// coop26_dbl / coop26_madd (ecc_coop.hip) paid a __syncthreads and an LDS write + read per level.
+//
+// Every lane executes the same instruction stream (a wave has one program counter): a level is one
+// fe26_mul / fe26_sqr whose operands are chosen per role, so the split must give all roles the same
+// operation at each level.  The formulas are CurveK1x's (ec26.h) with the same magnitudes:
+//
+//   dbl (3 levels):  L1  A = X^2          | B = Y^2            | B = Y^2   (redundant)
+//                    L2  F = (3A)^2       | C = B^2            | XB = X B
+//                    L3  --               | E (D - X3)         | Y Z       (lane 1 gathers E, F, XB)
+//                    D = 4 XB, X3 = F - 2D, Y3 = E (D - X3) - 8C, Z3 = 2 Y Z
+//   madd (5 levels): L1  Z^2              | y2 Z               | Z^2
+//                    L2  U2 = x2 Z^2      | S2 = y2 Z Z^2      | U2
+//                    L3  HH = H^2         | rr^2               | Z H       (H = U2 - X, rr = S2 - Y)
+//                    L4  J = H I          | --                 | V = X I   (I = 4 HH)
+//                    L5  rr (V - X3)      | Y J                | --
+//                    X3 = 4 rr^2 - J - 2V, Y3 = 2 (rr (V - X3) - Y J), Z3 = 2 Z H
+//
+// A point lives in the trio as TrioPt: S1 = (X | Y | Y) (the first doubling level's operand), Xs = X
+// and Zs = Z on lane 2 (lanes 0 and 1 hold don't-care values there), inf on every lane.  Magnitudes:
+// dbl -> (10, 10, 2), madd -> (9, 6, 2), as CurveK1x.
+#pragma once
+#include "ec26.h"
+
+#ifndef TRIO_DUMP
+#define TRIO_DUMP(slot, a) ((void)0)
+#endif
+
+namespace bcosgpu {
+
+struct TrioPt {
+    fe26 S1, Xs, Zs;
+    bool inf;
+};
+
+// lane role inside its trio and the three role predicates
+struct TrioLane {
+    bool r0, r1, r2;
+    F26_HD explicit TrioLane(int lane) {
+        const int role = (lane & 15) % 3;
+        r0 = role == 0;
+        r1 = role == 1;
+        r2 = role == 2;
+    }
+};
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// host emulation of a DPP row (tests/cpp/trio_test.cpp runs the 16 lanes of a row as threads)
+uint32_t trio_emu_dpp(uint32_t x, int ctrl);
+bool trio_emu_any(bool b);
+#endif
+
+namespace trio {
+// DPP fetches inside a 16-lane row: L1 / L2 = the value of lane i - 1 / i - 2 (row_shr), R1 / R2 = of
+// lane i + 1 / i + 2 (row_shl); out-of-row sources read 0 (bound_ctrl), which only phantom lanes see
+template <int CTRL>
+F26_HD uint32_t dpp(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(x), CTRL, 0xf, 0xf, true));
+#else
+    return trio_emu_dpp(x, CTRL);
+#endif
+}
+F26_HD bool any(bool b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __any(b);
+#else
+    return trio_emu_any(b);
+#endif
+}
+constexpr int kL1 = 0x111, kL2 = 0x112, kR1 = 0x101, kR2 = 0x102;
+
+// the magnitude of a fetched element travels with it in the checking build (a phantom lane's zero
+// reads as magnitude 1)
+#ifdef FE26_CHECK
+template <int CTRL>
+F26_HD int mdpp(int m) {
+    const int r = static_cast<int>(dpp<CTRL>(static_cast<uint32_t>(m)));
+    return r ? r : 1;
+}
+#endif
+
+template <int CTRL>
+F26_HD void fdpp(fe26& r, const fe26& a) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) r.v[i] = dpp<CTRL>(a.v[i]);
+    F26_SETM(r, mdpp<CTRL>(a.m));
+}
+// A DPP read needs two wait states after the VALU write of its source VGPR (gfx9 rule).  The compiler
+// pads its own code, but not the boundary after an inline-asm block (fe26_mul_asm / fe26_sqr_asm end
+// with VALU writes of their result limbs), so every product a lane may fetch goes through these: the
+// s_nop names the limbs as in/out operands, so any later DPP read of them is ordered after it.
+F26_HD void dpp_fence(fe26& r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("s_nop 1"
+                 : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+                   "+v"(r.v[6]), "+v"(r.v[7]), "+v"(r.v[8]), "+v"(r.v[9]));
+#else
+    (void)r;
+#endif
+}
+F26_HD void mul(fe26& r, const fe26& a, const fe26& b) {
+    fe26_mul(r, a, b);
+    dpp_fence(r);
+}
+F26_HD void sqr(fe26& r, const fe26& a) {
+    fe26_sqr(r, a);
+    dpp_fence(r);
+}
+F26_HD void sel(fe26& r, bool c, const fe26& a, const fe26& b) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+    F26_SETM(r, c ? a.m : b.m);
+}
+// c ? a : (d ? DPP<C1>(b) : DPP<C2>(b))
+template <int C1, int C2>
+F26_HD void sel_dpp2(fe26& r, bool c, const fe26& a, bool d, const fe26& b) {
+#ifdef FE26_CHECK
+    const int m1 = mdpp<C1>(b.m), m2 = mdpp<C2>(b.m);
+#endif
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t x = dpp<C1>(b.v[i]), y = dpp<C2>(b.v[i]);
+        r.v[i] = c ? a.v[i] : (d ? x : y);
+    }
+    F26_SETM(r, c ? a.m : d ? m1 : m2);
+}
+F26_HD uint32_t bdpp_from(uint32_t f, const TrioLane& T, int src) {
+    // the value of f held by role src of this lane's trio
+    const uint32_t l1 = dpp<kL1>(f), l2 = dpp<kL2>(f), r1 = dpp<kR1>(f), r2 = dpp<kR2>(f);
+    if (src == 0) return T.r0 ? f : T.r1 ? l1 : l2;
+    if (src == 1) return T.r1 ? f : T.r0 ? r1 : l1;
+    return T.r2 ? f : T.r1 ? r1 : r2;
+}
+}  // namespace trio
+
+F26_HD void trio_from_aff(TrioPt& P, const Aff26& Q, const TrioLane& T) {
+    trio::sel(P.S1, T.r0, Q.x, Q.y);
+    fe26_copy(P.Xs, Q.x);
+    fe26_one(P.Zs);
+    P.inf = false;
+}
+F26_HD void trio_set_inf(TrioPt& P) {
+    fe26_zero(P.S1);
+    fe26_zero(P.Xs);
+    fe26_zero(P.Zs);
+    P.inf = true;
+}
+F26_HD void trio_cmov(TrioPt& P, const TrioPt& Q, bool c) {
+    fe26_cmov(P.S1, Q.S1, c);
+    fe26_cmov(P.Xs, Q.Xs, c);
+    fe26_cmov(P.Zs, Q.Zs, c);
+    P.inf = c ? Q.inf : P.inf;
+}
+// the full Jacobian point on every lane of the trio (X from lane 0, Y from lane 1, Z from lane 2)
+F26_HD void trio_to_jac(Jac26& J, const TrioPt& P, const TrioLane& T) {
+    using namespace trio;
+    sel_dpp2<kL1, kL2>(J.X, T.r0, P.S1, T.r1, P.S1);   // lane 1 <- lane 0, lane 2 <- lane 0
+    sel_dpp2<kR1, kL1>(J.Y, T.r1, P.S1, T.r0, P.S1);   // lane 0 <- lane 1, lane 2 <- lane 1
+    sel_dpp2<kR1, kR2>(J.Z, T.r2, P.Zs, T.r1, P.Zs);   // lane 1 <- lane 2, lane 0 <- lane 2
+    J.inf = P.inf;
+}
+
+// P <- 2P  (X, Y <= 10, Z <= 16 -> (10, 10, 2))
+F26_HD void trio_dbl(TrioPt& P, const TrioLane& T) {
+    using namespace trio;
+    fe26 o1, T2, S2, o2, E, F, XB, D, X3, W, P3, Q3, o3, C8, Y3, t;
+    sqr(o1, P.S1);                                       // (A | B | B)                 m 1
+#pragma unroll
+    for (int i = 0; i < 10; ++i) T2.v[i] = o1.v[i] + (T.r0 ? o1.v[i] << 1 : 0u);  // (3A | B | B) m <= 3
+    F26_SETM(T2, T.r0 ? 3 : 1);
+    sel(S2, T.r2, P.Xs, T2);                             // (3A | B | X)                m <= 10
+    mul(o2, S2, T2);                                     // (F | C | XB)
+    fdpp<kL1>(E, T2);                                    // lane 1: E = 3A              m 3
+    fdpp<kL1>(F, o2);                                    // lane 1: F                   m 1
+    fdpp<kR1>(XB, o2);                                   // lane 1: X B                 m 1
+    fe26_mul_int<4>(D, XB);                              // D = 4 X B                   m 4
+    fe26_mul_int<2>(t, D);                               //                             m 8
+    fe26_sub<9>(X3, F, t);                               // X3 = F - 2D                 m 10
+    fe26_sub<11>(W, D, X3);                              // D - X3                      m 15
+    sel(P3, T.r2, P.S1, E);                              // lane 1: E, lane 2: Y
+    sel(Q3, T.r2, P.Zs, W);                              // lane 1: D - X3, lane 2: Z
+    mul(o3, P3, Q3);                                     // (- | E (D - X3) | Y Z)
+    fe26_mul_int<8>(C8, o2);                             // lane 1: 8C                  m 8
+    fe26_sub<9>(Y3, o3, C8);                             // lane 1: Y3                  m 10
+    fe26_mul_int<2>(P.Zs, o3);                           // lane 2: Z3 = 2 Y Z          m 2
+    // next state: S1 = (X3 | Y3 | Y3) from lane 1, Xs = X3 on lane 2
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t x0 = dpp<kR1>(X3.v[i]), y2 = dpp<kL1>(Y3.v[i]);
+        P.S1.v[i] = T.r0 ? x0 : T.r1 ? Y3.v[i] : y2;    // lane 0 <- X3, lane 2 <- Y3 of lane 1
+        P.Xs.v[i] = dpp<kL1>(X3.v[i]);                   // lane 2 <- X3 of lane 1
+    }
+#ifdef FE26_CHECK
+    {
+        const int mx0 = mdpp<kR1>(X3.m), my2 = mdpp<kL1>(Y3.m), mx2 = mdpp<kL1>(X3.m);
+        P.S1.m = T.r0 ? mx0 : T.r1 ? Y3.m : my2;
+        P.Xs.m = mx2;
+    }
+#endif
+}
+
+// R <- P + Q, Q affine (x, y <= 2) and never infinity; P: X, Y <= 10, Z <= 16 -> (9, 6, 2).  The
+// exceptional cases are those of CurveK1x::madd: P = Q doubles (computed on lane 2, which holds all of
+// P), P = -Q gives infinity, P = infinity gives Q.
+F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane& T) {
+    using namespace trio;
+    fe26 Zb, P1, o1, P2, Q2, o2, Xl, h, P3, o3, HHx, I, P4, o4, R2, V, X3, W, rr, P5, Q5, J1, o5, Y3, t;
+    sel_dpp2<kR1, kR2>(Zb, T.r2, P.Zs, T.r1, P.Zs);     // Z on every lane
+    sel(P1, T.r1, Q.y, Zb);
+    mul(o1, P1, Zb);                                     // (Z1Z1 | y2 Z | Z1Z1)
+    TRIO_DUMP(0, o1);
+    sel(P2, T.r1, o1, Q.x);
+    fdpp<kR1>(Q2, o1);
+    sel(Q2, T.r1, Q2, o1);                               // lane 1: Z1Z1 of lane 2
+    mul(o2, P2, Q2);                                     // (U2 | S2 | U2)
+    TRIO_DUMP(1, o2);
+    sel(Xl, T.r2, P.Xs, P.S1);                           // (X | Y | X)                 m <= 10
+    fe26_sub<11>(h, o2, Xl);                             // (H | rr | H)                m 12
+    sel(P3, T.r2, Zb, h);
+    mul(o3, P3, h);                                      // (HH | rr^2 | Z H)
+    TRIO_DUMP(2, h);
+    TRIO_DUMP(3, o3);
+    fdpp<kL2>(HHx, o3);
+    sel(HHx, T.r2, HHx, o3);                             // lanes 0, 2: HH
+    fe26_mul_int<4>(I, HHx);                             // I = 4 HH                    m 4
+    sel(P4, T.r2, P.Xs, h);
+    mul(o4, P4, I);                                      // (J | - | V)
+    TRIO_DUMP(4, o4);
+    // lane 0: X3 = 4 rr^2 - J - 2V and V - X3
+    fdpp<kR1>(R2, o3);
+    fe26_mul_int<4>(R2, R2);                             // 4 rr^2                      m 4
+    fdpp<kR2>(V, o4);                                    // V of lane 2                 m 1
+    fe26_sub<2>(X3, R2, o4);                             //                             m 6
+    fe26_mul_int<2>(t, V);                               //                             m 2
+    fe26_sub<3>(X3, X3, t);                              // X3                          m 9
+    fe26_sub<10>(W, V, X3);                              // V - X3                      m 11
+    fdpp<kR1>(rr, h);                                    // lane 0: rr                  m 12
+    sel(P5, T.r0, rr, P.S1);                             // lane 0: rr, lane 1: Y
+    fdpp<kL1>(J1, o4);                                   // lane 1: J of lane 0
+    sel(Q5, T.r0, W, J1);
+    mul(o5, P5, Q5);                                     // (rr (V - X3) | Y J | -)
+    TRIO_DUMP(5, o5);
+    TRIO_DUMP(6, X3);
+    fdpp<kR1>(t, o5);
+    fe26_sub<2>(Y3, o5, t);                              //                             m 3
+    fe26_mul_int<2>(Y3, Y3);                             // lane 0: Y3                  m 6
+    TRIO_DUMP(7, Y3);
+    // exceptional cases (flags shared across the trio)
+    const uint32_t zf = fe26_is_zero(h) ? 1u : 0u;
+    const bool hz = bdpp_from(zf, T, 0) != 0u && !P.inf;
+    const bool rz = bdpp_from(zf, T, 1) != 0u;
+    TrioPt O;
+    sel_dpp2<kL1, kL2>(O.S1, T.r0, X3, T.r1, Y3);      // (X3 | Y3 | Y3) from lane 0
+    fdpp<kL2>(O.Xs, X3);                                 // lane 2 <- X3 of lane 0
+    fe26_mul_int<2>(O.Zs, o3);                           // lane 2: Z3 = 2 Z H          m 2
+    O.inf = false;
+    if (any(hz && rz)) {                               // P == Q: double on lane 2 (rare)
+        Jac26 A, D;
+        fe26_copy(A.X, P.Xs);
+        fe26_copy(A.Y, P.S1);
+        fe26_copy(A.Z, P.Zs);
+        A.inf = P.inf;
+        CurveK1x::dbl(D, A);
+        TrioPt Dt;
+        sel_dpp2<kR2, kR1>(Dt.S1, T.r2, D.Y, T.r0, D.X);  // lane 0 <- X, lane 1 <- Y of lane 2
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            const uint32_t y = dpp<kR1>(D.Y.v[i]);
+            Dt.S1.v[i] = T.r1 ? y : Dt.S1.v[i];
+        }
+        F26_SETM(Dt.S1, 10);
+        fe26_copy(Dt.Xs, D.X);
+        fe26_copy(Dt.Zs, D.Z);
+        Dt.inf = false;
+        trio_cmov(O, Dt, hz && rz);
+    }
+    if (hz && !rz) O.inf = true;                         // P == -Q
+    if (P.inf) trio_from_aff(O, Q, T);
+    R = O;
+}
+
+}  // namespace bcosgpu

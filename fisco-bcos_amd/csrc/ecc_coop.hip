@@ -1,6 +1,9 @@
-// ecc_coop.hip -- small-batch secp256k1 tx verify: the 4-wave split kernel and the cooperative-pair kernels
-// (8 x 32 and fe26 point arithmetic).
+// ecc_coop.hip -- small-batch secp256k1 tx verify: the 4-wave split kernel, the cooperative-pair kernels
+// (8 x 32 and fe26 point arithmetic) and the lane-trio kernel.  Built with the DPP combiner off
+// (Makefile): folding the trio's DPP fetches into VOP2 arithmetic gave wrong sums on gfx950
+// (tools/triobench.hip reproduces it: v_subrev_u32_dpp in the mixed addition).
 #include "ecc_device.h"
+#include "ec26_trio.h"
 
 namespace bcosgpu {
 
@@ -996,18 +999,46 @@ __device__ __forceinline__ void lds_store_fe26(uint32_t (*dst)[64], const fe26& 
     lds_store_fe(dst, w, lane);
 }
 
-__global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t* __restrict__ pre,
-                                                                  const uint64_t* __restrict__ pre_off,
-                                                                  const uint8_t* __restrict__ sig,
-                                                                  const uint64_t* __restrict__ sig_off, uint64_t n,
-                                                                  const uint32_t* __restrict__ tab,
-                                                                  uint8_t* __restrict__ txhash,
-                                                                  uint8_t* __restrict__ sender,
-                                                                  uint8_t* __restrict__ status) {
+// ------------------------------------------------------------------ lane-trio phase C
+// The GLV chains of the trio kernel: wave w runs chain w & 1 for txs 20 (w >> 1) .. 20 (w >> 1) + 19
+// of the workgroup, one trio (three adjacent lanes, ec26_trio.h) per tx; lane position p of DPP row r
+// is trio p / 3 (p = 15 a phantom that mirrors trio 4 and stores nothing).
+__device__ __forceinline__ void trio_add_digit(TrioPt& acc, const Coop26Lds& L, int tl, int d, bool neg, bool phi,
+                                               const TrioLane& T) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &L.tab[0][0][0] + m * (16 * 64) + tl;
+    const uint32_t* bx = phi ? &L.tabphx[0][0][0] + m * (8 * 64) + tl : base;
+    Aff26 S;
+    {
+        uint32_t x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            x[k] = bx[k * 64];
+            y[k] = base[(8 + k) * 64];
+        }
+        fe26_from_words(S.x, x);
+        fe26_from_words(S.y, y);
+    }
+    fe26 ny;
+    fe26_neg<2>(ny, S.y);
+    fe26_cmov(S.y, ny, (d < 0) != neg);
+    TrioPt R;
+    trio_madd(R, acc, S, T);
+    trio_cmov(acc, R, d != 0);
+}
+
+// TRIO = false: tx_verify_coop26_kernel (64 txs per workgroup, wave-pair chains); TRIO = true:
+// tx_verify_trio26_kernel (40 txs per workgroup, lane-trio chains).  Phases A and D are the same code.
+template <bool TRIO>
+__device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, const uint64_t* __restrict__ pre_off,
+                                            const uint8_t* __restrict__ sig, const uint64_t* __restrict__ sig_off,
+                                            uint64_t n, const uint32_t* __restrict__ tab, uint8_t* __restrict__ txhash,
+                                            uint8_t* __restrict__ sender, uint8_t* __restrict__ status) {
+    constexpr int TPW = TRIO ? 40 : 64;  // txs per workgroup
     __shared__ Coop26Lds L;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
-    const bool active = i < n;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * TPW + lane;
+    const bool active = lane < TPW && i < n;
     COOP_T(0);
     uint64_t sa = 0, sb = 0, pa = 0, pb = 0;
     if (active) {
@@ -1135,40 +1166,69 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t*
     COOP_T(1);
     __syncthreads();
     // ---------------------------------------------------------------- phase C: two cooperative GLV chains
-    const uint32_t flags = L.flags[lane] | L.rflag[lane];
-    Coop26Ctx c{&L, wave >> 1, wave & 1, lane, false};
-    fe k;
-    fe_zero(k);
+    if constexpr (TRIO) {
+        const TrioLane T(lane);
+        const int pos = lane & 15, trio_idx = pos / 3;
+        const int chain = wave & 1, tl = (wave >> 1) * 20 + (lane >> 4) * 5 + (trio_idx < 5 ? trio_idx : 4);
+        const uint32_t tflags = L.flags[tl] | L.rflag[tl];
+        fe k;
+        fe_zero(k);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) k.v[q] = L.k[c.chain][q][lane];
-    const bool neg = c.chain == 0 ? (flags & 4u) != 0 : (flags & 8u) != 0;
-    const bool phi = c.chain == 1;
-    Jac26 acc;
-    CurveK1x::set_inf(acc);
-    coop26_add_digit(acc, c, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
+        for (int q = 0; q < 4; ++q) k.v[q] = L.k[chain][q][tl];
+        const bool neg = chain == 0 ? (tflags & 4u) != 0 : (tflags & 8u) != 0;
+        const bool phi = chain == 1;
+        TrioPt acc;
+        trio_set_inf(acc);
+        trio_add_digit(acc, L, tl, static_cast<int>(k.v[3] >> 31), neg, phi, T);  // digit 32 = bit 127
 #pragma unroll 1
-    for (int w = 31; w >= 0; --w) {
-        coop26_dbl<0>(acc, c);
-#ifdef BCOSGPU_COOP_TIMING
-        c.probe = blockIdx.x == 0 && w == 20;
-#endif
-        coop26_dbl<3>(acc, c);
-#ifdef BCOSGPU_COOP_TIMING
-        c.probe = false;
-        if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][5] = clock64();
-#endif
-        coop26_dbl<0>(acc, c);
-        coop26_dbl<3>(acc, c);
-#ifdef BCOSGPU_COOP_TIMING
-        if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][6] = clock64();
-#endif
-        coop26_add_digit(acc, c, booth_digit128(k), neg, phi);
-#ifdef BCOSGPU_COOP_TIMING
-        if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][7] = clock64();
-#endif
+        for (int w = 31; w >= 0; --w) {
+            trio_dbl(acc, T);
+            trio_dbl(acc, T);
+            trio_dbl(acc, T);
+            trio_dbl(acc, T);
+            trio_add_digit(acc, L, tl, booth_digit128(k), neg, phi, T);
+        }
+        COOP_T(2);
+        Jac26 J;
+        trio_to_jac(J, acc, T);
+        if (T.r0 && trio_idx < 5) coop26_store_jac(L.pt[chain], J, tl);
     }
-    COOP_T(2);
-    if (c.role == 0) coop26_store_jac(L.pt[c.chain], acc, lane);
+    const uint32_t flags = L.flags[lane] | L.rflag[lane];
+    if constexpr (!TRIO) {
+        Coop26Ctx c{&L, wave >> 1, wave & 1, lane, false};
+        fe k;
+        fe_zero(k);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) k.v[q] = L.k[c.chain][q][lane];
+        const bool neg = c.chain == 0 ? (flags & 4u) != 0 : (flags & 8u) != 0;
+        const bool phi = c.chain == 1;
+        Jac26 acc;
+        CurveK1x::set_inf(acc);
+        coop26_add_digit(acc, c, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
+#pragma unroll 1
+        for (int w = 31; w >= 0; --w) {
+            coop26_dbl<0>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+            c.probe = blockIdx.x == 0 && w == 20;
+#endif
+            coop26_dbl<3>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+            c.probe = false;
+            if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][5] = clock64();
+#endif
+            coop26_dbl<0>(acc, c);
+            coop26_dbl<3>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+            if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][6] = clock64();
+#endif
+            coop26_add_digit(acc, c, booth_digit128(k), neg, phi);
+#ifdef BCOSGPU_COOP_TIMING
+            if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][7] = clock64();
+#endif
+        }
+        COOP_T(2);
+        if (c.role == 0) coop26_store_jac(L.pt[c.chain], acc, lane);
+    }
     __syncthreads();
     // ---------------------------------------------------------------- phase D (on fe26 as well)
     if (wave == 1) {  // G part: partials 0 + 1 + 2
@@ -1220,6 +1280,33 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t*
     }
     COOP_T(3);
 }
+
+__global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t* __restrict__ pre,
+                                                                  const uint64_t* __restrict__ pre_off,
+                                                                  const uint8_t* __restrict__ sig,
+                                                                  const uint64_t* __restrict__ sig_off, uint64_t n,
+                                                                  const uint32_t* __restrict__ tab,
+                                                                  uint8_t* __restrict__ txhash,
+                                                                  uint8_t* __restrict__ sender,
+                                                                  uint8_t* __restrict__ status) {
+    coop26_body<false>(pre, pre_off, sig, sig_off, n, tab, txhash, sender, status);
+}
+
+// The trio kernel: phase C's doublings and mixed additions cost one multiplication of latency per
+// dependency level (3 per doubling, 5 per addition) with DPP exchanges inside a wave instead of LDS
+// exchanges and barriers between waves, and 40 txs per workgroup spread a 10k batch over 250 CUs
+// instead of 157.  Bit-identical to tx_verify_kernel<0, *>.
+__global__ __launch_bounds__(256, 1) void tx_verify_trio26_kernel(const uint8_t* __restrict__ pre,
+                                                                  const uint64_t* __restrict__ pre_off,
+                                                                  const uint8_t* __restrict__ sig,
+                                                                  const uint64_t* __restrict__ sig_off, uint64_t n,
+                                                                  const uint32_t* __restrict__ tab,
+                                                                  uint8_t* __restrict__ txhash,
+                                                                  uint8_t* __restrict__ sender,
+                                                                  uint8_t* __restrict__ status) {
+    coop26_body<true>(pre, pre_off, sig, sig_off, n, tab, txhash, sender, status);
+}
+
 int launch_tx_verify_small_secp(const TxKernelPolicy& pol, const uint8_t* d_pre, const uint64_t* d_pre_off,
                                 const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash,
                                 uint8_t* d_sender, uint8_t* d_status, hipStream_t st) {
@@ -1227,7 +1314,10 @@ int launch_tx_verify_small_secp(const TxKernelPolicy& pol, const uint8_t* d_pre,
     const int rc = tables8(&k1, &sm2);
     if (rc) return rc;
     const dim3 grid(static_cast<unsigned>((n + 63) / 64));
-    if (pol.coop && pol.f26)
+    if (pol.coop == 2 && pol.f26)
+        hipLaunchKernelGGL(tx_verify_trio26_kernel, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0, st, d_pre,
+                           d_pre_off, d_sig, d_sig_off, n, k1, d_txhash, d_sender, d_status);
+    else if (pol.coop && pol.f26)
         hipLaunchKernelGGL(tx_verify_coop26_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n, k1,
                            d_txhash, d_sender, d_status);
     else if (pol.coop)

@@ -534,7 +534,7 @@ __device__ __forceinline__ void lds_load_fe(fe& a, const uint32_t (*src)[64], in
 struct TxKernelPolicy {
     int split = -1;  // small-batch secp kernels: -1 by size (n <= 2^15), 0 never, 1 always
     int occ = 0;     // tx_verify_kernel occupancy: 0 by size (2 for n >= 2^17), 1 or 2 forced
-    int coop = 1;    // small-batch secp kernel: 1 cooperative-pair, 0 4-wave split
+    int coop = 2;    // small-batch secp kernel: 2 lane-trio (fe26 only), 1 cooperative-pair, 0 4-wave split
     int f26 = 1;     // throughput secp kernels: 1 point arithmetic on the 10 x 26-bit field, 0 on FieldK1
 };
 

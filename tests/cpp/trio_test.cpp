@@ -1,0 +1,201 @@
+// trio_test.cpp -- host build of ec26_trio.h with FE26_CHECK: the 16 lanes of one DPP row run as
+// threads in lockstep (every DPP fetch / wave vote is a barrier), so the lane-trio doubling and mixed
+// addition execute exactly as a wave does -- phantom lane 15 and the out-of-row zeros included -- while
+// every field operation asserts its magnitude contract on every lane.  Each trio's result is compared
+// with CurveK1x (ec26.h) on the same inputs: random elements at every magnitude the formulas accept,
+// bound-hugging limbs, and the exceptional additions (P = Q, P = -Q, P = infinity, infinity doubled).
+// Prints "trio ok <cases>" and exits 0, or the first mismatch and exits 1.
+#define FE26_CHECK 1
+#include "../../fisco-bcos_amd/csrc/ec26_trio.h"
+
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+using namespace bcosgpu;
+
+namespace {
+constexpr int kLanes = 16;
+std::mutex mu;
+std::condition_variable cv;
+int arrived = 0;
+unsigned long generation = 0;
+uint32_t slot[kLanes];
+thread_local int my_lane = 0;
+
+void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const unsigned long g = generation;
+    if (++arrived == kLanes) {
+        arrived = 0;
+        ++generation;
+        cv.notify_all();
+    } else {
+        cv.wait(lk, [&] { return generation != g; });
+    }
+}
+}  // namespace
+
+namespace bcosgpu {
+uint32_t trio_emu_dpp(uint32_t x, int ctrl) {
+    slot[my_lane] = x;
+    barrier();
+    int src = my_lane;
+    switch (ctrl) {
+        case 0x111: src = my_lane - 1; break;  // row_shr:1
+        case 0x112: src = my_lane - 2; break;  // row_shr:2
+        case 0x101: src = my_lane + 1; break;  // row_shl:1
+        case 0x102: src = my_lane + 2; break;  // row_shl:2
+        default: abort();
+    }
+    const uint32_t r = (src >= 0 && src < kLanes) ? slot[src] : 0u;
+    barrier();
+    return r;
+}
+bool trio_emu_any(bool b) {
+    slot[my_lane] = b ? 1u : 0u;
+    barrier();
+    bool r = false;
+    for (int i = 0; i < kLanes; ++i) r = r || slot[i] != 0u;
+    barrier();
+    return r;
+}
+}  // namespace bcosgpu
+
+namespace {
+uint64_t rng_state = 0x2545f4914f6cdd1dull;
+uint32_t rnd() {
+    rng_state ^= rng_state << 13;
+    rng_state ^= rng_state >> 7;
+    rng_state ^= rng_state << 17;
+    return static_cast<uint32_t>(rng_state >> 11);
+}
+void rand_fe(fe26& a, int m, int mode) {  // mode 0 random limbs, 1 every limb at its bound
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t bound = static_cast<uint64_t>(m) << (i == 9 ? 22 : 26);
+        a.v[i] = static_cast<uint32_t>(mode ? bound : ((static_cast<uint64_t>(rnd()) << 20 ^ rnd()) % (bound + 1)));
+    }
+    a.m = m;
+}
+bool same(const fe26& a, const fe26& b) {
+    fe26 x = a, y = b;
+    fe26_normalize(x);
+    fe26_normalize(y);
+    return memcmp(x.v, y.v, sizeof x.v) == 0;
+}
+// the affine-equivalence of two Jacobian points (X1 Z2^2 = X2 Z1^2, Y1 Z2^3 = Y2 Z1^3) or both infinity
+bool same_point(const Jac26& a, const Jac26& b) {
+    if (a.inf || b.inf) return a.inf == b.inf;
+    fe26 za2, zb2, za3, zb3, l, r;
+    fe26_sqr(za2, a.Z);
+    fe26_sqr(zb2, b.Z);
+    fe26_mul(l, a.X, zb2);
+    fe26_mul(r, b.X, za2);
+    if (!same(l, r)) return false;
+    fe26_mul(za3, za2, a.Z);
+    fe26_mul(zb3, zb2, b.Z);
+    fe26_mul(l, a.Y, zb3);
+    fe26_mul(r, b.Y, za3);
+    return same(l, r);
+}
+
+struct Case {
+    Jac26 P;
+    Aff26 Q;
+    int ops;  // bit 0: 4 doublings, bit 1: one madd; repeated `reps` times
+    int reps;
+};
+std::vector<Case> cases;
+std::vector<int> bad;  // per case: 0 ok, 1 mismatch
+int cases_per_round = 5;
+
+void lane_main(int lane, int round) {
+    my_lane = lane;
+    const TrioLane T(lane);
+    const int t = (lane % 16) / 3;
+    const int c = round * cases_per_round + (t < 5 ? t : 4);
+    const Case& K = cases[c];
+    TrioPt P;
+    trio::sel(P.S1, T.r0, K.P.X, K.P.Y);
+    P.Xs = K.P.X;
+    P.Zs = K.P.Z;
+    P.inf = K.P.inf;
+    Jac26 R = K.P;
+    for (int rep = 0; rep < K.reps; ++rep) {
+        if (K.ops & 1) {
+            for (int d = 0; d < 4; ++d) {
+                trio_dbl(P, T);
+                CurveK1x::dbl(R, R);
+            }
+        }
+        if (K.ops & 2) {
+            trio_madd(P, P, K.Q, T);
+            Jac26 S;
+            CurveK1x::madd(S, R, K.Q);
+            R = S;
+        }
+    }
+    Jac26 J;
+    trio_to_jac(J, P, T);
+    if (t < 5 && !same_point(J, R)) bad[c] = 1;
+}
+}  // namespace
+
+int main() {
+    // cases: random inputs at the largest magnitudes each entry accepts, bound-hugging limbs, and the
+    // exceptional madd inputs (P = Q, P = -Q, P = inf; on rounds whose sequence starts with a madd) and
+    // doubled infinities
+    for (int k = 0; k < 400; ++k) {
+        Case K;
+        const int mode = k % 7 == 6 ? 1 : 0;
+        const int mx = k % 3 == 0 ? 10 : 1 + static_cast<int>(rnd() % 10);
+        rand_fe(K.P.X, mx, mode);
+        rand_fe(K.P.Y, k % 3 == 0 ? 10 : 1 + static_cast<int>(rnd() % 10), mode);
+        rand_fe(K.P.Z, k % 3 == 0 ? 16 : 1 + static_cast<int>(rnd() % 16), mode);
+        rand_fe(K.Q.x, 1 + static_cast<int>(rnd() % 2), mode);
+        rand_fe(K.Q.y, 1 + static_cast<int>(rnd() % 2), mode);
+        K.P.inf = false;
+        // the op sequence is uniform across the five trios of a row (one program counter per wave)
+        const int round = k / cases_per_round;
+        K.ops = 1 + round % 3;
+        K.reps = 1 + round % 4;
+        const int special = k % 10;
+        if (special == 1 || special == 2) {  // P = (x Z^2, +-y Z^3, Z) equals +-Q
+            fe26 z2, z3;
+            rand_fe(K.P.Z, 2, 0);
+            rand_fe(K.Q.x, 1, 0);
+            rand_fe(K.Q.y, 1, 0);
+            fe26_sqr(z2, K.P.Z);
+            fe26_mul(z3, z2, K.P.Z);
+            fe26_mul(K.P.X, K.Q.x, z2);
+            fe26_mul(K.P.Y, K.Q.y, z3);
+            if (special == 2) fe26_neg<2>(K.P.Y, K.P.Y);
+        } else if (special == 3) {  // P = infinity
+            CurveK1x::set_inf(K.P);
+        }
+        cases.push_back(K);
+    }
+    bad.assign(cases.size(), 0);
+    const int rounds = static_cast<int>(cases.size()) / cases_per_round;
+    for (int r = 0; r < rounds; ++r) {
+        std::vector<std::thread> th;
+        for (int l = 0; l < kLanes; ++l) th.emplace_back(lane_main, l, r);
+        for (auto& x : th) x.join();
+    }
+    int nbad = 0;
+    for (size_t i = 0; i < bad.size(); ++i)
+        if (bad[i]) {
+            if (!nbad) printf("mismatch in case %zu (ops %d reps %d)\n", i, cases[i].ops, cases[i].reps);
+            ++nbad;
+        }
+    if (nbad) {
+        printf("trio mismatches %d of %zu\n", nbad, cases.size());
+        return 1;
+    }
+    printf("trio ok %zu\n", cases.size());
+    return 0;
+}
