@@ -247,7 +247,8 @@ def run_leg(ctx, wl_name, steps=None, warmup=3, warm_seconds=0.0, min_seconds=2.
     kname = _kernel_name(suite, n)
     f_alg = F_SECP_RECOVER if suite == 0 else F_SM2_VERIFY
     if suite == 0:
-        f_exec = F_SECP_EXEC_WIDE if kname.startswith("tx_verify_kernel") else F_SECP_EXEC_COMB8
+        wide = kname.startswith("tx_verify_kernel") or kname == "tx_verify_trio26_kernel"  # 16-bit comb for u1 G
+        f_exec = F_SECP_EXEC_WIDE if wide and os.environ.get("BCOSGPU_TABLES") != "small" else F_SECP_EXEC_COMB8
     else:
         f_exec = F_SM2_EXEC if kname.startswith("tx_verify_kernel") else F_SM2_EXEC_COMB8
     ex = n * f_exec * MAC_PER_F / (kernel_ms * 1e-3)

@@ -207,7 +207,9 @@ F26_HD void trio_dbl(TrioPt& P, const TrioLane& T) {
 
 // R <- P + Q, Q affine (x, y <= 2) and never infinity; P: X, Y <= 10, Z <= 16 -> (9, 6, 2).  The
 // exceptional cases are those of CurveK1x::madd: P = Q doubles (computed on lane 2, which holds all of
-// P), P = -Q gives infinity, P = infinity gives Q.
+// P), P = -Q gives infinity, P = infinity gives Q.  EXC = false drops the P = +-Q tests for callers
+// that exclude those cases (trio_add_digit in ecc_coop.hip states why a GLV chain does).
+template <bool EXC = true>
 F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane& T) {
     using namespace trio;
     fe26 Zb, P1, o1, P2, Q2, o2, Xl, h, P3, o3, HHx, I, P4, o4, R2, V, X3, W, rr, P5, Q5, J1, o5, Y3, t;
@@ -251,36 +253,37 @@ F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane
     fe26_sub<2>(Y3, o5, t);                              //                             m 3
     fe26_mul_int<2>(Y3, Y3);                             // lane 0: Y3                  m 6
     TRIO_DUMP(7, Y3);
-    // exceptional cases (flags shared across the trio)
-    const uint32_t zf = fe26_is_zero(h) ? 1u : 0u;
-    const bool hz = bdpp_from(zf, T, 0) != 0u && !P.inf;
-    const bool rz = bdpp_from(zf, T, 1) != 0u;
     TrioPt O;
     sel_dpp2<kL1, kL2>(O.S1, T.r0, X3, T.r1, Y3);      // (X3 | Y3 | Y3) from lane 0
     fdpp<kL2>(O.Xs, X3);                                 // lane 2 <- X3 of lane 0
     fe26_mul_int<2>(O.Zs, o3);                           // lane 2: Z3 = 2 Z H          m 2
     O.inf = false;
-    if (any(hz && rz)) {                               // P == Q: double on lane 2 (rare)
-        Jac26 A, D;
-        fe26_copy(A.X, P.Xs);
-        fe26_copy(A.Y, P.S1);
-        fe26_copy(A.Z, P.Zs);
-        A.inf = P.inf;
-        CurveK1x::dbl(D, A);
-        TrioPt Dt;
-        sel_dpp2<kR2, kR1>(Dt.S1, T.r2, D.Y, T.r0, D.X);  // lane 0 <- X, lane 1 <- Y of lane 2
+    if constexpr (EXC) {  // exceptional cases (flags shared across the trio)
+        const uint32_t zf = fe26_is_zero(h) ? 1u : 0u;
+        const bool hz = bdpp_from(zf, T, 0) != 0u && !P.inf;
+        const bool rz = bdpp_from(zf, T, 1) != 0u;
+        if (any(hz && rz)) {                             // P == Q: double on lane 2 (rare)
+            Jac26 A, D;
+            fe26_copy(A.X, P.Xs);
+            fe26_copy(A.Y, P.S1);
+            fe26_copy(A.Z, P.Zs);
+            A.inf = P.inf;
+            CurveK1x::dbl(D, A);
+            TrioPt Dt;
+            sel_dpp2<kR2, kR1>(Dt.S1, T.r2, D.Y, T.r0, D.X);  // lane 0 <- X, lane 1 <- Y of lane 2
 #pragma unroll
-        for (int i = 0; i < 10; ++i) {
-            const uint32_t y = dpp<kR1>(D.Y.v[i]);
-            Dt.S1.v[i] = T.r1 ? y : Dt.S1.v[i];
+            for (int i = 0; i < 10; ++i) {
+                const uint32_t y = dpp<kR1>(D.Y.v[i]);
+                Dt.S1.v[i] = T.r1 ? y : Dt.S1.v[i];
+            }
+            F26_SETM(Dt.S1, 10);
+            fe26_copy(Dt.Xs, D.X);
+            fe26_copy(Dt.Zs, D.Z);
+            Dt.inf = false;
+            trio_cmov(O, Dt, hz && rz);
         }
-        F26_SETM(Dt.S1, 10);
-        fe26_copy(Dt.Xs, D.X);
-        fe26_copy(Dt.Zs, D.Z);
-        Dt.inf = false;
-        trio_cmov(O, Dt, hz && rz);
+        if (hz && !rz) O.inf = true;                     // P == -Q
     }
-    if (hz && !rz) O.inf = true;                         // P == -Q
     if (P.inf) trio_from_aff(O, Q, T);
     R = O;
 }

@@ -948,22 +948,42 @@ __device__ __forceinline__ void coop26_add_digit(Jac26& acc, const Coop26Ctx& c,
     CurveK1x::cmov(acc, R, d != 0);
 }
 
-// acc = u1 * G restricted to 8-bit comb windows [lo, hi)
-__device__ __forceinline__ void comb_range26(Jac26& acc, const fe& k_plain, const uint32_t* __restrict__ tab, int lo,
-                                             int hi) {
+
+// acc = u1 * G restricted to the BITS-bit comb windows [lo, hi), the next window's entry fetched (raw
+// words) before the current addition, as comb_mul26
+template <int BITS>
+__device__ __forceinline__ void comb_range26w(Jac26& acc, const fe& k_plain, const uint32_t* __restrict__ tab, int lo,
+                                              int hi) {
+    constexpr uint32_t E = 1u << BITS, MASK = E - 1u;
     fe k;
     fe_copy(k, k_plain);
-    for (int i = 0; i < lo; ++i) shr8(k);
+    for (int i = 0; i < lo; ++i) shr_bits<BITS>(k);
     CurveK1x::set_inf(acc);
+    uint32_t b = k.v[0] & MASK;
+    shr_bits<BITS>(k);
+    const uint4* e = reinterpret_cast<const uint4*>(tab + (static_cast<size_t>(lo) * E + b) * 16);
+    uint4 q0 = e[0], q1 = e[1], q2 = e[2], q3 = e[3];
 #pragma unroll 1
     for (int i = lo; i < hi; ++i) {
-        const uint32_t b = k.v[0] & 255u;
-        shr8(k);
+        const uint32_t bi = b;
         Aff26 T;
-        load_aff26(T, tab + (static_cast<size_t>(i) * kCombEntries + b) * 16);
+        {
+            const uint32_t x[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+            const uint32_t y[8] = {q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+            fe26_from_words(T.x, x);
+            fe26_from_words(T.y, y);
+        }
+        const int in = i + 1 < hi ? i + 1 : i;  // last window: a harmless reload
+        b = k.v[0] & MASK;
+        shr_bits<BITS>(k);
+        e = reinterpret_cast<const uint4*>(tab + (static_cast<size_t>(in) * E + b) * 16);
+        q0 = e[0];
+        q1 = e[1];
+        q2 = e[2];
+        q3 = e[3];
         Jac26 S;
         CurveK1x::madd(S, acc, T);
-        CurveK1x::cmov(acc, S, b != 0u);
+        CurveK1x::cmov(acc, S, bi != 0u);
     }
 }
 
@@ -1003,27 +1023,53 @@ __device__ __forceinline__ void lds_store_fe26(uint32_t (*dst)[64], const fe26& 
 // The GLV chains of the trio kernel: wave w runs chain w & 1 for txs 20 (w >> 1) .. 20 (w >> 1) + 19
 // of the workgroup, one trio (three adjacent lanes, ec26_trio.h) per tx; lane position p of DPP row r
 // is trio p / 3 (p = 15 a phantom that mirrors trio 4 and stores nothing).
-__device__ __forceinline__ void trio_add_digit(TrioPt& acc, const Coop26Lds& L, int tl, int d, bool neg, bool phi,
+// The trio kernel's LDS: Coop26Lds without the wave-pair exchange slots, and the co-Z table (and
+// beta x) kept as canonical fe26 limbs, so a window's lookup is 20 LDS reads and no conversion.
+struct Trio26Lds {
+    uint32_t tab[8][20][64];          // [entry][x limbs 0..9, y limbs 0..9][tx]
+    uint32_t tabphx[8][10][64];       // beta * x
+    uint32_t zc[8][64];
+    uint32_t k[2][4][64];
+    uint32_t flags[64];
+    uint32_t pt[5][25][64];
+    uint32_t xe[8][64];
+    uint32_t xrinv[8][64];
+    uint32_t ys[8][64];
+    uint32_t rflag[64];
+    uint32_t post[2];
+};
+__device__ __forceinline__ void lds_store_limbs26(uint32_t (*dst)[64], const fe26& a, int lane) {
+    fe26 t;
+    fe26_copy(t, a);
+    fe26_normalize(t);
+#pragma unroll
+    for (int q = 0; q < 10; ++q) dst[q][lane] = t.v[q];
+}
+
+// A window of a GLV chain: acc <- acc + d * (table point), d a Booth digit in [-8, 8].  The madd runs
+// without its P = Q / P = -Q tests (trio_madd<false>): acc is K R for the digits K processed so far
+// and the table point is |d| R with |d| <= 8; once K != 0 every window makes |K| >= 16 before its
+// addition, so K = +-d (mod n) would need 16 <= |K| <= 8 -- impossible for |K| < 2^130 < n and R of
+// order n.  (An R that is not on the curve fails its verdict and its chain's value is discarded.)
+// K = 0 is the infinity flag, which the madd handles.
+__device__ __forceinline__ void trio_add_digit(TrioPt& acc, const Trio26Lds& L, int tl, int d, bool neg, bool phi,
                                                const TrioLane& T) {
     const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
-    const uint32_t* base = &L.tab[0][0][0] + m * (16 * 64) + tl;
-    const uint32_t* bx = phi ? &L.tabphx[0][0][0] + m * (8 * 64) + tl : base;
+    const uint32_t* base = &L.tab[0][0][0] + m * (20 * 64) + tl;
+    const uint32_t* bx = phi ? &L.tabphx[0][0][0] + m * (10 * 64) + tl : base;
     Aff26 S;
-    {
-        uint32_t x[8], y[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            x[k] = bx[k * 64];
-            y[k] = base[(8 + k) * 64];
-        }
-        fe26_from_words(S.x, x);
-        fe26_from_words(S.y, y);
+    for (int q = 0; q < 10; ++q) {
+        S.x.v[q] = bx[q * 64];
+        S.y.v[q] = base[(10 + q) * 64];
     }
+    F26_SETM(S.x, 1);
+    F26_SETM(S.y, 1);
     fe26 ny;
     fe26_neg<2>(ny, S.y);
     fe26_cmov(S.y, ny, (d < 0) != neg);
     TrioPt R;
-    trio_madd(R, acc, S, T);
+    trio_madd<false>(R, acc, S, T);
     trio_cmov(acc, R, d != 0);
 }
 
@@ -1032,10 +1078,11 @@ __device__ __forceinline__ void trio_add_digit(TrioPt& acc, const Coop26Lds& L, 
 template <bool TRIO>
 __device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, const uint64_t* __restrict__ pre_off,
                                             const uint8_t* __restrict__ sig, const uint64_t* __restrict__ sig_off,
-                                            uint64_t n, const uint32_t* __restrict__ tab, uint8_t* __restrict__ txhash,
+                                            uint64_t n, const uint32_t* __restrict__ tab, int tab_bits,
+                                            uint8_t* __restrict__ txhash,
                                             uint8_t* __restrict__ sender, uint8_t* __restrict__ status) {
     constexpr int TPW = TRIO ? 40 : 64;  // txs per workgroup
-    __shared__ Coop26Lds L;
+    __shared__ std::conditional_t<TRIO, Trio26Lds, Coop26Lds> L;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * TPW + lane;
     const bool active = lane < TPW && i < n;
@@ -1099,11 +1146,17 @@ __device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, con
             fe26_const(beta, kGlvBeta);
             Unroll<0, 8>::run([&](auto J) {
                 constexpr int j = decltype(J)::value;
-                lds_store_fe26(L.tab[j], A[j].x, lane);
-                lds_store_fe26(L.tab[j] + 8, A[j].y, lane);
                 fe26 bx;
                 fe26_mul(bx, A[j].x, beta);
-                lds_store_fe26(L.tabphx[j], bx, lane);
+                if constexpr (TRIO) {
+                    lds_store_limbs26(L.tab[j], A[j].x, lane);
+                    lds_store_limbs26(L.tab[j] + 10, A[j].y, lane);
+                    lds_store_limbs26(L.tabphx[j], bx, lane);
+                } else {
+                    lds_store_fe26(L.tab[j], A[j].x, lane);
+                    lds_store_fe26(L.tab[j] + 8, A[j].y, lane);
+                    lds_store_fe26(L.tabphx[j], bx, lane);
+                }
             });
             lds_store_fe26(L.zc, Zc, lane);
             COOP_T(6);
@@ -1156,11 +1209,16 @@ __device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, con
             }
             L.flags[lane] = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
         }
-        constexpr int kCombW0 = 12, kCombW1 = 24;
         Jac26 G;
-        const int lo = wave == 0 ? 0 : wave == 3 ? kCombW0 : kCombW1;
-        const int hi = wave == 0 ? kCombW0 : wave == 3 ? kCombW1 : 32;
-        comb_range26(G, u1, tab, lo, hi);
+        if (tab_bits == kWideBits) {  // 16 windows of the 16-bit comb: 6 / 7 / 3 (wave 1 also builds the table)
+            const int lo = wave == 0 ? 0 : wave == 3 ? 6 : 13;
+            const int hi = wave == 0 ? 6 : wave == 3 ? 13 : 16;
+            comb_range26w<kWideBits>(G, u1, tab, lo, hi);
+        } else {  // 32 windows of the 8-bit comb: 12 / 12 / 8
+            const int lo = wave == 0 ? 0 : wave == 3 ? 12 : 24;
+            const int hi = wave == 0 ? 12 : wave == 3 ? 24 : 32;
+            comb_range26w<8>(G, u1, tab, lo, hi);
+        }
         coop26_store_jac(L.pt[wave == 0 ? 2 : wave == 3 ? 3 : 4], G, lane);
     }
     COOP_T(1);
@@ -1289,7 +1347,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t*
                                                                   uint8_t* __restrict__ txhash,
                                                                   uint8_t* __restrict__ sender,
                                                                   uint8_t* __restrict__ status) {
-    coop26_body<false>(pre, pre_off, sig, sig_off, n, tab, txhash, sender, status);
+    coop26_body<false>(pre, pre_off, sig, sig_off, n, tab, 8, txhash, sender, status);
 }
 
 // The trio kernel: phase C's doublings and mixed additions cost one multiplication of latency per
@@ -1300,11 +1358,11 @@ __global__ __launch_bounds__(256, 1) void tx_verify_trio26_kernel(const uint8_t*
                                                                   const uint64_t* __restrict__ pre_off,
                                                                   const uint8_t* __restrict__ sig,
                                                                   const uint64_t* __restrict__ sig_off, uint64_t n,
-                                                                  const uint32_t* __restrict__ tab,
+                                                                  const uint32_t* __restrict__ tab, int tab_bits,
                                                                   uint8_t* __restrict__ txhash,
                                                                   uint8_t* __restrict__ sender,
                                                                   uint8_t* __restrict__ status) {
-    coop26_body<true>(pre, pre_off, sig, sig_off, n, tab, txhash, sender, status);
+    coop26_body<true>(pre, pre_off, sig, sig_off, n, tab, tab_bits, txhash, sender, status);
 }
 
 int launch_tx_verify_small_secp(const TxKernelPolicy& pol, const uint8_t* d_pre, const uint64_t* d_pre_off,
@@ -1314,10 +1372,15 @@ int launch_tx_verify_small_secp(const TxKernelPolicy& pol, const uint8_t* d_pre,
     const int rc = tables8(&k1, &sm2);
     if (rc) return rc;
     const dim3 grid(static_cast<unsigned>((n + 63) / 64));
-    if (pol.coop == 2 && pol.f26)
+    if (pol.coop == 2 && pol.f26) {
+        // u1 G on the 16-bit comb when the wide tables exist (16 windows instead of 32 in phase A)
+        const uint32_t *wk1, *wsm2;
+        int bits = 8;
+        const int rw = tables(&wk1, &wsm2, &bits);
+        if (rw) return rw;
         hipLaunchKernelGGL(tx_verify_trio26_kernel, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0, st, d_pre,
-                           d_pre_off, d_sig, d_sig_off, n, k1, d_txhash, d_sender, d_status);
-    else if (pol.coop && pol.f26)
+                           d_pre_off, d_sig, d_sig_off, n, wk1, bits, d_txhash, d_sender, d_status);
+    } else if (pol.coop && pol.f26)
         hipLaunchKernelGGL(tx_verify_coop26_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n, k1,
                            d_txhash, d_sender, d_status);
     else if (pol.coop)
