@@ -1,5 +1,5 @@
 // coopbench.hip -- phase timestamps (s_memtime cycles) of tx_verify_coop_kernel's (argv[1] = 26:
-// tx_verify_coop26_kernel's) workgroup 0 on a
+// tx_verify_coop26_kernel's, trio: tx_verify_trio26_kernel's) workgroup 0 on a
 // 10k-tx batch of random inputs (the schedule is input-independent), to see where C2's latency goes.
 #define BCOSGPU_COOP_TIMING 1
 #include "../csrc/ecc_tables.hip"
@@ -10,7 +10,8 @@
 int main(int argc, char** argv) {
     using namespace bcosgpu;
     const bool f26 = argc > 1 && argv[1][0] == '2';  // "26": tx_verify_coop26_kernel
-    if (ecc_init_tables(0, 1)) { printf("no device\n"); return 77; }
+    const bool trio = argc > 1 && argv[1][0] == 't';  // "trio": tx_verify_trio26_kernel (16-bit comb)
+    if (ecc_init_tables(0, trio ? 0 : 1)) { printf("no device\n"); return 77; }
     const uint64_t n = 10000;
     std::vector<uint8_t> pre(n * 151), sig(n * 65);
     std::vector<uint64_t> po(n + 1), so(n + 1);
@@ -30,7 +31,13 @@ int main(int argc, char** argv) {
     const uint32_t *k1, *sm2;
     tables8(&k1, &sm2);
     for (int rep = 0; rep < 3; ++rep) {
-        if (f26)
+        if (trio) {
+            const uint32_t *w1, *w2;
+            int bits = 8;
+            tables(&w1, &w2, &bits);
+            hipLaunchKernelGGL(tx_verify_trio26_kernel, dim3((n + 39) / 40), dim3(256), 0, 0, dp, dpo, ds, dso, n, w1,
+                               bits, dh, dsn, dst);
+        } else if (f26)
             hipLaunchKernelGGL(tx_verify_coop26_kernel, dim3((n + 63) / 64), dim3(256), 0, 0, dp, dpo, ds, dso, n, k1, dh,
                                dsn, dst);
         else
