@@ -770,7 +770,7 @@ struct Coop26Lds {
     uint32_t xrinv[8][64];
     uint32_t ys[8][64];
     uint32_t rflag[64];
-    uint32_t post[2];
+    uint32_t post[3];         // phase-A hand-offs: r^-1, e, G partial 0
 };
 
 struct Coop26Ctx {
@@ -1036,7 +1036,7 @@ struct Trio26Lds {
     uint32_t xrinv[8][64];
     uint32_t ys[8][64];
     uint32_t rflag[64];
-    uint32_t post[2];
+    uint32_t post[3];
 };
 __device__ __forceinline__ void lds_store_limbs26(uint32_t (*dst)[64], const fe26& a, int lane) {
     fe26 t;
@@ -1098,6 +1098,7 @@ __device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, con
     if (threadIdx.x == 0) {
         L.post[0] = 0u;
         L.post[1] = 0u;
+        L.post[2] = 0u;
     }
     __syncthreads();
     // ---------------------------------------------------------------- phase A (as tx_verify_coop_kernel)
@@ -1219,7 +1220,19 @@ __device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, con
             const int hi = wave == 0 ? 12 : wave == 3 ? 24 : 32;
             comb_range26w<8>(G, u1, tab, lo, hi);
         }
-        coop26_store_jac(L.pt[wave == 0 ? 2 : wave == 3 ? 3 : 4], G, lane);
+        // G0 + G3 on wave 3 while phase A waits for wave 1's last window (one addition off phase D)
+        if (wave == 0) {
+            coop26_store_jac(L.pt[2], G, lane);
+            coop_post(&L.post[2]);
+        } else if (wave == 3) {
+            Jac26 G0, S;
+            coop_wait(&L.post[2]);
+            coop26_load_jac(G0, L.pt[2], lane);
+            CurveK1x::add(S, G0, G);
+            coop26_store_jac(L.pt[3], S, lane);
+        } else {
+            coop26_store_jac(L.pt[4], G, lane);
+        }
     }
     COOP_T(1);
     __syncthreads();
@@ -1289,13 +1302,11 @@ __device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, con
     }
     __syncthreads();
     // ---------------------------------------------------------------- phase D (on fe26 as well)
-    if (wave == 1) {  // G part: partials 0 + 1 + 2
-        Jac26 G0, G1, T, U;
-        coop26_load_jac(G0, L.pt[2], lane);
-        coop26_load_jac(G1, L.pt[3], lane);
-        CurveK1x::add(T, G0, G1);
-        coop26_load_jac(G0, L.pt[4], lane);
-        CurveK1x::add(U, T, G0);
+    if (wave == 1) {  // G part: (partials 0 + 1, phase A) + 2
+        Jac26 G01, G2, U;
+        coop26_load_jac(G01, L.pt[3], lane);
+        coop26_load_jac(G2, L.pt[4], lane);
+        CurveK1x::add(U, G01, G2);
         coop26_store_jac(L.pt[2], U, lane);
     } else if (wave == 0) {  // R part: co-Z curve -> E_w (Z * Zc) -> E (Z * y)
         Jac26 P0, P1, Q;
