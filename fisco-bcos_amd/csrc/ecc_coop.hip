@@ -1,7 +1,8 @@
 // ecc_coop.hip -- small-batch secp256k1 tx verify: the 4-wave split kernel, the cooperative-pair kernels
 // (8 x 32 and fe26 point arithmetic) and the lane-trio kernel.  Built with the DPP combiner off
-// (Makefile): folding the trio's DPP fetches into VOP2 arithmetic gave wrong sums on gfx950
-// (tools/triobench.hip reproduces it: v_subrev_u32_dpp in the mixed addition).
+// (Makefile; hash_kernels.hip too, for the cooperative Keccak): folding the trio's DPP fetches into
+// VOP2 arithmetic gave wrong sums on gfx950 (tools/triobench.hip reproduces it: v_subrev_u32_dpp in
+// the mixed addition).
 #include "ecc_device.h"
 #include "ec26_trio.h"
 

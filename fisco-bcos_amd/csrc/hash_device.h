@@ -279,68 +279,98 @@ __device__ __forceinline__ void sm3_64(const uint32_t m_be[16], uint32_t out[8])
 
 // ------------------------------------------------------------------ lane-cooperative Keccak-256
 // For latency-bound hashing (the top levels of a Merkle tree: one 512-byte width-16 node is 4 serial
-// permutations), one state is spread over 25 lanes of a 32-lane group, lane t = x + 5y holding
-// A[x][y] as two 32-bit halves; a wave runs two states.  A round is ~20 VALU + 18 ds_bpermute per lane
-// (theta: 4 column gathers + C[x-1], C[x+1]; pi: 1 gather; chi: 2 row gathers) instead of ~170 VALU
-// in one lane.  Both 32-lane groups of the wave must call it together (ds_bpermute is wave-wide).
+// permutations), one state is spread over 25 lanes of a 32-lane group, each lane holding one
+// A[x][y] as two 32-bit halves; a wave runs two states.  Lanes are placed so that every 5-lane plane
+// y sits inside one 16-lane DPP row: row 0 of the group holds y = 0, 1, 2 (lanes 5y + x), row 1 holds
+// y = 3, 4 (lanes 16 + 5(y - 3) + x); lanes 15 and 26..31 are idle.  Then a round needs one LDS
+// round trip (pi's gather, ds_bpermute) and everything else is DPP row shifts, v_permlane16_swap
+// (row 0 <-> row 1) and per-lane selects:
+//   theta: t = A ^ A(y+1); plane y = 0 gets C[x] = t ^ A(y+2) ^ t(row 1) (permlane16_swap);
+//          D[x] = C[x-1] ^ rotl1(C[x+1]) on plane 0 (row shifts by 1 / 4 within the plane), then
+//          broadcast to planes 1, 2 (row_shr 5 / 10) and to row 1 (permlane16_swap)
+//   rho: per-lane rotation; pi: one ds_bpermute; chi: A(x+1), A(x+2) by row shifts within the plane
+// ~60 VALU per round per lane against ~180 in one lane, and one LDS latency instead of four (the
+// previous ds_bpermute-only version: theta's column and neighbour gathers, pi, chi's row gathers).
+// Both 32-lane groups of the wave must call it together (DPP and ds_bpermute are wave-wide).
 struct KeccakCoop {
-    int gl;            // lane within the 32-lane group
-    int col[4];        // bpermute byte addresses of the column mates (x, y + k), k = 1..4
-    int xm1, xp1, xp2; // (x - 1, y), (x + 1, y), (x + 2, y)
-    int pisrc;         // pi: source lane of this lane's B position
+    int gl;            // Keccak lane index x + 5y of this lane, >= 25 on idle lanes
+    int x, y;          // its position (idle lanes: x = 0, y = 0)
+    int pisrc;         // pi: bpermute byte address of the source lane of this lane's B position
     uint32_t sh;       // rho: 32 - (r mod 32), 0 when r mod 32 == 0
-    bool swap;         // rho: r >= 32
-    uint32_t m0;       // all-ones on lane 0 (iota)
+    bool swap;         // rho: swap the halves first (see the constructor)
+    uint32_t m0;       // all-ones on lane (0, 0) (iota)
+    __device__ static int lane_of(int base, int xx, int yy) {
+        return base + (yy < 3 ? 5 * yy + xx : 16 + 5 * (yy - 3) + xx);
+    }
     __device__ KeccakCoop() {
         const int lane = static_cast<int>(__lane_id());
-        gl = lane & 31;
-        const int base = lane & 32;
-        const int t = gl < 25 ? gl : 0;
-        const int x = t % 5, y = t / 5;
-        auto addr = [&](int xx, int yy) { return (base + ((xx + 5) % 5) + 5 * ((yy + 5) % 5)) * 4; };
-#pragma unroll
-        for (int k = 0; k < 4; ++k) col[k] = addr(x, y + 1 + k);
-        xm1 = addr(x - 1, y);
-        xp1 = addr(x + 1, y);
-        xp2 = addr(x + 2, y);
+        const int g = lane & 31, base = lane & 32;
+        const bool row0 = g < 15, row1 = g >= 16 && g < 26;
+        x = row0 ? g % 5 : row1 ? (g - 16) % 5 : 0;
+        y = row0 ? g / 5 : row1 ? 3 + (g - 16) / 5 : 0;
+        gl = row0 || row1 ? x + 5 * y : 31;
         // destination (X, Y) = (x, y) of this lane takes source (x', y') with y' = X, 2x' + 3y' = Y (mod 5)
         const int sx = ((3 * (y - 3 * x)) % 5 + 5) % 5;
-        pisrc = addr(sx, x);
+        pisrc = lane_of(base, sx, x) * 4;
         constexpr uint8_t R[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
                                    25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
-        const int r = R[t];
-        swap = r >= 32;
+        // rotl(r) of the (lo, hi) pair = two v_alignbit by 32 - (r mod 32) after swapping the halves when
+        // r >= 32; when r mod 32 == 0 the shift is 0, where alignbit(p, q, 0) = q, so the halves are
+        // swapped once more instead (no branch on the per-lane amount)
+        const int r = R[gl < 25 ? gl : 0];
+        swap = (r >= 32) != ((r & 31) == 0);
         sh = (r & 31) ? 32u - (r & 31) : 0u;
         m0 = gl == 0 ? 0xffffffffu : 0u;
     }
-    __device__ __forceinline__ static uint32_t bp(int addr, uint32_t v) {
-        return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(addr, static_cast<int>(v)));
+    template <int CTRL>
+    __device__ __forceinline__ static uint32_t dpp(uint32_t v) {
+        return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), CTRL, 0xf, 0xf, true));
+    }
+    // row_shl:k = the value of lane i + k, row_shr:k = of lane i - k (inside the 16-lane row)
+    static constexpr int kR1 = 0x101, kR2 = 0x102, kR5 = 0x105, kR10 = 0x10a, kR4 = 0x104;
+    static constexpr int kL1 = 0x111, kL3 = 0x113, kL4 = 0x114, kL5 = 0x115, kL10 = 0x11a;
+    __device__ __forceinline__ static uint32_t sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
+    __device__ __forceinline__ static uint32_t from_row1(uint32_t v) {  // row 0 lanes read lane + 16
+        return __builtin_amdgcn_permlane16_swap(v, v, false, false)[1];
+    }
+    __device__ __forceinline__ static uint32_t from_row0(uint32_t v) {  // row 1 lanes read lane - 16
+        return __builtin_amdgcn_permlane16_swap(v, v, false, false)[0];
+    }
+    // column parity C[x] (valid on plane y = 0)
+    __device__ __forceinline__ static uint32_t colpar(uint32_t a) {
+        const uint32_t t = a ^ dpp<kR5>(a);
+        return xor3(t, dpp<kR10>(a), from_row1(t));
     }
     __device__ __forceinline__ void permute(uint32_t& lo, uint32_t& hi) const {
+        const bool x0 = x == 0, x4 = x == 4, x34 = x >= 3, y1 = y == 1, y2 = y == 2, ry = y >= 3;
 #pragma unroll 1
         for (int round = 0; round < 24; ++round) {
             // theta
-            const uint32_t c_lo = xor3(xor3(lo, bp(col[0], lo), bp(col[1], lo)), bp(col[2], lo), bp(col[3], lo));
-            const uint32_t c_hi = xor3(xor3(hi, bp(col[0], hi), bp(col[1], hi)), bp(col[2], hi), bp(col[3], hi));
-            const uint32_t m_lo = bp(xm1, c_lo), m_hi = bp(xm1, c_hi);
-            const uint32_t p_lo = bp(xp1, c_lo), p_hi = bp(xp1, c_hi);
-            lo = xor3(lo, m_lo, __builtin_amdgcn_alignbit(p_lo, p_hi, 31));
-            hi = xor3(hi, m_hi, __builtin_amdgcn_alignbit(p_hi, p_lo, 31));
+            // (every cross-lane fetch is evaluated on all lanes, then selected: a fetch inside one arm
+            // of a conditional would run under a partial EXEC and read inactive lanes)
+            const uint32_t c_lo = colpar(lo), c_hi = colpar(hi);
+            const uint32_t m_lo = sel(x0, dpp<kR4>(c_lo), dpp<kL1>(c_lo));
+            const uint32_t m_hi = sel(x0, dpp<kR4>(c_hi), dpp<kL1>(c_hi));
+            const uint32_t p_lo = sel(x4, dpp<kL4>(c_lo), dpp<kR1>(c_lo));
+            const uint32_t p_hi = sel(x4, dpp<kL4>(c_hi), dpp<kR1>(c_hi));
+            uint32_t d_lo = m_lo ^ __builtin_amdgcn_alignbit(p_lo, p_hi, 31);
+            uint32_t d_hi = m_hi ^ __builtin_amdgcn_alignbit(p_hi, p_lo, 31);
+            d_lo = sel(y1, dpp<kL5>(d_lo), sel(y2, dpp<kL10>(d_lo), d_lo));
+            d_hi = sel(y1, dpp<kL5>(d_hi), sel(y2, dpp<kL10>(d_hi), d_hi));
+            const uint32_t e_lo = from_row0(d_lo), e_hi = from_row0(d_hi);
+            lo ^= ry ? e_lo : d_lo;
+            hi ^= ry ? e_hi : d_hi;
             // rho (per-lane rotation) then pi (gather)
-            uint32_t a = swap ? hi : lo, b = swap ? lo : hi;
-            if (sh) {
-                const uint32_t na = __builtin_amdgcn_alignbit(a, b, sh), nb = __builtin_amdgcn_alignbit(b, a, sh);
-                a = na;
-                b = nb;
-            }
-            lo = bp(pisrc, a);
-            hi = bp(pisrc, b);
-            // chi + iota
+            const uint32_t a = swap ? hi : lo, b = swap ? lo : hi;
+            const uint32_t na = __builtin_amdgcn_alignbit(a, b, sh), nb = __builtin_amdgcn_alignbit(b, a, sh);
+            lo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(pisrc, static_cast<int>(na)));
+            hi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(pisrc, static_cast<int>(nb)));
+            // chi + iota (A(x + 1) / A(x + 2) inside the plane, wrapping by row shifts of 4 / 3)
+            const uint32_t q_lo = sel(x4, dpp<kL4>(lo), dpp<kR1>(lo)), q_hi = sel(x4, dpp<kL4>(hi), dpp<kR1>(hi));
+            const uint32_t r_lo = sel(x34, dpp<kL3>(lo), dpp<kR2>(lo)), r_hi = sel(x34, dpp<kL3>(hi), dpp<kR2>(hi));
             const uint64_t rc = kKeccakRC[round];
-            const uint32_t n_lo = chi32(lo, bp(xp1, lo), bp(xp2, lo));
-            const uint32_t n_hi = chi32(hi, bp(xp1, hi), bp(xp2, hi));
-            lo = n_lo ^ (static_cast<uint32_t>(rc) & m0);
-            hi = n_hi ^ (static_cast<uint32_t>(rc >> 32) & m0);
+            lo = chi32(lo, q_lo, r_lo) ^ (static_cast<uint32_t>(rc) & m0);
+            hi = chi32(hi, q_hi, r_hi) ^ (static_cast<uint32_t>(rc >> 32) & m0);
         }
     }
     // Keccak-256 of msg[0..len) (len a multiple of 8, msg 8-byte aligned, global or LDS memory);
