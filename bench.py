@@ -110,7 +110,9 @@ def _kernel_name(suite, n):
             return "tx_verify_trio26_kernel"
         return "tx_verify_coop26_kernel" if f26 else "tx_verify_coop_kernel"
     if suite == 1 and small and coop:
-        return "tx_verify_sm2_pair26_kernel" if f26 else "tx_verify_sm2_pair_kernel"
+        if f26:
+            return "tx_verify_sm2_trio26_kernel" if coop == 2 else "tx_verify_sm2_pair26_kernel"
+        return "tx_verify_sm2_pair_kernel"
     occ = os.environ.get("BCOSGPU_TXV_OCC")
     occ = int(occ) if occ in ("1", "2") else (2 if n >= (1 << 17) else 1)
     return "tx_verify_kernel<%d,%d,%s>" % (suite, occ, "true" if f26 else "false")

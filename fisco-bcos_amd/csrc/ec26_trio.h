@@ -85,17 +85,19 @@ F26_HD int mdpp(int m) {
 }
 #endif
 
-template <int CTRL>
-F26_HD void fdpp(fe26& r, const fe26& a) {
+template <int CTRL, class E>
+F26_HD void fdpp(E& r, const E& a) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) r.v[i] = dpp<CTRL>(a.v[i]);
     F26_SETM(r, mdpp<CTRL>(a.m));
 }
 // A DPP read needs two wait states after the VALU write of its source VGPR (gfx9 rule).  The compiler
 // pads its own code, but not the boundary after an inline-asm block (fe26_mul_asm / fe26_sqr_asm end
-// with VALU writes of their result limbs), so every product a lane may fetch goes through these: the
+// with VALU writes of their result limbs; fp26_mul_asm / fp26_sqr_asm likewise), so every product a
+// lane may fetch goes through these: the
 // s_nop names the limbs as in/out operands, so any later DPP read of them is ordered after it.
-F26_HD void dpp_fence(fe26& r) {
+template <class E>
+F26_HD void dpp_fence(E& r) {
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("s_nop 1"
                  : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
@@ -112,14 +114,15 @@ F26_HD void sqr(fe26& r, const fe26& a) {
     fe26_sqr(r, a);
     dpp_fence(r);
 }
-F26_HD void sel(fe26& r, bool c, const fe26& a, const fe26& b) {
+template <class E>
+F26_HD void sel(E& r, bool c, const E& a, const E& b) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) r.v[i] = c ? a.v[i] : b.v[i];
     F26_SETM(r, c ? a.m : b.m);
 }
 // c ? a : (d ? DPP<C1>(b) : DPP<C2>(b))
-template <int C1, int C2>
-F26_HD void sel_dpp2(fe26& r, bool c, const fe26& a, bool d, const fe26& b) {
+template <int C1, int C2, class E>
+F26_HD void sel_dpp2(E& r, bool c, const E& a, bool d, const E& b) {
 #ifdef FE26_CHECK
     const int m1 = mdpp<C1>(b.m), m2 = mdpp<C2>(b.m);
 #endif

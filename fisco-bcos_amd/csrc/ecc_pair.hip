@@ -1,5 +1,6 @@
 // ecc_pair.hip -- small-batch SM2 tx verify: the pair kernels (8 x 32 and fp26 point arithmetic).
 #include "ecc_device.h"
+#include "ecp26_trio.h"
 
 namespace bcosgpu {
 
@@ -831,6 +832,221 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(const uint
         status[i] = ok ? 0 : 1;
     }
 }
+// ------------------------------------------------------------------ SM2 lane-trio kernel (fp26)
+// tx_verify_sm2_pair26_kernel with the t*P chain on lane trios (ecp26_trio.h) instead of a wave pair:
+// 40 txs per workgroup; waves 0 and 1 both build the affine tables of all 40 txs (identical values, so
+// neither waits for the other) and then run the chains of txs 0..19 / 20..39, three lanes per tx;
+// waves 2 and 3 hash, derive e and the address and run the two s*G comb halves as in the pair kernel.
+// The chain's additions skip the P = +-Q tests (trio_madd_sm2<false>): the accumulator is K P with
+// |K| >= 16 before each addition of |d| P, |d| <= 8, and |K| < n, so K = +-d (mod n) cannot occur for
+// a P of order n (SM2's cofactor is 1; a P off the curve fails its verdict).  Bit-identical to
+// tx_verify_kernel<1, *>.
+struct Sm2Trio26Lds {
+    uint32_t tab[8][20][64];         // affine 1P..8P in the R' domain as fp26 limbs: [entry][x, y][tx]
+    uint32_t kt[8][64];              // t = r + s mod n
+    uint32_t acc[25][64];            // the chains' results (canonical X, Y, Z, inf)
+    uint32_t g[25][64];
+    uint32_t gh[25][64];
+    uint32_t c[8][64];
+    uint32_t addr[5][64];
+    uint32_t ok2[64];
+    uint32_t seq[4];
+};
+
+__device__ __forceinline__ void trio_add_digit_sm2(TrioPtP& acc, const Sm2Trio26Lds& L, int tl, int d,
+                                                   const TrioLane& T) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &L.tab[0][0][0] + m * (20 * 64) + tl;
+    AffP26 S;
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+        S.x.v[q] = base[q * 64];
+        S.y.v[q] = base[(10 + q) * 64];
+    }
+    F26_SETM(S.x, 1);
+    F26_SETM(S.y, 1);
+    fp26 ny;
+    fp26_neg<2>(ny, S.y);
+    fp26_cmov(S.y, ny, d < 0);
+    fp26_normalize_weak(S.y);
+    TrioPtP R;
+    trio_madd_sm2<false>(R, acc, S, T);
+    trio_cmov_sm2(acc, R, d != 0);
+}
+
+__global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(const uint8_t* __restrict__ pre,
+                                                                      const uint64_t* __restrict__ pre_off,
+                                                                      const uint8_t* __restrict__ sig,
+                                                                      const uint64_t* __restrict__ sig_off,
+                                                                      uint64_t n, const uint32_t* __restrict__ tab,
+                                                                      uint8_t* __restrict__ txhash,
+                                                                      uint8_t* __restrict__ sender,
+                                                                      uint8_t* __restrict__ status) {
+    constexpr int TPW = 40;
+    __shared__ Sm2Trio26Lds L;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * TPW + lane;
+    const bool active = lane < TPW && i < n;
+    if (threadIdx.x < 4) L.seq[threadIdx.x] = 0u;
+    __syncthreads();
+    uint64_t sa = 0, sb = 0;
+    if (active) {
+        sa = sig_off[i];
+        sb = sig_off[i + 1];
+    }
+    const bool len_ok = active && sb - sa == 128u;
+    fe r, s, px, py;
+    uint32_t X[8], Y[8];
+    if (len_ok) {
+        ByteReader rd(sig + sa, 128);
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rd.word(k);
+        fe_from_be_words(r, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rd.word(8 + k);
+        fe_from_be_words(s, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            X[k] = bswap32(rd.word(16 + k));
+            Y[k] = bswap32(rd.word(24 + k));
+        }
+    } else {
+        fe_zero(r);
+        fe_zero(s);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) X[k] = Y[k] = 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        px.v[k] = X[7 - k];
+        py.v[k] = Y[7 - k];
+    }
+    bool ok = len_ok && fe_lt_k(px, ParamP2::M) && fe_lt_k(py, ParamP2::M);
+    ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN2::M) && fe_lt_k(s, ParamN2::M);
+    fe t;
+    FieldN2::add(t, r, s);
+    ok = ok && !fe_is_zero_raw(t);
+    AffP26 P;
+    fp26_from_plain(P.x, px);
+    fp26_from_plain(P.y, py);
+    if (wave <= 1) {
+        {
+            AffP26 A[8];
+            sm2_affine_table26(A, P);
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                fp26 x, y;
+                fp26_copy(x, A[j].x);
+                fp26_copy(y, A[j].y);
+                fp26_normalize(x);
+                fp26_normalize(y);
+#pragma unroll
+                for (int q = 0; q < 10; ++q) {
+                    L.tab[j][q][lane] = x.v[q];
+                    L.tab[j][10 + q][lane] = y.v[q];
+                }
+            });
+#pragma unroll
+            for (int q = 0; q < 8; ++q) L.kt[q][lane] = t.v[q];
+        }
+        // this wave's own LDS writes before its trio lanes read them (waves 0 and 1 write the same values)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const TrioLane T(lane);
+        const int pos = lane & 15, trio_idx = pos / 3;
+        const int tl = wave * 20 + (lane >> 4) * 5 + (trio_idx < 5 ? trio_idx : 4);
+        fe k;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) k.v[q] = L.kt[q][tl];
+        TrioPtP acc;
+        trio_set_inf_sm2(acc);
+        trio_add_digit_sm2(acc, L, tl, static_cast<int>(k.v[7] >> 31), T);  // digit 64 = bit 255
+#pragma unroll 1
+        for (int w = 63; w >= 0; --w) {
+            trio_dbl_sm2(acc, T);
+            trio_dbl_sm2(acc, T);
+            trio_dbl_sm2(acc, T);
+            trio_dbl_sm2(acc, T);
+            const uint32_t top = k.v[7];
+            const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
+            const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
+            shl4(k);
+            trio_add_digit_sm2(acc, L, tl, d, T);
+        }
+        JacP26 J;
+        trio_to_jac_sm2(J, acc, T);
+        if (T.r0 && trio_idx < 5) pair26_store_jac(L.acc, J, tl);
+    } else if (wave == 2) {
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (active) {
+            const uint64_t pa = pre_off[i], pb = pre_off[i + 1];
+            const uint32_t len = static_cast<uint32_t>(pb - pa);
+            ByteReader rd(pre + pa, len);
+            sm3_msg(rd, len, d);
+            store_digest(SM3, txhash + 32 * i, d);
+        }
+        fe h;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h.v[k] = d[7 - k];
+        uint32_t eb[8];
+        sm2_e(eb, X, Y, h);
+        fe e, cc;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e.v[k] = eb[7 - k];
+        reduce_once(e, ParamN2::M);
+        FieldN2::sub(cc, r, e);
+        lds_store_fe(L.c, cc, lane);
+        L.ok2[lane] = sm2_on_curve26(P) ? 1u : 0u;
+        uint32_t ad[5];
+        sm3_address(ad, px, py);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) L.addr[k][lane] = ad[k];
+        JacP26 G0, G1, G;
+        comb_range_sm2_26(G0, s, tab, 0, 16);
+        while (__hip_atomic_load(&L.seq[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+            __builtin_amdgcn_s_sleep(1);
+        }
+        pair26_load_jac(G1, L.gh, lane);
+        CurveSM2x::add(G, G0, G1);
+        pair26_store_jac(L.g, G, lane);
+    } else {
+        JacP26 G1;
+        comb_range_sm2_26(G1, s, tab, 16, 32);
+        pair26_store_jac(L.gh, G1, lane);
+        __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    __syncthreads();
+    if (wave == 0 && active) {
+        JacP26 G, A, Q;
+        pair26_load_jac(G, L.g, lane);
+        pair26_load_jac(A, L.acc, lane);
+        CurveSM2x::add(Q, G, A);
+        ok = ok && L.ok2[lane] != 0u && !Q.inf;
+        fe cc, c2;
+        lds_load_fe(cc, L.c, lane);
+        fp26 z2, cm, rhs, dlt;
+        fp26_sqr(z2, Q.Z);
+        fp26_from_plain(cm, cc);
+        fp26_mul(rhs, cm, z2);
+        fp26_sub<3>(dlt, rhs, Q.X);
+        bool match = fp26_is_zero(dlt);
+        const uint32_t carry = fe_add_k(c2, cc, ParamN2::M);
+        if (carry == 0u && fe_lt_k(c2, ParamP2::M)) {
+            fp26_from_plain(cm, c2);
+            fp26_mul(rhs, cm, z2);
+            fp26_sub<3>(dlt, rhs, Q.X);
+            match = match || fp26_is_zero(dlt);
+        }
+        ok = ok && match;
+        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = ok ? L.addr[k][lane] : 0u;
+        status[i] = ok ? 0 : 1;
+    }
+}
+
 int launch_tx_verify_small_sm2(const TxKernelPolicy& pol, const uint8_t* d_pre, const uint64_t* d_pre_off,
                                const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash,
                                uint8_t* d_sender, uint8_t* d_status, hipStream_t st) {
@@ -839,8 +1055,12 @@ int launch_tx_verify_small_sm2(const TxKernelPolicy& pol, const uint8_t* d_pre, 
         const uint32_t* t26;
         const int rc = tables8_sm2_26(&t26);
         if (rc) return rc;
-        hipLaunchKernelGGL(tx_verify_sm2_pair26_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n,
-                           t26, d_txhash, d_sender, d_status);
+        if (pol.coop == 2)
+            hipLaunchKernelGGL(tx_verify_sm2_trio26_kernel, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0, st,
+                               d_pre, d_pre_off, d_sig, d_sig_off, n, t26, d_txhash, d_sender, d_status);
+        else
+            hipLaunchKernelGGL(tx_verify_sm2_pair26_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off,
+                               n, t26, d_txhash, d_sender, d_status);
     } else {
         const uint32_t *k1, *sm2;
         const int rc = tables8(&k1, &sm2);

@@ -1,0 +1,192 @@
+// ecp26_trio.h -- SM2 (a = -3) doubling and mixed addition over fp26 split across a lane trio, as
+// ec26_trio.h does for secp256k1 (same lanes, same DPP routing and role selects, same fences).  The
+// formulas and magnitudes are CurveSM2x's (ecp26.h):
+//
+//   dbl (4 levels): L1  delta = Z^2       | gamma = Y^2       | Y Z
+//                   L2  (X - d)(X + d)    | beta = X gamma    | gamma^2     (lane 2 fetches gamma)
+//                   L3  alpha^2           | --                | --          (alpha = 3 (X - d)(X + d))
+//                   L4  alpha (4 beta - X3) on lane 0, which fetches beta and gamma^2
+//                   X3 = alpha^2 - 8 beta, Y3 = alpha (4 beta - X3) - 8 gamma^2, Z3 = 2 Y Z
+//   madd (5 levels): the secp256k1 split (Z^2 | y2 Z | Z^2 -> U2 | S2 | U2 -> H^2 | rr^2 | Z H ->
+//                   J | - | V -> rr (V - X3) | Y J), with CurveSM2x's weak normalisations
+//
+// a = -3 makes alpha^3 a degree-12 term, so the doubling keeps four product levels (secp256k1's has
+// three).  A point lives in the trio as TrioPtP: P1 = (Z | Y | Y) and Q1 = (Z | Y | Z) (the first
+// doubling level's operands), Xr = (X | X | -); inf on every lane.  dbl: X <= 5, Y, Z <= 8 ->
+// (2, 2, 2); madd: X, Y <= 2, Z <= 8, Q <= 2 -> (2, 2, 2).
+#pragma once
+#include "ec26_trio.h"
+#include "ecp26.h"
+
+namespace bcosgpu {
+
+namespace trio {
+F26_HD void mul(fp26& r, const fp26& a, const fp26& b) {
+    fp26_mul(r, a, b);
+    dpp_fence(r);
+}
+F26_HD void sqr(fp26& r, const fp26& a) {
+    fp26_sqr(r, a);
+    dpp_fence(r);
+}
+}  // namespace trio
+
+struct TrioPtP {
+    fp26 P1, Q1, Xr;
+    bool inf;
+};
+
+F26_HD void trio_from_aff_sm2(TrioPtP& P, const AffP26& Q, const TrioLane& T) {
+    fp26 one;
+    fp26_set(one, p26::ONE_R);
+    trio::sel(P.P1, T.r0, one, Q.y);
+    trio::sel(P.Q1, T.r1, Q.y, one);
+    fp26_copy(P.Xr, Q.x);
+    P.inf = false;
+}
+F26_HD void trio_set_inf_sm2(TrioPtP& P) {
+    fp26_zero(P.P1);
+    fp26_zero(P.Q1);
+    fp26_zero(P.Xr);
+    P.inf = true;
+}
+F26_HD void trio_cmov_sm2(TrioPtP& P, const TrioPtP& Q, bool c) {
+    fp26_cmov(P.P1, Q.P1, c);
+    fp26_cmov(P.Q1, Q.Q1, c);
+    fp26_cmov(P.Xr, Q.Xr, c);
+    P.inf = c ? Q.inf : P.inf;
+}
+// the full Jacobian point on every lane (X from lane 0's Xr, Y from lane 1's P1, Z from lane 2's Q1)
+F26_HD void trio_to_jac_sm2(JacP26& J, const TrioPtP& P, const TrioLane& T) {
+    using namespace trio;
+    sel_dpp2<kL1, kL2>(J.X, T.r0, P.Xr, T.r1, P.Xr);
+    sel_dpp2<kR1, kL1>(J.Y, T.r1, P.P1, T.r0, P.P1);
+    sel_dpp2<kR1, kR2>(J.Z, T.r2, P.Q1, T.r1, P.Q1);
+    J.inf = P.inf;
+}
+
+// next state from X3, Y3 on lane 0 and Z3 on lane 2
+F26_HD void trio_state_sm2(TrioPtP& O, const fp26& X3, const fp26& Y3, const fp26& Z3, const TrioLane& T) {
+    using namespace trio;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t z0 = dpp<kR2>(Z3.v[i]), y1 = dpp<kL1>(Y3.v[i]), y2 = dpp<kL2>(Y3.v[i]),
+                       x1 = dpp<kL1>(X3.v[i]);
+        O.P1.v[i] = T.r0 ? z0 : T.r1 ? y1 : y2;
+        O.Q1.v[i] = T.r0 ? z0 : T.r1 ? y1 : Z3.v[i];
+        O.Xr.v[i] = T.r0 ? X3.v[i] : x1;
+    }
+#ifdef FE26_CHECK
+    {
+        const int mz0 = mdpp<kR2>(Z3.m), my1 = mdpp<kL1>(Y3.m), my2 = mdpp<kL2>(Y3.m), mx1 = mdpp<kL1>(X3.m);
+        O.P1.m = T.r0 ? mz0 : T.r1 ? my1 : my2;
+        O.Q1.m = T.r0 ? mz0 : T.r1 ? my1 : Z3.m;
+        O.Xr.m = T.r0 ? X3.m : mx1;
+    }
+#endif
+}
+
+// P <- 2P
+F26_HD void trio_dbl_sm2(TrioPtP& P, const TrioLane& T) {
+    using namespace trio;
+    fp26 o1, t, u, g, P2, Q2, o2, al, o3, be, g2, b8, X3, t4, Y3p, Y3, Z3;
+    mul(o1, P.P1, P.Q1);                 // (delta | gamma | Y Z)
+    fp26_sub<2>(t, P.Xr, o1);            // lane 0: X - delta          m X + 3
+    fp26_add(u, P.Xr, o1);               // lane 0: X + delta          m X + 1
+    fdpp<kL1>(g, o1);                    // lane 2: gamma of lane 1
+    sel(P2, T.r0, t, P.Xr);
+    sel(P2, T.r2, g, P2);                // (X - d | X | gamma)
+    sel(Q2, T.r0, u, o1);
+    sel(Q2, T.r2, g, Q2);                // (X + d | gamma | gamma)
+    mul(o2, P2, Q2);                     // (alpha / 3 | beta | gamma^2)
+    fp26_mul_int<3>(al, o2);             // lane 0: alpha              m 3
+    sqr(o3, al);                         // lane 0: alpha^2
+    fdpp<kR1>(be, o2);                   // lane 0: beta
+    fdpp<kR2>(g2, o2);                   // lane 0: gamma^2
+    fp26_mul_int<8>(b8, be);             //                            m 8
+    fp26_sub<9>(X3, o3, b8);             //                            m 11
+    fp26_normalize_weak(X3);             // X3 = alpha^2 - 8 beta      m 2
+    fp26_mul_int<4>(t4, be);             //                            m 4
+    fp26_sub<3>(t4, t4, X3);             // 4 beta - X3                m 8
+    mul(Y3p, al, t4);
+    fp26_mul_int<8>(g2, g2);             //                            m 8
+    fp26_sub<9>(Y3, Y3p, g2);            //                            m 11
+    fp26_normalize_weak(Y3);             // Y3                         m 2
+    fp26_mul_int<2>(Z3, o1);             // lane 2: Z3 = 2 Y Z         m 2
+    trio_state_sm2(P, X3, Y3, Z3, T);
+}
+
+// R <- P + Q (Q affine, never infinity); exceptional cases as CurveSM2x::madd, EXC = false drops the
+// P = +-Q tests for callers that exclude them (see the SM2 trio kernel in ecc_pair.hip)
+template <bool EXC = true>
+F26_HD void trio_madd_sm2(TrioPtP& R, const TrioPtP& P, const AffP26& Q, const TrioLane& T) {
+    using namespace trio;
+    fp26 q1r, Zb, xl1, Xl, P1, o1, P2, Q2, o2, h, P3, o3, HHx, I, P4, o4, R2, V, X3, t, W, rr, P5, Q5, J1, o5, Y3, Z3;
+    fdpp<kR1>(q1r, P.Q1);
+    sel(Zb, T.r1, q1r, P.P1);
+    sel(Zb, T.r2, P.Q1, Zb);             // Z on every lane            m <= 8
+    fdpp<kL1>(xl1, P.Xr);
+    sel(Xl, T.r2, xl1, P.Xr);
+    sel(Xl, T.r1, P.P1, Xl);             // (X | Y | X)                m <= 2
+    sel(P1, T.r1, Q.y, Zb);
+    mul(o1, P1, Zb);                     // (Z1Z1 | y2 Z | Z1Z1)
+    sel(P2, T.r1, o1, Q.x);
+    fdpp<kR1>(Q2, o1);
+    sel(Q2, T.r1, Q2, o1);
+    mul(o2, P2, Q2);                     // (U2 | S2 | U2)
+    fp26_sub<3>(h, o2, Xl);              // (H | rr | H)               m 5
+    sel(P3, T.r2, Zb, h);
+    mul(o3, P3, h);                      // (HH | rr^2 | Z H)
+    fdpp<kL2>(HHx, o3);
+    sel(HHx, T.r2, HHx, o3);
+    fp26_mul_int<4>(I, HHx);             // I = 4 HH                   m 4
+    sel(P4, T.r2, Xl, h);
+    mul(o4, P4, I);                      // (J | - | V)
+    fdpp<kR1>(R2, o3);
+    fp26_mul_int<4>(R2, R2);             // lane 0: r^2 = 4 rr^2       m 4
+    fdpp<kR2>(V, o4);                    // lane 0: V
+    fp26_sub<2>(X3, R2, o4);             //                            m 7
+    fp26_mul_int<2>(t, V);               //                            m 2
+    fp26_sub<3>(X3, X3, t);              //                            m 11
+    fp26_normalize_weak(X3);             // X3 = r^2 - J - 2V          m 2
+    fp26_sub<3>(W, V, X3);               // V - X3                     m 5
+    fdpp<kR1>(rr, h);                    // lane 0: rr                 m 5
+    sel(P5, T.r0, rr, P.P1);             // lane 0: rr, lane 1: Y
+    fdpp<kL1>(J1, o4);
+    sel(Q5, T.r0, W, J1);                // lane 0: V - X3, lane 1: J
+    mul(o5, P5, Q5);                     // (rr (V - X3) | Y J | -)
+    fdpp<kR1>(t, o5);
+    fp26_sub<2>(Y3, o5, t);              //                            m 4
+    fp26_mul_int<2>(Y3, Y3);             //                            m 8
+    fp26_normalize_weak(Y3);             // Y3 = r (V - X3) - 2 Y J    m 2
+    fp26_mul_int<2>(Z3, o3);             // lane 2: Z3 = 2 Z H         m 2
+    TrioPtP O;
+    trio_state_sm2(O, X3, Y3, Z3, T);
+    O.inf = false;
+    if constexpr (EXC) {
+        const uint32_t zf = fp26_is_zero(h) ? 1u : 0u;
+        const bool hz = bdpp_from(zf, T, 0) != 0u && !P.inf;
+        const bool rz = bdpp_from(zf, T, 1) != 0u;
+        if (any(hz && rz)) {  // P == Q: double on lane 2, which holds X (Xl), Y (P1) and Z (Q1)
+            JacP26 A, D;
+            fp26_copy(A.X, Xl);
+            fp26_copy(A.Y, P.P1);
+            fp26_copy(A.Z, P.Q1);
+            A.inf = P.inf;
+            CurveSM2x::dbl(D, A);
+            // D on lane 2 -> X3, Y3 on lane 0 and Z3 on lane 2, then the usual state
+            fp26 dx, dy;
+            fdpp<kR2>(dx, D.X);
+            fdpp<kR2>(dy, D.Y);
+            TrioPtP Dt;
+            trio_state_sm2(Dt, dx, dy, D.Z, T);
+            Dt.inf = false;
+            trio_cmov_sm2(O, Dt, hz && rz);
+        }
+        if (hz && !rz) O.inf = true;  // P == -Q
+    }
+    if (P.inf) trio_from_aff_sm2(O, Q, T);
+    R = O;
+}
+
+}  // namespace bcosgpu

@@ -1,12 +1,12 @@
-// trio_test.cpp -- host build of ec26_trio.h with FE26_CHECK: the 16 lanes of one DPP row run as
+// trio_test.cpp -- host build of ec26_trio.h / ecp26_trio.h with FE26_CHECK: the 16 lanes of one DPP row run as
 // threads in lockstep (every DPP fetch / wave vote is a barrier), so the lane-trio doubling and mixed
 // addition execute exactly as a wave does -- phantom lane 15 and the out-of-row zeros included -- while
 // every field operation asserts its magnitude contract on every lane.  Each trio's result is compared
-// with CurveK1x (ec26.h) on the same inputs: random elements at every magnitude the formulas accept,
+// with CurveK1x (ec26.h) -- or, for SM2, CurveSM2x (ecp26.h) -- on the same inputs: random elements at every magnitude the formulas accept,
 // bound-hugging limbs, and the exceptional additions (P = Q, P = -Q, P = infinity, infinity doubled).
 // Prints "trio ok <cases>" and exits 0, or the first mismatch and exits 1.
 #define FE26_CHECK 1
-#include "../../fisco-bcos_amd/csrc/ec26_trio.h"
+#include "../../fisco-bcos_amd/csrc/ecp26_trio.h"
 
 #include <condition_variable>
 #include <cstdio>
@@ -143,6 +143,72 @@ void lane_main(int lane, int round) {
     trio_to_jac(J, P, T);
     if (t < 5 && !same_point(J, R)) bad[c] = 1;
 }
+// SM2: the same harness over fp26 / CurveSM2x (inputs X, Y <= 2, Z <= 8: what both ops accept)
+void rand_fp(fp26& a, int m, int mode) {
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t bound = static_cast<uint64_t>(m) << (i == 9 ? 22 : 26);
+        a.v[i] = static_cast<uint32_t>(mode ? bound : ((static_cast<uint64_t>(rnd()) << 20 ^ rnd()) % (bound + 1)));
+    }
+    a.m = m;
+}
+bool same_p(const fp26& a, const fp26& b) {
+    fp26 x = a, y = b;
+    fp26_normalize(x);
+    fp26_normalize(y);
+    return memcmp(x.v, y.v, sizeof x.v) == 0;
+}
+bool same_point_p(const JacP26& a, const JacP26& b) {
+    if (a.inf || b.inf) return a.inf == b.inf;
+    fp26 za2, zb2, za3, zb3, l, r;
+    fp26_sqr(za2, a.Z);
+    fp26_sqr(zb2, b.Z);
+    fp26_mul(l, a.X, zb2);
+    fp26_mul(r, b.X, za2);
+    if (!same_p(l, r)) return false;
+    fp26_mul(za3, za2, a.Z);
+    fp26_mul(zb3, zb2, b.Z);
+    fp26_mul(l, a.Y, zb3);
+    fp26_mul(r, b.Y, za3);
+    return same_p(l, r);
+}
+struct CaseP {
+    JacP26 P;
+    AffP26 Q;
+    int ops, reps;
+};
+std::vector<CaseP> pcases;
+std::vector<int> pbad;
+
+void lane_main_sm2(int lane, int round) {
+    my_lane = lane;
+    const TrioLane T(lane);
+    const int t = (lane % 16) / 3;
+    const int c = round * cases_per_round + (t < 5 ? t : 4);
+    const CaseP& K = pcases[c];
+    TrioPtP P;
+    trio::sel(P.P1, T.r0, K.P.Z, K.P.Y);
+    trio::sel(P.Q1, T.r1, K.P.Y, K.P.Z);
+    P.Xr = K.P.X;
+    P.inf = K.P.inf;
+    JacP26 R = K.P;
+    for (int rep = 0; rep < K.reps; ++rep) {
+        if (K.ops & 1) {
+            for (int d = 0; d < 4; ++d) {
+                trio_dbl_sm2(P, T);
+                CurveSM2x::dbl(R, R);
+            }
+        }
+        if (K.ops & 2) {
+            trio_madd_sm2(P, P, K.Q, T);
+            JacP26 S;
+            CurveSM2x::madd(S, R, K.Q);
+            R = S;
+        }
+    }
+    JacP26 J;
+    trio_to_jac_sm2(J, P, T);
+    if (t < 5 && !same_point_p(J, R)) pbad[c] = 1;
+}
 }  // namespace
 
 int main() {
@@ -186,6 +252,53 @@ int main() {
         for (int l = 0; l < kLanes; ++l) th.emplace_back(lane_main, l, r);
         for (auto& x : th) x.join();
     }
+    for (int k = 0; k < 300; ++k) {
+        CaseP K;
+        const int mode = k % 7 == 6 ? 1 : 0;
+        rand_fp(K.P.X, k % 3 == 0 ? 2 : 1 + static_cast<int>(rnd() % 2), mode);
+        rand_fp(K.P.Y, k % 3 == 0 ? 2 : 1 + static_cast<int>(rnd() % 2), mode);
+        rand_fp(K.P.Z, k % 3 == 0 ? 8 : 1 + static_cast<int>(rnd() % 8), mode);
+        rand_fp(K.Q.x, 1 + static_cast<int>(rnd() % 2), mode);
+        rand_fp(K.Q.y, 1 + static_cast<int>(rnd() % 2), mode);
+        K.P.inf = false;
+        const int round = k / cases_per_round;
+        K.ops = 1 + round % 3;
+        K.reps = 1 + round % 4;
+        const int special = k % 10;
+        if (special == 1 || special == 2) {  // P = (x Z^2, +-y Z^3, Z) equals +-Q
+            fp26 z2, z3;
+            rand_fp(K.P.Z, 2, 0);
+            rand_fp(K.Q.x, 1, 0);
+            rand_fp(K.Q.y, 1, 0);
+            fp26_sqr(z2, K.P.Z);
+            fp26_mul(z3, z2, K.P.Z);
+            fp26_mul(K.P.X, K.Q.x, z2);
+            fp26_mul(K.P.Y, K.Q.y, z3);
+            if (special == 2) {
+                fp26_neg<2>(K.P.Y, K.P.Y);
+                fp26_normalize_weak(K.P.Y);
+            }
+        } else if (special == 3) {
+            CurveSM2x::set_inf(K.P);
+        }
+        pcases.push_back(K);
+    }
+    pbad.assign(pcases.size(), 0);
+    for (int r = 0; r < static_cast<int>(pcases.size()) / cases_per_round; ++r) {
+        std::vector<std::thread> th;
+        for (int l = 0; l < kLanes; ++l) th.emplace_back(lane_main_sm2, l, r);
+        for (auto& x : th) x.join();
+    }
+    int npbad = 0;
+    for (size_t i = 0; i < pbad.size(); ++i)
+        if (pbad[i]) {
+            if (!npbad) printf("sm2 mismatch in case %zu (ops %d reps %d)\n", i, pcases[i].ops, pcases[i].reps);
+            ++npbad;
+        }
+    if (npbad) {
+        printf("trio sm2 mismatches %d of %zu\n", npbad, pcases.size());
+        return 1;
+    }
     int nbad = 0;
     for (size_t i = 0; i < bad.size(); ++i)
         if (bad[i]) {
@@ -196,6 +309,6 @@ int main() {
         printf("trio mismatches %d of %zu\n", nbad, cases.size());
         return 1;
     }
-    printf("trio ok %zu\n", cases.size());
+    printf("trio ok %zu secp256k1 + %zu sm2\n", cases.size(), pcases.size());
     return 0;
 }

@@ -264,10 +264,10 @@ def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
     pre, po, sg, so = (x.cpu().numpy() for x in (b.pre, b.pre_off, b.sig, b.sig_off))
     wh, ws, wst = oracle.tx_verify_packed(suite, pre, po.astype(np.uint64), sg, so.astype(np.uint64), nthreads=16)
     # secp256k1: lane-trio, cooperative-pair, 4-wave split, one-lane occ 1 / 2 on the 10 x 26-bit and on the
-    # 8 x 32-bit point arithmetic; SM2: pair kernel and one-lane occ 1 / 2, each on fp26 and 8 x 32
+    # 8 x 32-bit point arithmetic; SM2: lane-trio and pair kernels and one-lane occ 1 / 2, each on fp26 and 8 x 32
     variants = ([(1, 1, 2, 1), (1, 1, 1, 1), (1, 1, 0, 1), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)]
                 if suite == 0
-                else [(1, 1, 1, 1), (1, 1, 1, 0), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)])
+                else [(1, 1, 2, 1), (1, 1, 1, 1), (1, 1, 1, 0), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)])
     try:
         for split, occ, coop, field in variants:
             gpu.set_tx_kernel_policy(split, occ, coop, field)
