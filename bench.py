@@ -96,13 +96,30 @@ def kernel_source_sha():
     return h.hexdigest()[:16]
 
 
+def _auto_small_kernel(suite, n, cus):
+    """Mirror of ecc_txv.hip auto_small_kernel: 2 trio, 1 pair, 0 one-lane (rounds x latency)."""
+    lat = (1.77, 1.15, 1.0) if suite == 1 else (2.36, 1.19, 1.0)
+    per = (256 * cus, 64 * cus, 40 * cus)
+    best, cost = 2, float("inf")
+    for k in (2, 1, 0):
+        c = -(-n // per[k]) * lat[k]
+        if c < cost:
+            best, cost = k, c
+    return best
+
+
 def _kernel_name(suite, n):
     """Which tx-verify kernel the library launches for this batch (mirrors launch_tx_verify and its
     policy: BCOSGPU_TXV_* and BCOSGPU_K1_F26, read once by the library)."""
+    import torch
     f26 = os.environ.get("BCOSGPU_K1_F26", "1") != "0"
     split = os.environ.get("BCOSGPU_TXV_SPLIT")
     small = (split == "1") if split in ("0", "1") else n <= (1 << 15)
     coop = {"0": 0, "1": 1}.get(os.environ.get("BCOSGPU_TXV_COOP", "2"), 2)
+    if split not in ("0", "1") and coop == 2 and f26:
+        cus = torch.cuda.get_device_properties(0).multi_processor_count if torch.cuda.is_available() else 256
+        k = _auto_small_kernel(suite, n, cus) if n <= (1 << 16) else 0
+        small, coop = k != 0, (k if k else coop)
     if suite == 0 and small:
         if not coop:
             return "tx_verify_split_kernel"

@@ -58,6 +58,39 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(const uint8_t* __re
 }
 
 
+// The automatic choice for batches up to 2^16 (policy split = -1, coop = 2, field = 1): each kernel
+// runs its batch in rounds of resident workgroups -- the trio kernels take 40 txs per CU, the pair
+// kernels 64, the one-lane kernel 256 (one wave per SIMD) -- and a round costs a fixed latency, so
+// the cost is rounds x latency.  The latencies are relative to the trio kernel's, measured on MI355X
+// (tools/small_sweep.py, profiles/r02_small_sweep.json: secp256k1 trio 0.415 / pair 0.493 / one-lane
+// 0.98 ms per round; SM2 0.854 / 0.977 / 1.51).  Returns 2 (trio), 1 (pair) or 0 (one-lane).
+static int cu_count() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        cus[dev] = c;
+    }
+    return cus[dev];
+}
+static int auto_small_kernel(int suite, uint64_t n, int cus) {
+    const bool sm2 = suite == BCOSGPU_SUITE_SM2;
+    const double lat[3] = {sm2 ? 1.77 : 2.36, sm2 ? 1.15 : 1.19, 1.0};  // one-lane, pair, trio
+    const uint64_t per[3] = {256ull * cus, 64ull * cus, 40ull * cus};
+    int best = 2;
+    double cost = 1e30;
+    for (int k = 2; k >= 0; --k) {
+        const double c = static_cast<double>((n + per[k] - 1) / per[k]) * lat[k];
+        if (c < cost) {
+            cost = c;
+            best = k;
+        }
+    }
+    return best;
+}
+
 int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off, const uint8_t* d_sig,
                      const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash, uint8_t* d_sender, uint8_t* d_status,
                      hipStream_t st) {
@@ -66,10 +99,15 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
     int bits;
     int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    const TxKernelPolicy pol = tx_policy();
-    // small batches (SIMDs left idle by one tx per lane): the cooperative kernels on the L2-resident
-    // 8-bit comb tables -- secp256k1 (C2) in ecc_coop.hip, SM2 in ecc_pair.hip
-    const bool small = pol.split >= 0 ? pol.split == 1 : n <= (1ull << 15);
+    TxKernelPolicy pol = tx_policy();
+    // small batches (SIMDs left idle by one tx per lane): the cooperative kernels -- secp256k1 (C2) in
+    // ecc_coop.hip, SM2 in ecc_pair.hip -- chosen by rounds x latency when the policy is automatic
+    bool small = pol.split >= 0 ? pol.split == 1 : n <= (1ull << 15);
+    if (pol.split < 0 && pol.coop == 2 && pol.f26) {
+        const int k = n <= (1ull << 16) ? auto_small_kernel(suite, n, cu_count()) : 0;
+        small = k != 0;
+        if (small) pol.coop = k;
+    }
     if (suite == BCOSGPU_SUITE_SECP256K1 && small)
         return launch_tx_verify_small_secp(pol, d_pre, d_pre_off, d_sig, d_sig_off, n, d_txhash, d_sender, d_status, st);
     if (suite == BCOSGPU_SUITE_SM2 && small && pol.coop)
