@@ -156,6 +156,29 @@ def _traffic(workload, kernel):
     return None, None, None
 
 
+def _valu_issue(workload, kernel):
+    """VALU issue fraction of `kernel` from the same PMC file: wave64 VALU instructions per SIMD x 4
+    cycles (a SIMD16 issues one wave64 VALU op per 4 cycles) over the dispatch's cycles per XCD
+    (GRBM_GUI_ACTIVE is summed over the 8 XCDs).  Near 1 = the kernel is issue-bound, and only fewer
+    instructions make it faster."""
+    path = os.path.join(ROOT, "profiles", PMC_GLOB.format(workload))
+    try:
+        with open(path) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for name, c in pmc.get("kernels", {}).items():
+        if _norm(name) == _norm(kernel) and c.get("SQ_INSTS_VALU") and c.get("GRBM_GUI_ACTIVE") and c.get("SQ_WAVES"):
+            simds = 1024.0
+            cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+            return {"frac": c["SQ_INSTS_VALU"] * 4.0 / simds / cycles,
+                    "valu_per_wave": c["SQ_INSTS_VALU"] / c["SQ_WAVES"],
+                    "waves": c["SQ_WAVES"], "source": os.path.relpath(path, ROOT),
+                    "note": "VALU instructions x 4 cycles / 1,024 SIMDs / dispatch cycles per XCD; a lone "
+                            "wave per SIMD (latency kernels) cannot reach 1"}
+    return None
+
+
 def _block_plan(nblocks, world, rank):
     per = math.ceil(nblocks / world)
     return min(rank * per, nblocks), min((rank + 1) * per, nblocks)
@@ -273,10 +296,12 @@ def run_leg(ctx, wl_name, steps=None, warmup=3, warm_seconds=0.0, min_seconds=2.
     ex = n * f_exec * MAC_PER_F / (kernel_ms * 1e-3)
     alg = n * f_alg * MAC_PER_F / (kernel_ms * 1e-3)
     traffic, traffic_src, same_src = _traffic(wl_name, kname)
+    valu_issue = _valu_issue(wl_name, kname)
     roofline = {
         "bound": "int-valu", "achieved": ex / 1e12, "peak": PEAK_MAC_PER_S / 1e12, "unit": "TMAC/s",
         "frac": ex / PEAK_MAC_PER_S, "traffic": traffic, "traffic_source": traffic_src,
-        "traffic_same_kernel_source": same_src, "kernel": kname, "kernel_ms": kernel_ms, "units_per_launch": n,
+        "traffic_same_kernel_source": same_src, "valu_issue": valu_issue, "kernel": kname, "kernel_ms": kernel_ms,
+        "units_per_launch": n,
         "work_per_unit": "%d F x %d MAC executed (kernel schedule, DESIGN.md 9)" % (f_exec, MAC_PER_F),
         "algorithmic": {"work_per_unit": "%d F x %d MAC (SURVEY.md 8d, non-GLV count)" % (f_alg, MAC_PER_F),
                         "achieved": alg / 1e12, "frac": alg / PEAK_MAC_PER_S,
