@@ -38,14 +38,26 @@ struct TrioPt {
     bool inf;
 };
 
-// lane role inside its trio and the three role predicates
+// lane role inside its trio, the three role predicates and (device) their wave masks for
+// v_cndmask_b32_dpp (n* = complements)
 struct TrioLane {
     bool r0, r1, r2;
+    uint64_t m0, m1, m2, n0, n1, n2;
     F26_HD explicit TrioLane(int lane) {
         const int role = (lane & 15) % 3;
         r0 = role == 0;
         r1 = role == 1;
         r2 = role == 2;
+#if defined(__HIP_DEVICE_COMPILE__)
+        m0 = __builtin_amdgcn_ballot_w64(r0);
+        m1 = __builtin_amdgcn_ballot_w64(r1);
+        m2 = __builtin_amdgcn_ballot_w64(r2);
+#else
+        m0 = m1 = m2 = 0;
+#endif
+        n0 = ~m0;
+        n1 = ~m1;
+        n2 = ~m2;
     }
 };
 
@@ -133,6 +145,55 @@ F26_HD void sel_dpp2(E& r, bool c, const E& a, bool d, const E& b) {
     }
     F26_SETM(r, c ? a.m : d ? m1 : m2);
 }
+// r = c ? a : DPP<CTRL>(b) in one v_cndmask_b32_dpp per limb (the DPP combiner is off, so the fold
+// is written out): VCC = cm, the wave mask of c; s_nop 1 gives the DPP source its two wait states
+// after a VALU write (SALU -> VALU reads of VCC need none).  Five limbs per block (operand limit).
+#define TRIO_CSEL_INS(D, S0, S1, CTL) "v_cndmask_b32_dpp %" #D ", %" #S0 ", %" #S1 ", vcc " CTL \
+    " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+#define TRIO_CSEL5(CTL, r, a, b, o, cm)                                                                \
+    asm volatile("s_mov_b64 vcc, %15\n\ts_nop 1\n\t" TRIO_CSEL_INS(0, 10, 5, CTL) TRIO_CSEL_INS(1, 11, 6, CTL) \
+                 TRIO_CSEL_INS(2, 12, 7, CTL) TRIO_CSEL_INS(3, 13, 8, CTL) TRIO_CSEL_INS(4, 14, 9, CTL)      \
+                 : "=&v"((r).v[o]), "=&v"((r).v[o + 1]), "=&v"((r).v[o + 2]), "=&v"((r).v[o + 3]),       \
+                   "=&v"((r).v[o + 4])                                                                  \
+                 : "v"((a).v[o]), "v"((a).v[o + 1]), "v"((a).v[o + 2]), "v"((a).v[o + 3]), "v"((a).v[o + 4]), \
+                   "v"((b).v[o]), "v"((b).v[o + 1]), "v"((b).v[o + 2]), "v"((b).v[o + 3]), "v"((b).v[o + 4]), \
+                   "s"(cm)                                                                              \
+                 : "vcc")
+template <int CTRL, class E>
+F26_HD void csel(E& r, bool c, uint64_t cm, const E& a, const E& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    (void)c;
+    E t;
+    if constexpr (CTRL == kL1) {
+        TRIO_CSEL5("row_shr:1", t, a, b, 0, cm);
+        TRIO_CSEL5("row_shr:1", t, a, b, 5, cm);
+    } else if constexpr (CTRL == kL2) {
+        TRIO_CSEL5("row_shr:2", t, a, b, 0, cm);
+        TRIO_CSEL5("row_shr:2", t, a, b, 5, cm);
+    } else if constexpr (CTRL == kR1) {
+        TRIO_CSEL5("row_shl:1", t, a, b, 0, cm);
+        TRIO_CSEL5("row_shl:1", t, a, b, 5, cm);
+    } else {
+        static_assert(CTRL == kR2, "csel: row shift by 1 or 2");
+        TRIO_CSEL5("row_shl:2", t, a, b, 0, cm);
+        TRIO_CSEL5("row_shl:2", t, a, b, 5, cm);
+    }
+    r = t;
+#else
+    (void)cm;
+#ifdef FE26_CHECK
+    const int mb = mdpp<CTRL>(b.m);
+#endif
+    E t;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t x = dpp<CTRL>(b.v[i]);
+        t.v[i] = c ? a.v[i] : x;
+    }
+    F26_SETM(t, c ? a.m : mb);
+    r = t;
+#endif
+}
 F26_HD uint32_t bdpp_from(uint32_t f, const TrioLane& T, int src) {
     // the value of f held by role src of this lane's trio
     const uint32_t l1 = dpp<kL1>(f), l2 = dpp<kL2>(f), r1 = dpp<kR1>(f), r2 = dpp<kR2>(f);
@@ -172,40 +233,29 @@ F26_HD void trio_to_jac(Jac26& J, const TrioPt& P, const TrioLane& T) {
 // P <- 2P  (X, Y <= 10, Z <= 16 -> (10, 10, 2))
 F26_HD void trio_dbl(TrioPt& P, const TrioLane& T) {
     using namespace trio;
-    fe26 o1, T2, S2, o2, E, F, XB, D, X3, W, P3, Q3, o3, C8, Y3, t;
+    fe26 o1, T2, S2, o2, F, XB, D, X3, W, P3, Q3, o3, C8, Y3, t;
     sqr(o1, P.S1);                                       // (A | B | B)                 m 1
 #pragma unroll
     for (int i = 0; i < 10; ++i) T2.v[i] = o1.v[i] + (T.r0 ? o1.v[i] << 1 : 0u);  // (3A | B | B) m <= 3
     F26_SETM(T2, T.r0 ? 3 : 1);
     sel(S2, T.r2, P.Xs, T2);                             // (3A | B | X)                m <= 10
     mul(o2, S2, T2);                                     // (F | C | XB)
-    fdpp<kL1>(E, T2);                                    // lane 1: E = 3A              m 3
     fdpp<kL1>(F, o2);                                    // lane 1: F                   m 1
     fdpp<kR1>(XB, o2);                                   // lane 1: X B                 m 1
     fe26_mul_int<4>(D, XB);                              // D = 4 X B                   m 4
     fe26_mul_int<2>(t, D);                               //                             m 8
     fe26_sub<9>(X3, F, t);                               // X3 = F - 2D                 m 10
     fe26_sub<11>(W, D, X3);                              // D - X3                      m 15
-    sel(P3, T.r2, P.S1, E);                              // lane 1: E, lane 2: Y
+    csel<kL1>(P3, T.r2, T.m2, P.S1, T2);                 // lane 1: E = 3A (lane 0), lane 2: Y
     sel(Q3, T.r2, P.Zs, W);                              // lane 1: D - X3, lane 2: Z
     mul(o3, P3, Q3);                                     // (- | E (D - X3) | Y Z)
     fe26_mul_int<8>(C8, o2);                             // lane 1: 8C                  m 8
     fe26_sub<9>(Y3, o3, C8);                             // lane 1: Y3                  m 10
     fe26_mul_int<2>(P.Zs, o3);                           // lane 2: Z3 = 2 Y Z          m 2
     // next state: S1 = (X3 | Y3 | Y3) from lane 1, Xs = X3 on lane 2
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-        const uint32_t x0 = dpp<kR1>(X3.v[i]), y2 = dpp<kL1>(Y3.v[i]);
-        P.S1.v[i] = T.r0 ? x0 : T.r1 ? Y3.v[i] : y2;    // lane 0 <- X3, lane 2 <- Y3 of lane 1
-        P.Xs.v[i] = dpp<kL1>(X3.v[i]);                   // lane 2 <- X3 of lane 1
-    }
-#ifdef FE26_CHECK
-    {
-        const int mx0 = mdpp<kR1>(X3.m), my2 = mdpp<kL1>(Y3.m), mx2 = mdpp<kL1>(X3.m);
-        P.S1.m = T.r0 ? mx0 : T.r1 ? Y3.m : my2;
-        P.Xs.m = mx2;
-    }
-#endif
+    csel<kL1>(t, T.r1, T.m1, Y3, Y3);                    // lanes 1, 2: Y3 of lane 1
+    csel<kR1>(P.S1, !T.r0, T.n0, t, X3);                 // lane 0: X3 of lane 1
+    fdpp<kL1>(P.Xs, X3);                                 // lane 2 <- X3 of lane 1
 }
 
 // R <- P + Q, Q affine (x, y <= 2) and never infinity; P: X, Y <= 10, Z <= 16 -> (9, 6, 2).  The
@@ -215,14 +265,15 @@ F26_HD void trio_dbl(TrioPt& P, const TrioLane& T) {
 template <bool EXC = true>
 F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane& T) {
     using namespace trio;
-    fe26 Zb, P1, o1, P2, Q2, o2, Xl, h, P3, o3, HHx, I, P4, o4, R2, V, X3, W, rr, P5, Q5, J1, o5, Y3, t;
-    sel_dpp2<kR1, kR2>(Zb, T.r2, P.Zs, T.r1, P.Zs);     // Z on every lane
+    fe26 Zb, P1, o1, P2, Q2, o2, Xl, h, P3, o3, HHx, I, P4, o4, R2, V, X3, W, P5, Q5, o5, Y3, t;
+    fdpp<kR2>(t, P.Zs);
+    csel<kR1>(Zb, !T.r1, T.n1, t, P.Zs);                 // lane 0: Z of lane 2, lane 1 too
+    sel(Zb, T.r2, P.Zs, Zb);                             // Z on every lane
     sel(P1, T.r1, Q.y, Zb);
     mul(o1, P1, Zb);                                     // (Z1Z1 | y2 Z | Z1Z1)
     TRIO_DUMP(0, o1);
     sel(P2, T.r1, o1, Q.x);
-    fdpp<kR1>(Q2, o1);
-    sel(Q2, T.r1, Q2, o1);                               // lane 1: Z1Z1 of lane 2
+    csel<kR1>(Q2, !T.r1, T.n1, o1, o1);                  // lane 1: Z1Z1 of lane 2
     mul(o2, P2, Q2);                                     // (U2 | S2 | U2)
     TRIO_DUMP(1, o2);
     sel(Xl, T.r2, P.Xs, P.S1);                           // (X | Y | X)                 m <= 10
@@ -231,8 +282,7 @@ F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane
     mul(o3, P3, h);                                      // (HH | rr^2 | Z H)
     TRIO_DUMP(2, h);
     TRIO_DUMP(3, o3);
-    fdpp<kL2>(HHx, o3);
-    sel(HHx, T.r2, HHx, o3);                             // lanes 0, 2: HH
+    csel<kL2>(HHx, !T.r2, T.n2, o3, o3);                 // lanes 0, 2: HH
     fe26_mul_int<4>(I, HHx);                             // I = 4 HH                    m 4
     sel(P4, T.r2, P.Xs, h);
     mul(o4, P4, I);                                      // (J | - | V)
@@ -245,10 +295,8 @@ F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane
     fe26_mul_int<2>(t, V);                               //                             m 2
     fe26_sub<3>(X3, X3, t);                              // X3                          m 9
     fe26_sub<10>(W, V, X3);                              // V - X3                      m 11
-    fdpp<kR1>(rr, h);                                    // lane 0: rr                  m 12
-    sel(P5, T.r0, rr, P.S1);                             // lane 0: rr, lane 1: Y
-    fdpp<kL1>(J1, o4);                                   // lane 1: J of lane 0
-    sel(Q5, T.r0, W, J1);
+    csel<kR1>(P5, !T.r0, T.n0, P.S1, h);                 // lane 0: rr (lane 1), lane 1: Y   m 12
+    csel<kL1>(Q5, T.r0, T.m0, W, o4);                    // lane 0: V - X3, lane 1: J of lane 0
     mul(o5, P5, Q5);                                     // (rr (V - X3) | Y J | -)
     TRIO_DUMP(5, o5);
     TRIO_DUMP(6, X3);
@@ -257,7 +305,9 @@ F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane
     fe26_mul_int<2>(Y3, Y3);                             // lane 0: Y3                  m 6
     TRIO_DUMP(7, Y3);
     TrioPt O;
-    sel_dpp2<kL1, kL2>(O.S1, T.r0, X3, T.r1, Y3);      // (X3 | Y3 | Y3) from lane 0
+    fdpp<kL2>(t, Y3);
+    csel<kL1>(O.S1, !T.r1, T.n1, t, Y3);                 // lanes 1, 2: Y3 of lane 0
+    sel(O.S1, T.r0, X3, O.S1);                           // (X3 | Y3 | Y3)
     fdpp<kL2>(O.Xs, X3);                                 // lane 2 <- X3 of lane 0
     fe26_mul_int<2>(O.Zs, o3);                           // lane 2: Z3 = 2 Z H          m 2
     O.inf = false;
