@@ -236,7 +236,10 @@ F26_HD void trio_dbl(TrioPt& P, const TrioLane& T) {
     fe26 o1, T2, S2, o2, F, XB, D, X3, W, P3, Q3, o3, C8, Y3, t;
     sqr(o1, P.S1);                                       // (A | B | B)                 m 1
 #pragma unroll
-    for (int i = 0; i < 10; ++i) T2.v[i] = o1.v[i] + (T.r0 ? o1.v[i] << 1 : 0u);  // (3A | B | B) m <= 3
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t x3 = (o1.v[i] << 1) + o1.v[i];  // one v_lshl_add_u32
+        T2.v[i] = T.r0 ? x3 : o1.v[i];                  // (3A | B | B)               m <= 3
+    }
     F26_SETM(T2, T.r0 ? 3 : 1);
     sel(S2, T.r2, P.Xs, T2);                             // (3A | B | X)                m <= 10
     mul(o2, S2, T2);                                     // (F | C | XB)
