@@ -269,14 +269,13 @@ template <bool EXC = true>
 F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane& T) {
     using namespace trio;
     fe26 Zb, P1, o1, P2, Q2, o2, Xl, h, P3, o3, HHx, I, P4, o4, R2, V, X3, W, P5, Q5, o5, Y3, t;
-    fdpp<kR2>(t, P.Zs);
-    csel<kR1>(Zb, !T.r1, T.n1, t, P.Zs);                 // lane 0: Z of lane 2, lane 1 too
-    sel(Zb, T.r2, P.Zs, Zb);                             // Z on every lane
+    sel_dpp2<kR1, kR2>(Zb, T.r2, P.Zs, T.r1, P.Zs);     // Z on every lane
     sel(P1, T.r1, Q.y, Zb);
     mul(o1, P1, Zb);                                     // (Z1Z1 | y2 Z | Z1Z1)
     TRIO_DUMP(0, o1);
     sel(P2, T.r1, o1, Q.x);
-    csel<kR1>(Q2, !T.r1, T.n1, o1, o1);                  // lane 1: Z1Z1 of lane 2
+    fdpp<kR1>(Q2, o1);
+    sel(Q2, T.r1, Q2, o1);                               // lane 1: Z1Z1 of lane 2
     mul(o2, P2, Q2);                                     // (U2 | S2 | U2)
     TRIO_DUMP(1, o2);
     sel(Xl, T.r2, P.Xs, P.S1);                           // (X | Y | X)                 m <= 10
@@ -285,7 +284,8 @@ F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane
     mul(o3, P3, h);                                      // (HH | rr^2 | Z H)
     TRIO_DUMP(2, h);
     TRIO_DUMP(3, o3);
-    csel<kL2>(HHx, !T.r2, T.n2, o3, o3);                 // lanes 0, 2: HH
+    fdpp<kL2>(HHx, o3);
+    sel(HHx, T.r2, HHx, o3);                             // lanes 0, 2: HH
     fe26_mul_int<4>(I, HHx);                             // I = 4 HH                    m 4
     sel(P4, T.r2, P.Xs, h);
     mul(o4, P4, I);                                      // (J | - | V)
@@ -298,8 +298,10 @@ F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane
     fe26_mul_int<2>(t, V);                               //                             m 2
     fe26_sub<3>(X3, X3, t);                              // X3                          m 9
     fe26_sub<10>(W, V, X3);                              // V - X3                      m 11
-    csel<kR1>(P5, !T.r0, T.n0, P.S1, h);                 // lane 0: rr (lane 1), lane 1: Y   m 12
-    csel<kL1>(Q5, T.r0, T.m0, W, o4);                    // lane 0: V - X3, lane 1: J of lane 0
+    fdpp<kR1>(P5, h);
+    sel(P5, T.r0, P5, P.S1);                             // lane 0: rr (lane 1), lane 1: Y   m 12
+    fdpp<kL1>(Q5, o4);
+    sel(Q5, T.r0, W, Q5);                                // lane 0: V - X3, lane 1: J of lane 0
     mul(o5, P5, Q5);                                     // (rr (V - X3) | Y J | -)
     TRIO_DUMP(5, o5);
     TRIO_DUMP(6, X3);
@@ -308,9 +310,7 @@ F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane
     fe26_mul_int<2>(Y3, Y3);                             // lane 0: Y3                  m 6
     TRIO_DUMP(7, Y3);
     TrioPt O;
-    fdpp<kL2>(t, Y3);
-    csel<kL1>(O.S1, !T.r1, T.n1, t, Y3);                 // lanes 1, 2: Y3 of lane 0
-    sel(O.S1, T.r0, X3, O.S1);                           // (X3 | Y3 | Y3)
+    sel_dpp2<kL1, kL2>(O.S1, T.r0, X3, T.r1, Y3);      // (X3 | Y3 | Y3) from lane 0
     fdpp<kL2>(O.Xs, X3);                                 // lane 2 <- X3 of lane 0
     fe26_mul_int<2>(O.Zs, o3);                           // lane 2: Z3 = 2 Z H          m 2
     O.inf = false;
