@@ -69,7 +69,8 @@ KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_device.h", "fisco-bcos_amd/csrc/ecc_table
               "fisco-bcos_amd/csrc/fe_asm.h", "fisco-bcos_amd/csrc/fe.h",
               "fisco-bcos_amd/csrc/ec.h", "fisco-bcos_amd/csrc/hash_device.h", "fisco-bcos_amd/csrc/modinv.h",
               "fisco-bcos_amd/csrc/fe26.h", "fisco-bcos_amd/csrc/ec26.h", "fisco-bcos_amd/csrc/recover26.h",
-              "fisco-bcos_amd/csrc/fp26.h", "fisco-bcos_amd/csrc/ecp26.h", "fisco-bcos_amd/csrc/verify_sm2_26.h"]
+              "fisco-bcos_amd/csrc/fp26.h", "fisco-bcos_amd/csrc/ecp26.h", "fisco-bcos_amd/csrc/verify_sm2_26.h",
+              "fisco-bcos_amd/csrc/ec26_trio.h", "fisco-bcos_amd/csrc/ecp26_trio.h"]
 
 WORKLOADS = {
     "c2": dict(suite=0, n=10_000, scaling="weak",

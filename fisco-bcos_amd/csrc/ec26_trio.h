@@ -27,7 +27,7 @@
 #pragma once
 #include "ec26.h"
 
-#ifndef TRIO_DUMP
+#ifndef TRIO_DUMP  // tools/triobench.hip defines it to dump the addition's per-level values
 #define TRIO_DUMP(slot, a) ((void)0)
 #endif
 
