@@ -283,6 +283,67 @@ def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
         gpu.set_tx_kernel_policy()
 
 
+def _mutate_sm2(rng, sig, kind):
+    s = bytearray(sig)
+    if kind == 1:
+        s[rng.integers(0, 128)] ^= 1 << int(rng.integers(0, 8))
+    elif kind == 2:
+        s[0:32] = N_SM2.to_bytes(32, "big")  # r = n
+    elif kind == 3:
+        s[32:64] = bytes(32)  # s = 0
+    elif kind == 4:  # r + s = n
+        r = int.from_bytes(bytes(s[0:32]), "big")
+        s[32:64] = ((N_SM2 - r) % N_SM2).to_bytes(32, "big")
+    elif kind == 5:
+        s[64:96] = b"\xff" * 32  # pubkey x >= p
+    elif kind == 6:
+        s[127] ^= 1  # pubkey off the curve
+    elif kind == 7:
+        s[0:32] = bytes(32)  # r = 0
+    return bytes(s)
+
+
+@pytest.mark.parametrize("suite", [0, 1])
+def test_tx_verify_kernel_variants_edge_signatures(gpu, oracle, suite):
+    """The small-batch kernels (lane-trio, pair, split) and the one-lane kernels on the signature edge cases
+    the reference rejects or accepts specially -- r or s = 0, r = n, v out of range, x off the curve,
+    v = 2 / 3 with r + n as the x-coordinate (secp256k1), r + s = n, a public key off the curve or >= p
+    (SM2) -- through the fused Transaction::verify path, against the oracle.  The automatic policy is
+    the first variant (at this size it takes the lane-trio kernel)."""
+    import torch
+    from bcos_gpu import device, synth
+    rng = np.random.default_rng(97 + suite)
+    n = 640 + 7
+    b = synth.make_batch(suite, n, seed=131 + suite, flip_frac=0.0, bad_v_frac=0.0)
+    sig = b.sig.view(n, b.sig_len).cpu().numpy()
+    mutated = np.array([np.frombuffer(_mutate(rng, sig[i].tobytes(), i % 9) if suite == 0
+                                      else _mutate_sm2(rng, sig[i].tobytes(), i % 8), dtype=np.uint8)
+                        for i in range(n)])
+    d_sig = torch.from_numpy(mutated.reshape(-1).copy()).cuda()
+    pre, po, so = (x.cpu().numpy() for x in (b.pre, b.pre_off, b.sig_off))
+    wh, ws, wst = oracle.tx_verify_packed(suite, pre, po.astype(np.uint64), mutated.reshape(-1),
+                                          so.astype(np.uint64), nthreads=16)
+    assert (wst == 0).sum() > n // 10 and (wst != 0).sum() > n // 4
+    variants = [None, (1, 1, 2, 1), (1, 1, 1, 1), (1, 1, 0, 1) if suite == 0 else (1, 1, 1, 0), (0, 2, 0, 1),
+                (0, 2, 0, 0)]
+    try:
+        for v in variants:
+            if v is None:
+                gpu.set_tx_kernel_policy()
+            else:
+                gpu.set_tx_kernel_policy(*v)
+            th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+            snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
+            st = torch.empty(n, dtype=torch.uint8, device="cuda")
+            device.tx_verify(suite, b.pre, b.pre_off, d_sig, b.sig_off, th, snd, st)
+            torch.cuda.synchronize()
+            assert np.array_equal(st.cpu().numpy(), wst), v
+            assert np.array_equal(snd.cpu().numpy(), ws), v
+            assert np.array_equal(th.cpu().numpy(), wh), v
+    finally:
+        gpu.set_tx_kernel_policy()
+
+
 _SMALL_TABLES_SCRIPT = """
 import sys
 import numpy as np
