@@ -343,7 +343,7 @@ struct KeccakCoop {
     }
     __device__ __forceinline__ void permute(uint32_t& lo, uint32_t& hi) const {
         const bool x0 = x == 0, x4 = x == 4, x34 = x >= 3, y1 = y == 1, y2 = y == 2, ry = y >= 3;
-#pragma unroll 1
+#pragma unroll
         for (int round = 0; round < 24; ++round) {
             // theta
             // (every cross-lane fetch is evaluated on all lanes, then selected: a fetch inside one arm
