@@ -78,6 +78,20 @@ def test_merkle_property_small(gpu, oracle):
                 assert got == [want[i].tobytes() for i in range(want.shape[0])], (width, n, hasher)
 
 
+@pytest.mark.parametrize("width", [2, 3, 16, 64])
+def test_merkle_full_tree_through_top_kernel(gpu, oracle, width):
+    """Trees tall enough for the single-workgroup top kernel (levels kept in LDS between passes, cooperative
+    and one-lane passes): every entry of the output vector, both hashers, a generic width included."""
+    rng = np.random.default_rng(40 + width)
+    n = 70_001
+    leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    for hasher, H in ((0, gpu.Keccak256()), (1, gpu.SM3())):
+        got = gpu.Merkle(H, width).generate_merkle([leaves[i].tobytes() for i in range(n)])
+        _, want = oracle.merkle(hasher, width, leaves, want_tree=True)
+        assert len(got) == want.shape[0]
+        assert got == [want[i].tobytes() for i in range(want.shape[0])], (width, hasher)
+
+
 def test_merkle_empty_throws(gpu):
     with pytest.raises(ValueError):
         gpu.Merkle(gpu.SM3(), 2).generate_merkle([])
