@@ -97,43 +97,54 @@ def kernel_source_sha():
     return h.hexdigest()[:16]
 
 
-def _auto_small_kernel(suite, n, cus):
-    """Mirror of ecc_txv.hip auto_small_kernel: 2 trio, 1 pair, 0 one-lane (rounds x latency)."""
-    lat = (1.77, 1.15, 1.0) if suite == 1 else (2.36, 1.19, 1.0)
-    per = (256 * cus, 64 * cus, 40 * cus)
-    best, cost = 2, float("inf")
-    for k in (2, 1, 0):
+def _auto_kernel(suite, n, cus, small_ok=True):
+    """Mirror of ecc_txv.hip auto_kernel (rounds x latency): 2 trio, 1 pair, 0 one-lane at occupancy 1,
+    -2 one-lane at occupancy 2 (whose tail round of <= one wave per SIMD costs an occupancy-1 round)."""
+    lat = (3.13, 1.77, 1.15, 1.0) if suite == 1 else (4.13, 2.36, 1.19, 1.0)
+    per = (512 * cus, 256 * cus, 64 * cus, 40 * cus)
+    code = (-2, 0, 1, 2)
+    best, cost = 0, float("inf")
+    for k in (3, 2, 1, 0) if small_ok else (1, 0):
         c = -(-n // per[k]) * lat[k]
+        if k == 0:
+            tail = n % per[0]
+            c = (n // per[0]) * lat[0] + (0 if tail == 0 else lat[1] if tail <= per[1] else lat[0])
         if c < cost:
-            best, cost = k, c
+            best, cost = code[k], c
     return best
 
 
 def _kernel_name(suite, n):
-    """Which tx-verify kernel the library launches for this batch (mirrors launch_tx_verify and its
+    """Which tx-verify kernel the library launches for this batch (mirrors launch_verify and its
     policy: BCOSGPU_TXV_* and BCOSGPU_K1_F26, read once by the library)."""
     import torch
     f26 = os.environ.get("BCOSGPU_K1_F26", "1") != "0"
     split = os.environ.get("BCOSGPU_TXV_SPLIT")
     small = (split == "1") if split in ("0", "1") else n <= (1 << 15)
     coop = {"0": 0, "1": 1}.get(os.environ.get("BCOSGPU_TXV_COOP", "2"), 2)
+    occ = os.environ.get("BCOSGPU_TXV_OCC")
+    occ = int(occ) if occ in ("1", "2") else 0
     if split not in ("0", "1") and coop == 2 and f26:
         cus = torch.cuda.get_device_properties(0).multi_processor_count if torch.cuda.is_available() else 256
-        k = _auto_small_kernel(suite, n, cus) if n <= (1 << 16) else 0
-        small, coop = k != 0, (k if k else coop)
+        k = _auto_kernel(suite, n, cus, n <= (1 << 16))
+        small = k > 0
+        if small:
+            coop = k
+        elif not occ:
+            occ = 2 if k == -2 else 1
+    if not occ:
+        occ = 2 if n >= (1 << 17) else 1
     if suite == 0 and small:
         if not coop:
             return "tx_verify_split_kernel"
         if coop == 2 and f26:
-            return "tx_verify_trio26_kernel"
-        return "tx_verify_coop26_kernel" if f26 else "tx_verify_coop_kernel"
+            return "tx_verify_trio26_kernel<TxIO>"
+        return "tx_verify_coop26_kernel<TxIO>" if f26 else "tx_verify_coop_kernel"
     if suite == 1 and small and coop:
         if f26:
-            return "tx_verify_sm2_trio26_kernel" if coop == 2 else "tx_verify_sm2_pair26_kernel"
+            return "tx_verify_sm2_trio26_kernel<TxIO>" if coop == 2 else "tx_verify_sm2_pair26_kernel<TxIO>"
         return "tx_verify_sm2_pair_kernel"
-    occ = os.environ.get("BCOSGPU_TXV_OCC")
-    occ = int(occ) if occ in ("1", "2") else (2 if n >= (1 << 17) else 1)
-    return "tx_verify_kernel<%d,%d,%s>" % (suite, occ, "true" if f26 else "false")
+    return "tx_verify_kernel<%d,%d,%s,TxIO>" % (suite, occ, "true" if f26 else "false")
 
 
 def _norm(name):
@@ -380,25 +391,45 @@ def merkle_work(n, width, keccak):
     return units, units * (KECCAK_F_OPS if keccak else SM3_C_OPS)
 
 
+def _median_time(fn, reps=5):
+    """one warm-up, then `reps` timed repetitions; the median (s) and all times."""
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2], ts
+
+
 def merkle_cpu(threads):
-    """The oracle's Merkle restatement (per-level std::thread parallelism, as TBB Merkle.h:248) on the
-    host over 1M leaves, widths 16 and 2, Keccak256 and SM3."""
+    """The reference's Merkle CPU path on the host: Merkle<H, width>::generateMerkle (Merkle.h:170-261) with
+    its OpenSSL 1.1.1 hashers (OpenSSLHasher.h:22-143: EVP_sm3; EVP_sha3_256 with the Keccak pad poke), the
+    hashers merkleBench.cpp times -- oracle/standin_openssl.c, levels parallel over `threads` like the
+    reference's tbb::parallel_for -- at configs[0]'s 100k leaves and at 1M; median of 5 repetitions.
+    Without the OpenSSL stand-in, the oracle's portable C restatement (kind "port")."""
     import numpy as np
     from oracle import oracle
     rng = np.random.default_rng(3)
     leaves = rng.integers(0, 256, size=(1_000_000, 32), dtype=np.uint8)
+    use_ossl = oracle.standin() is not None
     res = {}
-    for hname, h in (("keccak256", oracle.KECCAK256), ("sm3", oracle.SM3)):
-        for width in (16, 2):
-            oracle.merkle(h, width, leaves[:1000], nthreads=threads)
-            reps, t0 = 0, time.perf_counter()
-            while reps < 1 or time.perf_counter() - t0 < 0.5:
-                oracle.merkle(h, width, leaves, nthreads=threads)
-                reps += 1
-            dt = (time.perf_counter() - t0) / reps
-            res["%s_w%d_1M" % (hname, width)] = {"ms": dt * 1e3, "GB_per_s": 32e6 / dt / 1e9}
-    return {"legs": res, "threads": threads, "kind": "port",
-            "impl": "oracle/merkle.c restatement of Merkle.h:170-261, level-parallel pthreads"}
+    for n in (100_000, 1_000_000):
+        for hname, h in (("keccak256", oracle.KECCAK256), ("sm3", oracle.SM3)):
+            for width in (16, 2):
+                lv = leaves[:n]
+                if use_ossl:
+                    fn = lambda: oracle.standin_merkle_root(h, width, lv, nthreads=threads)  # noqa: E731
+                else:
+                    fn = lambda: oracle.merkle(h, width, lv, nthreads=threads)  # noqa: E731
+                med, ts = _median_time(fn)
+                res["%s_w%d_%s" % (hname, width, _count(n))] = {
+                    "ms": med * 1e3, "GB_per_s": n * 32 / med / 1e9, "reps_ms": [round(t * 1e3, 3) for t in ts]}
+    return {"legs": res, "threads": threads, "kind": "reference" if use_ossl else "port",
+            "impl": ("Merkle.h:170-261 over the reference's OpenSSL hashers (OpenSSLHasher.h, EVP_sm3 / EVP_sha3_256 "
+                     "with the 0x01 pad poke; OpenSSL %s), level-parallel pthreads" % oracle.standin_version())
+            if use_ossl else "oracle/merkle.c restatement of Merkle.h:170-261, level-parallel pthreads",
+            "note": "median of 5 repetitions after a warm-up (BASELINE.md 3)"}
 
 
 def _cpu_info():
@@ -422,11 +453,12 @@ def cpu_threads():
     return min(int(env), aff) if env and env.isdigit() and int(env) > 0 else aff
 
 
-def cpu_baseline(batches, threads, min_seconds=1.0):
+def cpu_baseline(batches, threads):
     """Transaction::verify (Transaction.h:68-82) per tx on the host (TransactionSync.cpp:516-548's
     parallel_for) over bounded samples of the benchmark batches: the OpenSSL 1.1.1 EC stand-in
-     and the oracle's portable C restatement, secp256k1 and SM2.  value = the faster
-    secp256k1 leg (the headline metric's CPU counterpart)."""
+     and the oracle's portable C restatement, secp256k1 and SM2; each the median of 5
+    timed passes after a warm-up.  value = the faster secp256k1 leg (the headline
+    metric's CPU counterpart); kind follows that leg."""
     import numpy as np
     from oracle import oracle
     legs = {}
@@ -439,19 +471,19 @@ def cpu_baseline(batches, threads, min_seconds=1.0):
         if oracle.standin() is not None:
             impls.append(("openssl", oracle.standin_tx_verify_packed))
         for name, fn in impls:
-            fn(suite, pre, pre_off[:65], sig, sig_off[:65], nthreads=threads)  # warm-up
-            reps, t0 = 0, time.perf_counter()
-            while reps < 1 or time.perf_counter() - t0 < min_seconds:
-                fn(suite, pre, pre_off, sig, sig_off, nthreads=threads)
-                reps += 1
-            dt = time.perf_counter() - t0
+            med, ts = _median_time(lambda: fn(suite, pre, pre_off, sig, sig_off, nthreads=threads))
             legs["%s_%s" % ("secp256k1" if suite == 0 else "sm2", name)] = {
-                "value": reps * sample / dt, "unit": "tx/s", "per_thread": reps * sample / dt / threads,
-                "sample": "%d x %d txs (%.1f s wall)" % (reps, sample, dt)}
+                "value": sample / med, "unit": "tx/s", "per_thread": sample / med / threads,
+                "sample": "%d txs per pass, median of %d passes (%.2f s total)" % (sample, len(ts), sum(ts)),
+                "passes_s": [round(t, 4) for t in ts]}
     best = max((v for k, v in legs.items() if k.startswith("secp256k1")), key=lambda v: v["value"])
     best_name = [k for k, v in legs.items() if v is best][0]
     logical = os.cpu_count()
-    return {"value": best["value"], "unit": "tx/s", "cores": threads, "kind": "port",
+    openssl = best_name.endswith("openssl")
+    return {"value": best["value"], "unit": "tx/s", "cores": threads, "kind": "reference" if openssl else "port",
+            "kind_detail": ("the reference's per-tx path with its third-party ECC replaced by the reference-class "
+                            "library in this image (OpenSSL 1.1.1 libcrypto EC for wedpr's libsecp256k1 / TASSL)"
+                            if openssl else "the oracle's portable C restatement of the path"),
             "impl": best_name, "sample": best["sample"],
             "host": {"cpu_model": _cpu_info(), "nproc": logical, "affinity": len(os.sched_getaffinity(0)),
                      "threads_used": threads, "libcrypto": oracle.standin_version()},
@@ -481,6 +513,81 @@ def host_api_rate(b, suite, n, reps=5):
     dt = (time.perf_counter() - t0) / reps
     return {"value": n / dt, "unit": "tx/s", "ms_per_batch": dt * 1e3,
             "path": "bcosgpu_tx_verify_batch (host buffers: H2D + kernel + D2H + sync)"}
+
+
+def interface_legs(batches, threads=64, calls=1000, reps=20):
+    """The reference-interface entry points on the C2-size batches (rank 0, N = 1), per suite:
+      recover_batch: SignatureCrypto::recover for a whole batch -- bcosgpu_secp256k1_recover_batch_dev /
+                     bcosgpu_sm2_verify_batch_dev (HIP events, the same rounds x latency kernel choice as
+                     the tx path) and the host-pointer ABI (bcosgpu_*_batch: H2D + kernel + D2H);
+      single_call:   `threads` host threads x `calls` single calls each (bcosgpu_secp256k1_recover /
+                     bcosgpu_sm2_verify, the per-tx SignatureCrypto::recover of TxPool's submitter pool,
+                     TxPool.h:48-49), coalesced by the engine -- fisco-bcos_amd/lib/callbench, every
+                     result checked against the batch path's."""
+    import struct
+    import tempfile
+    import numpy as np
+    import torch
+    import bcos_gpu
+    from bcos_gpu import device
+    out = {}
+    for suite, b in batches:
+        n, sl = b.n, b.sig_len
+        name = "secp256k1" if suite == 0 else "sm2"
+        hashes = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+        device.hash_batch(device.SM3 if suite else device.KECCAK256, b.pre, b.pre_off, hashes)
+        sigs = b.sig.view(n, sl)
+        pub = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
+        ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+
+        def launch():
+            if suite == 0:
+                device.secp256k1_recover(hashes, sigs, pub, None, ok)
+            else:
+                device.sm2_verify(hashes, sigs, None, ok)
+        for _ in range(5):
+            launch()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            launch()
+            c.record()
+            c.synchronize()
+            ts.append(a.elapsed_time(c))
+        ts.sort()
+        rec = {"n": n, "kernel_ms_median": ts[len(ts) // 2], "path": "bcosgpu_%s_batch_dev" % (
+            "secp256k1_recover" if suite == 0 else "sm2_verify")}
+        h_h, h_s = hashes.cpu().numpy(), sigs.cpu().numpy()
+        crypto = bcos_gpu.Secp256k1Crypto() if suite == 0 else bcos_gpu.SM2Crypto()
+        want_pub, want_ok = crypto.recover_batch(h_h, h_s)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            crypto.recover_batch(h_h, h_s)
+        rec["host_abi_ms"] = (time.perf_counter() - t0) / 5 * 1e3
+        dev_ok = ok.cpu().numpy().astype(bool)
+        rec["matches_host_abi"] = bool(np.array_equal(dev_ok, want_ok)) and (
+            suite == 1 or bool(np.array_equal(pub.cpu().numpy()[want_ok], want_pub[want_ok])))
+        out["recover_batch_%s" % name] = rec
+        exe = os.path.join(ROOT, "fisco-bcos_amd", "lib", "callbench")
+        if os.path.exists(exe):
+            m = min(n, 8192)
+            with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+                f.write(b"BGCT" + struct.pack("<II", suite, m))
+                kp = want_pub[:m] if suite == 0 else h_s[:m, 64:128]
+                for arr in (h_h[:m], h_s[:m], want_ok[:m].astype(np.uint8), kp):
+                    f.write(np.ascontiguousarray(arr, dtype=np.uint8).tobytes())
+                path = f.name
+            try:
+                r = subprocess.run([exe, path, str(threads), str(calls)], capture_output=True, text=True, timeout=300)
+                line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else "{}"
+                res = json.loads(line)
+                res["rc"] = r.returncode
+                out["single_call_%dt_%s" % (threads, name)] = res
+            finally:
+                os.unlink(path)
+    return out
 
 
 def create_transaction_leg(b, suite, n, want_status, reps=20):
@@ -525,7 +632,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--warm-seconds", type=float, default=2.0, help="minimum warm-up before the timed region")
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS), help="the headline leg")
-    ap.add_argument("--legs", default="c2sm2,c3,c4", help="comma-separated sub-legs ('' for none)")
+    ap.add_argument("--legs", default="c2sm2,c3,c4,c5", help="comma-separated sub-legs ('' for none)")
     ap.add_argument("--leg-seconds", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
@@ -602,6 +709,9 @@ def main():
             b = head_state["batch"]
             line["pcie_inclusive"] = host_api_rate(b, b.suite, head_state["n"])
             line["create_transaction"] = create_transaction_leg(b, b.suite, head_state["n"], head_state["status"])
+            from bcos_gpu import synth
+            sm2b = synth.make_batch(1, 10_000, seed=0x5A3)
+            line["interface"] = interface_legs([(0, b), (1, sm2b)])
         if not args.no_merkle:
             line["merkle"] = merkle_legs(0 if args.no_cpu_baseline else threads)
             line["merkle_c1"] = {h: line["merkle"]["%s_w16_100k" % h] for h in ("keccak256", "sm3")}

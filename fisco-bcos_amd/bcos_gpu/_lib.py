@@ -12,6 +12,7 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libbcosgpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "bcos_gpu.h")
 
 OK, E_ARG, E_HIP, E_NODEV, E_EMPTY = 0, -1, -2, -3, -4
+WEDPR_ENGINE_ERROR = -2
 KECCAK256, SM3 = 0, 1
 SUITE_SECP256K1, SUITE_SM2 = 0, 1
 MERKLE_NEW, MERKLE_OLD = 0, 1
@@ -72,6 +73,9 @@ _SIGS = {
     "bcosgpu_tars_tx_verify_batch": (_I, [_I, _P, _P, _SZ, _I, _I, _P, _P, _P]),
     "bcosgpu_tars_tx_verify_batch_dev": (_I, [_I, _P, _P, _SZ, _I, _I, _P, _P, _P, _P, _P, ctypes.c_uint64, _P, _P,
                                               _P, _P]),
+    "bcosgpu_secp256k1_recover": (_I, [_I, _P, _P, _SZ, _P]),
+    "bcosgpu_secp256k1_verify": (_I, [_I, _P, _P, _P, _SZ]),
+    "bcosgpu_sm2_verify": (_I, [_I, _P, _P, _P]),
     "bcosgpu_wedpr_secp256k1_recover_public_key": (ctypes.c_int8, [_P, _P, _P]),
     "bcosgpu_wedpr_sm2_verify": (ctypes.c_int8, [_P, _P, _P]),
     "bcosgpu_wedpr_secp256k1_verify": (ctypes.c_int8, [_P, _P, _P]),

@@ -200,16 +200,14 @@ def calculate_merkle_proof_root(hasher: Hash, leaves) -> bytes:
 
 
 class SignatureCrypto:
-    """bcos::crypto::SignatureCrypto (Signature.h:31-59)."""
+    """bcos::crypto::SignatureCrypto (Signature.h:31-59).  Single-item recover / verify go through the
+    engine's explicit-device single calls (coalesced across threads, csrc/coalesce.hip); *_batch through
+    the batch ABI.  An engine failure raises BcosGpuError, never InvalidSignature."""
     SIG_LEN = None
     SUITE = None
 
-    def verify(self, pub: bytes, hash32: bytes, sig: bytes) -> bool:
-        """SignatureCrypto::verify(pub, hash, sig) (Signature.h:40-46) with a known key; only
-        sig[0:64] = r || s is read (SM2Crypto.cpp:66-79; wedpr_secp256k1_verify, Secp256k1Crypto.cpp:51-63)."""
-        if len(sig) < 64 or len(pub) != 64:
-            return False
-        return bool(self.verify_batch(_u8(pub, (1, 64)), _u8(hash32, (1, 32)), _u8(bytes(sig[:64]), (1, 64)))[0])
+    def __init__(self, device=0):
+        self.device = device
 
     def verify_batch(self, pubs, hashes, sigs):
         """Batched verify (bcosgpu_verify_batch): pubs uint8[n,64], hashes uint8[n,32],
@@ -222,22 +220,39 @@ class SignatureCrypto:
             raise ValueError("signatures must hold at least r || s (64 bytes)")
         ok = np.zeros(n, dtype=np.uint8)
         if n:
-            ensure_device()
+            ensure_device(self.device)
             check(lib().bcosgpu_verify_batch(self.SUITE, _ptr(pubs), _ptr(hashes), _ptr(sigs), sigs.shape[1], n,
                                              _ptr(ok)))
         return ok.astype(bool)
 
-    def recover(self, hash32: bytes, sig: bytes) -> bytes:
-        pubs, ok = self.recover_batch(_u8(hash32, (1, 32)), [bytes(sig)])
-        if not ok[0]:
-            raise InvalidSignature("invalid signature: recover failed, msgHash : " + bytes(hash32).hex())
-        return pubs[0].tobytes()
+    @staticmethod
+    def _single(rc):
+        if rc < 0:
+            check(rc)
+        return rc == 1
 
 
 class Secp256k1Crypto(SignatureCrypto):
     """Secp256k1Crypto (Secp256k1Crypto.h:37-72); recover -> wedpr_secp256k1_recover_public_key."""
     SIG_LEN = 65
     SUITE = _lib.SUITE_SECP256K1
+
+    def recover(self, hash32: bytes, sig: bytes) -> bytes:
+        """Secp256k1Crypto::recover (Secp256k1Crypto.cpp:79-93): raises InvalidSignature."""
+        h, s = bytes(hash32), bytes(sig)
+        if len(h) != 32:
+            raise ValueError("hash must be 32 bytes")
+        pub = ctypes.create_string_buffer(64)
+        if not self._single(lib().bcosgpu_secp256k1_recover(self.device, h, s, len(s), pub)):
+            raise InvalidSignature("invalid signature: secp256k1Recover failed, msgHash : " + h.hex())
+        return pub.raw
+
+    def verify(self, pub: bytes, hash32: bytes, sig: bytes) -> bool:
+        """secp256k1Verify (Secp256k1Crypto.cpp:51-63): libsecp256k1 verify, only sig[0:64] read."""
+        p, h, s = bytes(pub), bytes(hash32), bytes(sig)
+        if len(p) != 64 or len(h) != 32 or len(s) < 64:
+            return False
+        return self._single(lib().bcosgpu_secp256k1_verify(self.device, p, h, s, len(s)))
 
     def recover_batch(self, hashes, sigs, want_address=False):
         """hashes uint8[n,32]; sigs uint8[n,65] (or list of bytes; non-65-byte entries fail).
@@ -259,7 +274,7 @@ class Secp256k1Crypto(SignatureCrypto):
         addr = np.zeros((n, 20), dtype=np.uint8)
         ok = np.zeros(n, dtype=np.uint8)
         if n:
-            ensure_device()
+            ensure_device(self.device)
             check(lib().bcosgpu_secp256k1_recover_batch(_ptr(hashes), _ptr(sigs), n, _ptr(pub),
                                                         _ptr(addr), _ptr(ok)))
         okb = ok.astype(bool) & ~bad
@@ -270,6 +285,20 @@ class SM2Crypto(SignatureCrypto):
     """SM2Crypto / FastSM2Crypto: recover = verify against the embedded public key (SM2Crypto.cpp:81-92)."""
     SIG_LEN = 128
     SUITE = _lib.SUITE_SM2
+
+    def verify(self, pub: bytes, hash32: bytes, sig: bytes) -> bool:
+        """SM2Crypto::verify (SM2Crypto.cpp:66-79): r || s = sig[0:64], the given key."""
+        p, h, s = bytes(pub), bytes(hash32), bytes(sig)
+        if len(p) != 64 or len(h) != 32 or len(s) < 64:
+            return False
+        return self._single(lib().bcosgpu_sm2_verify(self.device, p, h, s[:64]))
+
+    def recover(self, hash32: bytes, sig: bytes) -> bytes:
+        """SM2Crypto::recover (SM2Crypto.cpp:81-92): sig = r || s || pub; raises InvalidSignature."""
+        s = bytes(sig)
+        if len(s) != 128 or not self.verify(s[64:], hash32, s[:64]):
+            raise InvalidSignature("invalid signature: sm2 recover public key failed, msgHash : " + bytes(hash32).hex())
+        return s[64:]
 
     def recover_batch(self, hashes, sigs, want_address=False):
         hashes = _u8(hashes).reshape(-1, 32)
@@ -287,7 +316,7 @@ class SM2Crypto(SignatureCrypto):
         addr = np.zeros((n, 20), dtype=np.uint8)
         ok = np.zeros(n, dtype=np.uint8)
         if n:
-            ensure_device()
+            ensure_device(self.device)
             check(lib().bcosgpu_sm2_verify_batch(_ptr(hashes), _ptr(sigs), n, _ptr(addr), _ptr(ok)))
         okb = ok.astype(bool) & ~bad
         pub = sigs[:, 64:128].copy()

@@ -1,5 +1,6 @@
 // api.hip -- the C ABI (include/bcos_gpu.h): argument checks, per-device workspaces for the
 // host-pointer entry points, and the wedpr-shaped single-call shims.  No exceptions cross the ABI.
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -51,6 +52,7 @@ struct Workspace {
 };
 std::mutex g_mu;
 std::vector<Workspace*> g_ws;
+std::atomic<bool> g_ready[64];  // device initialised (tables built): the single-call fast path
 
 int current_device(int* dev) {
     int n = 0;
@@ -74,6 +76,35 @@ int get_ws(Workspace** out) {
 }
 
 inline hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
+
+int init_device(int device, int flags);
+
+// The explicit-device entry points: initialise `device` once, without changing the calling thread's
+// current device.
+int ready_device(int device) {
+    if (device >= 0 && device < 64 && g_ready[device].load(std::memory_order_acquire)) return 0;
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) {
+        (void)hipGetLastError();
+        prev = -1;
+    }
+    const int rc = init_device(device, 0);
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    return rc;
+}
+
+// A host-pointer signature call as a coalesced job (coalesce.hip) on `device`.
+int run_job(int device, SigJob& job) {
+    int rc = ready_device(device);
+    if (rc) return rc;
+    rc = coalesced_run(device, job);
+    return rc ? set_err(rc, job.err) : 0;
+}
+
+int calling_device(int* dev) {
+    int rc = current_device(dev);
+    return rc ? rc : ready_device(*dev);
+}
 
 }  // namespace
 
@@ -99,7 +130,13 @@ uint64_t bcosgpu_merkle_size(uint64_t n, int width) {
 
 int bcosgpu_init(int device) { return bcosgpu_init_ex(device, 0); }
 
-int bcosgpu_init_ex(int device, int flags) {
+int bcosgpu_init_ex(int device, int flags) { return init_device(device, flags); }
+
+}  // extern "C"
+
+namespace {
+// selects `device` on the calling thread and builds its tables once
+int init_device(int device, int flags) {
     int n = bcosgpu_device_count();
     if (n <= 0) return set_err(BCOSGPU_E_NODEV, "no HIP device visible");
     if (device < 0 || device >= n) return set_err(BCOSGPU_E_ARG, "device index out of range");
@@ -117,9 +154,13 @@ int bcosgpu_init_ex(int device, int flags) {
         int rc = ecc_init_tables(device, (flags & BCOSGPU_INIT_SMALL_TABLES) != 0);
         if (rc) return set_err(rc, "ecc table setup failed");
         w->ready = true;
+        if (device < 64) g_ready[device].store(true, std::memory_order_release);
     }
     return 0;
 }
+}  // namespace
+
+extern "C" {
 
 int bcosgpu_set_tx_kernel_policy(int split, int occupancy, int coop, int field) {
     set_tx_kernel_policy(split, occupancy, coop, field);
@@ -370,26 +411,18 @@ int bcosgpu_secp256k1_recover_batch(const uint8_t* hash32, const uint8_t* sig65,
                                     uint8_t* pub64, uint8_t* addr20, uint8_t* ok) {
     if (n == 0) return 0;
     if (!hash32 || !sig65 || !ok) return set_err(BCOSGPU_E_ARG, "null pointer");
-    Workspace* w;
-    int rc = get_ws(&w);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> g(w->mu);
-    HIP_OK(w->b[0].ensure(n * 32));
-    HIP_OK(w->b[1].ensure(n * 65 + 8));
-    HIP_OK(w->b[2].ensure(n * 64));
-    HIP_OK(w->b[3].ensure(n * 20));
-    HIP_OK(w->b[4].ensure(n));
-    HIP_OK(hipMemcpyAsync(w->b[0].p, hash32, n * 32, hipMemcpyHostToDevice, w->stream));
-    HIP_OK(hipMemcpyAsync(w->b[1].p, sig65, n * 65, hipMemcpyHostToDevice, w->stream));
-    rc = launch_secp256k1_recover(w->b[0].as<uint8_t>(), w->b[1].as<uint8_t>(), 65, n,
-                                  pub64 ? w->b[2].as<uint8_t>() : nullptr,
-                                  addr20 ? w->b[3].as<uint8_t>() : nullptr, w->b[4].as<uint8_t>(), w->stream);
-    if (rc) return set_err(rc, "secp256k1 recover launch failed");
-    if (pub64) HIP_OK(hipMemcpyAsync(pub64, w->b[2].p, n * 64, hipMemcpyDeviceToHost, w->stream));
-    if (addr20) HIP_OK(hipMemcpyAsync(addr20, w->b[3].p, n * 20, hipMemcpyDeviceToHost, w->stream));
-    HIP_OK(hipMemcpyAsync(ok, w->b[4].p, n, hipMemcpyDeviceToHost, w->stream));
-    HIP_OK(hipStreamSynchronize(w->stream));
-    return 0;
+    int dev = 0;
+    if (int rc = calling_device(&dev)) return rc;
+    SigJob job;
+    job.kind = kSigJobRecoverK1;
+    job.n = n;
+    job.hash32 = hash32;
+    job.sig = sig65;
+    job.sig_stride = 65;
+    job.out_pub64 = pub64;
+    job.out_addr20 = addr20;
+    job.out_ok = ok;
+    return run_job(dev, job);
 }
 
 int bcosgpu_sm2_verify_batch_dev(const uint8_t* d_hash32, const uint8_t* d_sig128, size_t n,
@@ -403,23 +436,17 @@ int bcosgpu_sm2_verify_batch(const uint8_t* hash32, const uint8_t* sig128, size_
                              uint8_t* addr20, uint8_t* ok) {
     if (n == 0) return 0;
     if (!hash32 || !sig128 || !ok) return set_err(BCOSGPU_E_ARG, "null pointer");
-    Workspace* w;
-    int rc = get_ws(&w);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> g(w->mu);
-    HIP_OK(w->b[0].ensure(n * 32));
-    HIP_OK(w->b[1].ensure(n * 128));
-    HIP_OK(w->b[3].ensure(n * 20));
-    HIP_OK(w->b[4].ensure(n));
-    HIP_OK(hipMemcpyAsync(w->b[0].p, hash32, n * 32, hipMemcpyHostToDevice, w->stream));
-    HIP_OK(hipMemcpyAsync(w->b[1].p, sig128, n * 128, hipMemcpyHostToDevice, w->stream));
-    rc = launch_sm2_verify(w->b[0].as<uint8_t>(), w->b[1].as<uint8_t>(), 128, n,
-                           addr20 ? w->b[3].as<uint8_t>() : nullptr, w->b[4].as<uint8_t>(), w->stream);
-    if (rc) return set_err(rc, "sm2 verify launch failed");
-    if (addr20) HIP_OK(hipMemcpyAsync(addr20, w->b[3].p, n * 20, hipMemcpyDeviceToHost, w->stream));
-    HIP_OK(hipMemcpyAsync(ok, w->b[4].p, n, hipMemcpyDeviceToHost, w->stream));
-    HIP_OK(hipStreamSynchronize(w->stream));
-    return 0;
+    int dev = 0;
+    if (int rc = calling_device(&dev)) return rc;
+    SigJob job;
+    job.kind = kSigJobVerifySM2;
+    job.n = n;
+    job.hash32 = hash32;
+    job.sig = sig128;
+    job.sig_stride = 128;
+    job.out_addr20 = addr20;
+    job.out_ok = ok;
+    return run_job(dev, job);
 }
 
 int bcosgpu_secp256k1_sign_batch_dev(const uint8_t* d_sk32, const uint8_t* d_hash32, size_t n,
@@ -453,23 +480,17 @@ int bcosgpu_verify_batch(int suite, const uint8_t* pub64, const uint8_t* hash32,
     if (sig_stride < 64 || sig_stride > 0xFFFFFFFFull) return set_err(BCOSGPU_E_ARG, "signature stride must be >= 64");
     if (n == 0) return 0;
     if (!pub64 || !hash32 || !sig || !ok) return set_err(BCOSGPU_E_ARG, "null pointer");
-    Workspace* w;
-    int rc = get_ws(&w);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> g(w->mu);
-    HIP_OK(w->b[0].ensure(n * 64));
-    HIP_OK(w->b[1].ensure(n * 32));
-    HIP_OK(w->b[2].ensure(n * sig_stride + 8));
-    HIP_OK(w->b[3].ensure(n));
-    HIP_OK(hipMemcpyAsync(w->b[0].p, pub64, n * 64, hipMemcpyHostToDevice, w->stream));
-    HIP_OK(hipMemcpyAsync(w->b[1].p, hash32, n * 32, hipMemcpyHostToDevice, w->stream));
-    HIP_OK(hipMemcpyAsync(w->b[2].p, sig, n * sig_stride, hipMemcpyHostToDevice, w->stream));
-    rc = launch_sig_verify(suite, w->b[0].as<uint8_t>(), w->b[1].as<uint8_t>(), w->b[2].as<uint8_t>(),
-                           static_cast<uint32_t>(sig_stride), n, w->b[3].as<uint8_t>(), w->stream);
-    if (rc) return set_err(rc, "verify launch failed");
-    HIP_OK(hipMemcpyAsync(ok, w->b[3].p, n, hipMemcpyDeviceToHost, w->stream));
-    HIP_OK(hipStreamSynchronize(w->stream));
-    return 0;
+    int dev = 0;
+    if (int rc = calling_device(&dev)) return rc;
+    SigJob job;
+    job.kind = suite == BCOSGPU_SUITE_SM2 ? kSigJobVerifySM2 : kSigJobVerifyK1;
+    job.n = n;
+    job.hash32 = hash32;
+    job.sig = sig;
+    job.sig_stride = sig_stride;
+    job.pub64 = pub64;
+    job.out_ok = ok;
+    return run_job(dev, job);
 }
 
 int bcosgpu_ecrecover_batch_dev(const uint8_t* d_in128, size_t n, uint8_t* d_out32, uint8_t* d_ok, void* stream) {
@@ -628,39 +649,102 @@ int bcosgpu_tars_tx_verify_batch(int suite, const uint8_t* enc, const uint64_t* 
     return 0;
 }
 
+// ------------------------------------------------------------------ single calls (coalesced)
+int bcosgpu_secp256k1_recover(int device, const uint8_t* hash32, const uint8_t* sig, size_t sig_len, uint8_t* pub64) {
+    if (!hash32 || !sig || !pub64) return set_err(BCOSGPU_E_ARG, "null pointer");
+    if (int rc = ready_device(device)) return rc;
+    if (sig_len != 65) {  // SECP256K1_SIGNATURE_LEN (Secp256k1Crypto.h:29): InvalidSignature
+        std::memset(pub64, 0, 64);
+        return 0;
+    }
+    uint8_t ok = 0;
+    SigJob job;
+    job.kind = kSigJobRecoverK1;
+    job.n = 1;
+    job.hash32 = hash32;
+    job.sig = sig;
+    job.sig_stride = 65;
+    job.out_pub64 = pub64;
+    job.out_ok = &ok;
+    if (int rc = run_job(device, job)) return rc;
+    return ok ? 1 : 0;
+}
+
+int bcosgpu_secp256k1_verify(int device, const uint8_t* pub64, const uint8_t* hash32, const uint8_t* sig,
+                             size_t sig_len) {
+    if (!pub64 || !hash32 || !sig) return set_err(BCOSGPU_E_ARG, "null pointer");
+    if (int rc = ready_device(device)) return rc;
+    if (sig_len < 64) return 0;
+    uint8_t ok = 0;
+    SigJob job;
+    job.kind = kSigJobVerifyK1;
+    job.n = 1;
+    job.hash32 = hash32;
+    job.sig = sig;
+    job.sig_stride = 64;
+    job.pub64 = pub64;
+    job.out_ok = &ok;
+    if (int rc = run_job(device, job)) return rc;
+    return ok ? 1 : 0;
+}
+
+int bcosgpu_sm2_verify(int device, const uint8_t* pub64, const uint8_t* hash32, const uint8_t* sig64) {
+    if (!pub64 || !hash32 || !sig64) return set_err(BCOSGPU_E_ARG, "null pointer");
+    if (int rc = ready_device(device)) return rc;
+    uint8_t ok = 0;
+    SigJob job;
+    job.kind = kSigJobVerifySM2;
+    job.n = 1;
+    job.hash32 = hash32;
+    job.sig = sig64;
+    job.sig_stride = 64;
+    job.pub64 = pub64;
+    job.out_ok = &ok;
+    if (int rc = run_job(device, job)) return rc;
+    return ok ? 1 : 0;
+}
+
 // ------------------------------------------------------------------ wedpr-ABI shims
+// On the calling thread's current device.  0 = WEDPR_SUCCESS, -1 = WEDPR_ERROR (invalid input or
+// signature), BCOSGPU_WEDPR_ENGINE_ERROR = the engine failed (no device, HIP error): the message is in
+// bcosgpu_last_error().
+static int shim_device() {
+    int dev = 0;
+    return current_device(&dev) ? -1 : dev;
+}
+
 int8_t bcosgpu_wedpr_secp256k1_recover_public_key(const bcosgpu_CInputBuffer* hash,
                                                    const bcosgpu_CInputBuffer* sig,
                                                    bcosgpu_COutputBuffer* pub) {
     if (!hash || !sig || !pub || hash->len != 32 || pub->len < 64) return -1;
-    if (sig->len != 65) return -1;  // SECP256K1_SIGNATURE_LEN (Secp256k1Crypto.h:29)
-    uint8_t ok = 0;
-    if (bcosgpu_secp256k1_recover_batch(reinterpret_cast<const uint8_t*>(hash->data),
-                                        reinterpret_cast<const uint8_t*>(sig->data), 1,
-                                        reinterpret_cast<uint8_t*>(pub->data), nullptr, &ok))
-        return -1;
-    return ok ? 0 : -1;
+    const int dev = shim_device();
+    if (dev < 0) return BCOSGPU_WEDPR_ENGINE_ERROR;
+    const int rc = bcosgpu_secp256k1_recover(dev, reinterpret_cast<const uint8_t*>(hash->data),
+                                             reinterpret_cast<const uint8_t*>(sig->data), sig->len,
+                                             reinterpret_cast<uint8_t*>(pub->data));
+    return rc < 0 ? BCOSGPU_WEDPR_ENGINE_ERROR : rc == 1 ? 0 : -1;
 }
 
 int8_t bcosgpu_wedpr_sm2_verify(const bcosgpu_CInputBuffer* pub, const bcosgpu_CInputBuffer* hash,
                                  const bcosgpu_CInputBuffer* sig) {
     if (!pub || !hash || !sig || hash->len != 32 || sig->len != 64 || pub->len != 64) return -1;
-    uint8_t s[128], ok = 0;
-    std::memcpy(s, sig->data, 64);
-    std::memcpy(s + 64, pub->data, 64);
-    if (bcosgpu_sm2_verify_batch(reinterpret_cast<const uint8_t*>(hash->data), s, 1, nullptr, &ok)) return -1;
-    return ok ? 0 : -1;
+    const int dev = shim_device();
+    if (dev < 0) return BCOSGPU_WEDPR_ENGINE_ERROR;
+    const int rc = bcosgpu_sm2_verify(dev, reinterpret_cast<const uint8_t*>(pub->data),
+                                      reinterpret_cast<const uint8_t*>(hash->data),
+                                      reinterpret_cast<const uint8_t*>(sig->data));
+    return rc < 0 ? BCOSGPU_WEDPR_ENGINE_ERROR : rc == 1 ? 0 : -1;
 }
 
 int8_t bcosgpu_wedpr_secp256k1_verify(const bcosgpu_CInputBuffer* pub, const bcosgpu_CInputBuffer* hash,
                                       const bcosgpu_CInputBuffer* sig) {
     if (!pub || !hash || !sig || hash->len != 32 || pub->len != 64 || sig->len < 64) return -1;
-    uint8_t ok = 0;
-    if (bcosgpu_verify_batch(BCOSGPU_SUITE_SECP256K1, reinterpret_cast<const uint8_t*>(pub->data),
-                             reinterpret_cast<const uint8_t*>(hash->data), reinterpret_cast<const uint8_t*>(sig->data),
-                             64, 1, &ok))
-        return -1;
-    return ok ? 0 : -1;
+    const int dev = shim_device();
+    if (dev < 0) return BCOSGPU_WEDPR_ENGINE_ERROR;
+    const int rc = bcosgpu_secp256k1_verify(dev, reinterpret_cast<const uint8_t*>(pub->data),
+                                            reinterpret_cast<const uint8_t*>(hash->data),
+                                            reinterpret_cast<const uint8_t*>(sig->data), sig->len);
+    return rc < 0 ? BCOSGPU_WEDPR_ENGINE_ERROR : rc == 1 ? 0 : -1;
 }
 
 }  // extern "C"

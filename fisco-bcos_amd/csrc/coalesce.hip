@@ -1,0 +1,278 @@
+// coalesce.hip -- per-device coalescing of the host-pointer signature calls.
+//
+// The reference verifies one signature per call on its hot admission path: TxPool's submitter pool
+// (hardware_concurrency threads, TxPool.h:48-49) runs TxValidator::verify -> Transaction::verify ->
+// SignatureCrypto::recover once per transaction (TxValidator.cpp:56, Transaction.h:68-82).  A kernel
+// launch per call would serialise those threads behind one latency-bound launch each.  Instead every
+// host-pointer recover / verify call (single or batched) becomes a job in its device's queue; a caller
+// that finds a free launch slot takes EVERY queued job of its kind (up to kMaxBatch items) and runs them
+// as one batch -- assemble into pinned staging, one H2D copy, one launch (the same rounds x latency
+// kernel choice as the tx path, ecc_txv.hip launch_verify), one D2H copy, synchronise, scatter -- while
+// the other callers sleep on the queue.  No dispatcher thread: the callers themselves lead batches
+// (leader / follower), so nothing runs when nobody calls and nothing needs shutting down.  Up to
+// slots_in_use() batches can be in flight per device at once, each on its own stream: small
+// latency-bound batches occupy a few CUs each, so they overlap on the device instead of queueing.
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <vector>
+#include <cstdlib>
+#include <cstring>
+#include "engine.h"
+
+namespace bcosgpu {
+namespace {
+
+constexpr int kMaxSlots = 16;
+constexpr size_t kMaxBatch = 65536;
+
+// batches in flight per device: 4 (GPU_MAX_HW_QUEUES' default), BCOSGPU_COALESCE_SLOTS = 1..16 to tune
+int slots_in_use() {
+    static const int n = [] {
+        const char* e = getenv("BCOSGPU_COALESCE_SLOTS");
+        const int v = e ? atoi(e) : 4;
+        return v < 1 ? 1 : v > kMaxSlots ? kMaxSlots : v;
+    }();
+    return n;
+}
+
+struct Slot {
+    int index = 0;
+    bool busy = false;
+    hipStream_t stream = nullptr;
+    uint8_t* h_in = nullptr;  // pinned, device-mapped staging
+    uint8_t* h_out = nullptr;
+    uint8_t* hd_in = nullptr;  // their device addresses (zero-copy small batches)
+    uint8_t* hd_out = nullptr;
+    size_t h_in_cap = 0, h_out_cap = 0;
+    uint8_t* d_in = nullptr;
+    uint8_t* d_out = nullptr;
+    size_t d_in_cap = 0, d_out_cap = 0;
+};
+
+struct DeviceQueue {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<SigJob*> pending[kSigJobKinds];
+    Slot slots[kMaxSlots];
+};
+
+std::mutex g_qmu;
+DeviceQueue* g_queues[64] = {};  // never freed: no teardown races with the HIP runtime at exit
+
+DeviceQueue* queue_of(int device) {
+    std::lock_guard<std::mutex> g(g_qmu);
+    if (!g_queues[device]) {
+        g_queues[device] = new DeviceQueue();
+        for (int k = 0; k < kMaxSlots; ++k) g_queues[device]->slots[k].index = k;
+    }
+    return g_queues[device];
+}
+
+size_t grow(size_t want) { return want < 65536 ? 65536 : want + want / 4; }
+
+hipError_t ensure_pinned(uint8_t*& p, uint8_t*& dp, size_t& cap, size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = dp = nullptr;
+    cap = 0;
+    const size_t want = grow(bytes);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&dp), p, 0);
+    if (e == hipSuccess) cap = want;
+    return e;
+}
+
+// Batches up to this many items are read and written by the kernel in place, in the mapped staging
+// (zero-copy: no copy dispatches, which cost a latency-bound single call ~2 x 20-60 us of queue time);
+// larger ones are copied by the DMA engines.
+constexpr size_t kZeroCopyMax = 2048;
+
+hipError_t ensure_dev(uint8_t*& p, size_t& cap, size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = grow(bytes);
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), want);
+    if (e == hipSuccess) cap = want;
+    return e;
+}
+
+// Bytes per item of the staged input and output of each job kind.
+//   recover secp256k1: in  hash[32] .. | sig[65] ..          out pub[64] .. | addr[20] .. | ok ..
+//   verify SM2:        in  hash[32] .. | r||s||pub[128] ..   out addr[20] .. | ok ..
+//   verify secp256k1:  in  pub[64] .. | hash[32] .. | r||s[64] ..   out ok ..
+constexpr size_t kInPer[kSigJobKinds] = {32 + 65, 32 + 128, 64 + 32 + 64};
+constexpr size_t kOutPer[kSigJobKinds] = {64 + 20 + 1, 20 + 1, 1};
+
+int fail(std::vector<SigJob*>& batch, int rc, const std::string& msg) {
+    for (SigJob* j : batch) {
+        j->rc = rc;
+        j->err = msg;
+    }
+    return rc;
+}
+
+#define BATCH_HIP(call)                                                                        \
+    do {                                                                                       \
+        hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess) return fail(batch, BCOSGPU_E_HIP, std::string(#call ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// One coalesced launch for `batch` (all of one kind) on `slot` of `device`.
+int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
+    size_t n = 0;
+    bool want_addr = false, want_pub = false;
+    for (SigJob* j : batch) {
+        n += j->n;
+        want_addr = want_addr || j->out_addr20;
+        want_pub = want_pub || j->out_pub64;
+    }
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != device) BATCH_HIP(hipSetDevice(device));
+    struct Restore {
+        int prev, dev;
+        ~Restore() {
+            if (prev != dev) (void)hipSetDevice(prev);
+        }
+    } restore{prev, device};
+    if (!slot.stream) {
+        // Streams of one priority share a few hardware queues (GPU_MAX_HW_QUEUES), and kernels on one
+        // queue run in order, so slot k takes priority level k mod levels: each level brings its own
+        // queues and the batches in flight really overlap (BCOSGPU_COALESCE_PRIO=0: all at the default).
+        static const bool prio = !getenv("BCOSGPU_COALESCE_PRIO") || atoi(getenv("BCOSGPU_COALESCE_PRIO")) != 0;
+        int least = 0, greatest = 0;
+        if (prio) BATCH_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        const int levels = least >= greatest ? least - greatest + 1 : 1;
+        BATCH_HIP(hipStreamCreateWithPriority(&slot.stream, hipStreamNonBlocking, least - slot.index % levels));
+    }
+    const size_t in_bytes = kInPer[kind] * n, out_bytes = kOutPer[kind] * n;
+    BATCH_HIP(ensure_pinned(slot.h_in, slot.hd_in, slot.h_in_cap, in_bytes));
+    BATCH_HIP(ensure_pinned(slot.h_out, slot.hd_out, slot.h_out_cap, out_bytes));
+    static const size_t zero_copy_max = [] {
+        const char* e = getenv("BCOSGPU_COALESCE_ZEROCOPY");  // items; tuning
+        return e ? static_cast<size_t>(atol(e)) : kZeroCopyMax;
+    }();
+    const bool zero_copy = n <= zero_copy_max;
+    if (!zero_copy) {
+        BATCH_HIP(ensure_dev(slot.d_in, slot.d_in_cap, in_bytes + 16));
+        BATCH_HIP(ensure_dev(slot.d_out, slot.d_out_cap, out_bytes + 16));
+    }
+    // assemble the SoA input
+    uint8_t* in = slot.h_in;
+    size_t at = 0;
+    for (SigJob* j : batch) {
+        const size_t m = j->n;
+        if (kind == kSigJobRecoverK1) {
+            std::memcpy(in + 32 * at, j->hash32, 32 * m);
+            uint8_t* s = in + 32 * n + 65 * at;
+            if (j->sig_stride == 65) std::memcpy(s, j->sig, 65 * m);
+            else for (size_t i = 0; i < m; ++i) std::memcpy(s + 65 * i, j->sig + j->sig_stride * i, 65);
+        } else if (kind == kSigJobVerifySM2) {
+            std::memcpy(in + 32 * at, j->hash32, 32 * m);
+            uint8_t* s = in + 32 * n + 128 * at;
+            if (!j->pub64 && j->sig_stride == 128) {
+                std::memcpy(s, j->sig, 128 * m);
+            } else {
+                for (size_t i = 0; i < m; ++i) {
+                    std::memcpy(s + 128 * i, j->sig + j->sig_stride * i, 64);
+                    std::memcpy(s + 128 * i + 64, j->pub64 ? j->pub64 + 64 * i : j->sig + j->sig_stride * i + 64, 64);
+                }
+            }
+        } else {
+            std::memcpy(in + 64 * at, j->pub64, 64 * m);
+            std::memcpy(in + 64 * n + 32 * at, j->hash32, 32 * m);
+            uint8_t* s = in + 96 * n + 64 * at;
+            for (size_t i = 0; i < m; ++i) std::memcpy(s + 64 * i, j->sig + j->sig_stride * i, 64);
+        }
+        at += m;
+    }
+    if (!zero_copy) BATCH_HIP(hipMemcpyAsync(slot.d_in, slot.h_in, in_bytes, hipMemcpyHostToDevice, slot.stream));
+    const uint8_t* di = zero_copy ? slot.hd_in : slot.d_in;
+    uint8_t* dout = zero_copy ? slot.hd_out : slot.d_out;
+    int rc;
+    if (kind == kSigJobRecoverK1)
+        rc = launch_secp256k1_recover(di, di + 32 * n, 65, n, want_pub ? dout : nullptr,
+                                      want_addr ? dout + 64 * n : nullptr, dout + 84 * n, slot.stream);
+    else if (kind == kSigJobVerifySM2)
+        rc = launch_sm2_verify(di, di + 32 * n, 128, n, want_addr ? dout : nullptr, dout + 20 * n, slot.stream);
+    else
+        rc = launch_sig_verify(BCOSGPU_SUITE_SECP256K1, di, di + 64 * n, di + 96 * n, 64, n, dout, slot.stream);
+    if (rc) {
+        hipError_t e = hipGetLastError();
+        return fail(batch, rc, std::string("signature batch launch failed: ") + hipGetErrorString(e));
+    }
+    if (!zero_copy) BATCH_HIP(hipMemcpyAsync(slot.h_out, slot.d_out, out_bytes, hipMemcpyDeviceToHost, slot.stream));
+    BATCH_HIP(hipStreamSynchronize(slot.stream));
+    // scatter
+    const uint8_t* out = slot.h_out;
+    at = 0;
+    for (SigJob* j : batch) {
+        const size_t m = j->n;
+        if (kind == kSigJobRecoverK1) {
+            if (j->out_pub64) std::memcpy(j->out_pub64, out + 64 * at, 64 * m);
+            if (j->out_addr20) std::memcpy(j->out_addr20, out + 64 * n + 20 * at, 20 * m);
+            std::memcpy(j->out_ok, out + 84 * n + at, m);
+        } else if (kind == kSigJobVerifySM2) {
+            if (j->out_addr20) std::memcpy(j->out_addr20, out + 20 * at, 20 * m);
+            std::memcpy(j->out_ok, out + 20 * n + at, m);
+        } else {
+            std::memcpy(j->out_ok, out + at, m);
+        }
+        j->rc = 0;
+        at += m;
+    }
+    return 0;
+}
+
+}  // namespace
+
+int coalesced_run(int device, SigJob& job) {
+    if (device < 0 || device >= 64 || job.kind < 0 || job.kind >= kSigJobKinds) {
+        job.err = "bad device or job kind";
+        return job.rc = BCOSGPU_E_ARG;
+    }
+    if (job.n == 0) return job.rc = 0;
+    DeviceQueue& q = *queue_of(device);
+    std::unique_lock<std::mutex> lk(q.mu);
+    job.done = false;
+    job.queued = true;
+    q.pending[job.kind].push_back(&job);
+    // Every queued job's owner is in this loop, so a caller leads only while its own job is still
+    // queued (a caller whose job is in flight just waits for it): each freed slot wakes the owners.
+    while (!job.done) {
+        Slot* free_slot = nullptr;
+        for (int k = 0; k < slots_in_use(); ++k)
+            if (!q.slots[k].busy) {
+                free_slot = &q.slots[k];
+                break;
+            }
+        if (!free_slot || !job.queued) {
+            q.cv.wait(lk);
+            continue;
+        }
+        // lead: take every queued job of this kind, oldest first, up to kMaxBatch items (at least one)
+        auto& pend = q.pending[job.kind];
+        std::vector<SigJob*> batch;
+        size_t items = 0;
+        while (!pend.empty() && (batch.empty() || items + pend.front()->n <= kMaxBatch)) {
+            items += pend.front()->n;
+            pend.front()->queued = false;
+            batch.push_back(pend.front());
+            pend.pop_front();
+        }
+        free_slot->busy = true;
+        lk.unlock();
+        run_batch(device, job.kind, *free_slot, batch);
+        lk.lock();
+        free_slot->busy = false;
+        for (SigJob* j : batch) j->done = true;
+        q.cv.notify_all();
+    }
+    return job.rc;
+}
+
+}  // namespace bcosgpu

@@ -1076,26 +1076,16 @@ __device__ __forceinline__ void trio_add_digit(TrioPt& acc, const Trio26Lds& L, 
 
 // TRIO = false: tx_verify_coop26_kernel (64 txs per workgroup, wave-pair chains); TRIO = true:
 // tx_verify_trio26_kernel (40 txs per workgroup, lane-trio chains).  Phases A and D are the same code.
-template <bool TRIO>
-__device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, const uint64_t* __restrict__ pre_off,
-                                            const uint8_t* __restrict__ sig, const uint64_t* __restrict__ sig_off,
-                                            uint64_t n, const uint32_t* __restrict__ tab, int tab_bits,
-                                            uint8_t* __restrict__ txhash,
-                                            uint8_t* __restrict__ sender, uint8_t* __restrict__ status) {
+template <bool TRIO, class IO>
+__device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint32_t* __restrict__ tab, int tab_bits) {
     constexpr int TPW = TRIO ? 40 : 64;  // txs per workgroup
     __shared__ std::conditional_t<TRIO, Trio26Lds, Coop26Lds> L;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * TPW + lane;
     const bool active = lane < TPW && i < n;
     COOP_T(0);
-    uint64_t sa = 0, sb = 0, pa = 0, pb = 0;
-    if (active) {
-        sa = sig_off[i];
-        sb = sig_off[i + 1];
-        pa = pre_off[i];
-        pb = pre_off[i + 1];
-    }
-    const uint32_t slen = (sb - sa) > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(sb - sa);
+    const uint8_t* sp = nullptr;
+    const uint32_t slen = active ? io.sig_span(i, sp) : 0u;
     if (threadIdx.x == 0) {
         L.post[0] = 0u;
         L.post[1] = 0u;
@@ -1106,7 +1096,7 @@ __device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, con
     fe r, s;
     uint32_t v = 0;
     bool ok = false;
-    if (active) ok = parse_sig65(sig + sa, slen, r, s, v);
+    if (active) ok = parse_sig65(sp, slen, r, s, v);
     else { fe_zero(r); fe_zero(s); }
     if (wave == 1 || wave == 2) {
         fe x;
@@ -1170,15 +1160,9 @@ __device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, con
         fe_zero(s);
     }
     if (wave == 3) {
-        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (active) {
-            const uint32_t len = static_cast<uint32_t>(pb - pa);
-            ByteReader rd(pre + pa, len);
-            keccak256_msg(rd, len, d);
-            store_digest(KECCAK256, txhash + 32 * i, d);
-        }
         fe e;
-        fe_from_be_words(e, d);
+        fe_zero(e);
+        if (active) io.template digest<KECCAK256>(i, e);
         reduce_once(e, ParamN1::M);
         lds_store_fe(L.xe, e, lane);
         coop_post(&L.post[1]);
@@ -1342,44 +1326,29 @@ __device__ __forceinline__ void coop26_body(const uint8_t* __restrict__ pre, con
         fe26_to_fe(ax, X);
         fe26_to_fe(ay, Y);
         uint32_t ad[5] = {0, 0, 0, 0, 0};
-        if (ok2) keccak_address(ad, ax, ay);
-        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
-#pragma unroll
-        for (int q = 0; q < 5; ++q) o[q] = ad[q];
-        status[i] = ok2 ? 0 : 1;
+        if (ok2 && io.want_addr()) keccak_address(ad, ax, ay);
+        io.finish(i, ok2, ad, &ax, &ay);
     }
     COOP_T(3);
 }
 
-__global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(const uint8_t* __restrict__ pre,
-                                                                  const uint64_t* __restrict__ pre_off,
-                                                                  const uint8_t* __restrict__ sig,
-                                                                  const uint64_t* __restrict__ sig_off, uint64_t n,
-                                                                  const uint32_t* __restrict__ tab,
-                                                                  uint8_t* __restrict__ txhash,
-                                                                  uint8_t* __restrict__ sender,
-                                                                  uint8_t* __restrict__ status) {
-    coop26_body<false>(pre, pre_off, sig, sig_off, n, tab, 8, txhash, sender, status);
+template <class IO>
+__global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab) {
+    coop26_body<false>(io, n, tab, 8);
 }
 
 // The trio kernel: phase C's doublings and mixed additions cost one multiplication of latency per
 // dependency level (3 per doubling, 5 per addition) with DPP exchanges inside a wave instead of LDS
 // exchanges and barriers between waves, and 40 txs per workgroup spread a 10k batch over 250 CUs
 // instead of 157.  Bit-identical to tx_verify_kernel<0, *>.
-__global__ __launch_bounds__(256, 1) void tx_verify_trio26_kernel(const uint8_t* __restrict__ pre,
-                                                                  const uint64_t* __restrict__ pre_off,
-                                                                  const uint8_t* __restrict__ sig,
-                                                                  const uint64_t* __restrict__ sig_off, uint64_t n,
-                                                                  const uint32_t* __restrict__ tab, int tab_bits,
-                                                                  uint8_t* __restrict__ txhash,
-                                                                  uint8_t* __restrict__ sender,
-                                                                  uint8_t* __restrict__ status) {
-    coop26_body<true>(pre, pre_off, sig, sig_off, n, tab, tab_bits, txhash, sender, status);
+template <class IO>
+__global__ __launch_bounds__(256, 1) void tx_verify_trio26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab,
+                                                                  int tab_bits) {
+    coop26_body<true>(io, n, tab, tab_bits);
 }
 
-int launch_tx_verify_small_secp(const TxKernelPolicy& pol, const uint8_t* d_pre, const uint64_t* d_pre_off,
-                                const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash,
-                                uint8_t* d_sender, uint8_t* d_status, hipStream_t st) {
+template <class IO>
+int launch_verify_small_secp(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st) {
     const uint32_t *k1, *sm2;
     const int rc = tables8(&k1, &sm2);
     if (rc) return rc;
@@ -1390,18 +1359,23 @@ int launch_tx_verify_small_secp(const TxKernelPolicy& pol, const uint8_t* d_pre,
         int bits = 8;
         const int rw = tables(&wk1, &wsm2, &bits);
         if (rw) return rw;
-        hipLaunchKernelGGL(tx_verify_trio26_kernel, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0, st, d_pre,
-                           d_pre_off, d_sig, d_sig_off, n, wk1, bits, d_txhash, d_sender, d_status);
-    } else if (pol.coop && pol.f26)
-        hipLaunchKernelGGL(tx_verify_coop26_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n, k1,
-                           d_txhash, d_sender, d_status);
-    else if (pol.coop)
-        hipLaunchKernelGGL(tx_verify_coop_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n, k1,
-                           d_txhash, d_sender, d_status);
-    else
-        hipLaunchKernelGGL(tx_verify_split_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n, k1,
-                           d_txhash, d_sender, d_status);
+        hipLaunchKernelGGL(tx_verify_trio26_kernel<IO>, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0, st, io,
+                           n, wk1, bits);
+    } else if (pol.coop && pol.f26) {
+        hipLaunchKernelGGL(tx_verify_coop26_kernel<IO>, grid, dim3(256), 0, st, io, n, k1);
+    } else if constexpr (std::is_same_v<IO, TxIO>) {
+        if (pol.coop)
+            hipLaunchKernelGGL(tx_verify_coop_kernel, grid, dim3(256), 0, st, io.pre, io.pre_off, io.sig, io.sig_off, n,
+                               k1, io.txhash, io.sender, io.status);
+        else
+            hipLaunchKernelGGL(tx_verify_split_kernel, grid, dim3(256), 0, st, io.pre, io.pre_off, io.sig, io.sig_off,
+                               n, k1, io.txhash, io.sender, io.status);
+    } else {
+        return BCOSGPU_E_ARG;  // the 8 x 32-bit small-batch kernels are TxIO only (launch_verify never asks)
+    }
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
+template int launch_verify_small_secp<TxIO>(const TxKernelPolicy&, const TxIO&, uint64_t, hipStream_t);
+template int launch_verify_small_secp<SigIO>(const TxKernelPolicy&, const SigIO&, uint64_t, hipStream_t);
 
 }  // namespace bcosgpu

@@ -538,8 +538,8 @@ struct TxKernelPolicy {
     int f26 = 1;     // throughput secp kernels: 1 point arithmetic on the 10 x 26-bit field, 0 on FieldK1
 };
 
-// host-side state (ecc_tables.hip)
-const TxKernelPolicy& tx_policy();
+// host-side state (ecc_tables.hip); a snapshot taken under the policy lock
+TxKernelPolicy tx_policy();
 // The comb tables of the current device: the 16-bit ones when present (*bits = 16), else the 8-bit
 // ones (*bits = 8).
 int tables(const uint32_t** k1, const uint32_t** sm2, int* bits);
@@ -548,13 +548,14 @@ int tables_sm2_26(const uint32_t** tab, int* bits);
 // 8-bit comb tables (and the 8-bit SM2 table in the R' domain)
 int tables8(const uint32_t** k1, const uint32_t** sm2);
 int tables8_sm2_26(const uint32_t** tab);
-// small-batch tx-verify launchers (ecc_coop.hip: secp256k1; ecc_pair.hip: SM2)
-int launch_tx_verify_small_secp(const TxKernelPolicy& pol, const uint8_t* d_pre, const uint64_t* d_pre_off,
-                                const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash,
-                                uint8_t* d_sender, uint8_t* d_status, hipStream_t st);
-int launch_tx_verify_small_sm2(const TxKernelPolicy& pol, const uint8_t* d_pre, const uint64_t* d_pre_off,
-                               const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash,
-                               uint8_t* d_sender, uint8_t* d_status, hipStream_t st);
+// small-batch verify launchers (ecc_coop.hip: secp256k1; ecc_pair.hip: SM2), instantiated for TxIO and
+// SigIO (the I/O policies below); SigIO has the fe26 / fp26 lane-trio and pair kernels only
+struct TxIO;
+struct SigIO;
+template <class IO>
+int launch_verify_small_secp(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st);
+template <class IO>
+int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st);
 static inline unsigned grid_of(uint64_t n) { return static_cast<unsigned>((n + 255) / 256); }
 
 // ------------------------------------------------------------------ secp256k1 recover (one lane)
@@ -662,6 +663,95 @@ __device__ __forceinline__ void sm3_address(uint32_t a[5], const fe& x, const fe
 #pragma unroll
     for (int i = 0; i < 5; ++i) a[i] = bswap32(d[3 + i]);
 }
+
+// ------------------------------------------------------------------ kernel I/O policies
+// Every verification kernel body (one-lane, lane-trio, cooperative pair) is written once over one of:
+//   TxIO  -- Transaction::verify (Transaction.h:68-82): the digest is H(preimage) and is an output
+//            (txhash); signature i = sig[sig_off[i] .. sig_off[i+1]); results sender20 and status
+//            (0 ok / 1 InvalidSignature).
+//   SigIO -- SignatureCrypto::recover with the digest given (Secp256k1Crypto::recover,
+//            Secp256k1Crypto.cpp:79-93; SM2Crypto::recover, SM2Crypto.cpp:81-92): 32-byte digests,
+//            signatures at a fixed stride and length; results pub64 (secp256k1 only, nullable), addr20
+//            (nullable) and ok (1 valid / 0 invalid).  Output rows need 4-byte alignment only.
+struct TxIO {
+    const uint8_t* pre;
+    const uint64_t* pre_off;
+    const uint8_t* sig;
+    const uint64_t* sig_off;
+    uint8_t* txhash;
+    uint8_t* sender;
+    uint8_t* status;
+
+    __device__ __forceinline__ uint32_t sig_span(uint64_t i, const uint8_t*& p) const {
+        const uint64_t a = sig_off[i], b = sig_off[i + 1];
+        p = sig + a;
+        return b - a > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(b - a);
+    }
+    // the digest as the field element the recover / verify bodies take (hash_be)
+    template <int H>
+    __device__ __forceinline__ void digest(uint64_t i, fe& h) const {
+        const uint64_t a = pre_off[i];
+        const uint32_t len = static_cast<uint32_t>(pre_off[i + 1] - a);
+        ByteReader rd(pre + a, len);
+        uint32_t d[8];
+        if constexpr (H == SM3) {
+            sm3_msg(rd, len, d);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) h.v[k] = d[7 - k];
+        } else {
+            keccak256_msg(rd, len, d);
+            fe_from_be_words(h, d);
+        }
+        store_digest(H, txhash + 32 * i, d);
+    }
+    __device__ __forceinline__ bool want_addr() const { return true; }
+    // ad = right160(H(pub)) as 5 memory words (zero when !ok); x, y = the recovered key (unused here)
+    __device__ __forceinline__ void finish(uint64_t i, bool ok, const uint32_t ad[5], const fe*, const fe*) const {
+        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = ad[k];
+        status[i] = ok ? 0 : 1;
+    }
+};
+
+struct SigIO {
+    const uint8_t* hash;
+    const uint8_t* sig;
+    uint32_t stride;
+    uint32_t siglen;
+    uint8_t* pub;
+    uint8_t* addr;
+    uint8_t* ok;
+
+    __device__ __forceinline__ uint32_t sig_span(uint64_t i, const uint8_t*& p) const {
+        p = sig + static_cast<uint64_t>(stride) * i;
+        return siglen;
+    }
+    template <int H>
+    __device__ __forceinline__ void digest(uint64_t i, fe& h) const {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(hash + 32 * i);
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = q[k];
+        fe_from_be_words(h, w);
+    }
+    __device__ __forceinline__ bool want_addr() const { return addr != nullptr; }
+    __device__ __forceinline__ void finish(uint64_t i, bool valid, const uint32_t ad[5], const fe* x, const fe* y) const {
+        if (pub && x && y) {
+            fe zx, zy;
+            fe_zero(zx);
+            fe_zero(zy);
+            store_be256_u32(pub + 64 * i, valid ? *x : zx);
+            store_be256_u32(pub + 64 * i + 32, valid ? *y : zy);
+        }
+        if (addr) {
+            uint32_t* o = reinterpret_cast<uint32_t*>(addr + 20 * i);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) o[k] = valid ? ad[k] : 0u;
+        }
+        ok[i] = valid ? 1 : 0;
+    }
+};
 
 // ------------------------------------------------------------------ SM2 (one lane)
 // e = SM3(Z_A || hash) as 8 big-endian words; X, Y: public key as big-endian word arrays

@@ -678,30 +678,20 @@ __device__ __forceinline__ void pair26_load_jac(JacP26& P, const uint32_t (*src)
     P.inf = src[24][lane] != 0u;
 }
 
-__global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(const uint8_t* __restrict__ pre,
-                                                                      const uint64_t* __restrict__ pre_off,
-                                                                      const uint8_t* __restrict__ sig,
-                                                                      const uint64_t* __restrict__ sig_off,
-                                                                      uint64_t n, const uint32_t* __restrict__ tab,
-                                                                      uint8_t* __restrict__ txhash,
-                                                                      uint8_t* __restrict__ sender,
-                                                                      uint8_t* __restrict__ status) {
+template <class IO>
+__global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab) {
     __shared__ Sm2Pair26Lds L;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 64 + lane;
     const bool active = i < n;
     if (threadIdx.x < 4) L.seq[threadIdx.x] = 0u;
     __syncthreads();
-    uint64_t sa = 0, sb = 0;
-    if (active) {
-        sa = sig_off[i];
-        sb = sig_off[i + 1];
-    }
-    const bool len_ok = active && sb - sa == 128u;
+    const uint8_t* sp = nullptr;
+    const bool len_ok = active && io.sig_span(i, sp) == 128u;
     fe r, s, px, py;
     uint32_t X[8], Y[8];
     if (len_ok) {
-        ByteReader rd(sig + sa, 128);
+        ByteReader rd(sp, 128);
         uint32_t w[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) w[k] = rd.word(k);
@@ -766,17 +756,9 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(const uint
             pair26_add_digit(acc, c, d);
         }
     } else if (wave == 2) {
-        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (active) {
-            const uint64_t pa = pre_off[i], pb = pre_off[i + 1];
-            const uint32_t len = static_cast<uint32_t>(pb - pa);
-            ByteReader rd(pre + pa, len);
-            sm3_msg(rd, len, d);
-            store_digest(SM3, txhash + 32 * i, d);
-        }
         fe h;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) h.v[k] = d[7 - k];
+        fe_zero(h);
+        if (active) io.template digest<SM3>(i, h);
         uint32_t eb[8];
         sm2_e(eb, X, Y, h);
         fe e, cc;
@@ -786,8 +768,8 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(const uint
         FieldN2::sub(cc, r, e);
         lds_store_fe(L.c, cc, lane);
         L.ok2[lane] = sm2_on_curve26(P) ? 1u : 0u;
-        uint32_t ad[5];
-        sm3_address(ad, px, py);
+        uint32_t ad[5] = {0, 0, 0, 0, 0};
+        if (io.want_addr()) sm3_address(ad, px, py);
 #pragma unroll
         for (int k = 0; k < 5; ++k) L.addr[k][lane] = ad[k];
         JacP26 G0, G1, G;
@@ -826,10 +808,10 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(const uint
             match = match || fp26_is_zero(dlt);
         }
         ok = ok && match;
-        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+        uint32_t ad[5];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) o[k] = ok ? L.addr[k][lane] : 0u;
-        status[i] = ok ? 0 : 1;
+        for (int k = 0; k < 5; ++k) ad[k] = ok ? L.addr[k][lane] : 0u;
+        io.finish(i, ok, ad, nullptr, nullptr);
     }
 }
 // ------------------------------------------------------------------ SM2 lane-trio kernel (fp26)
@@ -874,14 +856,8 @@ __device__ __forceinline__ void trio_add_digit_sm2(TrioPtP& acc, const Sm2Trio26
     trio_cmov_sm2(acc, R, d != 0);
 }
 
-__global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(const uint8_t* __restrict__ pre,
-                                                                      const uint64_t* __restrict__ pre_off,
-                                                                      const uint8_t* __restrict__ sig,
-                                                                      const uint64_t* __restrict__ sig_off,
-                                                                      uint64_t n, const uint32_t* __restrict__ tab,
-                                                                      uint8_t* __restrict__ txhash,
-                                                                      uint8_t* __restrict__ sender,
-                                                                      uint8_t* __restrict__ status) {
+template <class IO>
+__global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab) {
     constexpr int TPW = 40;
     __shared__ Sm2Trio26Lds L;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -889,16 +865,12 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(const uint
     const bool active = lane < TPW && i < n;
     if (threadIdx.x < 4) L.seq[threadIdx.x] = 0u;
     __syncthreads();
-    uint64_t sa = 0, sb = 0;
-    if (active) {
-        sa = sig_off[i];
-        sb = sig_off[i + 1];
-    }
-    const bool len_ok = active && sb - sa == 128u;
+    const uint8_t* sp = nullptr;
+    const bool len_ok = active && io.sig_span(i, sp) == 128u;
     fe r, s, px, py;
     uint32_t X[8], Y[8];
     if (len_ok) {
-        ByteReader rd(sig + sa, 128);
+        ByteReader rd(sp, 128);
         uint32_t w[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) w[k] = rd.word(k);
@@ -979,17 +951,9 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(const uint
         trio_to_jac_sm2(J, acc, T);
         if (T.r0 && trio_idx < 5) pair26_store_jac(L.acc, J, tl);
     } else if (wave == 2) {
-        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (active) {
-            const uint64_t pa = pre_off[i], pb = pre_off[i + 1];
-            const uint32_t len = static_cast<uint32_t>(pb - pa);
-            ByteReader rd(pre + pa, len);
-            sm3_msg(rd, len, d);
-            store_digest(SM3, txhash + 32 * i, d);
-        }
         fe h;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) h.v[k] = d[7 - k];
+        fe_zero(h);
+        if (active) io.template digest<SM3>(i, h);
         uint32_t eb[8];
         sm2_e(eb, X, Y, h);
         fe e, cc;
@@ -999,8 +963,8 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(const uint
         FieldN2::sub(cc, r, e);
         lds_store_fe(L.c, cc, lane);
         L.ok2[lane] = sm2_on_curve26(P) ? 1u : 0u;
-        uint32_t ad[5];
-        sm3_address(ad, px, py);
+        uint32_t ad[5] = {0, 0, 0, 0, 0};
+        if (io.want_addr()) sm3_address(ad, px, py);
 #pragma unroll
         for (int k = 0; k < 5; ++k) L.addr[k][lane] = ad[k];
         JacP26 G0, G1, G;
@@ -1040,35 +1004,37 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(const uint
             match = match || fp26_is_zero(dlt);
         }
         ok = ok && match;
-        uint32_t* o = reinterpret_cast<uint32_t*>(sender + 20 * i);
+        uint32_t ad[5];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) o[k] = ok ? L.addr[k][lane] : 0u;
-        status[i] = ok ? 0 : 1;
+        for (int k = 0; k < 5; ++k) ad[k] = ok ? L.addr[k][lane] : 0u;
+        io.finish(i, ok, ad, nullptr, nullptr);
     }
 }
 
-int launch_tx_verify_small_sm2(const TxKernelPolicy& pol, const uint8_t* d_pre, const uint64_t* d_pre_off,
-                               const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n, uint8_t* d_txhash,
-                               uint8_t* d_sender, uint8_t* d_status, hipStream_t st) {
+template <class IO>
+int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st) {
     const dim3 grid(static_cast<unsigned>((n + 63) / 64));
     if (pol.f26) {  // fp26 point arithmetic over the R'-domain 8-bit table
         const uint32_t* t26;
         const int rc = tables8_sm2_26(&t26);
         if (rc) return rc;
         if (pol.coop == 2)
-            hipLaunchKernelGGL(tx_verify_sm2_trio26_kernel, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0, st,
-                               d_pre, d_pre_off, d_sig, d_sig_off, n, t26, d_txhash, d_sender, d_status);
+            hipLaunchKernelGGL(tx_verify_sm2_trio26_kernel<IO>, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0,
+                               st, io, n, t26);
         else
-            hipLaunchKernelGGL(tx_verify_sm2_pair26_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off,
-                               n, t26, d_txhash, d_sender, d_status);
-    } else {
+            hipLaunchKernelGGL(tx_verify_sm2_pair26_kernel<IO>, grid, dim3(256), 0, st, io, n, t26);
+    } else if constexpr (std::is_same_v<IO, TxIO>) {
         const uint32_t *k1, *sm2;
         const int rc = tables8(&k1, &sm2);
         if (rc) return rc;
-        hipLaunchKernelGGL(tx_verify_sm2_pair_kernel, grid, dim3(256), 0, st, d_pre, d_pre_off, d_sig, d_sig_off, n,
-                           sm2, d_txhash, d_sender, d_status);
+        hipLaunchKernelGGL(tx_verify_sm2_pair_kernel, grid, dim3(256), 0, st, io.pre, io.pre_off, io.sig, io.sig_off, n,
+                           sm2, io.txhash, io.sender, io.status);
+    } else {
+        return BCOSGPU_E_ARG;  // the 8 x 32-bit pair kernel is TxIO only (launch_verify never asks)
     }
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
+template int launch_verify_small_sm2<TxIO>(const TxKernelPolicy&, const TxIO&, uint64_t, hipStream_t);
+template int launch_verify_small_sm2<SigIO>(const TxKernelPolicy&, const SigIO&, uint64_t, hipStream_t);
 
 }  // namespace bcosgpu

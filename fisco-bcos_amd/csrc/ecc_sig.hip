@@ -1,61 +1,12 @@
-// ecc_sig.hip -- one-lane signature kernels: secp256k1 recover, SM2 verify, known-key verify, the ecRecover
-// precompile, and the deterministic signing used to build synthetic batches; their launchers.
+// ecc_sig.hip -- one-lane signature kernels: known-key verify, the ecRecover precompile, and the
+// deterministic signing used to build synthetic batches; their launchers.  (Recover and SM2 verify with
+// the digest given run the tx-verify kernels over SigIO: ecc_txv.hip launch_secp256k1_recover /
+// launch_sm2_verify.)
 #include "ecc_device.h"
 
 namespace bcosgpu {
 
 // ------------------------------------------------------------------ kernels
-template <bool F26>
-__global__ __launch_bounds__(256) void secp256k1_recover_kernel(const uint8_t* __restrict__ hash,
-                                                                const uint8_t* __restrict__ sig, uint32_t stride,
-                                                                uint64_t n, const uint32_t* __restrict__ tab, int tbits,
-                                                                uint8_t* __restrict__ pub, uint8_t* __restrict__ addr,
-                                                                uint8_t* __restrict__ okout) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    fe h, x, y;
-    load_be256_aligned(h, hash + 32 * i);
-    const bool ok = F26 ? secp256k1_recover_lane26(h, sig + static_cast<uint64_t>(stride) * i, 65u, CombTab{tab, tbits}, x, y)
-                        : secp256k1_recover_lane(h, sig + static_cast<uint64_t>(stride) * i, 65u, CombTab{tab, tbits}, x, y);
-    if (!ok) {
-        fe_zero(x);
-        fe_zero(y);
-    }
-    if (pub) {
-        store_be256(pub + 64 * i, x);
-        store_be256(pub + 64 * i + 32, y);
-    }
-    if (addr) {
-        uint32_t a[5] = {0, 0, 0, 0, 0};
-        if (ok) keccak_address(a, x, y);
-        uint32_t* o = reinterpret_cast<uint32_t*>(addr + 20 * i);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) o[k] = a[k];
-    }
-    okout[i] = ok ? 1 : 0;
-}
-
-template <bool F26>
-__global__ __launch_bounds__(256) void sm2_verify_kernel(const uint8_t* __restrict__ hash,
-                                                         const uint8_t* __restrict__ sig, uint32_t stride,
-                                                         uint64_t n, const uint32_t* __restrict__ tab, int tbits,
-                                                         uint8_t* __restrict__ addr, uint8_t* __restrict__ okout) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    fe h, x, y;
-    load_be256_aligned(h, hash + 32 * i);
-    const bool ok = F26 ? sm2_verify_lane26(h, sig + static_cast<uint64_t>(stride) * i, 128u, CombTab{tab, tbits}, x, y)
-                        : sm2_verify_lane(h, sig + static_cast<uint64_t>(stride) * i, 128u, CombTab{tab, tbits}, x, y);
-    if (addr) {
-        uint32_t a[5] = {0, 0, 0, 0, 0};
-        if (ok) sm3_address(a, x, y);
-        uint32_t* o = reinterpret_cast<uint32_t*>(addr + 20 * i);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) o[k] = a[k];
-    }
-    okout[i] = ok ? 1 : 0;
-}
-
 // SignatureCrypto::verify(pub, hash, sig) for a batch (sealer signatures: BlockValidator.cpp:141-182,
 // PBFTCacheProcessor.cpp:795-821).  SM2: SM2Crypto::verify reads the first 64 signature bytes (r || s)
 // and verifies against the GIVEN key (SM2Crypto.cpp:66-79); secp256k1: secp256k1_verify_lane.
@@ -276,43 +227,6 @@ __global__ __launch_bounds__(256) void sm2_sign_kernel(const uint8_t* __restrict
         for (int q = 0; q < 8; ++q) reinterpret_cast<uint32_t*>(so + 32 * p)[q] = w[q];
     }
     okout[i] = ok ? 1 : 0;
-}
-
-int launch_secp256k1_recover(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride, uint64_t n,
-                             uint8_t* d_pub, uint8_t* d_addr, uint8_t* d_ok, hipStream_t st) {
-    if (n == 0) return 0;
-    const uint32_t *k1, *sm2;
-    int bits;
-    int rc = tables(&k1, &sm2, &bits);
-    if (rc) return rc;
-    if (tx_policy().f26)
-        hipLaunchKernelGGL(secp256k1_recover_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n,
-                           k1, bits, d_pub, d_addr, d_ok);
-    else
-        hipLaunchKernelGGL(secp256k1_recover_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n,
-                           k1, bits, d_pub, d_addr, d_ok);
-    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
-}
-
-int launch_sm2_verify(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride, uint64_t n, uint8_t* d_addr,
-                      uint8_t* d_ok, hipStream_t st) {
-    if (n == 0) return 0;
-    const uint32_t *k1, *sm2;
-    int bits;
-    int rc = tables(&k1, &sm2, &bits);
-    if (rc) return rc;
-    if (tx_policy().f26) {
-        const uint32_t* t26;
-        int b26;
-        rc = tables_sm2_26(&t26, &b26);
-        if (rc) return rc;
-        hipLaunchKernelGGL(sm2_verify_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, t26,
-                           b26, d_addr, d_ok);
-    } else {
-        hipLaunchKernelGGL(sm2_verify_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, d_hash, d_sig, stride, n, sm2,
-                           bits, d_addr, d_ok);
-    }
-    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
 // Signing exists to build the synthetic benchmark / test batches on the device.  It is NOT

@@ -201,7 +201,10 @@ int ecc_init_tables(int device, int small) {
     return 0;
 }
 
-const TxKernelPolicy& tx_policy() { return g_policy; }
+TxKernelPolicy tx_policy() {
+    std::lock_guard<std::mutex> g(g_tab_mu);
+    return g_policy;
+}
 
 static int current_device() {
     int dev = 0;

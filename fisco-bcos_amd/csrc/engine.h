@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string>
 #include "../../include/bcos_gpu.h"
 
 namespace bcosgpu {
@@ -44,6 +45,25 @@ int launch_ecrecover(const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint8_t* d
 int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
                      const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n,
                      uint8_t* d_txhash, uint8_t* d_sender, uint8_t* d_status, hipStream_t st);
+
+// coalesce.hip: the host-pointer signature calls as jobs of a per-device queue, coalesced into shared
+// launches (see the file header).  coalesced_run blocks until the job's results are written.
+enum SigJobKind { kSigJobRecoverK1 = 0, kSigJobVerifySM2 = 1, kSigJobVerifyK1 = 2, kSigJobKinds = 3 };
+struct SigJob {
+    int kind = 0;
+    size_t n = 0;
+    const uint8_t* hash32 = nullptr;  // n x 32
+    const uint8_t* sig = nullptr;     // item i at sig + sig_stride * i: r||s||v (recover), r||s[||pub] (verify)
+    size_t sig_stride = 0;
+    const uint8_t* pub64 = nullptr;   // verify: the known keys (SM2: null = the key is sig[64..128))
+    uint8_t* out_pub64 = nullptr;     // recover only, nullable
+    uint8_t* out_addr20 = nullptr;    // recover / SM2 verify, nullable
+    uint8_t* out_ok = nullptr;        // n bytes: 1 valid, 0 invalid
+    int rc = 0;                       // filled in by the engine: 0 or BCOSGPU_E_*, with err
+    std::string err;
+    bool queued = false, done = false;
+};
+int coalesced_run(int device, SigJob& job);
 
 // tars_kernels.hip
 uint64_t tars_decode_work_bytes(uint64_t n);

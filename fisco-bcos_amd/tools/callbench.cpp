@@ -1,0 +1,79 @@
+// callbench.cpp -- single-call throughput of the engine's coalesced entry points (bench.py leg
+// single_call_<T>t): T host threads, each making K calls of bcosgpu_secp256k1_recover / bcosgpu_sm2_verify
+// (one signature per call, the reference's per-tx SignatureCrypto::recover pattern), every result checked
+// against the expected verdict and key.
+//
+//   callbench <datafile> <threads> <calls_per_thread> [device]
+// datafile: "BGCT", u32 suite, u32 m, m x 32 hashes, m x siglen signatures (65 / 128), m verdicts,
+// m x 64 keys (the format of tests/cpp/concurrent_test.cpp).  One JSON line on stdout.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "../../include/bcos_gpu.h"
+
+int main(int argc, char** argv) {
+    if (argc < 4) {
+        fprintf(stderr, "usage: %s datafile threads calls_per_thread [device]\n", argv[0]);
+        return 2;
+    }
+    FILE* f = fopen(argv[1], "rb");
+    if (!f) return 2;
+    char magic[4];
+    uint32_t suite = 0, m = 0;
+    if (fread(magic, 1, 4, f) != 4 || std::memcmp(magic, "BGCT", 4) != 0 || fread(&suite, 4, 1, f) != 1 ||
+        fread(&m, 4, 1, f) != 1 || m == 0)
+        return 2;
+    const size_t siglen = suite == 0 ? 65 : 128;
+    std::vector<uint8_t> hashes(32ull * m), sigs(siglen * m), ok(m), pubs(64ull * m);
+    if (fread(hashes.data(), 1, hashes.size(), f) != hashes.size() || fread(sigs.data(), 1, sigs.size(), f) != sigs.size() ||
+        fread(ok.data(), 1, ok.size(), f) != ok.size() || fread(pubs.data(), 1, pubs.size(), f) != pubs.size())
+        return 2;
+    fclose(f);
+    const int threads = atoi(argv[2]), calls = atoi(argv[3]);
+    const int dev = argc > 4 ? atoi(argv[4]) : 0;
+    auto one = [&](size_t i, uint8_t* pub) {
+        if (suite == 0) return bcosgpu_secp256k1_recover(dev, hashes.data() + 32 * i, sigs.data() + 65 * i, 65, pub);
+        return bcosgpu_sm2_verify(dev, sigs.data() + 128 * i + 64, hashes.data() + 32 * i, sigs.data() + 128 * i);
+    };
+    uint8_t warm[64];
+    if (one(0, warm) < 0) {
+        printf("{\"error\": \"%s\"}\n", bcosgpu_last_error());
+        return 1;
+    }
+    std::atomic<long> mismatches{0}, errors{0};
+    std::vector<std::vector<float>> lat(threads);
+    std::vector<std::thread> pool;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int t = 0; t < threads; ++t) {
+        pool.emplace_back([&, t] {
+            lat[t].reserve(calls);
+            uint8_t pub[64];
+            for (int j = 0; j < calls; ++j) {
+                const size_t i = (static_cast<size_t>(j) * threads + t) % m;
+                const auto a = std::chrono::steady_clock::now();
+                const int rc = one(i, pub);
+                lat[t].push_back(std::chrono::duration<float, std::micro>(std::chrono::steady_clock::now() - a).count());
+                if (rc < 0) ++errors;
+                else if ((rc == 1) != (ok[i] != 0) || (suite == 0 && rc == 1 && std::memcmp(pub, pubs.data() + 64 * i, 64)))
+                    ++mismatches;
+            }
+        });
+    }
+    for (auto& th : pool) th.join();
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::vector<float> all;
+    for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
+    std::sort(all.begin(), all.end());
+    const long total = static_cast<long>(threads) * calls;
+    printf("{\"suite\": %u, \"threads\": %d, \"calls\": %ld, \"seconds\": %.4f, \"calls_per_s\": %.1f, "
+           "\"latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}, \"mismatches\": %ld, \"engine_errors\": %ld}\n",
+           suite, threads, total, dt, total / dt, all[all.size() / 2], all[all.size() * 99 / 100], all.back(),
+           mismatches.load(), errors.load());
+    return mismatches.load() || errors.load() ? 1 : 0;
+}

@@ -143,7 +143,11 @@ int bcosgpu_merkle_verify_proofs_dev(int hasher, const uint8_t* d_proofs, uint64
                                      uint8_t* d_ok, void* stream);
 
 /* ---------------------------------------------------------------- signatures (SignatureCrypto, batched) */
-/* secp256k1 public-key recovery (Secp256k1Crypto::recover, Secp256k1Crypto.h:57-60).
+/* The host-pointer signature calls below (batched, single and the wedpr shims) are jobs of a
+ * per-device queue: concurrent callers are coalesced into shared launches, each batch taking the
+ * kernel the batch size calls for (the lane-trio / pair kernels for small batches, the one-lane kernel
+ * at occupancy 1 or 2 for large ones; see bcosgpu_set_tx_kernel_policy).  Results are per call.
+ * secp256k1 public-key recovery (Secp256k1Crypto::recover, Secp256k1Crypto.h:57-60).
  * pub64 / addr20 nullable; addr20 = right160(Keccak256(pub)) (calculateAddress, KeyPair.h:30-33). */
 int bcosgpu_secp256k1_recover_batch(const uint8_t* hash32, const uint8_t* sig65, size_t n,
                                     uint8_t* pub64, uint8_t* addr20, uint8_t* ok);
@@ -246,11 +250,35 @@ uint64_t bcosgpu_tx_preimage_size(const bcosgpu_TransactionData* txs, size_t n);
 int bcosgpu_pack_tx_preimages(const bcosgpu_TransactionData* txs, size_t n, uint8_t* out, uint64_t cap,
                               uint64_t* offsets);
 
+/* ---------------------------------------------------------------- single calls on an explicit device */
+/* One signature per call, for the reference's per-transaction call sites: TxPool's submitter threads
+ * (TxPool.h:48-49) -> TxValidator::verify (TxValidator.cpp:56) -> Transaction::verify (Transaction.h:68-82)
+ * -> SignatureCrypto::recover.  Concurrent calls on one device are coalesced into shared launches (one
+ * H2D copy, one kernel, one D2H copy per batch; up to 4 batches in flight per device).  `device` is
+ * initialised on first use; the calling thread's current device is left unchanged.
+ * Return 1 = valid, 0 = invalid signature (the reference throws InvalidSignature / returns false),
+ * < 0 = engine error (BCOSGPU_E_*, message in bcosgpu_last_error()). */
+/* Secp256k1Crypto::recover (Secp256k1Crypto.cpp:79-93): sig = r||s||v, sig_len must be 65;
+ * pub64 = X||Y (zero when invalid). */
+int bcosgpu_secp256k1_recover(int device, const uint8_t* hash32, const uint8_t* sig, size_t sig_len, uint8_t* pub64);
+/* secp256k1Verify -> wedpr_secp256k1_verify (Secp256k1Crypto.cpp:51-63): libsecp256k1 verify (low-S);
+ * only sig[0..64) = r||s is read; sig_len < 64 is invalid. */
+int bcosgpu_secp256k1_verify(int device, const uint8_t* pub64, const uint8_t* hash32, const uint8_t* sig,
+                             size_t sig_len);
+/* SM2Crypto::verify (SM2Crypto.cpp:66-79) -> fast_sm2_verify: sig64 = r||s, with the given key. */
+int bcosgpu_sm2_verify(int device, const uint8_t* pub64, const uint8_t* hash32, const uint8_t* sig64);
+
 /* ---------------------------------------------------------------- wedpr-ABI single-call shims */
-/* Same layout as wedpr-crypto's CInputBuffer / COutputBuffer; return 0 (WEDPR_SUCCESS) or -1.
+/* Same layout as wedpr-crypto's CInputBuffer / COutputBuffer; on the calling thread's current device.
+ * Return 0 (WEDPR_SUCCESS), -1 (WEDPR_ERROR: invalid input or signature) or
+ * BCOSGPU_WEDPR_ENGINE_ERROR when the engine itself failed (no gfx950 device, HIP error; message in
+ * bcosgpu_last_error()) -- a reference caller that only tests "!= WEDPR_SUCCESS" reads that as an
+ * invalid signature, so the SignatureCrypto adapters (bcos_gpu_crypto.hpp) check for it and throw
+ * SignException instead.
  * A reference translation unit that already has wedpr's types (<wedpr-crypto/WedprCrypto.h>) includes
  * bcos_gpu_wedpr.h instead, which declares these two symbols over CInputBuffer / COutputBuffer so they
  * bind to SM2Crypto::m_verifier (SM2Crypto.h:64-65) and to wedpr's call sites unchanged. */
+#define BCOSGPU_WEDPR_ENGINE_ERROR (-2)
 typedef struct { const char* data; uintptr_t len; } bcosgpu_CInputBuffer;
 typedef struct { char* data; uintptr_t len; } bcosgpu_COutputBuffer;
 #ifndef BCOSGPU_WEDPR_TYPES

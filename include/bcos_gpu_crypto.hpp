@@ -3,11 +3,15 @@
  * meant to be compiled INSIDE the reference tree (its bcos-crypto headers, wedpr-crypto, Boost).
  *
  *   GpuSecp256k1Crypto : bcos::crypto::Secp256k1Crypto        (Secp256k1Crypto.h:37-72)
- *       recover (Secp256k1Crypto.cpp:79-93) and verify (:51-63) run on the GPU through the C ABI;
- *       sign / key generation stay on the host (wedpr), as signing must be constant-time.
+ *       recover (Secp256k1Crypto.cpp:79-93), both verify overloads (:51-63, :126-131) and
+ *       recoverAddress (:95-124) run on the GPU through the explicit-device single calls, which the
+ *       engine coalesces across threads; sign / key generation stay on the host (wedpr), as signing
+ *       must be constant-time.
  *   GpuSM2Crypto : bcos::crypto::SM2Crypto                    (SM2Crypto.h:31-67)
- *       m_verifier = bcosgpu_wedpr_sm2_verify, so SM2Crypto::verify and ::recover
- *       (SM2Crypto.cpp:66-92) run on the GPU unchanged; m_signer stays wedpr's.
+ *       verify(PublicPtr) (SM2Crypto.cpp:66-79) is overridden, so SM2Crypto::recover (:81-92), the bytes
+ *       overload (:29-34) and recoverAddress (:94-122) -- all of which call it -- run on the GPU;
+ *       m_verifier is a wedpr-shaped lambda over the same call; m_signer stays wedpr's.
+ *   Both take the device at construction and use it from every thread (TBB workers included).
  *   recoverBatch(hashes, signatures) on both: one device call for a whole batch -- the hook the
  *       batch sites (TransactionSync::importDownloadedTxs' parallel_for, TransactionSync.cpp:516-548)
  *       are rewired to; entry i is the recovered key or nullptr where SignatureCrypto::recover would
@@ -15,7 +19,8 @@
  *
  * Failures throw what the reference throws: InvalidSignature via BOOST_THROW_EXCEPTION with an
  * errinfo_comment (Secp256k1Crypto.cpp:86-91, SM2Crypto.cpp:89-91); an engine error (no gfx950 device,
- * HIP failure) throws bcos::crypto::SignException with the engine's message.  Selection in
+ * HIP failure, bad device index) throws bcos::crypto::SignException with the engine's message, on
+ * both suites, never InvalidSignature.  Selection in
  * ProtocolInitializer::createCryptoSuite (libinitializer/ProtocolInitializer.cpp:102-124) is the only
  * other line to change: INTEGRATION.md §2.  tests/cpp/sigcrypto_test.cpp compiles this header against
  * a mirror of those interfaces (tests/cpp/mirror/) and runs the reference KATs through it.
@@ -41,44 +46,42 @@ namespace bcosgpu
 {
 namespace ref
 {
-inline void initDevice(int device)
-{
-    if (bcosgpu_init(device) != BCOSGPU_OK)
-    {
-        BOOST_THROW_EXCEPTION(bcos::crypto::SignException() << bcos::errinfo_comment(
-                                  std::string("bcosgpu_init: ") + bcosgpu_last_error()));
-    }
-}
-
+// An engine error (no gfx950 device, HIP failure, device index out of range) is a SignException, never
+// an InvalidSignature: a dead GPU must not make TxPool reject every transaction (TxValidator.cpp:54-61).
 inline void engineCheck(int rc, const char* what)
 {
-    if (rc != BCOSGPU_OK)
+    if (rc < 0)
     {
         BOOST_THROW_EXCEPTION(bcos::crypto::SignException() << bcos::errinfo_comment(
                                   std::string(what) + ": " + bcosgpu_last_error()));
     }
 }
 
+// calculateAddress (bcos-crypto/interfaces/crypto/KeyPair.h): right160(H(pub))
+inline bcos::bytes rightAddress(bcos::crypto::Hash::Ptr _hashImpl, const bcos::crypto::KeyInterface& _pub)
+{
+    auto h = _hashImpl->hash(bcos::bytesConstRef((const bcos::byte*)_pub.constData(), _pub.size()));
+    return bcos::bytes(h.data() + 12, h.data() + 32);
+}
+
 class GpuSecp256k1Crypto : public bcos::crypto::Secp256k1Crypto
 {
 public:
     using Ptr = std::shared_ptr<GpuSecp256k1Crypto>;
-    explicit GpuSecp256k1Crypto(int _device = 0) { initDevice(_device); }
+    // every call runs on `_device` (initialised on first use), whichever thread makes it
+    explicit GpuSecp256k1Crypto(int _device = 0) : m_device(_device) {}
     ~GpuSecp256k1Crypto() override = default;
 
-    // Secp256k1Crypto::recover -> secp256k1Recover (Secp256k1Crypto.cpp:79-93)
+    // Secp256k1Crypto::recover -> secp256k1Recover (Secp256k1Crypto.cpp:79-93); concurrent calls are
+    // coalesced into shared launches by the engine
     bcos::crypto::PublicPtr recover(
         const bcos::crypto::HashType& _hash, bcos::bytesConstRef _signatureData) const override
     {
         auto pub = std::make_shared<bcos::crypto::KeyImpl>(bcos::crypto::SECP256K1_PUBLIC_LEN);
-        uint8_t ok = 0;
-        if (_signatureData.size() == (size_t)bcos::crypto::SECP256K1_SIGNATURE_LEN)
-        {
-            engineCheck(bcosgpu_secp256k1_recover_batch(_hash.data(), _signatureData.data(), 1,
-                            (uint8_t*)pub->mutableData(), nullptr, &ok),
-                "bcosgpu_secp256k1_recover_batch");
-        }
-        if (!ok)
+        const int rc = bcosgpu_secp256k1_recover(m_device, _hash.data(), _signatureData.data(),
+            _signatureData.size(), (uint8_t*)pub->mutableData());
+        engineCheck(rc, "bcosgpu_secp256k1_recover");
+        if (rc != 1)
         {
             BOOST_THROW_EXCEPTION(bcos::crypto::InvalidSignature() << bcos::errinfo_comment(
                                       "invalid signature: secp256k1Recover failed, msgHash : " +
@@ -97,15 +100,54 @@ public:
         {
             return false;
         }
-        uint8_t ok = 0;
-        engineCheck(bcosgpu_verify_batch(BCOSGPU_SUITE_SECP256K1, (const uint8_t*)_pubKey->constData(),
-                        _hash.data(), _signatureData.data(), 64, 1, &ok),
-            "bcosgpu_verify_batch");
-        return ok != 0;
+        const int rc = bcosgpu_secp256k1_verify(m_device, (const uint8_t*)_pubKey->constData(),
+            _hash.data(), _signatureData.data(), _signatureData.size());
+        engineCheck(rc, "bcosgpu_secp256k1_verify");
+        return rc == 1;
     }
-    using bcos::crypto::Secp256k1Crypto::verify;
 
-    // batch hook: recover every signature of a batch in one device call
+    // Secp256k1Crypto::verify(bytes) (Secp256k1Crypto.cpp:126-131) calls the free secp256k1Verify, not
+    // the virtual overload, so it is overridden too: the key as KeyImpl(64, bytes), then the GPU
+    bool verify(std::shared_ptr<bcos::bytes const> _pubKeyBytes, const bcos::crypto::HashType& _hash,
+        bcos::bytesConstRef _signatureData) const override
+    {
+        return verify(std::make_shared<bcos::crypto::KeyImpl>(
+                          bcos::crypto::SECP256K1_PUBLIC_LEN, _pubKeyBytes),
+            _hash, _signatureData);
+    }
+
+    // Secp256k1Crypto::recoverAddress -> secp256k1Recover(hashImpl, input) (Secp256k1Crypto.cpp:95-124):
+    // input = hash || v || r || s (32 bytes each, zero-padded); v must be 27 or 28 as a 256-bit number;
+    // {true, right160(H(pub))} or {false, {}}.  (The reference copies min(size, sizeof(bytesConstRef))
+    // bytes of the input into its struct -- 16 -- and reads the rest uninitialised; this reads all 128.)
+    std::pair<bool, bcos::bytes> recoverAddress(
+        bcos::crypto::Hash::Ptr _hashImpl, bcos::bytesConstRef _in) const override
+    {
+        uint8_t in[128] = {0};
+        std::memcpy(in, _in.data(), _in.size() < 128 ? _in.size() : 128);
+        bool vOk = in[63] == 27 || in[63] == 28;
+        for (int i = 32; i < 63; ++i)
+        {
+            vOk = vOk && in[i] == 0;
+        }
+        if (!vOk)
+        {
+            return {false, {}};
+        }
+        uint8_t sig[65];
+        std::memcpy(sig, in + 64, 64);
+        sig[64] = (uint8_t)(in[63] - 27);
+        bcos::crypto::KeyImpl pub(bcos::crypto::SECP256K1_PUBLIC_LEN);
+        const int rc = bcosgpu_secp256k1_recover(m_device, in, sig, 65, (uint8_t*)pub.mutableData());
+        engineCheck(rc, "bcosgpu_secp256k1_recover");
+        if (rc != 1)
+        {
+            return {false, {}};
+        }
+        return {true, rightAddress(_hashImpl, pub)};
+    }
+
+    // batch hook: recover every signature of a batch in one engine call
     std::vector<bcos::crypto::PublicPtr> recoverBatch(const std::vector<bcos::crypto::HashType>& _hashes,
         const std::vector<bcos::bytesConstRef>& _signatures) const
     {
@@ -126,6 +168,7 @@ public:
                 std::memcpy(s.data() + 65 * i, _signatures[i].data(), 65);
             }
         }
+        engineCheck(bcosgpu_init(m_device), "bcosgpu_init");  // the batch ABI runs on the current device
         engineCheck(
             bcosgpu_secp256k1_recover_batch(h.data(), s.data(), n, pub.data(), nullptr, ok.data()),
             "bcosgpu_secp256k1_recover_batch");
@@ -140,18 +183,51 @@ public:
         }
         return out;
     }
+
+    int device() const { return m_device; }
+
+private:
+    int m_device;
 };
 
 class GpuSM2Crypto : public bcos::crypto::SM2Crypto
 {
 public:
     using Ptr = std::shared_ptr<GpuSM2Crypto>;
-    explicit GpuSM2Crypto(int _device = 0)
+    explicit GpuSM2Crypto(int _device = 0) : m_device(_device)
     {
-        initDevice(_device);
-        m_verifier = bcosgpu_wedpr_sm2_verify;  // SM2Crypto.h:64-65: verify and recover on the GPU
+        // SM2Crypto.h:64-65: the wedpr-shaped verifier, for any code that calls m_verifier directly;
+        // an engine failure comes back as BCOSGPU_WEDPR_ENGINE_ERROR, which verify() below turns into
+        // SignException
+        const int dev = _device;
+        m_verifier = [dev](const CInputBuffer* _pub, const CInputBuffer* _hash,
+                         const CInputBuffer* _sig) -> int8_t {
+            if (!_pub || !_hash || !_sig || _pub->len != 64 || _hash->len != 32 || _sig->len != 64)
+            {
+                return WEDPR_ERROR;
+            }
+            const int rc = bcosgpu_sm2_verify(dev, (const uint8_t*)_pub->data,
+                (const uint8_t*)_hash->data, (const uint8_t*)_sig->data);
+            return rc < 0 ? (int8_t)BCOSGPU_WEDPR_ENGINE_ERROR : rc == 1 ? WEDPR_SUCCESS : WEDPR_ERROR;
+        };
     }
     ~GpuSM2Crypto() override = default;
+
+    // SM2Crypto::verify (SM2Crypto.cpp:66-79): r || s = the first 64 signature bytes, the given key.
+    // SM2Crypto::recover (:81-92) and the bytes overload (:29-34) call this virtual, so they run here too.
+    bool verify(bcos::crypto::PublicPtr _pubKey, const bcos::crypto::HashType& _hash,
+        bcos::bytesConstRef _signatureData) const override
+    {
+        if (!_pubKey || _pubKey->size() != 64 || _signatureData.size() < 64)
+        {
+            return false;
+        }
+        const int rc = bcosgpu_sm2_verify(
+            m_device, (const uint8_t*)_pubKey->constData(), _hash.data(), _signatureData.data());
+        engineCheck(rc, "bcosgpu_sm2_verify");
+        return rc == 1;
+    }
+    using bcos::crypto::SM2Crypto::verify;
 
     // batch hook: SM2Crypto::recover (verify against the embedded key) for a whole batch
     std::vector<bcos::crypto::PublicPtr> recoverBatch(const std::vector<bcos::crypto::HashType>& _hashes,
@@ -175,6 +251,7 @@ public:
                 std::memcpy(s.data() + 128 * i, _signatures[i].data(), 128);
             }
         }
+        engineCheck(bcosgpu_init(m_device), "bcosgpu_init");  // the batch ABI runs on the current device
         engineCheck(bcosgpu_sm2_verify_batch(h.data(), s.data(), n, nullptr, ok.data()),
             "bcosgpu_sm2_verify_batch");
         for (size_t i = 0; i < n; ++i)
@@ -188,6 +265,11 @@ public:
         }
         return out;
     }
+
+    int device() const { return m_device; }
+
+private:
+    int m_device;
 };
 }  // namespace ref
 }  // namespace bcosgpu

@@ -275,6 +275,10 @@ def standin():
         L.standin_version.argtypes = []
         L.standin_tx_verify_batch.restype = None
         L.standin_tx_verify_batch.argtypes = [I, P, P, P, P, S, P, P, P, I]
+        L.standin_hash.restype = I
+        L.standin_hash.argtypes = [I, P, S, P]
+        L.standin_merkle_root.restype = I
+        L.standin_merkle_root.argtypes = [I, I, P, S, P, I]
         _standin = L
     return _standin
 
@@ -292,3 +296,22 @@ def standin_tx_verify_packed(suite, pre, pre_off, sig, sig_off, nthreads=1):
     standin().standin_tx_verify_batch(suite, _p(pre), _p(pre_off), _p(sig), _p(sig_off), n, _p(txhash),
                                       _p(sender), _p(status), nthreads)
     return txhash, sender, status
+
+
+def standin_hash(hasher, data):
+    """OpenSSLHasher<SM3 | Keccak256> (OpenSSLHasher.h:22-143) over OpenSSL 1.1.1's EVP (stand-in build)."""
+    out = np.zeros(32, dtype=np.uint8)
+    d = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
+    if standin().standin_hash(hasher, _p(d), len(data), _p(out)) != 0:
+        raise RuntimeError("OpenSSL hasher failed (KECCAK1600_CTX layout?)")
+    return out.tobytes()
+
+
+def standin_merkle_root(hasher, width, leaves, nthreads=1):
+    """Merkle<H, width>::generateMerkle's root (Merkle.h:170-261) with the reference's OpenSSL hashers,
+    levels parallel over nthreads (the reference CPU path merkleBench.cpp times)."""
+    leaves = np.ascontiguousarray(leaves, dtype=np.uint8).reshape(-1, 32)
+    root = np.zeros(32, dtype=np.uint8)
+    if standin().standin_merkle_root(hasher, width, _p(leaves), leaves.shape[0], _p(root), nthreads) != 0:
+        raise RuntimeError("standin_merkle_root failed")
+    return root.tobytes()

@@ -14,8 +14,12 @@
  *              EC_POINT_mul (OpenSSL's generic wNAF), pub = affine Q;
  *   SM2:       EVP_DigestVerify with SM3 and the user ID "1234567812345678" (fast_sm2.cpp:34,203) over
  *              the DER-encoded (r, s) and the 32-byte tx hash, against the embedded pubkey;
- *   hashes:    SM3 by EVP; Keccak-256 by the oracle's portable C (OpenSSL 1.1.1 has no pad-0x01
- *              Keccak EVP; the reference pokes its SHA3 context, OpenSSLHasher.h:51-80).
+ *   hashes:    SM3 by EVP; Keccak-256 in the tx path by the oracle's portable C.
+ * And the reference's Merkle CPU path (standin_merkle_root): Merkle<H, width>::generateMerkle
+ * (Merkle.h:170-261) with its OpenSSL hashers (OpenSSLHasher.h:22-143, as merkleBench.cpp uses them) --
+ * EVP_sm3, and EVP_sha3_256 with the KECCAK1600_CTX pad byte poked from 0x06 to 0x01 for Keccak-256,
+ * exactly the reference's trick (OpenSSLHasher.h:51-80) -- levels computed in parallel like its
+ * tbb::parallel_for, one hasher per range.
  * Contexts (EC_GROUP, BN_CTX) are per thread, as libsecp256k1's static context would be; the SM2 leg
  * builds its EVP objects per call, as fast_sm2_verify does (fast_sm2.cpp:139-227).
  * Verdicts equal the oracle's on well-formed signatures (tests/test_standin.py).
@@ -29,6 +33,7 @@
 #include <openssl/err.h>
 #include <openssl/evp.h>
 #include <openssl/obj_mac.h>
+#include <stdlib.h>
 #include <string.h>
 
 const char* standin_version(void) { return OpenSSL_version(OPENSSL_VERSION); }
@@ -179,4 +184,93 @@ void standin_tx_verify_batch(int suite, const uint8_t* pre, const uint64_t* pre_
 {
     tx_job j = {suite, pre, sig, pre_off, sig_off, txhash32, sender20, status};
     oracle_parallel_for(n, nthreads, tx_range, &j);
+}
+
+/* ------------------------------------------------------------------ the reference's Merkle CPU path */
+/* OpenSSL 1.1.1's KECCAK1600_CTX and EVP_MD_CTX head (the layout OpenSSLHasher.h:51-75 relies on) */
+typedef struct {
+    uint64_t A[5][5];
+    size_t block_size;
+    size_t md_size;
+    size_t num;
+    unsigned char buf[1600 / 8 - 32];
+    unsigned char pad;
+} standin_keccak1600_ctx;
+typedef struct {
+    const EVP_MD* digest;
+    void* engine;
+    unsigned long flags;
+    standin_keccak1600_ctx* md_data;
+} standin_evp_md_ctx_head;
+
+/* OpenSSLHasher<H>::init: EVP_DigestInit, and for Keccak-256 the pad poke; 0 on a layout mismatch */
+static int ossl_hasher_init(EVP_MD_CTX* m, int hasher)
+{
+    if (hasher == ORACLE_SM3) return EVP_DigestInit(m, EVP_sm3()) == 1;
+    if (EVP_DigestInit(m, EVP_sha3_256()) != 1) return 0;
+    standin_evp_md_ctx_head* h = (standin_evp_md_ctx_head*)m;
+    if (!h->md_data || h->md_data->pad != 0x06) return 0;
+    h->md_data->pad = 0x01;
+    return 1;
+}
+
+int standin_hash(int hasher, const uint8_t* in, size_t len, uint8_t out[32])
+{
+    EVP_MD_CTX* m = EVP_MD_CTX_new();
+    int ok = m && ossl_hasher_init(m, hasher) && EVP_DigestUpdate(m, in, len) == 1 &&
+             EVP_DigestFinal(m, out, NULL) == 1;
+    EVP_MD_CTX_free(m);
+    return ok ? 0 : -1;
+}
+
+typedef struct {
+    int hasher, width, fail;
+    const uint8_t* in;
+    size_t nin;
+    uint8_t* out;
+} level_job;
+
+/* calculateLevelHashes (Merkle.h:243-261): one hasher per range, node i = H(in[i*w] .. in[i*w+w-1]) */
+static void level_range(void* p, size_t lo, size_t hi)
+{
+    level_job* j = (level_job*)p;
+    EVP_MD_CTX* m = EVP_MD_CTX_new();
+    for (size_t i = lo; i < hi; ++i) {
+        const size_t a = i * (size_t)j->width, b = a + (size_t)j->width < j->nin ? a + (size_t)j->width : j->nin;
+        if (!m || !ossl_hasher_init(m, j->hasher) || EVP_DigestUpdate(m, j->in + 32 * a, 32 * (b - a)) != 1 ||
+            EVP_DigestFinal(m, j->out + 32 * i, NULL) != 1)
+            j->fail = 1;
+    }
+    EVP_MD_CTX_free(m);
+}
+
+/* Merkle<H, width>::generateMerkle's root over n 32-byte leaves on nthreads threads (levels in
+ * sequence, each level's nodes in parallel).  Returns 0, or -1 (n == 0 / OpenSSL layout mismatch). */
+int standin_merkle_root(int hasher, int width, const uint8_t* leaves, size_t n, uint8_t root[32], int nthreads)
+{
+    if (n == 0 || width < 2) return -1;
+    if (n == 1) {
+        memcpy(root, leaves, 32);
+        return 0;
+    }
+    size_t cap = (n + (size_t)width - 1) / (size_t)width;
+    uint8_t* a = (uint8_t*)malloc(32 * cap);
+    uint8_t* b = (uint8_t*)malloc(32 * cap);
+    int rc = a && b ? 0 : -1;
+    const uint8_t* in = leaves;
+    size_t nin = n;
+    uint8_t* out = a;
+    while (!rc && nin > 1) {
+        const size_t nout = (nin + (size_t)width - 1) / (size_t)width;
+        level_job j = {hasher, width, 0, in, nin, out};
+        oracle_parallel_for(nout, nthreads, level_range, &j);
+        if (j.fail) rc = -1;
+        in = out;
+        nin = nout;
+        out = out == a ? b : a;
+    }
+    if (!rc) memcpy(root, in, 32);
+    free(a);
+    free(b);
+    return rc;
 }

@@ -90,11 +90,12 @@ public:
     using UniquePtr = std::unique_ptr<KeyPairInterface>;
     virtual ~KeyPairInterface() {}
 };
-class Hash
+class Hash  // interfaces/crypto/Hash.h:37-44
 {
 public:
     using Ptr = std::shared_ptr<Hash>;
     virtual ~Hash() {}
+    virtual HashType hash(bytesConstRef _data) = 0;
 };
 
 class SignatureCrypto

@@ -3,6 +3,7 @@
 #pragma once
 #include <bcos-crypto/signature/Exceptions.h>
 #include <bcos-crypto/signature/key/KeyImpl.h>
+#include <bcos-crypto/signature/sm2/SM2KeyPair.h>
 #include <wedpr-crypto/WedprCrypto.h>
 #include <functional>
 namespace bcos
@@ -50,7 +51,30 @@ public:
     {
         throw SignException() << errinfo_comment("host-side (wedpr) in the reference");
     }
-    std::pair<bool, bytes> recoverAddress(Hash::Ptr, bytesConstRef) const override { return {false, {}}; }
+    // SM2Crypto.cpp:94-122: input = hash || pub || r || s; verify (the virtual) against pub, then
+    // calculateAddress = right160(H(pub)); any exception -> {false, {}}
+    std::pair<bool, bytes> recoverAddress(Hash::Ptr _hashImpl, bytesConstRef _input) const override
+    {
+        byte in[160] = {0};
+        std::memcpy(in, _input.data(), _input.size() < 160 ? _input.size() : 160);
+        HashType h;
+        std::memcpy(h.data(), in, 32);
+        bytes sig(in + 96, in + 160);
+        sig.insert(sig.end(), in + 32, in + 96);
+        try
+        {
+            auto pub = std::make_shared<KeyImpl>(64, std::make_shared<const bytes>(in + 32, in + 96));
+            if (verify(pub, h, bytesConstRef(sig)))
+            {
+                auto d = _hashImpl->hash(bytesConstRef(pub->data()));
+                return {true, bytes(d.data() + 12, d.data() + 32)};
+            }
+        }
+        catch (const std::exception&)
+        {
+        }
+        return {false, {}};
+    }
     KeyPairInterface::UniquePtr createKeyPair(SecretPtr) const override
     {
         throw SignException() << errinfo_comment("host-side (wedpr) in the reference");

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 
 using namespace bcos;
 using namespace bcos::crypto;
@@ -40,6 +41,39 @@ static bool throws_invalid(F&& f) {
     }
     return false;
 }
+// an engine error must surface as SignException, never as InvalidSignature
+template <class F>
+static bool throws_sign_exception(F&& f) {
+    try {
+        f();
+    } catch (const InvalidSignature&) {
+        return false;
+    } catch (const SignException&) {
+        return true;
+    }
+    return false;
+}
+
+// Hash::hash over the engine's Keccak256 (the Hash::Ptr that recoverAddress takes)
+struct GpuKeccak : Hash {
+    HashType hash(bytesConstRef d) override {
+        HashType h;
+        uint64_t off[2] = {0, d.size()};
+        static const uint8_t zero = 0;
+        if (bcosgpu_keccak256_batch(d.size() ? d.data() : &zero, off, 1, h.data()) != 0) throw SignException();
+        return h;
+    }
+};
+
+// exposes SM2Crypto::m_verifier (SM2Crypto.h:64-65)
+struct SM2Probe : bcosgpu::ref::GpuSM2Crypto {
+    using bcosgpu::ref::GpuSM2Crypto::GpuSM2Crypto;
+    int8_t callVerifier(const bytes& pub, const HashType& h, const bytes& sig) const {
+        CInputBuffer p{(const char*)pub.data(), pub.size()}, hh{(const char*)h.data(), 32},
+            s{(const char*)sig.data(), 64};
+        return m_verifier(&p, &hh, &s);
+    }
+};
 
 int main() {
     if (bcosgpu_device_count() <= 0) {
@@ -67,7 +101,26 @@ int main() {
                                      0x46, 0x9b, 0xd3, 0x6b, 0xa5, 0x01, 0xf2, 0x8b, 0x69, 0x9d};
     CHECK(std::memcmp(d + 12, want, 20) == 0);
     CHECK(k1.verify(pub, mh, bytesConstRef(sig)));  // known-key verify (Secp256k1Crypto.cpp:51-63)
+    // the bytes overload: the reference calls the free secp256k1Verify (Secp256k1Crypto.cpp:126-131),
+    // which the mirror makes throw -- so this passes only through the adapter's own override
     CHECK(k1.verify(std::make_shared<const bytes>(pub->data()), mh, bytesConstRef(sig)));
+    CHECK(!k1.verify(std::make_shared<const bytes>(pub->data()), hash_of(
+        "48bed44d1bcd124a28c27f343a817e5f5243190d3c52bf347daf876de1dbbf77"), bytesConstRef(sig)));
+    // recoverAddress (Secp256k1Crypto.cpp:95-124): hash || v || r || s, v = 27 / 28
+    auto keccak = std::make_shared<GpuKeccak>();
+    {
+        bytes in(128, 0);
+        std::memcpy(in.data(), mh.data(), 32);
+        in[63] = 27;
+        std::memcpy(in.data() + 64, sig.data(), 64);
+        auto ra = k1.recoverAddress(keccak, bytesConstRef(in));
+        CHECK(ra.first && ra.second.size() == 20 && std::memcmp(ra.second.data(), want, 20) == 0);
+        in[63] = 29;
+        CHECK(!k1.recoverAddress(keccak, bytesConstRef(in)).first);
+        in[63] = 27;
+        in[40] = 1;  // v = 27 + 2^k is not 27
+        CHECK(!k1.recoverAddress(keccak, bytesConstRef(in)).first);
+    }
     // v = 4 must throw InvalidSignature (SignatureTest.cpp:156-162); a wrong length too
     bytes bad = sig;
     bad[64] = 4;
@@ -99,6 +152,55 @@ int main() {
     CHECK(throws_invalid([&] { s2.recover(mh, bytesConstRef(sm2sig)); }));  // wrong hash: SM2 rejects
     auto sb = sm2.recoverBatch({sm3abcd, sm3abcd}, {bytesConstRef(sm2sig), bytesConstRef(sm2bad)});
     CHECK(sb.size() == 2 && sb[0] && !sb[1]);
+    // the bytes overload (SM2Crypto.cpp:29-34) and recoverAddress (:94-122) reach the GPU through verify
+    bytes sm2pub(sm2sig.begin() + 64, sm2sig.end());
+    CHECK(s2.verify(std::make_shared<const bytes>(sm2pub), sm3abcd, bytesConstRef(sm2sig)));
+    CHECK(!s2.verify(std::make_shared<const bytes>(sm2pub), sm3abcd, bytesConstRef(sm2bad)));
+    {
+        bytes in(160, 0);
+        std::memcpy(in.data(), sm3abcd.data(), 32);
+        std::memcpy(in.data() + 32, sm2pub.data(), 64);
+        std::memcpy(in.data() + 96, sm2sig.data(), 64);
+        auto ra = s2.recoverAddress(keccak, bytesConstRef(in));
+        HashType kp = keccak->hash(bytesConstRef(sm2pub));
+        CHECK(ra.first && ra.second.size() == 20 && std::memcmp(ra.second.data(), kp.data() + 12, 20) == 0);
+        in[100] ^= 1;
+        CHECK(!s2.recoverAddress(keccak, bytesConstRef(in)).first);
+    }
+    // the wedpr-shaped m_verifier: WEDPR_SUCCESS / WEDPR_ERROR
+    SM2Probe probe(0);
+    CHECK(probe.callVerifier(sm2pub, sm3abcd, sm2sig) == WEDPR_SUCCESS);
+    CHECK(probe.callVerifier(sm2pub, sm3abcd, sm2bad) == WEDPR_ERROR);
+
+    // calls from another thread run on the object's device without any per-thread setup
+    {
+        bool okThread = false;
+        std::thread t([&] { okThread = k1.recover(mh, bytesConstRef(sig))->data() == pub->data() &&
+                                       s2.recover(sm3abcd, bytesConstRef(sm2sig)) != nullptr; });
+        t.join();
+        CHECK(okThread);
+    }
+
+    // injected engine failure (a device index the engine rejects): SignException on both suites, from
+    // every entry point, never InvalidSignature (TxValidator.cpp:54-61 would reject the tx); the
+    // wedpr-shaped verifier returns BCOSGPU_WEDPR_ENGINE_ERROR
+    {
+        bcosgpu::ref::GpuSecp256k1Crypto badK1(64);
+        bcosgpu::ref::GpuSM2Crypto badSm2(64);
+        SignatureCrypto& bk = badK1;
+        SignatureCrypto& bs = badSm2;
+        CHECK(throws_sign_exception([&] { bk.recover(mh, bytesConstRef(sig)); }));
+        CHECK(throws_sign_exception([&] { bk.verify(pub, mh, bytesConstRef(sig)); }));
+        CHECK(throws_sign_exception([&] { bk.verify(std::make_shared<const bytes>(pub->data()), mh, bytesConstRef(sig)); }));
+        CHECK(throws_sign_exception([&] { badK1.recoverBatch({mh}, {bytesConstRef(sig)}); }));
+        CHECK(throws_sign_exception([&] { bs.recover(sm3abcd, bytesConstRef(sm2sig)); }));
+        CHECK(throws_sign_exception([&] { bs.verify(sp, sm3abcd, bytesConstRef(sm2sig)); }));
+        CHECK(throws_sign_exception([&] { badSm2.recoverBatch({sm3abcd}, {bytesConstRef(sm2sig)}); }));
+        SM2Probe badProbe(64);
+        CHECK(badProbe.callVerifier(sm2pub, sm3abcd, sm2sig) == BCOSGPU_WEDPR_ENGINE_ERROR);
+        uint8_t out64[64];
+        CHECK(bcosgpu_secp256k1_recover(64, mh.data(), sig.data(), 65, out64) < 0);
+    }
 
     printf(fails ? "sigcrypto_test: %d failures\n" : "sigcrypto_test: ok\n", fails);
     return fails ? 1 : 0;

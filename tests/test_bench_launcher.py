@@ -32,30 +32,37 @@ def test_world_size_mismatch_is_refused():
 
 
 def test_small_batch_choice_mirrors_library():
-    """bench.py's mirror of the library's automatic small-batch kernel choice (ecc_txv.hip
-    auto_small_kernel) uses the same latency ratios, and picks the measured-best kernel per size
-    (profiles/r02_small_sweep.json: 256 CUs)."""
+    """bench.py's mirror of the library's automatic kernel choice (ecc_txv.hip auto_kernel) uses the
+    same latency ratios, and picks the measured-best kernel per size (profiles/r02_small_sweep.json,
+    profiles/r03_occ_sweep.json when present: 256 CUs)."""
     import re
     src = open(os.path.join(ROOT, "fisco-bcos_amd", "csrc", "ecc_txv.hip")).read()
-    m = re.search(r"lat\[3\] = \{sm2 \? ([\d.]+) : ([\d.]+), sm2 \? ([\d.]+) : ([\d.]+), ([\d.]+)\}", src)
-    assert m, "auto_small_kernel latency table not found"
-    sm2_c = (float(m.group(1)), float(m.group(3)), float(m.group(5)))
-    secp_c = (float(m.group(2)), float(m.group(4)), float(m.group(5)))
+    m = re.search(r"lat\[4\] = \{sm2 \? ([\d.]+) : ([\d.]+), sm2 \? ([\d.]+) : ([\d.]+), "
+                  r"sm2 \? ([\d.]+) : ([\d.]+), ([\d.]+)\}", src)
+    assert m, "auto_kernel latency table not found"
+    sm2_c = tuple(float(m.group(i)) for i in (1, 3, 5, 7))
+    secp_c = tuple(float(m.group(i)) for i in (2, 4, 6, 7))
     bsrc = open(os.path.join(ROOT, "bench.py")).read()
-    mb = re.search(r"lat = \(([\d.]+), ([\d.]+), ([\d.]+)\) if suite == 1 else \(([\d.]+), ([\d.]+), ([\d.]+)\)", bsrc)
+    mb = re.search(r"lat = \(([\d.]+), ([\d.]+), ([\d.]+), ([\d.]+)\) if suite == 1 else "
+                   r"\(([\d.]+), ([\d.]+), ([\d.]+), ([\d.]+)\)", bsrc)
     assert mb, "bench mirror not found"
-    assert tuple(float(mb.group(i)) for i in (1, 2, 3)) == sm2_c
-    assert tuple(float(mb.group(i)) for i in (4, 5, 6)) == secp_c
+    assert tuple(float(mb.group(i)) for i in (1, 2, 3, 4)) == sm2_c
+    assert tuple(float(mb.group(i)) for i in (5, 6, 7, 8)) == secp_c
     ns = {"__name__": "bench_mirror", "__file__": os.path.join(ROOT, "bench.py")}
-    exec(bsrc[bsrc.index("def _auto_small_kernel"):bsrc.index("def _kernel_name")], ns)
-    pick = ns["_auto_small_kernel"]
-    sweep = json.load(open(os.path.join(ROOT, "profiles", "r02_small_sweep.json")))
-    names = {2: "trio", 1: "pair", 0: "occ2"}
-    for key, ms in sweep.items():
-        suite_name, n, variant = key.split("_")
-        if variant != "trio":
+    exec(bsrc[bsrc.index("def _auto_kernel"):bsrc.index("def _kernel_name")], ns)
+    pick = ns["_auto_kernel"]
+    names = {2: "trio", 1: "pair", 0: "occ1", -2: "occ2"}
+    for fname in ("r02_small_sweep.json", "r03_occ_sweep.json"):
+        path = os.path.join(ROOT, "profiles", fname)
+        if not os.path.exists(path):
             continue
-        suite, n = (1 if suite_name == "sm2" else 0), int(n)
-        best = min(sweep["%s_%d_%s" % (suite_name, n, v)] for v in ("trio", "pair", "occ1", "occ2"))
-        chosen = sweep["%s_%d_%s" % (suite_name, n, names[pick(suite, n, 256)])]
-        assert chosen <= best * 1.05, (key, chosen, best)
+        sweep = json.load(open(path))
+        for key in sweep:
+            suite_name, n, variant = key.split("_")
+            if variant != "occ1":
+                continue
+            suite, n = (1 if suite_name == "sm2" else 0), int(n)
+            cands = [v for v in ("trio", "pair", "occ1", "occ2") if "%s_%d_%s" % (suite_name, n, v) in sweep]
+            best = min(sweep["%s_%d_%s" % (suite_name, n, v)] for v in cands)
+            chosen = sweep["%s_%d_%s" % (suite_name, n, names[pick(suite, n, 256, n <= (1 << 16))])]
+            assert chosen <= best * 1.05, (key, chosen, best)

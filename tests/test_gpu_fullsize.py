@@ -94,3 +94,32 @@ def test_c5_64_blocks_x_20k(gpu, oracle):
     got = roots.cpu().numpy()
     for k in range(nb):
         assert got[k].tobytes() == oracle.merkle(oracle.KECCAK256, 2, want[0][k * per:(k + 1) * per]), k
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("suite", [0, 1])
+def test_c4_8gpu_shard_size(gpu, oracle, suite):
+    """One rank's C4 shard at world 8 (parallel.shard_plan: 125,952 txs, width^L-aligned): the size the
+    scaling run launches per GPU, where the rounds x latency rule picks the occupancy-2 one-lane kernel
+    (profiles/r03_occ_sweep.json: 1.71 vs 1.99 ms at occupancy 1).  Both suites against the oracle,
+    plus the SigIO recover / SM2-verify batch at the same size."""
+    import torch
+    from bcos_gpu import device, parallel, synth
+    n = 125_952
+    plan = parallel.gpu_sharded_tx_root(1_000_000, 8, 0, device.KECCAK256, 2, "cuda")
+    assert plan.local_range == (0, n)
+    b = synth.make_batch(suite, n, seed=0xC48 + suite)
+    th, snd, st = _verify(suite, b)
+    want = _oracle_verify(oracle, suite, b)
+    _check_all(th, snd, st, want, b, suite)
+    sigs = b.sig.view(n, b.sig_len)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    addr = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
+    if suite == 0:
+        pub = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
+        device.secp256k1_recover(th, sigs, pub, addr, ok)
+    else:
+        device.sm2_verify(th, sigs, addr, ok)
+    torch.cuda.synchronize()
+    assert np.array_equal(ok.cpu().numpy(), (want[2] == 0).astype(np.uint8))
+    assert np.array_equal(addr.cpu().numpy(), want[1])
