@@ -15,7 +15,7 @@ OK, E_ARG, E_HIP, E_NODEV, E_EMPTY = 0, -1, -2, -3, -4
 WEDPR_ENGINE_ERROR = -2
 KECCAK256, SM3 = 0, 1
 SUITE_SECP256K1, SUITE_SM2 = 0, 1
-MERKLE_NEW, MERKLE_OLD = 0, 1
+MERKLE_NEW, MERKLE_OLD, MERKLE_NEW_BYTES = 0, 1, 2
 
 
 class BcosGpuError(RuntimeError):
@@ -45,6 +45,8 @@ _SIGS = {
     "bcosgpu_hash_batch_dev": (_I, [_I, _P, _P, _SZ, _P, _P]),
     "bcosgpu_merkle_root": (_I, [_I, _I, _I, _P, _SZ, _P, _P]),
     "bcosgpu_merkle_root_dev": (_I, [_I, _I, _P, _SZ, _P, _P, _P]),
+    "bcosgpu_merkle_bytes_size": (ctypes.c_uint64, [ctypes.c_uint64, _I]),
+    "bcosgpu_merkle_tree_bytes_dev": (_I, [_I, _P, _SZ, _P, _P]),
     "bcosgpu_merkle_frontier_dev": (_I, [_I, _I, _P, _SZ, _I, _P, _P, _P]),
     "bcosgpu_merkle_roots_work_size": (ctypes.c_uint64, [ctypes.c_uint64, _SZ, _I]),
     "bcosgpu_merkle_roots_batch": (_I, [_I, _I, _P, _P, _SZ, _P]),

@@ -104,6 +104,22 @@ class Merkle:
                                         _ptr(root), _ptr(levels)))
         return [levels[i].tobytes() for i in range(size)]
 
+    def generate_merkle_bytes(self, origin_hashes):
+        """generateMerkle into a std::vector<bytes> (BlockImpl's transactionsMerkle, BlockImpl.h:136;
+        merkleBench.cpp:53-56): a list of entries, 4-byte count records and 32-byte nodes
+        (bcosgpu_merkle_root with BCOSGPU_MERKLE_NEW_BYTES)."""
+        leaves = _u8(b"".join(bytes(h) for h in origin_hashes)).reshape(-1, 32)
+        n = leaves.shape[0]
+        if n == 0:
+            raise ValueError("Empty input")
+        ensure_device()
+        size = int(lib().bcosgpu_merkle_bytes_size(n, self.width))
+        flat = np.zeros(size, dtype=np.uint8)
+        root = np.zeros(32, dtype=np.uint8)
+        check(lib().bcosgpu_merkle_root(self.hasher.kind, self.width, _lib.MERKLE_NEW_BYTES, _ptr(leaves), n,
+                                        _ptr(root), _ptr(flat)))
+        return split_merkle_bytes(flat.tobytes(), n)
+
     def root(self, leaves):
         """Root only (last element of generateMerkle's output); leaves: uint8[n,32] or list of bytes."""
         leaves = _u8(b"".join(bytes(h) for h in leaves) if isinstance(leaves, list) else leaves).reshape(-1, 32)
@@ -186,6 +202,22 @@ class Merkle:
 
     def verify_merkle_proof(self, proof, h, root):
         return bool(self.verify_merkle_proofs([proof], [bytes(h)], bytes(root))[0])
+
+
+def split_merkle_bytes(flat: bytes, n: int):
+    """The packed vector<bytes> layout -> its entries: each count record (4 bytes, big-endian) is
+    followed by that many 32-byte nodes; n == 1 is the single 32-byte leaf."""
+    if n == 1:
+        return [flat[:32]]
+    out, at = [], 0
+    while at < len(flat):
+        cnt = int.from_bytes(flat[at:at + 4], "big")
+        out.append(flat[at:at + 4])
+        at += 4
+        for _ in range(cnt):
+            out.append(flat[at:at + 32])
+            at += 32
+    return out
 
 
 def calculate_merkle_proof_root(hasher: Hash, leaves) -> bytes:

@@ -221,10 +221,25 @@ int bcosgpu_merkle_root_dev(int hasher, int width, const uint8_t* d_leaves32, si
     return rc ? hip_err(hipGetLastError(), "merkle launch") : 0;
 }
 
+uint64_t bcosgpu_merkle_bytes_size(uint64_t n, int width) {
+    if (width < 2 || n == 0) return 0;
+    return n == 1 ? 32 : 32 * merkle_size(n, width) - 28 * merkle_levels(n, width);
+}
+
+int bcosgpu_merkle_tree_bytes_dev(int width, const uint8_t* d_tree, size_t n, uint8_t* d_out, void* stream) {
+    if (width < 2 || width > 64) return set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
+    if (n == 0) return set_err(BCOSGPU_E_EMPTY, "Empty input");
+    if (!d_tree || !d_out) return set_err(BCOSGPU_E_ARG, "null pointer");
+    int rc = launch_merkle_compact(d_tree, n, width, d_out, as_stream(stream));
+    return rc ? hip_err(hipGetLastError(), "merkle compact launch") : 0;
+}
+
 int bcosgpu_merkle_root(int hasher, int width, int variant, const uint8_t* leaves32, size_t n,
                         uint8_t* root32, uint8_t* levels) {
     if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
     if (!root32 || (n && !leaves32)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    const bool bytes_layout = variant == BCOSGPU_MERKLE_NEW_BYTES;
+    if (bytes_layout) variant = BCOSGPU_MERKLE_NEW;
     if (variant == BCOSGPU_MERKLE_NEW) {
         if (n == 0) return set_err(BCOSGPU_E_EMPTY, "Empty input");
         if (width < 2 || width > 64) return set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
@@ -239,14 +254,19 @@ int bcosgpu_merkle_root(int hasher, int width, int variant, const uint8_t* leave
     HIP_OK(w->b[0].ensure(n * 32 + 32));
     HIP_OK(w->b[1].ensure(tree * 32 + 32));
     HIP_OK(w->b[2].ensure(32));
+    if (levels && bytes_layout) HIP_OK(w->b[3].ensure(tree * 32 + 32));
     if (n) HIP_OK(hipMemcpyAsync(w->b[0].p, leaves32, n * 32, hipMemcpyHostToDevice, w->stream));
     if (variant == BCOSGPU_MERKLE_NEW)
         rc = launch_merkle(hasher, width, w->b[0].as<uint8_t>(), n, w->b[1].as<uint8_t>(), w->b[2].as<uint8_t>(), w->stream);
     else
         rc = launch_merkle_old(hasher, w->b[0].as<uint8_t>(), n, w->b[1].as<uint8_t>(), w->b[2].as<uint8_t>(), w->stream);
+    if (!rc && levels && bytes_layout)
+        rc = launch_merkle_compact(w->b[1].as<uint8_t>(), n, width, w->b[3].as<uint8_t>(), w->stream);
     if (rc) return rc == BCOSGPU_E_ARG ? set_err(rc, "bad merkle arguments") : hip_err(hipGetLastError(), "merkle launch");
     HIP_OK(hipMemcpyAsync(root32, w->b[2].p, 32, hipMemcpyDeviceToHost, w->stream));
-    if (levels && variant == BCOSGPU_MERKLE_NEW)
+    if (levels && bytes_layout)
+        HIP_OK(hipMemcpyAsync(levels, w->b[3].p, bcosgpu_merkle_bytes_size(n, width), hipMemcpyDeviceToHost, w->stream));
+    else if (levels && variant == BCOSGPU_MERKLE_NEW)
         HIP_OK(hipMemcpyAsync(levels, w->b[1].p, tree * 32, hipMemcpyDeviceToHost, w->stream));
     HIP_OK(hipStreamSynchronize(w->stream));
     return 0;

@@ -26,6 +26,9 @@ int launch_merkle_verify(int hasher, const uint8_t* d_proofs, uint64_t stride, c
                          hipStream_t st);
 int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* d_scratch,
                       uint8_t* d_root, hipStream_t st);
+uint64_t merkle_levels(uint64_t n, int width);
+// the output vector -> the packed vector<bytes> layout (4-byte count records)
+int launch_merkle_compact(const uint8_t* d_tree, uint64_t n, int width, uint8_t* d_out, hipStream_t st);
 
 // ecc_kernels.hip
 int ecc_init_tables(int device, int small_tables);

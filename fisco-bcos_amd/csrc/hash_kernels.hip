@@ -620,3 +620,55 @@ int launch_merkle_old(int hasher, const uint8_t* d_leaves, uint64_t n, uint8_t* 
 }
 
 }  // namespace bcosgpu
+
+namespace bcosgpu {
+// ------------------------------------------------------------------ the vector<bytes> tree layout
+// BlockImpl::calculateTransactionRoot stores the tree in m_inner->transactionsMerkle, a
+// vector<vector<char>> (BlockImpl.h:136, tars field 9), and merkleBench fills a vector<bytes>
+// (merkleBench.cpp:53-56): there setNumberToHash's resizeTo(output, 4) (Merkle.h:213-217,
+// concepts/bcos-concepts/Basic.h:50-61) leaves every count record a 4-byte entry, while the nodes are
+// 32 bytes.  This moves the 32-byte-entry output vector into that layout, packed: entry e goes to byte
+// 32 e - 28 c(e), c(e) = count records before it, and count records keep their bytes 0..3.
+uint64_t merkle_levels(uint64_t n, int width) {
+    uint64_t levels = 0;
+    while (n > 1) {
+        n = (n + width - 1) / width;
+        ++levels;
+    }
+    return levels;
+}
+
+__global__ __launch_bounds__(256) void merkle_compact_kernel(const uint32_t* __restrict__ tree, uint64_t entries,
+                                                             uint64_t n, int width, uint32_t* __restrict__ out) {
+    const uint64_t e = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= entries) return;
+    uint64_t pos = 0, m = n, before = 0;
+    bool record = false;
+    while (m > 1) {
+        m = (m + width - 1) / width;
+        if (e == pos) {
+            record = true;
+            break;
+        }
+        ++before;
+        if (e <= pos + m) break;
+        pos += m + 1;
+    }
+    const uint32_t* src = tree + 8 * e;
+    uint32_t* dst = out + 8 * e - 7 * before;
+    if (record) {
+        dst[0] = src[0];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) dst[k] = src[k];
+    }
+}
+
+int launch_merkle_compact(const uint8_t* d_tree, uint64_t n, int width, uint8_t* d_out, hipStream_t st) {
+    const uint64_t entries = n == 1 ? 1 : merkle_size(n, width);
+    if (entries == 0) return 0;
+    hipLaunchKernelGGL(merkle_compact_kernel, dim3(static_cast<unsigned>((entries + 255) / 256)), dim3(256), 0, st,
+                       reinterpret_cast<const uint32_t*>(d_tree), entries, n, width, reinterpret_cast<uint32_t*>(d_out));
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+}  // namespace bcosgpu

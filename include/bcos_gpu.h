@@ -56,6 +56,7 @@ extern "C" {
 /* Merkle variants */
 #define BCOSGPU_MERKLE_NEW 0 /* Merkle<H,width>::generateMerkle (Merkle.h:170-208) */
 #define BCOSGPU_MERKLE_OLD 1 /* calculateMerkleProofRoot, width 16 (ParallelMerkleProof.cpp:32-69) */
+#define BCOSGPU_MERKLE_NEW_BYTES 2 /* NEW, with `levels` in the vector<bytes> layout (bcosgpu_merkle_bytes_size) */
 
 int bcosgpu_version(void);
 /* Number of visible HIP devices (0 when none). */
@@ -94,12 +95,25 @@ int bcosgpu_hash_batch_dev(int hasher, const uint8_t* d_data, const uint64_t* d_
 /* root32 receives the root; levels (nullable) receives bcosgpu_merkle_size(n,width) x 32 bytes laid
  * out as the reference's output vector: per level a count record (uint32 big-endian in bytes 0..3,
  * zero elsewhere) followed by the level's nodes; for n == 1 the single leaf.  variant OLD ignores
- * width (always 16) and levels; n == 0 returns H("") for OLD and BCOSGPU_E_EMPTY for NEW. */
+ * width (always 16) and levels; n == 0 returns H("") for OLD and BCOSGPU_E_EMPTY for NEW.
+ * Variant NEW_BYTES: as NEW, with levels in the packed vector<bytes> layout (below). */
 int bcosgpu_merkle_root(int hasher, int width, int variant, const uint8_t* leaves32, size_t n,
                         uint8_t* root32, uint8_t* levels);
 /* d_tree must hold bcosgpu_merkle_size(n,width) x 32 bytes (>= 32 for n == 1). */
 int bcosgpu_merkle_root_dev(int hasher, int width, const uint8_t* d_leaves32, size_t n,
                             uint8_t* d_tree, uint8_t* d_root32, void* stream);
+/* The stored-tree layout of BlockImpl (m_inner->transactionsMerkle, a vector<vector<char>>,
+ * BlockImpl.h:136) and merkleBench (vector<bytes>, merkleBench.cpp:53-56): generateMerkle into a
+ * vector of byte buffers leaves each count record a 4-byte entry (setNumberToHash -> resizeTo(out, 4),
+ * Merkle.h:213-217, concepts/bcos-concepts/Basic.h:50-61) and each node a 32-byte one.  Packed: the
+ * entries back to back, count record (BE u32, 4 bytes) then that level's nodes (32 bytes each);
+ * bcosgpu_merkle_bytes_size(n, width) bytes (32 for n == 1).  The 32-byte-entry layout above is the
+ * one of fixed-size HashType vectors (Ledger proofs, LedgerTypeDef.h:27).
+ * bcosgpu_merkle_tree_bytes_dev converts an output vector d_tree (of bcosgpu_merkle_root_dev for the
+ * same n, width) into that layout at d_out (4-byte aligned, not overlapping d_tree);
+ * bcosgpu_merkle_root(..., BCOSGPU_MERKLE_NEW_BYTES, ..., levels) returns it directly. */
+uint64_t bcosgpu_merkle_bytes_size(uint64_t n, int width);
+int bcosgpu_merkle_tree_bytes_dev(int width, const uint8_t* d_tree, size_t n, uint8_t* d_out, void* stream);
 
 /* Multi-GPU tx root: compute `levels` levels of the reference tree over one shard of leaves.  The
  * shard's first global leaf index must be a multiple of width^levels; then its ceil(n / width^levels)

@@ -18,6 +18,7 @@
  */
 #ifndef BCOS_GPU_HPP
 #define BCOS_GPU_HPP
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <stdexcept>
@@ -144,6 +145,35 @@ public:
         HashType root{};
         check(bcosgpu_merkle_root(HASHER, static_cast<int>(width), BCOSGPU_MERKLE_NEW, originHashes[0].data(),
                                   originHashes.size(), root.data(), out[0].data()));
+    }
+    /* generateMerkle into a vector of byte buffers -- BlockImpl's m_inner->transactionsMerkle
+     * (vector<vector<char>>, BlockImpl.h:136) and merkleBench's vector<bytes> (merkleBench.cpp:53-56):
+     * count records are 4-byte entries (Merkle.h:213-217 resizeTo(output, 4)), nodes 32 bytes.
+     * Bytes = any resizable byte container (std::vector<char>, std::vector<uint8_t>, bcos::bytes). */
+    template <class Bytes>
+    void generateMerkle(const std::vector<HashType>& originHashes, std::vector<Bytes>& out) const {
+        if (originHashes.empty()) throw std::invalid_argument("Empty input");
+        const size_t n = originHashes.size();
+        std::vector<uint8_t> flat(bcosgpu_merkle_bytes_size(n, static_cast<int>(width)));
+        HashType root{};
+        check(bcosgpu_merkle_root(HASHER, static_cast<int>(width), BCOSGPU_MERKLE_NEW_BYTES, originHashes[0].data(), n,
+                                  root.data(), flat.data()));
+        out.clear();
+        auto put = [&out](const uint8_t* p, size_t len) {
+            out.emplace_back(len);
+            std::copy(p, p + len, reinterpret_cast<uint8_t*>(&out.back()[0]));
+        };
+        if (n == 1) {
+            put(flat.data(), 32);
+            return;
+        }
+        for (size_t at = 0; at < flat.size();) {
+            const uint32_t cnt = (uint32_t(flat[at]) << 24) | (uint32_t(flat[at + 1]) << 16) |
+                                 (uint32_t(flat[at + 2]) << 8) | uint32_t(flat[at + 3]);
+            put(flat.data() + at, 4);
+            at += 4;
+            for (uint32_t k = 0; k < cnt; ++k, at += 32) put(flat.data() + at, 32);
+        }
     }
     /* generateMerkleProof(originHashes, index, out) (Merkle.h:121-168): out is replaced (the reference
      * appends to a caller-cleared vector); index out of range throws std::invalid_argument */

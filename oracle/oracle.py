@@ -96,6 +96,29 @@ def merkle(hasher, width, leaves, want_tree=False, nthreads=1):
     return (root.raw, tree) if want_tree else root.raw
 
 
+def merkle_bytes_vector(hasher, width, leaves):
+    """generateMerkle(originHashes, out) into a FRESH std::vector<bytes> -- BlockImpl's
+    m_inner->transactionsMerkle (BlockImpl.h:136) and merkleBench's output (merkleBench.cpp:53-56):
+    resizeTo(out, merkleNodes) appends empty buffers (Merkle.h:185-186, concepts/bcos-concepts/Basic.h:50-61),
+    setNumberToHash's resizeTo(output, 4) makes each count record 4 bytes (Merkle.h:213-217), and
+    hasher.final resizes each node to 32 (OpenSSLHasher.h:97-99); n == 1 is the single leaf
+    (Merkle.h:177-182).  Pure Python over the C hashes: small inputs only."""
+    leaves = np.ascontiguousarray(leaves, dtype=np.uint8).reshape(-1, 32)
+    n = leaves.shape[0]
+    if n == 0:
+        raise ValueError("Empty input")
+    h = keccak256 if hasher == KECCAK256 else sm3
+    if n == 1:
+        return [leaves[0].tobytes()]
+    out, level = [], [leaves[i].tobytes() for i in range(n)]
+    while len(level) > 1:
+        nxt = [h(b"".join(level[i:i + width])) for i in range(0, len(level), width)]
+        out.append(len(nxt).to_bytes(4, "big"))
+        out.extend(nxt)
+        level = nxt
+    return out
+
+
 def merkle_old(hasher, leaves):
     leaves = np.ascontiguousarray(leaves, dtype=np.uint8).reshape(-1, 32)
     root = ctypes.create_string_buffer(32)

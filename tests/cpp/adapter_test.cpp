@@ -82,6 +82,18 @@ int main() {
     threw = false;
     try { GpuMerkle<BCOSGPU_SM3, 16>().generateMerkle({}, out); } catch (const std::invalid_argument&) { threw = true; }
     CHECK(threw);
+    // the same tree as merkleBench stores it (vector<bytes>, merkleBench.cpp:53-56): 4-byte count records
+    std::vector<std::vector<char>> vb;
+    GpuMerkle<BCOSGPU_SM3, 16>().generateMerkle(leaves, vb);
+    CHECK(vb.size() == out.size());
+    for (size_t i = 0; i < vb.size() && i < out.size(); ++i) {
+        const bool record = i == 0 || i == 3;  // [count 2][2 nodes][count 1][root]
+        CHECK(vb[i].size() == (record ? 4u : 32u));
+        CHECK(std::memcmp(vb[i].data(), out[i].data(), vb[i].size()) == 0);
+    }
+    std::vector<bytes> one;
+    GpuMerkle<BCOSGPU_KECCAK256, 2>().generateMerkle({leaves[0]}, one);
+    CHECK(one.size() == 1 && one[0].size() == 32 && std::memcmp(one[0].data(), leaves[0].data(), 32) == 0);
     // Merkle proofs (testMerkle.cpp:91-121): every leaf verifies, a zero hash does not, empty proof throws
     GpuMerkle<BCOSGPU_SM3, 16> m16;
     for (uint64_t i = 0; i < leaves.size(); ++i) {

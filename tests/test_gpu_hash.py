@@ -126,3 +126,34 @@ def test_device_api_torch(gpu, oracle):
     device.merkle_root(device.KECCAK256, 2, leaves, tree, root)
     torch.cuda.synchronize()
     assert root.cpu().numpy().tobytes() == oracle.merkle(0, 2, d_out.cpu().numpy())
+
+
+@pytest.mark.parametrize("hasher", [0, 1])
+def test_merkle_bytes_layout_vs_oracle(gpu, oracle, hasher):
+    """BlockImpl's stored tree (vector<vector<char>>, BlockImpl.h:136) and merkleBench's vector<bytes>
+    (merkleBench.cpp:53-56): 4-byte count records, 32-byte nodes -- through the host ABI
+    (BCOSGPU_MERKLE_NEW_BYTES) and the device conversion (bcosgpu_merkle_tree_bytes_dev), against the
+    restatement of Merkle.h:213-217 + Basic.h:50-61; the 32-byte-entry layout of the same call stays the
+    fixed-size HashType one (LedgerTypeDef.h:27)."""
+    import torch
+    import bcos_gpu
+    from bcos_gpu import device
+    hs = gpu.Keccak256() if hasher == 0 else gpu.SM3()
+    rng = np.random.default_rng(90 + hasher)
+    for width in (2, 3, 16):
+        for n in (1, 2, 3, 16, 17, 257, 4097, 70000):
+            leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+            want = oracle.merkle_bytes_vector(hasher, width, leaves)
+            got = gpu.Merkle(hs, width).generate_merkle_bytes([leaves[i].tobytes() for i in range(n)])
+            assert got == want, (width, n)
+            d_leaves = torch.from_numpy(leaves).cuda()
+            tree = torch.empty((max(device.merkle_size(n, width), 1), 32), dtype=torch.uint8, device="cuda")
+            root = torch.empty(32, dtype=torch.uint8, device="cuda")
+            device.merkle_root(hasher, width, d_leaves, tree, root)
+            size = int(bcos_gpu.lib().bcosgpu_merkle_bytes_size(n, width))
+            flat = torch.zeros(size + 4, dtype=torch.uint8, device="cuda")
+            bcos_gpu.check(bcos_gpu.lib().bcosgpu_merkle_tree_bytes_dev(width, tree.data_ptr(), n, flat.data_ptr(),
+                                                                        torch.cuda.current_stream().cuda_stream))
+            torch.cuda.synchronize()
+            assert flat[:size].cpu().numpy().tobytes() == b"".join(want), (width, n)
+            assert int(flat[size:].sum()) == 0  # nothing written past the packed size

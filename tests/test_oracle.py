@@ -136,3 +136,24 @@ def test_merkle_proof_restatement(oracle):
                 oracle.merkle_proof(0, width, leaves, n)
             with pytest.raises(ValueError):
                 oracle.merkle_verify_proof(0, [], leaves[0].tobytes(), root)
+
+
+def test_merkle_bytes_vector_restatement(oracle):
+    """The vector<bytes> restatement (Merkle.h:170-217 with resizeTo, Basic.h:50-61) carries the same nodes
+    and root as the 32-byte-entry output vector; only the count records shrink to 4 bytes."""
+    import numpy as np
+    rng = np.random.default_rng(41)
+    for hasher in (oracle.KECCAK256, oracle.SM3):
+        for width in (2, 3, 16):
+            for n in (1, 2, 3, 17, 257, 1000):
+                leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+                ent = oracle.merkle_bytes_vector(hasher, width, leaves)
+                root, tree = oracle.merkle(hasher, width, leaves, want_tree=True)
+                assert ent[-1] == root and len(ent) == tree.shape[0]
+                for e, t in zip(ent, tree):
+                    assert e == (t.tobytes() if len(e) == 32 else t[:4].tobytes())
+                    assert len(e) == 32 or t[4:].tobytes() == bytes(28)
+                levels, m = 0, n
+                while m > 1:
+                    m, levels = -(-m // width), levels + 1
+                assert sum(len(e) == 4 for e in ent) == levels
