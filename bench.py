@@ -63,7 +63,7 @@ PEAK_ALU_PER_S = 3.7497e13      # full-rate 32-bit VALU (v_alignbit_b32)
 # SURVEY §8d ALU ops per permutation / compression
 KECCAK_F_OPS = 6240
 SM3_C_OPS = 2100
-PMC_GLOB = "r02_pmc_{}.json"
+PMC_GLOB = "r03_pmc_{}.json"
 KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_device.h", "fisco-bcos_amd/csrc/ecc_tables.hip", "fisco-bcos_amd/csrc/ecc_sig.hip",
               "fisco-bcos_amd/csrc/ecc_txv.hip", "fisco-bcos_amd/csrc/ecc_coop.hip", "fisco-bcos_amd/csrc/ecc_pair.hip",
               "fisco-bcos_amd/csrc/fe_asm.h", "fisco-bcos_amd/csrc/fe.h",

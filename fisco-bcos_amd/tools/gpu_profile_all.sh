@@ -1,5 +1,5 @@
 # rocprofv3 kernel-trace + PMC passes for every bench workload at the current tree, summarised into
-# gpurun_out/prof/r02_pmc_<wl>.json (copy into profiles/ to make bench.py's traffic cite them).
+# gpurun_out/prof/<round>_pmc_<wl>.json (copy into profiles/ to make bench.py's traffic cite them).
 # usage: bash fisco-bcos_amd/tools/gpu_profile_all.sh [workloads...]
 set -o pipefail
 mkdir -p gpurun_out/prof
@@ -10,8 +10,8 @@ for tag in $WLS; do
   [ $tag = c4comb8 ] && { wl=c4; envs="BCOSGPU_TABLES=small"; }
   case $wl in c2|c2sm2) st=30;; *) st=3;; esac
   env $envs bash fisco-bcos_amd/tools/gpu_profile.sh $wl $st 240 $tag || exit $?
-  python3 fisco-bcos_amd/tools/prof_summary.py gpurun_out/prof/r02_pmc_$tag.json gpurun_out/prof/$tag/trace \
+  python3 fisco-bcos_amd/tools/prof_summary.py gpurun_out/prof/${R:-r03}_pmc_$tag.json gpurun_out/prof/$tag/trace \
     gpurun_out/prof/$tag/fetch gpurun_out/prof/$tag/write gpurun_out/prof/$tag/sq gpurun_out/prof/$tag/valu || exit $?
-  cp $(find gpurun_out/prof/$tag/trace -name '*kernel_stats.csv' | head -1) gpurun_out/prof/r02_kernel_stats_$tag.csv
+  cp $(find gpurun_out/prof/$tag/trace -name '*kernel_stats.csv' | head -1) gpurun_out/prof/${R:-r03}_kernel_stats_$tag.csv
 done
 echo done
