@@ -357,7 +357,10 @@ def merkle_legs(cpu_threads):
                 torch.cuda.synchronize()
                 ms = a.elapsed_time(c) / reps
                 units, ops = merkle_work(n, width, h == device.KECCAK256)
+                floor = merkle_floor(n, width, h == device.KECCAK256)
                 rec = {"ms": ms, "GB_per_s": n * 32 / (ms * 1e-3) / 1e9, "reps": reps,
+                       "latency_floor_ms": floor["ms"] if floor else None,
+                       "frac_of_latency_floor": floor["ms"] / ms if floor else None, "latency_floor": floor,
                        "roofline": {"bound": "int-valu", "achieved": ops / (ms * 1e-3) / 1e12,
                                     "peak": PEAK_ALU_PER_S / 1e12, "unit": "Tops/s",
                                     "frac": ops / (ms * 1e-3) / PEAK_ALU_PER_S,
@@ -375,6 +378,33 @@ def merkle_legs(cpu_threads):
 
 def _count(n):
     return "%dk" % (n // 1000) if n < 1_000_000 else "%dM" % (n // 1_000_000)
+
+
+HASH_LATENCY = "r03_hash_latency.json"  # tools/keccakpair_check.hip on MI355X: cycles per unit, lone wave
+CLOCK_HZ = 2.4e9                        # MI355X peak engine clock (MI355X_MICROARCH.md)
+
+
+def merkle_floor(n, width, keccak):
+    """Serial-hash floor of Merkle<H,width> over n leaves (Merkle.h:243-261): each level waits for its
+    slowest node -- a full group of `width` children, or the level's whole input when smaller -- so the
+    critical path is the sum over levels of that node's Keccak-f permutations / SM3 compressions, times
+    the fastest measured per-unit latency of a lone wave (cooperative 25-lane Keccak-f; one-lane SM3)
+    at the peak clock.  No schedule of this hash on this GPU beats it."""
+    try:
+        with open(os.path.join(ROOT, "profiles", HASH_LATENCY)) as f:
+            lat = json.load(f)
+    except (OSError, ValueError):
+        return None
+    cyc = min(lat["cycles_per_perm_coop25"], lat["cycles_per_perm_pair"]) if keccak else lat["cycles_per_sm3_compression"]
+    units, m = 0, n
+    while m > 1:
+        k = min(width, m)
+        units += (32 * k // 136 + 1) if keccak else ((32 * k + 8) // 64 + 1)
+        m = -(-m // width)
+    return {"ms": units * cyc / CLOCK_HZ * 1e3, "serial_units": units, "cycles_per_unit": cyc,
+            "source": os.path.join("profiles", HASH_LATENCY),
+            "note": "critical-path %s x the measured lone-wave latency at %.1f GHz" % (
+                "Keccak-f permutations" if keccak else "SM3 compressions", CLOCK_HZ / 1e9)}
 
 
 def merkle_work(n, width, keccak):

@@ -399,6 +399,86 @@ struct KeccakCoop {
     }
 };
 
+// ------------------------------------------------------------------ lane-pair Keccak-256
+// One state over two adjacent lanes (2k, 2k + 1): the even lane holds the low 32-bit halves of the 25
+// 64-bit Keccak lanes, the odd lane the high halves.  theta's column parities, the theta XOR, chi and
+// iota are lane-local; a 64-bit rotation of a (lo, hi) pair is, in BOTH lanes, one v_alignbit of the
+// lane's own half and its partner's (rotl r < 32: alignbit(own, partner, 32 - r); r > 32:
+// alignbit(partner, own, 64 - r)), the partner half fetched by one DPP quad_perm swap.  A round is
+// ~120 VALU per lane (10 parity + 25 theta + 29 swaps + 29 alignbit + 25 chi + iota) against ~180 for a
+// whole state in one lane, with no LDS and no cross-row traffic, so a latency-bound hash (a Merkle
+// level with fewer nodes than the GPU has lanes) runs at two lanes per state.
+struct KeccakPair {
+    uint32_t odd;  // 0 on the even (low-half) lane, all-ones on the odd (high-half) lane
+    __device__ KeccakPair() : odd(0u - (__lane_id() & 1u)) {}
+    __device__ __forceinline__ static uint32_t partner(uint32_t v) {  // quad_perm [1, 0, 3, 2]
+        return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0xB1, 0xf, 0xf, false));
+    }
+    template <int R>
+    __device__ __forceinline__ static uint32_t rot(uint32_t own, uint32_t par) {
+        if constexpr (R == 0) return own;
+        else if constexpr (R < 32) return __builtin_amdgcn_alignbit(own, par, 32 - R);
+        else return __builtin_amdgcn_alignbit(par, own, 64 - R);
+    }
+    __device__ __forceinline__ void permute(uint32_t a[25]) const {
+#pragma unroll 1
+        for (int round = 0; round < 24; ++round) {
+            const uint64_t rc64 = kKeccakRC[round];
+            uint32_t c[5], e[5], t[25], b[25];
+#pragma unroll
+            for (int x = 0; x < 5; ++x) c[x] = xor3(xor3(a[x], a[x + 5], a[x + 10]), a[x + 15], a[x + 20]);
+#pragma unroll
+            for (int x = 0; x < 5; ++x) {
+                const uint32_t cx = c[(x + 1) % 5];
+                e[x] = rot<1>(cx, partner(cx));
+            }
+#pragma unroll
+            for (int i = 0; i < 25; ++i) t[i] = xor3(a[i], c[(i + 4) % 5], e[i % 5]);
+            // rho + pi: b[y + 5((2x + 3y) % 5)] = rotl(t[x + 5y], r[x][y])
+#define KP_RP(SRC, R, DST) b[DST] = rot<R>(t[SRC], R ? partner(t[SRC]) : 0u)
+            KP_RP(0, 0, 0);   KP_RP(1, 1, 10);  KP_RP(2, 62, 20); KP_RP(3, 28, 5);  KP_RP(4, 27, 15);
+            KP_RP(5, 36, 16); KP_RP(6, 44, 1);  KP_RP(7, 6, 11);  KP_RP(8, 55, 21); KP_RP(9, 20, 6);
+            KP_RP(10, 3, 7);  KP_RP(11, 10, 17); KP_RP(12, 43, 2); KP_RP(13, 25, 12); KP_RP(14, 39, 22);
+            KP_RP(15, 41, 23); KP_RP(16, 45, 8); KP_RP(17, 15, 18); KP_RP(18, 21, 3); KP_RP(19, 8, 13);
+            KP_RP(20, 18, 14); KP_RP(21, 2, 24); KP_RP(22, 61, 9); KP_RP(23, 56, 19); KP_RP(24, 14, 4);
+#undef KP_RP
+#pragma unroll
+            for (int y = 0; y < 25; y += 5) {
+#pragma unroll
+                for (int x = 0; x < 5; ++x) a[y + x] = chi32(b[y + x], b[y + (x + 1) % 5], b[y + (x + 2) % 5]);
+            }
+            const uint32_t rlo = static_cast<uint32_t>(rc64), rhi = static_cast<uint32_t>(rc64 >> 32);
+            a[0] ^= (rlo & ~odd) | (rhi & odd);
+        }
+    }
+    // Keccak-256 of msg[0..len) (len a multiple of 4, msg 4-byte aligned, global or LDS memory): the even lane absorbs the
+    // low word of every 8-byte block lane, the odd lane the high word.  Returns digest words 2j + half
+    // (half = this lane's) in d[j], j < 4.
+    __device__ __forceinline__ void hash(const uint8_t* msg, uint32_t len, uint32_t d[4]) const {
+        uint32_t a[25];
+#pragma unroll
+        for (int i = 0; i < 25; ++i) a[i] = 0;
+        const uint32_t half = odd & 1u;
+        const uint32_t nblocks = len / 136u + 1u;
+        const uint32_t padw = len >> 2, padb = (len & 3u) * 8u;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(msg);
+        const uint32_t nw = (len + 3u) >> 2;
+        for (uint32_t blk = 0; blk < nblocks; ++blk) {
+#pragma unroll
+            for (int j = 0; j < 17; ++j) {
+                const uint32_t wi = blk * 34u + 2u * j + half;
+                uint32_t v = wi < nw ? w[wi] : 0u;
+                if (wi == padw) v ^= 1u << padb;  // Keccak pad byte 0x01 (OpenSSLHasher.h:74-79)
+                a[j] ^= v;
+            }
+            if (blk + 1 == nblocks) a[16] ^= 0x80000000u & odd;  // final 0x80
+            permute(a);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = a[j];
+    }
+};
+
 // Store a 32-byte digest.  Keccak words are little-endian lanes (byte order == memory order);
 // SM3 words are big-endian.
 __device__ __forceinline__ void store_digest(int hasher, uint8_t* dst, const uint32_t d[8]) {

@@ -7,6 +7,9 @@
 //     (per-level calculateLevelHashes :243-261 -> merkle_level_kernel, one node per lane)
 //   protocol::calculateMerkleProofRoot    bcos-protocol/bcos-protocol/ParallelMerkleProof.cpp:32-69
 #include <cstdlib>
+#include <mutex>
+#include <utility>
+#include <vector>
 #include "hash_device.h"
 #include "engine.h"
 
@@ -151,17 +154,58 @@ __device__ __forceinline__ void coop_level_pass(const KeccakCoop& kc, const uint
     }
 }
 
+// One tree node per lane PAIR (KeccakPair): lanes 2j, 2j + 1 hash node j of a level (idle pairs on a
+// dummy input, so whole pairs stay in step); each lane writes its four digest words (2k + half) to
+// dst + 32 j (and dst2 + 32 j when non-null).
+__device__ __forceinline__ void pair_level_pass(const KeccakPair& kp, const uint8_t* in, uint64_t nin, uint32_t width,
+                                                uint64_t j, uint64_t nout, uint8_t* dst, uint8_t* dst2) {
+    const bool act = j < nout;
+    const uint64_t first = act ? j * width : 0;
+    const uint32_t c = act ? static_cast<uint32_t>(nin - first < width ? nin - first : width) : 1u;
+    uint32_t d[4];
+    kp.hash(in + 32ull * first, 32u * c, d);
+    if (act) {
+        const uint32_t half = __lane_id() & 1u;
+        uint32_t* o = reinterpret_cast<uint32_t*>(dst + 32ull * j) + half;
+        uint32_t* o2 = dst2 ? reinterpret_cast<uint32_t*>(dst2 + 32ull * j) + half : nullptr;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            o[2 * k] = d[k];
+            if (o2) o2[2 * k] = d[k];
+        }
+    }
+}
+
+// How a latency-bound Keccak level is hashed: 25 lanes per node while the level fits one node per
+// 32-lane group, two lanes per node while it fits one node per lane pair (and `pair` allows it),
+// else one lane per node.
+enum LevelMode : int { kOneLane = 0, kPair = 1, kCoop = 2 };
+template <int H>
+__device__ __forceinline__ int level_mode(uint64_t nout, uint32_t threads, int pair) {
+    if (H != KECCAK256) return kOneLane;
+    if (nout <= threads / 32) return kCoop;
+    if (pair && 2 * nout <= threads) return kPair;
+    return kOneLane;
+}
+
+// `pair`: level 1 (from the leaves) and the LDS levels may run on lane pairs (the host sets it when
+// the tree's level 1 leaves most of the GPU idle; a throughput-sized level 1 stays one lane per node,
+// which costs fewer instructions per node)
 template <int H, int W>
 __global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w, int kin,
                                                         int B, uint8_t* __restrict__ tree, const TreeLevels t,
-                                                        uint8_t* __restrict__ root) {
+                                                        uint8_t* __restrict__ root, int pair) {
     __shared__ uint4 lds[2][256][2];
     const uint32_t width = W ? W : static_cast<uint32_t>(w);
-    const uint32_t tid = threadIdx.x, groups = blockDim.x / 32;
+    const uint32_t tid = threadIdx.x;
     uint64_t base = static_cast<uint64_t>(blockIdx.x) * B;  // first level-1 node of this workgroup
     uint32_t nodes = static_cast<uint32_t>(t.cnt[0] - base < static_cast<uint64_t>(B) ? t.cnt[0] - base : B);
     uint32_t d[8];
-    if (tid < nodes) {
+    if (level_mode<H>(B, blockDim.x, pair) == kPair) {
+        const KeccakPair kp;
+        pair_level_pass(kp, leaves + 32ull * base * width, n - base * width, width, tid >> 1, nodes,
+                        tree + 32ull * (t.pos[0] + 1 + base), reinterpret_cast<uint8_t*>(&lds[0][0][0]));
+    } else if (tid < nodes) {
         const uint64_t first = (base + tid) * width;
         const uint32_t c = static_cast<uint32_t>(n - first < width ? n - first : width);
         hash_nodes<H>(leaves + 32ull * first, c, d);
@@ -175,11 +219,17 @@ __global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restric
         const uint64_t nbase = base / width;
         const uint32_t nn = (nodes + width - 1) / width;
         const uint8_t* in = reinterpret_cast<const uint8_t*>(&lds[cur][0][0]);
-        if (H == KECCAK256 && nn <= groups) {  // latency-bound level: 25 lanes per node
+        // (the mode is decided on the full group count B / width^l so every workgroup runs alike)
+        const int mode = level_mode<H>((B + width - 1) / width, blockDim.x, pair);
+        if (mode == kCoop) {  // latency-bound level: 25 lanes per node
             const KeccakCoop kc;
             const uint32_t g = tid / 32;
             coop_level_pass<W>(kc, in, nodes, width, g, nn, tree + 32ull * (t.pos[l] + 1 + nbase + g),
                                reinterpret_cast<uint8_t*>(&lds[cur ^ 1][g < 256 ? g : 0][0]));
+        } else if (mode == kPair) {
+            const KeccakPair kp;
+            pair_level_pass(kp, in, nodes, width, tid >> 1, nn, tree + 32ull * (t.pos[l] + 1 + nbase),
+                            reinterpret_cast<uint8_t*>(&lds[cur ^ 1][0][0]));
         } else if (tid < nn) {
             const uint32_t c = nodes - tid * width < width ? nodes - tid * width : width;
             hash_nodes<H>(in + 32u * tid * width, c, d);
@@ -189,6 +239,7 @@ __global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restric
         cur ^= 1;
         nodes = nn;
         base = nbase;
+        B = (B + width - 1) / width;
     }
     if (blockIdx.x == 0 && tid < static_cast<uint32_t>(t.nlev)) {  // count records (Merkle.h:189-204)
         uint32_t* e = reinterpret_cast<uint32_t*>(tree + 32ull * t.pos[tid]);
@@ -209,16 +260,19 @@ __global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restric
 // levels [l0, t.nlev) (0-based, level l0 - 1 already in the tree) in ONE workgroup; root copy
 template <int H, int W>
 __global__ __launch_bounds__(1024) void merkle_top_kernel(int w, int l0, uint8_t* __restrict__ tree, const TreeLevels t,
-                                                          uint8_t* __restrict__ root) {
+                                                          uint8_t* __restrict__ root, int pair) {
     const uint32_t width = W ? W : static_cast<uint32_t>(w);
-    const uint32_t groups = blockDim.x / 32;
     for (int l = l0; l < t.nlev; ++l) {
         const uint64_t nin = t.cnt[l - 1];
         const uint8_t* in = tree + 32ull * (t.pos[l - 1] + 1);
-        if (H == KECCAK256 && t.cnt[l] <= groups) {  // latency-bound level: 25 lanes per node
+        const int mode = level_mode<H>(t.cnt[l], blockDim.x, pair);
+        if (mode == kCoop) {  // latency-bound level: 25 lanes per node
             const KeccakCoop kc;
             const uint32_t g = threadIdx.x / 32;
             coop_level_pass<W>(kc, in, nin, width, g, t.cnt[l], tree + 32ull * (t.pos[l] + 1 + g), nullptr);
+        } else if (mode == kPair) {
+            const KeccakPair kp;
+            pair_level_pass(kp, in, nin, width, threadIdx.x >> 1, t.cnt[l], tree + 32ull * (t.pos[l] + 1), nullptr);
         } else {
             for (uint64_t j = threadIdx.x; j < t.cnt[l]; j += blockDim.x) {
                 const uint64_t first = j * width;
@@ -236,7 +290,220 @@ __global__ __launch_bounds__(1024) void merkle_top_kernel(int w, int l0, uint8_t
     }
 }
 
+// ------------------------------------------------------------------ latency-sized trees: one launch
+// At merkleBench sizes (100k leaves, width 16: 6,250 level-1 nodes) the tree is a chain of serial
+// permutations, and what costs is how many of them share a SIMD: the workgroup-per-256-nodes kernel
+// puts level 1 on 25 CUs at two waves per SIMD and the single-workgroup top kernel runs level 3's
+// 25 cooperative hashes at four waves per SIMD.  Here every wave is its own workgroup (one wave per
+// SIMD across the GPU): wave b hashes the S = width^a level-1 nodes under one level-(a+1) node (lane
+// pairs for Keccak, one lane per node for SM3), the levels above them inside the wave through LDS
+// (Keccak: pairs, then 25-lane groups for the last one or two nodes), and then climbs: it publishes
+// its node and bumps the arrival counter of the parent, and the wave that completes a parent's group
+// hashes the parent (one 25-lane group / one lane) and climbs on, up to the root.
+// Cross-wave hand-off without cache-wide fences: a published node is written with device-coherent
+// stores (agent-scope atomic stores: write-through past the per-XCD L2), the wave waits for them
+// (s_waitcnt) before its counter atomic, and the completing wave gathers the children with
+// device-coherent loads into LDS; the last arriver resets the counter, so the slot is clean for the
+// next launch on the stream.
+struct FusedTree {
+    TreeLevels t;
+    uint32_t ctr_off[64];  // first counter of level l (levels a + 1 .. nlev - 1)
+    int a;                 // levels above level 1 computed inside a wave (S = width^a)
+    uint32_t S;
+};
+
+__device__ __forceinline__ void st_dev(uint8_t* p, uint32_t v) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_dev(const uint8_t* p) {
+    return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// hash node j of a level from its children at `in` (nin of them) -- gathered into LDS `buf` with
+// device-coherent loads -- with one 25-lane group (Keccak; group 1 hashes a dummy copy) or lane 0
+// (SM3); publishes the digest at dst with device-coherent stores
+template <int H>
+__device__ __forceinline__ void fused_one_node(const uint8_t* in, uint64_t nin, uint32_t width, uint64_t j,
+                                               uint8_t* dst, uint8_t* buf) {
+    const uint64_t first = j * width;
+    const uint32_t c = static_cast<uint32_t>(nin - first < width ? nin - first : width);
+    const uint32_t lane = __lane_id();
+    for (uint32_t q = lane; q < 8u * c; q += 64u)
+        reinterpret_cast<uint32_t*>(buf)[q] = ld_dev(in + 32ull * first + 4u * q);
+    __syncthreads();
+    if constexpr (H == KECCAK256) {
+        const KeccakCoop kc;
+        uint32_t lo, hi;
+        kc.hash(buf, 32u * c, lo, hi);
+        if (lane < 32 && kc.gl < 4) {
+            st_dev(dst + 8 * kc.gl, lo);
+            st_dev(dst + 8 * kc.gl + 4, hi);
+        }
+    } else {
+        if (lane == 0) {
+            uint32_t d[8];
+            hash_nodes<H>(buf, c, d);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) st_dev(dst + 4 * k, bswap32(d[k]));
+        }
+    }
+}
+
+// one level of a wave's subtree: `nodes` nodes (of `full` under a full wave) from `nin` children at
+// `in`, written to the tree at dst (node k at dst + 32 k) and to LDS dl
+template <int H, int W>
+__device__ __forceinline__ void fused_level(const uint8_t* in, uint64_t nin, uint32_t width, uint32_t full,
+                                            uint32_t nodes, uint8_t* dst, uint8_t* dl) {
+    const uint32_t lane = __lane_id();
+    if (H == KECCAK256 && full > 2) {  // lane pairs (uniform per level: decided on the full count)
+        const KeccakPair kp;
+        pair_level_pass(kp, in, nin, width, lane >> 1, nodes, dst, dl);
+    } else if (H == KECCAK256) {      // one or two nodes: a 25-lane group each
+        const KeccakCoop kc;
+        coop_level_pass<W>(kc, in, nin, width, lane >> 5, nodes, dst + 32 * (lane >> 5), dl + 32 * (lane >> 5));
+    } else if (lane < nodes) {
+        uint32_t d[8];
+        const uint64_t first = static_cast<uint64_t>(lane) * width;
+        const uint32_t c = static_cast<uint32_t>(nin - first < width ? nin - first : width);
+        hash_nodes<H>(in + 32ull * first, c, d);
+        store_digest(H, dst + 32ull * lane, d);
+        store_digest(H, dl + 32ull * lane, d);
+    }
+}
+
+template <int H, int W>
+__global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w,
+                                                          uint8_t* __restrict__ tree, const FusedTree f,
+                                                          uint8_t* __restrict__ root, uint32_t* __restrict__ ctr) {
+    __shared__ uint4 lds[2][64][2];
+    const TreeLevels& t = f.t;
+    const uint32_t width = W ? W : static_cast<uint32_t>(w);
+    const uint32_t lane = threadIdx.x;
+    if (blockIdx.x == 0 && lane < static_cast<uint32_t>(t.nlev)) {  // count records (Merkle.h:189-204)
+        uint32_t* e = reinterpret_cast<uint32_t*>(tree + 32ull * t.pos[lane]);
+        e[0] = bswap32(static_cast<uint32_t>(t.cnt[lane]));
+#pragma unroll
+        for (int k = 1; k < 8; ++k) e[k] = 0;
+    }
+    // ---- level 0 (from the leaves, global memory) and levels 1 .. a inside the wave (from LDS); the
+    // two kinds of source stay separate so every load has a known address space (no flat loads)
+    uint64_t base = static_cast<uint64_t>(blockIdx.x) * f.S;  // first level-0 node of this wave
+    uint32_t nodes = static_cast<uint32_t>(t.cnt[0] - base < f.S ? t.cnt[0] - base : f.S);
+    const int inner = f.a + 1 < t.nlev ? f.a + 1 : t.nlev;  // levels this wave computes before climbing
+    fused_level<H, W>(leaves + 32ull * base * width, n - base * width, width, f.S, nodes,
+                      tree + 32ull * (t.pos[0] + 1 + base), reinterpret_cast<uint8_t*>(&lds[0][0][0]));
+    __syncthreads();
+    int cur = 0;
+    uint32_t full = f.S;  // nodes of the level under a full wave
+    for (int l = 1; l < inner; ++l) {
+        const uint32_t nin = nodes;
+        nodes = (nodes + width - 1) / width;
+        base /= width;
+        full /= width;
+        fused_level<H, W>(reinterpret_cast<const uint8_t*>(&lds[cur][0][0]), nin, width, full, nodes,
+                          tree + 32ull * (t.pos[l] + 1 + base), reinterpret_cast<uint8_t*>(&lds[cur ^ 1][0][0]));
+        cur ^= 1;
+        __syncthreads();
+    }
+    // ---- climb: the wave completing a parent's group of children hashes the parent
+    uint64_t j = base;  // this wave's node at level inner - 1 (lds[cur][0])
+    if (inner < t.nlev && lane < 8)  // publish it (device-coherent)
+        st_dev(tree + 32ull * (t.pos[inner - 1] + 1 + j) + 4 * lane, reinterpret_cast<const uint32_t*>(&lds[cur][0][0])[lane]);
+    for (int l = inner; l < t.nlev; ++l) {
+        const uint64_t p = j / width;
+        const uint32_t kids = static_cast<uint32_t>(t.cnt[l - 1] - p * width < width ? t.cnt[l - 1] - p * width : width);
+        uint32_t arrived = 0;
+        __builtin_amdgcn_s_waitcnt(0);  // the published node's stores have completed (whole wave)
+        __syncthreads();
+        if (lane == 0) {
+            uint32_t* c = ctr + f.ctr_off[l] + p;
+            arrived = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+            if (arrived == kids) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        arrived = __shfl(arrived, 0);
+        if (arrived != kids) return;  // a sibling's wave finishes the parent
+        fused_one_node<H>(tree + 32ull * (t.pos[l - 1] + 1), t.cnt[l - 1], width, p, tree + 32ull * (t.pos[l] + 1 + p),
+                          reinterpret_cast<uint8_t*>(&lds[0][0][0]));
+        j = p;
+    }
+    if (root && lane < 8 && j == 0) {  // this wave wrote the root node (or the whole tree fit in it)
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        reinterpret_cast<uint32_t*>(root)[lane] = ld_dev(tree + 32ull * (t.pos[t.nlev - 1] + 1) + 4 * lane);
+    }
+}
+
+// one counter slot (kFusedCounters zeroed counters) per (device, stream): launches on one stream run
+// in order, and each launch leaves its counters at zero
+static constexpr uint32_t kFusedCounters = 16384, kFusedSlots = 64;
+static uint32_t* fused_counter_slot(hipStream_t st) {
+    static std::mutex mu;
+    struct Pool {
+        int device;
+        uint32_t* base;
+        std::vector<hipStream_t> owners;
+    };
+    static std::vector<Pool> pools;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    Pool* pool = nullptr;
+    for (auto& q : pools)
+        if (q.device == dev) pool = &q;
+    if (!pool) {
+        void* b = nullptr;
+        const size_t bytes = sizeof(uint32_t) * kFusedCounters * kFusedSlots;
+        if (hipMalloc(&b, bytes) != hipSuccess) return nullptr;
+        if (hipMemset(b, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void)hipFree(b);
+            return nullptr;
+        }
+        pools.push_back(Pool{dev, static_cast<uint32_t*>(b), {}});
+        pool = &pools.back();
+    }
+    for (size_t k = 0; k < pool->owners.size(); ++k)
+        if (pool->owners[k] == st) return pool->base + k * kFusedCounters;
+    if (pool->owners.size() >= kFusedSlots) return nullptr;  // caller takes the multi-launch path
+    pool->owners.push_back(st);
+    return pool->base + (pool->owners.size() - 1) * kFusedCounters;
+}
+
+static constexpr uint64_t kFusedMaxWaves = 2048;  // level-1 waves (two per SIMD) up to which the one-launch path runs
+
+// the latency path; returns 1 when it does not apply (too wide a tree, no counter slot)
+static int launch_merkle_fused(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
+                               uint8_t* d_root, const TreeLevels& t, bool force, hipStream_t st) {
+    FusedTree f{};
+    f.t = t;
+    // S = width^a: Keccak level 0 on lane pairs (S <= 32), SM3 one lane per node (S <= 64)
+    const uint32_t cap = hasher == KECCAK256 ? 32u : 64u;
+    f.S = 1;
+    f.a = 0;
+    while (f.S * static_cast<uint32_t>(width) <= cap) {
+        f.S *= width;
+        ++f.a;
+    }
+    uint32_t off = 0;
+    for (int l = 0; l < t.nlev; ++l) {
+        f.ctr_off[l] = off;
+        if (l > f.a) off += static_cast<uint32_t>(t.cnt[l]);
+    }
+    if (off > kFusedCounters || (!force && (t.cnt[0] + f.S - 1) / f.S > kFusedMaxWaves)) return 1;
+    uint32_t* ctr = fused_counter_slot(st);
+    if (!ctr) return 1;
+    const dim3 g(static_cast<unsigned>((t.cnt[0] + f.S - 1) / f.S)), b(64);
+#define FUSED(HH, WW) hipLaunchKernelGGL((merkle_fused_kernel<HH, WW>), g, b, 0, st, d_leaves, n, width, d_tree, f, d_root, ctr)
+    if (hasher == SM3) {
+        if (width == 2) FUSED(SM3, 2); else if (width == 16) FUSED(SM3, 16); else FUSED(SM3, 0);
+    } else {
+        if (width == 2) FUSED(KECCAK256, 2); else if (width == 16) FUSED(KECCAK256, 16); else FUSED(KECCAK256, 0);
+    }
+#undef FUSED
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
 static constexpr uint64_t kTopKernelMaxIn = 16384;  // inputs per level the single-workgroup kernel takes
+static constexpr uint64_t kPairMaxNodes = 32768;    // level-1 nodes up to which Keccak levels use lane pairs
 
 int launch_merkle_levelwise(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
                             uint8_t* d_root, hipStream_t st);
@@ -265,6 +532,15 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
         pos += m + 1;
         ++t.nlev;
     }
+    // latency-sized trees: one launch, one wave per workgroup (BCOSGPU_MERKLE_FUSED=0/1 forces it off/on)
+    static const int fused_env = [] {
+        const char* e = getenv("BCOSGPU_MERKLE_FUSED");
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    }();
+    if (fused_env == 1 || (fused_env < 0 && hasher == KECCAK256)) {
+        const int rf = launch_merkle_fused(hasher, width, d_leaves, n, d_tree, d_root, t, fused_env == 1, st);
+        if (rf <= 0) return rf;
+    }
     int kin = 0;
     uint32_t B = 1;
     while (B * static_cast<uint32_t>(width) <= 256u) {
@@ -272,11 +548,20 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
         ++kin;
     }
     const dim3 g1(static_cast<unsigned>((t.cnt[0] + B - 1) / B));
-    // Keccak: enough 32-lane groups that the second level runs one cooperative pass (B / width nodes)
-    uint32_t threads = B;
+    // Keccak levels on lane pairs while level 1 is latency-sized: at most one pair per lane of a wave
+    // per SIMD (kPairMaxNodes); beyond that one lane per node, which issues fewer instructions per node.
+    // BCOSGPU_MERKLE_PAIR=0/1 forces it off/on (A/B), read once per process.
+    static const int pair_env = [] {
+        const char* e = getenv("BCOSGPU_MERKLE_PAIR");
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    }();
+    const int pair = hasher == KECCAK256 && (pair_env >= 0 ? pair_env : t.cnt[0] <= kPairMaxNodes) ? 1 : 0;
+    // Keccak: enough 32-lane groups that the second level runs one cooperative pass (B / width nodes),
+    // two lanes per level-1 node in pair mode
+    uint32_t threads = pair ? 2u * B : B;
     if (hasher == KECCAK256 && kin >= 1 && 32u * (B / width) > threads && 32u * (B / width) <= 512u) threads = 32u * (B / width);
     const dim3 b1(threads);
-#define WG(HH, WW) hipLaunchKernelGGL((merkle_wg_kernel<HH, WW>), g1, b1, 0, st, d_leaves, n, width, kin, static_cast<int>(B), d_tree, t, d_root)
+#define WG(HH, WW) hipLaunchKernelGGL((merkle_wg_kernel<HH, WW>), g1, b1, 0, st, d_leaves, n, width, kin, static_cast<int>(B), d_tree, t, d_root, pair)
     if (hasher == SM3) {
         if (width == 2) WG(SM3, 2); else if (width == 16) WG(SM3, 16); else WG(SM3, 0);
     } else {
@@ -290,7 +575,7 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
         ++l;
     }
     if (l < t.nlev) {
-#define TOP(HH, WW) hipLaunchKernelGGL((merkle_top_kernel<HH, WW>), dim3(1), dim3(1024), 0, st, width, l, d_tree, t, d_root)
+#define TOP(HH, WW) hipLaunchKernelGGL((merkle_top_kernel<HH, WW>), dim3(1), dim3(1024), 0, st, width, l, d_tree, t, d_root, pair)
         if (hasher == SM3) {
             if (width == 2) TOP(SM3, 2); else if (width == 16) TOP(SM3, 16); else TOP(SM3, 0);
         } else {

@@ -157,3 +157,46 @@ def test_merkle_bytes_layout_vs_oracle(gpu, oracle, hasher):
             torch.cuda.synchronize()
             assert flat[:size].cpu().numpy().tobytes() == b"".join(want), (width, n)
             assert int(flat[size:].sum()) == 0  # nothing written past the packed size
+
+
+def test_merkle_one_launch_path_trees(gpu, oracle):
+    """The one-launch Keccak path (merkle_fused_kernel: waves publish their subtree roots and the wave that
+    completes a group hashes the parent) over widths 2..64 and sizes around its wave boundaries
+    (S = width^a level-1 nodes per wave): every entry of the output vector."""
+    rng = np.random.default_rng(77)
+    H = gpu.Keccak256()
+    for width in (2, 3, 4, 5, 7, 16, 17, 31, 32, 33, 64):
+        S = 1
+        while S * width <= 32:
+            S *= width
+        for n in sorted({1, 2, width, width + 1, S * width, S * width + 1, 3 * S * width - 1, 40 * S * width + 5}):
+            leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+            got = gpu.Merkle(H, width).generate_merkle([leaves[i].tobytes() for i in range(n)])
+            _, want = oracle.merkle(0, width, leaves, want_tree=True)
+            assert got == [want[i].tobytes() for i in range(want.shape[0])], (width, n)
+
+
+def test_merkle_one_launch_repeat_two_streams(gpu, oracle):
+    """The one-launch path's arrival counters reset themselves (back-to-back launches on one stream) and
+    are per stream (two torch streams at once): 40 C1-sized roots per stream, each equal to the oracle."""
+    import torch
+    from bcos_gpu import device
+    rng = np.random.default_rng(78)
+    cases = []
+    for width in (16, 2):
+        leaves = rng.integers(0, 256, size=(100_000, 32), dtype=np.uint8)
+        cases.append((width, torch.from_numpy(leaves).cuda(), oracle.merkle(0, width, leaves, nthreads=16)))
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for k, st in enumerate(streams):
+        width, d_leaves, _ = cases[k]
+        tree = torch.empty((device.merkle_size(100_000, width), 32), dtype=torch.uint8, device="cuda")
+        roots = torch.zeros((40, 32), dtype=torch.uint8, device="cuda")
+        outs.append(roots)
+        with torch.cuda.stream(st):
+            for r in range(40):
+                device.merkle_root(device.KECCAK256, width, d_leaves, tree, roots[r], st)
+    torch.cuda.synchronize()
+    for (width, _, want), roots in zip(cases, outs):
+        got = roots.cpu().numpy()
+        assert all(got[r].tobytes() == want for r in range(40)), width
