@@ -344,4 +344,114 @@ F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane
     R = O;
 }
 
+// R <- P + Q, both Jacobian in trio form (lane 2 holds all of each point at entry); CurveK1x::add's
+// formulas, magnitudes and exceptional cases (P = Q doubles on lane 2, P = -Q gives infinity, an
+// infinite operand gives the other), 16 products in 6 levels:
+//   L1  Z1Z1 = Z1^2      | Z2Z2 = Z2^2     | A = Y1 Z2
+//   L2  U2 = X2 Z1Z1     | U1 = X1 Z2Z2    | B = Y2 Z1
+//   L3  S2 = B Z1Z1      | S1 = A Z2Z2     | I = (2H)^2          (H = U2 - U1 on lane 2)
+//   L4  J = H I          | V = U1 I        | r^2                 (r = 2 (S2 - S1) on lane 2)
+//   L5  r (V - X3)       | S1 J            | Z1 Z2               (X3 = r^2 - J - 2V on lane 0)
+//   L6  --               | --              | Z1 Z2 H
+//   X3 = r^2 - J - 2V, Y3 = r (V - X3) - 2 S1 J, Z3 = 2 Z1 Z2 H.  X, Y, Z <= 16 (both) -> (6, 4, 2).
+F26_HD void trio_add(TrioPt& R, const TrioPt& P, const TrioPt& Q, const TrioLane& T) {
+    using namespace trio;
+    fe26 a, b, P1, Q1, o1, P2, Q2, o2, u2, u1, h, h2, P3, Q3, o3, s2, s1, rr, P4, Q4, o4, rv, X3, W, P5, Q5, o5,
+        Y3, Z3, t;
+    // L1: lane 0 Z1 Z1 (Z1 of lane 2), lane 1 Z2 Z2 (Z2 of lane 2), lane 2 Y1 Z2
+    fdpp<kR2>(a, P.Zs);                                  // lane 0: Z1
+    fdpp<kR1>(b, Q.Zs);                                  // lane 1: Z2
+    sel(P1, T.r0, a, b);
+    sel(P1, T.r2, P.S1, P1);
+    sel(Q1, T.r2, Q.Zs, P1);
+    mul(o1, P1, Q1);                                     // (Z1Z1 | Z2Z2 | A)            m 1
+    // L2: lane 0 X2 Z1Z1, lane 1 X1 Z2Z2 (X1 of lane 0), lane 2 Y2 Z1
+    fdpp<kL1>(a, P.S1);                                  // lane 1: X1
+    sel(P2, T.r1, a, Q.S1);                              // (X2 | X1 | Y2)
+    sel(Q2, T.r2, P.Zs, o1);                             // (Z1Z1 | Z2Z2 | Z1)
+    mul(o2, P2, Q2);                                     // (U2 | U1 | B)
+    // lane 2: H = U2 - U1, 2H
+    fdpp<kL2>(u2, o2);                                   // lane 0's U2 at lane 2
+    fdpp<kL1>(u1, o2);                                   // lane 1's U1 at lane 2
+    fe26_sub<2>(h, u2, u1);                              // H                            m 3
+    fe26_mul_int<2>(h2, h);                              // 2H                           m 6
+    // L3: lane 0 B Z1Z1 (B of lane 2), lane 1 A Z2Z2 (A of lane 2), lane 2 (2H)^2
+    fdpp<kR2>(a, o2);                                    // lane 0: B
+    fdpp<kR1>(b, o1);                                    // lane 1: A
+    sel(P3, T.r0, a, b);
+    sel(P3, T.r2, h2, P3);
+    sel(Q3, T.r2, h2, o1);
+    mul(o3, P3, Q3);                                     // (S2 | S1 | I)
+    // lane 2: r = 2 (S2 - S1)
+    fdpp<kL2>(s2, o3);                                   // lane 0's S2 at lane 2
+    fdpp<kL1>(s1, o3);                                   // lane 1's S1 at lane 2
+    fe26_sub<2>(rr, s2, s1);                             //                              m 3
+    fe26_mul_int<2>(rr, rr);                             // r                            m 6
+    // L4: lane 0 J = H I, lane 1 V = U1 I, lane 2 r^2 (H and I of lane 2)
+    fdpp<kR2>(a, h);                                     // lane 0: H
+    sel(P4, T.r0, a, o2);                                // (H | U1 | -)
+    sel(P4, T.r2, rr, P4);                               // (H | U1 | r)
+    fdpp<kR2>(a, o3);                                    // lane 0: I
+    fdpp<kR1>(b, o3);                                    // lane 1: I
+    sel(Q4, T.r0, a, b);
+    sel(Q4, T.r2, rr, Q4);                               // (I | I | r)
+    mul(o4, P4, Q4);                                     // (J | V | r^2)
+    // lane 0: X3 = r^2 - J - 2V (r^2 of lane 2, V of lane 1), V - X3
+    fdpp<kR2>(rv, o4);                                   // lane 0: r^2
+    fdpp<kR1>(b, o4);                                    // lane 0: V
+    fe26_sub<2>(X3, rv, o4);                             //                              m 3
+    fe26_mul_int<2>(t, b);                               //                              m 2
+    fe26_sub<3>(X3, X3, t);                              // X3                           m 6
+    fe26_sub<7>(W, b, X3);                               // V - X3                       m 8
+    // L5: lane 0 r (V - X3) (r of lane 2), lane 1 S1 J (J of lane 0), lane 2 Z1 Z2
+    fdpp<kR2>(a, rr);                                    // lane 0: r
+    sel(P5, T.r0, a, o3);                                // (r | S1 | -)
+    sel(P5, T.r2, P.Zs, P5);                             // (r | S1 | Z1)
+    fdpp<kL1>(b, o4);                                    // lane 1: J
+    sel(Q5, T.r0, W, b);
+    sel(Q5, T.r2, Q.Zs, Q5);                             // (V - X3 | J | Z2)
+    mul(o5, P5, Q5);                                     // (r (V - X3) | S1 J | Z1 Z2)
+    // L6 (lane 2): Z3 = 2 Z1 Z2 H
+    mul(Z3, o5, h);
+    fe26_mul_int<2>(Z3, Z3);                             //                              m 2
+    // lane 0: Y3 = r (V - X3) - 2 S1 J
+    fdpp<kR1>(t, o5);                                    // lane 0: S1 J
+    fe26_mul_int<2>(t, t);                               //                              m 2
+    fe26_sub<3>(Y3, o5, t);                              // Y3                           m 4
+    TrioPt O;
+    sel_dpp2<kL1, kL2>(O.S1, T.r0, X3, T.r1, Y3);      // (X3 | Y3 | Y3) from lane 0
+    fdpp<kL2>(O.Xs, X3);                                 // lane 2 <- X3 of lane 0
+    fe26_copy(O.Zs, Z3);
+    O.inf = false;
+    // exceptional cases (flags of lane 2, shared across the trio)
+    const uint32_t zf = (fe26_is_zero(h) ? 1u : 0u) | (fe26_is_zero(rr) ? 2u : 0u);
+    const uint32_t f = bdpp_from(zf, T, 2);
+    const bool hz = (f & 1u) != 0u && !P.inf && !Q.inf;
+    const bool rz = (f & 2u) != 0u;
+    if (any(hz && rz)) {                                 // P == Q: double P on lane 2 (rare)
+        Jac26 A, D;
+        fe26_copy(A.X, P.Xs);
+        fe26_copy(A.Y, P.S1);
+        fe26_copy(A.Z, P.Zs);
+        A.inf = P.inf;
+        CurveK1x::dbl(D, A);
+        TrioPt Dt;
+        sel_dpp2<kR2, kR1>(Dt.S1, T.r2, D.Y, T.r0, D.X);  // lane 0 <- X, lane 1 <- Y of lane 2
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            const uint32_t y = dpp<kR1>(D.Y.v[i]);
+            Dt.S1.v[i] = T.r1 ? y : Dt.S1.v[i];
+        }
+        F26_SETM(Dt.S1, 10);
+        fe26_copy(Dt.Xs, D.X);
+        fe26_copy(Dt.Zs, D.Z);
+        Dt.inf = false;
+        trio_cmov(O, Dt, hz && rz);
+    }
+    if (hz && !rz) O.inf = true;                         // P == -Q
+    trio_cmov(O, Q, P.inf);                              // (element-wise: no struct select through memory)
+    trio_cmov(O, P, !P.inf && Q.inf);
+    R = O;
+}
+
 }  // namespace bcosgpu

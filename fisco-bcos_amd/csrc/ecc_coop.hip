@@ -1047,6 +1047,35 @@ __device__ __forceinline__ void lds_store_limbs26(uint32_t (*dst)[64], const fe2
     for (int q = 0; q < 10; ++q) dst[q][lane] = t.v[q];
 }
 
+// a TrioPt through LDS (phase D of the trio kernel): [S1 limbs, Xs limbs, Zs limbs, inf][lane], the raw
+// limbs (magnitudes travel with the values)
+constexpr int kTrioWords = 31;
+__device__ __forceinline__ void trio_store(uint32_t* buf, const TrioPt& P, int lane) {
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+        buf[q * 64 + lane] = P.S1.v[q];
+        buf[(10 + q) * 64 + lane] = P.Xs.v[q];
+        buf[(20 + q) * 64 + lane] = P.Zs.v[q];
+    }
+    buf[30 * 64 + lane] = P.inf ? 1u : 0u;
+}
+__device__ __forceinline__ void trio_load(TrioPt& P, const uint32_t* buf, int lane) {
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+        P.S1.v[q] = buf[q * 64 + lane];
+        P.Xs.v[q] = buf[(10 + q) * 64 + lane];
+        P.Zs.v[q] = buf[(20 + q) * 64 + lane];
+    }
+    P.inf = buf[30 * 64 + lane] != 0u;
+}
+// a Jacobian point held whole by every lane of the trio into trio form
+__device__ __forceinline__ void trio_from_jac(TrioPt& P, const Jac26& J, const TrioLane& T) {
+    trio::sel(P.S1, T.r0, J.X, J.Y);
+    fe26_copy(P.Xs, J.X);
+    fe26_copy(P.Zs, J.Z);
+    P.inf = J.inf;
+}
+
 // A window of a GLV chain: acc <- acc + d * (table point), d a Booth digit in [-8, 8].  The madd runs
 // without its P = Q / P = -Q tests (trio_madd<false>): acc is K R for the digits K processed so far
 // and the table point is |d| R with |d| <= 8; once K != 0 every window makes |K| >= 16 before its
@@ -1196,9 +1225,9 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             L.flags[lane] = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
         }
         Jac26 G;
-        if (tab_bits == kWideBits) {  // 16 windows of the 16-bit comb: 6 / 7 / 3 (wave 1 also builds the table)
-            const int lo = wave == 0 ? 0 : wave == 3 ? 6 : 13;
-            const int hi = wave == 0 ? 6 : wave == 3 ? 13 : 16;
+        if (tab_bits == kWideBits) {  // 16 windows of the 16-bit comb: 7 / 7 / 2 (wave 1 also builds the table)
+            const int lo = wave == 0 ? 0 : wave == 3 ? 7 : 14;
+            const int hi = wave == 0 ? 7 : wave == 3 ? 14 : 16;
             comb_range26w<kWideBits>(G, u1, tab, lo, hi);
         } else {  // 32 windows of the 8-bit comb: 12 / 12 / 8
             const int lo = wave == 0 ? 0 : wave == 3 ? 12 : 24;
@@ -1227,109 +1256,198 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
         const int pos = lane & 15, trio_idx = pos / 3;
         const int chain = wave & 1, tl = (wave >> 1) * 20 + (lane >> 4) * 5 + (trio_idx < 5 ? trio_idx : 4);
         const uint32_t tflags = L.flags[tl] | L.rflag[tl];
-        fe k;
-        fe_zero(k);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) k.v[q] = L.k[chain][q][tl];
-        const bool neg = chain == 0 ? (tflags & 4u) != 0 : (tflags & 8u) != 0;
-        const bool phi = chain == 1;
         TrioPt acc;
-        trio_set_inf(acc);
-        trio_add_digit(acc, L, tl, static_cast<int>(k.v[3] >> 31), neg, phi, T);  // digit 32 = bit 127
-#pragma unroll 1
-        for (int w = 31; w >= 0; --w) {
-            trio_dbl(acc, T);
-            trio_dbl(acc, T);
-            trio_dbl(acc, T);
-            trio_dbl(acc, T);
-            trio_add_digit(acc, L, tl, booth_digit128(k), neg, phi, T);
-        }
-        COOP_T(2);
-        Jac26 J;
-        trio_to_jac(J, acc, T);
-        if (T.r0 && trio_idx < 5) coop26_store_jac(L.pt[chain], J, tl);
-    }
-    const uint32_t flags = L.flags[lane] | L.rflag[lane];
-    if constexpr (!TRIO) {
-        Coop26Ctx c{&L, wave >> 1, wave & 1, lane, false};
-        fe k;
-        fe_zero(k);
+        {
+            fe k;
+            fe_zero(k);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) k.v[q] = L.k[c.chain][q][lane];
-        const bool neg = c.chain == 0 ? (flags & 4u) != 0 : (flags & 8u) != 0;
-        const bool phi = c.chain == 1;
-        Jac26 acc;
-        CurveK1x::set_inf(acc);
-        coop26_add_digit(acc, c, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
+            for (int q = 0; q < 4; ++q) k.v[q] = L.k[chain][q][tl];
+            const bool neg = chain == 0 ? (tflags & 4u) != 0 : (tflags & 8u) != 0;
+            const bool phi = chain == 1;
+            trio_set_inf(acc);
+            trio_add_digit(acc, L, tl, static_cast<int>(k.v[3] >> 31), neg, phi, T);  // digit 32 = bit 127
 #pragma unroll 1
-        for (int w = 31; w >= 0; --w) {
-            coop26_dbl<0>(acc, c);
-#ifdef BCOSGPU_COOP_TIMING
-            c.probe = blockIdx.x == 0 && w == 20;
-#endif
-            coop26_dbl<3>(acc, c);
-#ifdef BCOSGPU_COOP_TIMING
-            c.probe = false;
-            if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][5] = clock64();
-#endif
-            coop26_dbl<0>(acc, c);
-            coop26_dbl<3>(acc, c);
-#ifdef BCOSGPU_COOP_TIMING
-            if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][6] = clock64();
-#endif
-            coop26_add_digit(acc, c, booth_digit128(k), neg, phi);
-#ifdef BCOSGPU_COOP_TIMING
-            if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][7] = clock64();
-#endif
+            for (int w = 31; w >= 0; --w) {
+                trio_dbl(acc, T);
+                trio_dbl(acc, T);
+                trio_dbl(acc, T);
+                trio_dbl(acc, T);
+                trio_add_digit(acc, L, tl, booth_digit128(k), neg, phi, T);
+            }
         }
         COOP_T(2);
-        if (c.role == 0) coop26_store_jac(L.pt[c.chain], acc, lane);
+        // ------------------------------------------------------------ phase D on the trios
+        // chain 0 (waves 0, 2) takes chain 1's point through LDS and adds it (E_w), maps to E (Z Zc y)
+        // and adds the G part, which chain 1 (waves 1, 3) sums meanwhile from phase A's two comb
+        // partials; all three additions are trio_add (6 product levels instead of 16 products on one
+        // lane).  Then the inversion and the affine map on lane 2 of each trio, the address Keccak on
+        // lane PAIRS (KeccakPair) of the chain-0 waves, and the outputs from lane 2.  The buffers reuse
+        // the table's LDS once every wave is past phase C.
+        uint32_t* const xbuf = &L.tab[0][0][0] + (wave >> 1) * kTrioWords * 64;
+        uint32_t* const gbuf = &L.tab[0][0][0] + (2 + (wave >> 1)) * kTrioWords * 64;
+        uint32_t* const mbuf = &L.tabphx[0][0][0];  // [40][16] pubkey messages, then [40][8] digests
+        const uint64_t ti = static_cast<uint64_t>(blockIdx.x) * TPW + tl;
+        const bool real = T.r2 && trio_idx < 5, tactive = ti < n;
+        fe26 zcy;
+        fe ax, ay;
+        bool ok2 = false;
+        __syncthreads();  // no wave reads the table any more
+        if (chain == 1) {
+            trio_store(xbuf, acc, lane);
+        } else {
+            fe26 zc, y;
+            lds_load_fe26(zc, L.zc, tl);
+            lds_load_fe26(y, L.ys, tl);
+            fe26_mul(zcy, zc, y);
+        }
+        __syncthreads();
+        if (chain == 1) {  // G = (G0 + G3) + G1 (phase A's partials)
+            Jac26 Ga, Gb;
+            TrioPt A, B;
+            coop26_load_jac(Ga, L.pt[3], tl);
+            coop26_load_jac(Gb, L.pt[4], tl);
+            trio_from_jac(A, Ga, T);
+            trio_from_jac(B, Gb, T);
+            trio_add(A, A, B, T);
+            trio_store(gbuf, A, lane);
+        } else {  // R = (k1 R' + k2 phi(R')) on E_w, then (X, Y, Z Zc y) on E
+            TrioPt P1;
+            trio_load(P1, xbuf, lane);
+            trio_add(acc, acc, P1, T);
+            fe26_mul(acc.Zs, acc.Zs, zcy);
+        }
+        __syncthreads();
+        if (chain == 0) {
+            TrioPt G;
+            trio_load(G, gbuf, lane);
+            trio_add(acc, acc, G, T);
+            ok2 = (tflags & 3u) == 3u && !acc.inf;
+            COOP_T(4);
+            fe z, zi;
+            fe26_to_fe(z, acc.Zs);
+            FieldInv<FieldK1>::inv(zi, z);
+            COOP_T(5);
+            fe26 zi26, zi2, zi3, X, Y;  // lane 2 holds X (Xs), Y (S1), Z
+            fe26_from_fe(zi26, zi);
+            fe26_sqr(zi2, zi26);
+            fe26_mul(X, acc.Xs, zi2);
+            fe26_mul(zi3, zi2, zi26);
+            fe26_mul(Y, acc.S1, zi3);
+            fe26_to_fe(ax, X);
+            fe26_to_fe(ay, Y);
+            if (real) {
+                uint32_t m[16];
+                fe_to_be_words(m, ax);
+                fe_to_be_words(m + 8, ay);
+#pragma unroll
+                for (int q = 0; q < 16; ++q) mbuf[16 * tl + q] = m[q];
+            }
+        }
+        __syncthreads();
+        if (chain == 0 && io.want_addr()) {  // Keccak256(x || y) on lane pairs: tx j = lane / 2 of the wave
+            const KeccakPair kp;
+            const int j = lane >> 1, t = (wave >> 1) * 20 + (j < 20 ? j : 0);
+            uint32_t d[4];
+            kp.hash(reinterpret_cast<const uint8_t*>(mbuf + 16 * t), 64u, d);
+            if (j < 20) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) mbuf[640 + 8 * t + 2 * q + (lane & 1)] = d[q];
+            }
+        }
+        __syncthreads();
+        if (chain == 0 && real && tactive) {
+            uint32_t ad[5] = {0, 0, 0, 0, 0};
+            if (ok2 && io.want_addr()) {
+#pragma unroll
+                for (int q = 0; q < 5; ++q) ad[q] = mbuf[640 + 8 * tl + 3 + q];  // right160
+            }
+            io.finish(ti, ok2, ad, &ax, &ay);
+        }
+        COOP_T(3);
     }
-    __syncthreads();
-    // ---------------------------------------------------------------- phase D (on fe26 as well)
-    if (wave == 1) {  // G part: (partials 0 + 1, phase A) + 2
-        Jac26 G01, G2, U;
-        coop26_load_jac(G01, L.pt[3], lane);
-        coop26_load_jac(G2, L.pt[4], lane);
-        CurveK1x::add(U, G01, G2);
-        coop26_store_jac(L.pt[2], U, lane);
-    } else if (wave == 0) {  // R part: co-Z curve -> E_w (Z * Zc) -> E (Z * y)
-        Jac26 P0, P1, Q;
-        coop26_load_jac(P0, L.pt[0], lane);
-        coop26_load_jac(P1, L.pt[1], lane);
-        fe26 Zc, y;
-        lds_load_fe26(Zc, L.zc, lane);
-        lds_load_fe26(y, L.ys, lane);
-        CurveK1x::add(Q, P0, P1);
-        fe26_mul(Zc, Zc, y);
-        fe26_mul(Q.Z, Q.Z, Zc);
-        coop26_store_jac(L.pt[0], Q, lane);
+    if constexpr (!TRIO) {
+        const uint32_t flags = L.flags[lane] | L.rflag[lane];
+        {
+            Coop26Ctx c{&L, wave >> 1, wave & 1, lane, false};
+            fe k;
+            fe_zero(k);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) k.v[q] = L.k[c.chain][q][lane];
+            const bool neg = c.chain == 0 ? (flags & 4u) != 0 : (flags & 8u) != 0;
+            const bool phi = c.chain == 1;
+            Jac26 acc;
+            CurveK1x::set_inf(acc);
+            coop26_add_digit(acc, c, static_cast<int>(k.v[3] >> 31), neg, phi);  // digit 32 = bit 127
+#pragma unroll 1
+            for (int w = 31; w >= 0; --w) {
+                coop26_dbl<0>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+                c.probe = blockIdx.x == 0 && w == 20;
+#endif
+                coop26_dbl<3>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+                c.probe = false;
+                if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][5] = clock64();
+#endif
+                coop26_dbl<0>(acc, c);
+                coop26_dbl<3>(acc, c);
+#ifdef BCOSGPU_COOP_TIMING
+                if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][6] = clock64();
+#endif
+                coop26_add_digit(acc, c, booth_digit128(k), neg, phi);
+#ifdef BCOSGPU_COOP_TIMING
+                if (blockIdx.x == 0 && w == 20 && (threadIdx.x & 63) == 0) g_dbl_t[threadIdx.x >> 6][7] = clock64();
+#endif
+            }
+            COOP_T(2);
+            if (c.role == 0) coop26_store_jac(L.pt[c.chain], acc, lane);
+        }
+        __syncthreads();
+        // ---------------------------------------------------------------- phase D (on fe26 as well)
+        if (wave == 1) {  // G part: (partials 0 + 1, phase A) + 2
+            Jac26 G01, G2, U;
+            coop26_load_jac(G01, L.pt[3], lane);
+            coop26_load_jac(G2, L.pt[4], lane);
+            CurveK1x::add(U, G01, G2);
+            coop26_store_jac(L.pt[2], U, lane);
+        } else if (wave == 0) {  // R part: co-Z curve -> E_w (Z * Zc) -> E (Z * y)
+            Jac26 P0, P1, Q;
+            coop26_load_jac(P0, L.pt[0], lane);
+            coop26_load_jac(P1, L.pt[1], lane);
+            fe26 Zc, y;
+            lds_load_fe26(Zc, L.zc, lane);
+            lds_load_fe26(y, L.ys, lane);
+            CurveK1x::add(Q, P0, P1);
+            fe26_mul(Zc, Zc, y);
+            fe26_mul(Q.Z, Q.Z, Zc);
+            coop26_store_jac(L.pt[0], Q, lane);
+        }
+        __syncthreads();
+        if (wave == 0 && active) {
+            Jac26 Q, G, R;
+            coop26_load_jac(Q, L.pt[0], lane);
+            coop26_load_jac(G, L.pt[2], lane);
+            CurveK1x::add(R, Q, G);
+            const bool ok2 = (flags & 3u) == 3u && !R.inf;
+            COOP_T(4);
+            fe z, zi, ax, ay;
+            fe26_to_fe(z, R.Z);
+            FieldInv<FieldK1>::inv(zi, z);
+            COOP_T(5);
+            fe26 zi26, zi2, zi3, X, Y;
+            fe26_from_fe(zi26, zi);
+            fe26_sqr(zi2, zi26);
+            fe26_mul(X, R.X, zi2);
+            fe26_mul(zi3, zi2, zi26);
+            fe26_mul(Y, R.Y, zi3);
+            fe26_to_fe(ax, X);
+            fe26_to_fe(ay, Y);
+            uint32_t ad[5] = {0, 0, 0, 0, 0};
+            if (ok2 && io.want_addr()) keccak_address(ad, ax, ay);
+            io.finish(i, ok2, ad, &ax, &ay);
+        }
+        COOP_T(3);
     }
-    __syncthreads();
-    if (wave == 0 && active) {
-        Jac26 Q, G, R;
-        coop26_load_jac(Q, L.pt[0], lane);
-        coop26_load_jac(G, L.pt[2], lane);
-        CurveK1x::add(R, Q, G);
-        const bool ok2 = (flags & 3u) == 3u && !R.inf;
-        COOP_T(4);
-        fe z, zi, ax, ay;
-        fe26_to_fe(z, R.Z);
-        FieldInv<FieldK1>::inv(zi, z);
-        COOP_T(5);
-        fe26 zi26, zi2, zi3, X, Y;
-        fe26_from_fe(zi26, zi);
-        fe26_sqr(zi2, zi26);
-        fe26_mul(X, R.X, zi2);
-        fe26_mul(zi3, zi2, zi26);
-        fe26_mul(Y, R.Y, zi3);
-        fe26_to_fe(ax, X);
-        fe26_to_fe(ay, Y);
-        uint32_t ad[5] = {0, 0, 0, 0, 0};
-        if (ok2 && io.want_addr()) keccak_address(ad, ax, ay);
-        io.finish(i, ok2, ad, &ax, &ay);
-    }
-    COOP_T(3);
 }
 
 template <class IO>

@@ -30,16 +30,15 @@ int main(int argc, char** argv) {
     hipMemcpy(dso, so.data(), 8 * (n + 1), hipMemcpyHostToDevice);
     const uint32_t *k1, *sm2;
     tables8(&k1, &sm2);
+    const TxIO io{dp, dpo, ds, dso, dh, dsn, dst};
     for (int rep = 0; rep < 3; ++rep) {
         if (trio) {
             const uint32_t *w1, *w2;
             int bits = 8;
             tables(&w1, &w2, &bits);
-            hipLaunchKernelGGL(tx_verify_trio26_kernel, dim3((n + 39) / 40), dim3(256), 0, 0, dp, dpo, ds, dso, n, w1,
-                               bits, dh, dsn, dst);
+            hipLaunchKernelGGL(tx_verify_trio26_kernel<TxIO>, dim3((n + 39) / 40), dim3(256), 0, 0, io, n, w1, bits);
         } else if (f26)
-            hipLaunchKernelGGL(tx_verify_coop26_kernel, dim3((n + 63) / 64), dim3(256), 0, 0, dp, dpo, ds, dso, n, k1, dh,
-                               dsn, dst);
+            hipLaunchKernelGGL(tx_verify_coop26_kernel<TxIO>, dim3((n + 63) / 64), dim3(256), 0, 0, io, n, k1);
         else
             hipLaunchKernelGGL(tx_verify_coop_kernel, dim3((n + 63) / 64), dim3(256), 0, 0, dp, dpo, ds, dso, n, k1, dh,
                                dsn, dst);

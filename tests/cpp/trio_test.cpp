@@ -143,6 +143,43 @@ void lane_main(int lane, int round) {
     trio_to_jac(J, P, T);
     if (t < 5 && !same_point(J, R)) bad[c] = 1;
 }
+// trio_add (Jacobian + Jacobian) against CurveK1x::add, chained `reps` times (R <- R + Q) so the
+// outputs' magnitudes feed back in
+struct CaseA {
+    Jac26 P, Q;
+    int reps;
+};
+std::vector<CaseA> acases;
+std::vector<int> abad;
+
+void to_trio(TrioPt& P, const Jac26& J, const TrioLane& T) {
+    trio::sel(P.S1, T.r0, J.X, J.Y);
+    P.Xs = J.X;
+    P.Zs = J.Z;
+    P.inf = J.inf;
+}
+
+void lane_main_add(int lane, int round) {
+    my_lane = lane;
+    const TrioLane T(lane);
+    const int t = (lane % 16) / 3;
+    const int c = round * cases_per_round + (t < 5 ? t : 4);
+    const CaseA& K = acases[c];
+    TrioPt P, Q;
+    to_trio(P, K.P, T);
+    to_trio(Q, K.Q, T);
+    Jac26 R = K.P;
+    for (int rep = 0; rep < K.reps; ++rep) {
+        trio_add(P, P, Q, T);
+        Jac26 S;
+        CurveK1x::add(S, R, K.Q);
+        R = S;
+    }
+    Jac26 J;
+    trio_to_jac(J, P, T);
+    if (t < 5 && !same_point(J, R)) abad[c] = 1;
+}
+
 // SM2: the same harness over fp26 / CurveSM2x (inputs X, Y <= 2, Z <= 8: what both ops accept)
 void rand_fp(fp26& a, int m, int mode) {
     for (int i = 0; i < 10; ++i) {
@@ -253,6 +290,56 @@ int main() {
         for (auto& x : th) x.join();
     }
     for (int k = 0; k < 300; ++k) {
+        CaseA K;
+        const int mode = k % 7 == 6 ? 1 : 0;
+        rand_fe(K.P.X, k % 3 == 0 ? 16 : 1 + static_cast<int>(rnd() % 16), mode);
+        rand_fe(K.P.Y, k % 3 == 0 ? 16 : 1 + static_cast<int>(rnd() % 16), mode);
+        rand_fe(K.P.Z, k % 3 == 0 ? 16 : 1 + static_cast<int>(rnd() % 16), mode);
+        rand_fe(K.Q.X, k % 3 == 0 ? 16 : 1 + static_cast<int>(rnd() % 16), mode);
+        rand_fe(K.Q.Y, k % 3 == 0 ? 16 : 1 + static_cast<int>(rnd() % 16), mode);
+        rand_fe(K.Q.Z, k % 3 == 0 ? 16 : 1 + static_cast<int>(rnd() % 16), mode);
+        K.P.inf = K.Q.inf = false;
+        K.reps = 1 + (k / cases_per_round) % 3;
+        const int special = k % 10;
+        if (special == 1 || special == 2) {  // Q = (X l^2, +-Y l^3, Z l): the same point as +-P
+            fe26 l, l2, l3;
+            rand_fe(l, 1, 0);
+            rand_fe(K.P.X, 2, 0);
+            rand_fe(K.P.Y, 2, 0);
+            rand_fe(K.P.Z, 2, 0);
+            fe26_sqr(l2, l);
+            fe26_mul(l3, l2, l);
+            fe26_mul(K.Q.X, K.P.X, l2);
+            fe26_mul(K.Q.Y, K.P.Y, l3);
+            fe26_mul(K.Q.Z, K.P.Z, l);
+            if (special == 2) fe26_neg<2>(K.Q.Y, K.Q.Y);
+        } else if (special == 3) {
+            CurveK1x::set_inf(K.P);
+        } else if (special == 4) {
+            CurveK1x::set_inf(K.Q);
+        } else if (special == 5) {
+            CurveK1x::set_inf(K.P);
+            CurveK1x::set_inf(K.Q);
+        }
+        acases.push_back(K);
+    }
+    abad.assign(acases.size(), 0);
+    for (int r = 0; r < static_cast<int>(acases.size()) / cases_per_round; ++r) {
+        std::vector<std::thread> th;
+        for (int l = 0; l < kLanes; ++l) th.emplace_back(lane_main_add, l, r);
+        for (auto& x : th) x.join();
+    }
+    int nabad = 0;
+    for (size_t i = 0; i < abad.size(); ++i)
+        if (abad[i]) {
+            if (!nabad) printf("add mismatch in case %zu (reps %d)\n", i, acases[i].reps);
+            ++nabad;
+        }
+    if (nabad) {
+        printf("trio add mismatches %d of %zu\n", nabad, acases.size());
+        return 1;
+    }
+    for (int k = 0; k < 300; ++k) {
         CaseP K;
         const int mode = k % 7 == 6 ? 1 : 0;
         rand_fp(K.P.X, k % 3 == 0 ? 2 : 1 + static_cast<int>(rnd() % 2), mode);
@@ -309,6 +396,6 @@ int main() {
         printf("trio mismatches %d of %zu\n", nbad, cases.size());
         return 1;
     }
-    printf("trio ok %zu secp256k1 + %zu sm2\n", cases.size(), pcases.size());
+    printf("trio ok %zu secp256k1 + %zu secp256k1 add + %zu sm2\n", cases.size(), acases.size(), pcases.size());
     return 0;
 }
