@@ -1199,7 +1199,8 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
     } else if (wave == 0) {
         fe rm, rinv;
         FieldN1::from_plain(rm, r);
-        FieldInv<FieldN1>::inv(rinv, rm);
+        if constexpr (TRIO) FieldInv<FieldN1>::inv_pipe(rinv, rm);  // (pipelined: this kernel has the registers)
+        else FieldInv<FieldN1>::inv(rinv, rm);
         lds_store_fe(L.xrinv, rinv, lane);
         coop_post(&L.post[0]);
         COOP_T(7);
@@ -1325,7 +1326,7 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             COOP_T(4);
             fe z, zi;
             fe26_to_fe(z, acc.Zs);
-            FieldInv<FieldK1>::inv(zi, z);
+            FieldInv<FieldK1>::inv_pipe(zi, z);
             COOP_T(5);
             fe26 zi26, zi2, zi3, X, Y;  // lane 2 holds X (Xs), Y (S1), Z
             fe26_from_fe(zi26, zi);

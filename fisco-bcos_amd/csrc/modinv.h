@@ -153,9 +153,8 @@ __device__ __forceinline__ void normalize_30(S30& r, int32_t sign, const ModInfo
     }
 }
 
-// r = x^-1 mod m (x in [0, m); x = 0 gives 0) -- the plain loop (tools/invbench.hip compares it with
-// modinv_safegcd below)
-__device__ __forceinline__ void modinv_safegcd_plain(fe& r, const fe& x, const ModInfo30& mi) {
+// r = x^-1 mod m (x in [0, m); x = 0 gives 0)
+__device__ __forceinline__ void modinv_safegcd(fe& r, const fe& x, const ModInfo30& mi) {
     S30 d, e, f, g;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
@@ -184,8 +183,10 @@ __device__ __forceinline__ void modinv_safegcd_plain(fe& r, const fe& x, const M
 // r = x^-1 mod m, software-pipelined: the (d, e) update of batch i needs only batch i's matrix, so it
 // is issued beside batch i + 1's divstep chain (a serial dependency chain on a lone wave, whose issue
 // slots the independent update fills); f, g stay on the critical path as before.  Same result as
-// modinv_safegcd_plain; 85.0k -> 74.4k cycles on a lone wave (tools/invbench.hip).
-__device__ __forceinline__ void modinv_safegcd(fe& r, const fe& x, const ModInfo30& mi) {
+// modinv_safegcd; 85.0k -> 74.4k cycles on a lone wave (tools/invbench.hip).  It keeps more values
+// live, so it is used where registers are not the constraint (the C2 lane-trio kernel, via
+// FieldInv<F>::inv_pipe): in the SM2 trio kernel's table build it measured 5 % slower overall.
+__device__ __forceinline__ void modinv_safegcd_pipe(fe& r, const fe& x, const ModInfo30& mi) {
     S30 d, e, f, g;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
@@ -233,11 +234,18 @@ struct FieldInv<FieldK1> {
         FieldK1::normalize(t);
         modinv_safegcd(r, t, kMod30K1P);
     }
+    __device__ static __forceinline__ void inv_pipe(fe& r, const fe& a) {
+        fe t;
+        fe_copy(t, a);
+        FieldK1::normalize(t);
+        modinv_safegcd_pipe(r, t, kMod30K1P);
+    }
 };
-template <class P>
+template <class P, bool PIPE = false>
 __device__ __forceinline__ void mont_inv_safegcd(fe& r, const fe& a, const ModInfo30& mi, const uint32_t* r3) {
     fe t, k;
-    modinv_safegcd(t, a, mi);
+    if constexpr (PIPE) modinv_safegcd_pipe(t, a, mi);
+    else modinv_safegcd(t, a, mi);
     fe_set(k, r3);
     Mont<P>::mul(r, t, k);
 }
@@ -248,6 +256,9 @@ struct FieldInv<FieldP2> {
 template <>
 struct FieldInv<FieldN1> {
     __device__ static __forceinline__ void inv(fe& r, const fe& a) { mont_inv_safegcd<ParamN1>(r, a, kMod30N1, kR3N1); }
+    __device__ static __forceinline__ void inv_pipe(fe& r, const fe& a) {
+        mont_inv_safegcd<ParamN1, true>(r, a, kMod30N1, kR3N1);
+    }
 };
 template <>
 struct FieldInv<FieldN2> {
