@@ -344,6 +344,97 @@ F26_HD void trio_madd(TrioPt& R, const TrioPt& P, const Aff26& Q, const TrioLane
     R = O;
 }
 
+// P <- 2P as trio_dbl, and ZZ = Z3^2 on lane 0 for the mixed addition that follows (trio_madd_zz): the
+// first level's redundant lane-2 square becomes Z^2 (lane 2's B comes from lane 1), and the third
+// level's idle lane 0 computes B Z^2, so Z3^2 = (2 Y Z)^2 = 4 B Z^2 costs no product level.
+// (X, Y <= 10, Z <= 16 -> (10, 10, 2), ZZ m 4)
+F26_HD void trio_dbl_zz(TrioPt& P, fe26& ZZ, const TrioLane& T) {
+    using namespace trio;
+    fe26 S0, o1, T2, S2, o2, F, XB, D, X3, W, P3, Q3, o3, C8, Y3, t;
+    sel(S0, T.r2, P.Zs, P.S1);                           // (X | Y | Z)
+    sqr(o1, S0);                                         // (A | B | Z^2)                m 1
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t x3 = (o1.v[i] << 1) + o1.v[i];  // one v_lshl_add_u32
+        T2.v[i] = T.r0 ? x3 : o1.v[i];                  // (3A | B | Z^2)
+    }
+    F26_SETM(T2, T.r0 ? 3 : 1);
+    csel<kL1>(T2, !T.r2, T.n2, T2, o1);                  // lane 2: B of lane 1 -> (3A | B | B)
+    sel(S2, T.r2, P.Xs, T2);                             // (3A | B | X)                 m <= 10
+    mul(o2, S2, T2);                                     // (F | C | XB)
+    fdpp<kL1>(F, o2);                                    // lane 1: F                    m 1
+    fdpp<kR1>(XB, o2);                                   // lane 1: X B                  m 1
+    fe26_mul_int<4>(D, XB);                              // D = 4 X B                    m 4
+    fe26_mul_int<2>(t, D);                               //                              m 8
+    fe26_sub<9>(X3, F, t);                               // X3 = F - 2D                  m 10
+    fe26_sub<11>(W, D, X3);                              // D - X3                       m 15
+    csel<kL1>(P3, T.r2, T.m2, P.S1, T2);                 // lane 1: E = 3A (lane 0), lane 2: Y
+    csel<kR1>(P3, !T.r0, T.n0, P3, o1);                  // lane 0: B (lane 1)
+    sel(Q3, T.r2, P.Zs, W);                              // lane 1: D - X3, lane 2: Z
+    csel<kR2>(Q3, !T.r0, T.n0, Q3, o1);                  // lane 0: Z^2 (lane 2)
+    mul(o3, P3, Q3);                                     // (B Z^2 | E (D - X3) | Y Z)
+    fe26_mul_int<4>(ZZ, o3);                             // lane 0: Z3^2 = 4 B Z^2       m 4
+    fe26_mul_int<8>(C8, o2);                             // lane 1: 8C                   m 8
+    fe26_sub<9>(Y3, o3, C8);                             // lane 1: Y3                   m 10
+    fe26_mul_int<2>(P.Zs, o3);                           // lane 2: Z3 = 2 Y Z           m 2
+    csel<kL1>(t, T.r1, T.m1, Y3, Y3);                    // lanes 1, 2: Y3 of lane 1
+    csel<kR1>(P.S1, !T.r0, T.n0, t, X3);                 // lane 0: X3 of lane 1
+    fdpp<kL1>(P.Xs, X3);                                 // lane 2 <- X3 of lane 1
+}
+
+// R <- P + Q, Q affine, given ZZ = Z1^2 on lane 0 (trio_dbl_zz): CurveK1x::madd in 4 product levels
+// instead of 5 (the Z1^2 level is gone), without the P = +-Q tests (the GLV chain's additions, see
+// trio_add_digit in ecc_coop.hip); P = infinity gives Q.  X, Y <= 10, Z <= 16, ZZ <= 4; Q <= 2
+// -> (9, 6, 2).
+//   L1  U2 = x2 ZZ       | T = y2 Z        | --
+//   L2  HH = H^2         | S2 = T ZZ       | Z H          (H = U2 - X on lane 0)
+//   L3  J = H I          | rr^2            | V = X I      (I = 4 HH, rr = S2 - Y on lane 1)
+//   L4  rr (V - X3)      | Y J             | --           (X3 = 4 rr^2 - J - 2V on lane 0)
+F26_HD void trio_madd_zz(TrioPt& R, const TrioPt& P, const fe26& ZZ, const Aff26& Q, const TrioLane& T) {
+    using namespace trio;
+    fe26 P1, Q1, o1, h, P2, Q2, a, b, o2, I, rr, P3, Q3, o3, R2, V, X3, W, P4, Q4, o4, Y3, t;
+    sel(P1, T.r1, Q.y, Q.x);                             // (x2 | y2 | x2)
+    csel<kR1>(Q1, T.r0, T.m0, ZZ, P.Zs);                 // (ZZ | Z of lane 2 | -)
+    mul(o1, P1, Q1);                                     // (U2 | T | -)
+    fe26_sub<11>(h, o1, P.S1);                           // lane 0: H = U2 - X           m 12
+    sel(P2, T.r1, o1, P.Zs);
+    sel(P2, T.r0, h, P2);                                // (H | T | Z)
+    fdpp<kL1>(a, ZZ);                                    // lane 1: ZZ
+    fdpp<kL2>(b, h);                                     // lane 2: H
+    sel(Q2, T.r1, a, b);
+    sel(Q2, T.r0, h, Q2);                                // (H | ZZ | H)
+    mul(o2, P2, Q2);                                     // (HH | S2 | Z H)
+    fe26_mul_int<4>(I, o2);                              // lane 0: I = 4 HH             m 4
+    fe26_sub<11>(rr, o2, P.S1);                          // lane 1: rr = S2 - Y          m 12
+    sel(P3, T.r1, rr, P.Xs);
+    sel(P3, T.r0, h, P3);                                // (H | rr | X)
+    fdpp<kL2>(b, I);                                     // lane 2: I
+    sel(Q3, T.r1, rr, b);
+    sel(Q3, T.r0, I, Q3);                                // (I | rr | I)
+    mul(o3, P3, Q3);                                     // (J | rr^2 | V)
+    // lane 0: X3 = 4 rr^2 - J - 2V and V - X3
+    fdpp<kR1>(R2, o3);
+    fe26_mul_int<4>(R2, R2);                             // 4 rr^2                       m 4
+    fdpp<kR2>(V, o3);                                    // V of lane 2                  m 1
+    fe26_sub<2>(X3, R2, o3);                             //                              m 6
+    fe26_mul_int<2>(t, V);                               //                              m 2
+    fe26_sub<3>(X3, X3, t);                              // X3                           m 9
+    fe26_sub<10>(W, V, X3);                              // V - X3                       m 11
+    csel<kR1>(P4, !T.r0, T.n0, P.S1, rr);                // lane 0: rr (lane 1), lane 1: Y   m 12
+    csel<kL1>(Q4, T.r0, T.m0, W, o3);                    // lane 0: V - X3, lane 1: J of lane 0
+    mul(o4, P4, Q4);                                     // (rr (V - X3) | Y J | -)
+    fdpp<kR1>(t, o4);
+    fe26_sub<2>(Y3, o4, t);                              //                              m 3
+    fe26_mul_int<2>(Y3, Y3);                             // lane 0: Y3                   m 6
+    TrioPt O;
+    sel_dpp2<kL1, kL2>(O.S1, T.r0, X3, T.r1, Y3);      // (X3 | Y3 | Y3) from lane 0
+    fdpp<kL2>(O.Xs, X3);                                 // lane 2 <- X3 of lane 0
+    fe26_mul_int<2>(O.Zs, o2);                           // lane 2: Z3 = 2 Z H           m 2
+    O.inf = false;
+    if (P.inf) trio_from_aff(O, Q, T);
+    R = O;
+}
+
 // R <- P + Q, both Jacobian in trio form (lane 2 holds all of each point at entry); CurveK1x::add's
 // formulas, magnitudes and exceptional cases (P = Q doubles on lane 2, P = -Q gives infinity, an
 // infinite operand gives the other), 16 products in 6 levels:

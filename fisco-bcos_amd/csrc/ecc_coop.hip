@@ -1103,6 +1103,30 @@ __device__ __forceinline__ void trio_add_digit(TrioPt& acc, const Trio26Lds& L, 
     trio_cmov(acc, R, d != 0);
 }
 
+// the same window step after trio_dbl_zz: the addition in 4 product levels (trio_madd_zz).  (Reading
+// the table entry before the window's doublings, to take the LDS latency off the first level, measured
+// no gain: 893k cycles either way.)
+__device__ __forceinline__ void trio_add_digit_zz(TrioPt& acc, const Trio26Lds& L, int tl, int d, bool neg, bool phi,
+                                                  const fe26& ZZ, const TrioLane& T) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &L.tab[0][0][0] + m * (20 * 64) + tl;
+    const uint32_t* bx = phi ? &L.tabphx[0][0][0] + m * (10 * 64) + tl : base;
+    Aff26 S;
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+        S.x.v[q] = bx[q * 64];
+        S.y.v[q] = base[(10 + q) * 64];
+    }
+    F26_SETM(S.x, 1);
+    F26_SETM(S.y, 1);
+    fe26 ny;
+    fe26_neg<2>(ny, S.y);
+    fe26_cmov(S.y, ny, (d < 0) != neg);
+    TrioPt R;
+    trio_madd_zz(R, acc, ZZ, S, T);
+    trio_cmov(acc, R, d != 0);
+}
+
 // TRIO = false: tx_verify_coop26_kernel (64 txs per workgroup, wave-pair chains); TRIO = true:
 // tx_verify_trio26_kernel (40 txs per workgroup, lane-trio chains).  Phases A and D are the same code.
 template <bool TRIO, class IO>
@@ -1269,11 +1293,12 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             trio_add_digit(acc, L, tl, static_cast<int>(k.v[3] >> 31), neg, phi, T);  // digit 32 = bit 127
 #pragma unroll 1
             for (int w = 31; w >= 0; --w) {
+                fe26 zz;
                 trio_dbl(acc, T);
                 trio_dbl(acc, T);
                 trio_dbl(acc, T);
-                trio_dbl(acc, T);
-                trio_add_digit(acc, L, tl, booth_digit128(k), neg, phi, T);
+                trio_dbl_zz(acc, zz, T);  // + Z^2 for the addition
+                trio_add_digit_zz(acc, L, tl, booth_digit128(k), neg, phi, zz, T);
             }
         }
         COOP_T(2);

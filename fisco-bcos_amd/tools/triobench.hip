@@ -59,6 +59,14 @@ __global__ __launch_bounds__(256, 1) void trio_bench(const uint32_t* __restrict_
                 trio_dbl(P, T);
             }
             if (ops & 2) trio_madd(P, P, Q, T);
+            if (ops & 4) {  // the kernel's window: 3 doublings, the Z^2-carrying one, the 4-level addition
+                fe26 zz;
+                trio_dbl(P, T);
+                trio_dbl(P, T);
+                trio_dbl(P, T);
+                trio_dbl_zz(P, zz, T);
+                trio_madd_zz(P, P, zz, Q, T);
+            }
         }
         t1 = clock64();
         trio_to_jac(J, P, T);
@@ -72,7 +80,13 @@ __global__ __launch_bounds__(256, 1) void trio_bench(const uint32_t* __restrict_
                 CurveK1x::dbl(J, J);
                 CurveK1x::dbl(J, J);
             }
-            if (ops & 2) {
+            if (ops & 6) {
+                if (ops & 4) {
+                    CurveK1x::dbl(J, J);
+                    CurveK1x::dbl(J, J);
+                    CurveK1x::dbl(J, J);
+                    CurveK1x::dbl(J, J);
+                }
                 Jac26 R;
                 CurveK1x::madd(R, J, Q);
                 J = R;

@@ -143,6 +143,37 @@ void lane_main(int lane, int round) {
     trio_to_jac(J, P, T);
     if (t < 5 && !same_point(J, R)) bad[c] = 1;
 }
+// the GLV chain's window as the kernel runs it: 3 trio_dbl + trio_dbl_zz + trio_madd_zz (no P = +-Q
+// tests, so no such cases), against 4 CurveK1x::dbl + CurveK1x::madd
+std::vector<int> zbad;
+void lane_main_zz(int lane, int round) {
+    my_lane = lane;
+    const TrioLane T(lane);
+    const int t = (lane % 16) / 3;
+    const int c = round * cases_per_round + (t < 5 ? t : 4);
+    const Case& K = cases[c];
+    TrioPt P;
+    trio::sel(P.S1, T.r0, K.P.X, K.P.Y);
+    P.Xs = K.P.X;
+    P.Zs = K.P.Z;
+    P.inf = K.P.inf;
+    Jac26 R = K.P;
+    for (int rep = 0; rep < K.reps; ++rep) {
+        fe26 ZZ;
+        trio_dbl(P, T);
+        trio_dbl(P, T);
+        trio_dbl(P, T);
+        trio_dbl_zz(P, ZZ, T);
+        trio_madd_zz(P, P, ZZ, K.Q, T);
+        for (int d = 0; d < 4; ++d) CurveK1x::dbl(R, R);
+        Jac26 S;
+        CurveK1x::madd(S, R, K.Q);
+        R = S;
+    }
+    Jac26 J;
+    trio_to_jac(J, P, T);
+    if (t < 5 && !same_point(J, R)) zbad[c] = 1;
+}
 // trio_add (Jacobian + Jacobian) against CurveK1x::add, chained `reps` times (R <- R + Q) so the
 // outputs' magnitudes feed back in
 struct CaseA {
@@ -289,6 +320,29 @@ int main() {
         for (int l = 0; l < kLanes; ++l) th.emplace_back(lane_main, l, r);
         for (auto& x : th) x.join();
     }
+    // the zz window over the same inputs, minus the P = +-Q cases (kept as plain random inputs)
+    {
+        std::vector<Case> saved = cases;
+        for (size_t k = 0; k < cases.size(); ++k)
+            if (k % 10 == 1 || k % 10 == 2) rand_fe(cases[k].P.Z, 3, 0);  // P no longer +-Q
+        zbad.assign(cases.size(), 0);
+        for (int r = 0; r < rounds; ++r) {
+            std::vector<std::thread> th;
+            for (int l = 0; l < kLanes; ++l) th.emplace_back(lane_main_zz, l, r);
+            for (auto& x : th) x.join();
+        }
+        int nz = 0;
+        for (size_t i = 0; i < zbad.size(); ++i)
+            if (zbad[i]) {
+                if (!nz) printf("zz window mismatch in case %zu (reps %d)\n", i, cases[i].reps);
+                ++nz;
+            }
+        if (nz) {
+            printf("trio zz mismatches %d of %zu\n", nz, cases.size());
+            return 1;
+        }
+        cases = saved;
+    }
     for (int k = 0; k < 300; ++k) {
         CaseA K;
         const int mode = k % 7 == 6 ? 1 : 0;
@@ -396,6 +450,7 @@ int main() {
         printf("trio mismatches %d of %zu\n", nbad, cases.size());
         return 1;
     }
-    printf("trio ok %zu secp256k1 + %zu secp256k1 add + %zu sm2\n", cases.size(), acases.size(), pcases.size());
+    printf("trio ok %zu secp256k1 + %zu zz windows + %zu secp256k1 add + %zu sm2\n", cases.size(), cases.size(),
+           acases.size(), pcases.size());
     return 0;
 }
