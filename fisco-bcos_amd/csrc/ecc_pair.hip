@@ -856,6 +856,28 @@ __device__ __forceinline__ void trio_add_digit_sm2(TrioPtP& acc, const Sm2Trio26
     trio_cmov_sm2(acc, R, d != 0);
 }
 
+// the window step after trio_dbl_sm2_zz: the addition in 4 product levels (trio_madd_sm2_zz)
+__device__ __forceinline__ void trio_add_digit_sm2_zz(TrioPtP& acc, const Sm2Trio26Lds& L, int tl, int d, const fp26& ZZ,
+                                                      const TrioLane& T) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &L.tab[0][0][0] + m * (20 * 64) + tl;
+    AffP26 S;
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+        S.x.v[q] = base[q * 64];
+        S.y.v[q] = base[(10 + q) * 64];
+    }
+    F26_SETM(S.x, 1);
+    F26_SETM(S.y, 1);
+    fp26 ny;
+    fp26_neg<2>(ny, S.y);
+    fp26_cmov(S.y, ny, d < 0);
+    fp26_normalize_weak(S.y);
+    TrioPtP R;
+    trio_madd_sm2_zz(R, acc, ZZ, S, T);
+    trio_cmov_sm2(acc, R, d != 0);
+}
+
 template <class IO>
 __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab) {
     constexpr int TPW = 40;
@@ -937,15 +959,16 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
         trio_add_digit_sm2(acc, L, tl, static_cast<int>(k.v[7] >> 31), T);  // digit 64 = bit 255
 #pragma unroll 1
         for (int w = 63; w >= 0; --w) {
+            fp26 zz;
             trio_dbl_sm2(acc, T);
             trio_dbl_sm2(acc, T);
             trio_dbl_sm2(acc, T);
-            trio_dbl_sm2(acc, T);
+            trio_dbl_sm2_zz(acc, zz, T);  // + Z^2 for the addition
             const uint32_t top = k.v[7];
             const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
             const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
             shl4(k);
-            trio_add_digit_sm2(acc, L, tl, d, T);
+            trio_add_digit_sm2_zz(acc, L, tl, d, zz, T);
         }
         JacP26 J;
         trio_to_jac_sm2(J, acc, T);
