@@ -856,9 +856,9 @@ __device__ __forceinline__ void trio_add_digit_sm2(TrioPtP& acc, const Sm2Trio26
     trio_cmov_sm2(acc, R, d != 0);
 }
 
-// the window step after trio_dbl_sm2_zz: the addition in 4 product levels (trio_madd_sm2_zz)
-__device__ __forceinline__ void trio_add_digit_sm2_zz(TrioPtP& acc, const Sm2Trio26Lds& L, int tl, int d, const fp26& ZZ,
-                                                      const TrioLane& T) {
+// the window's addition on the delta-carrying chain (trio_madd_sm2_d): D = Z^2 on lane 0 in and out
+__device__ __forceinline__ void trio_add_digit_sm2_d(TrioPtP& acc, fp26& D, const Sm2Trio26Lds& L, int tl, int d,
+                                                     const TrioLane& T) {
     const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
     const uint32_t* base = &L.tab[0][0][0] + m * (20 * 64) + tl;
     AffP26 S;
@@ -874,8 +874,10 @@ __device__ __forceinline__ void trio_add_digit_sm2_zz(TrioPtP& acc, const Sm2Tri
     fp26_cmov(S.y, ny, d < 0);
     fp26_normalize_weak(S.y);
     TrioPtP R;
-    trio_madd_sm2_zz(R, acc, ZZ, S, T);
+    fp26 Dn;
+    trio_madd_sm2_d(R, Dn, acc, D, S, T);
     trio_cmov_sm2(acc, R, d != 0);
+    fp26_cmov(D, Dn, d != 0);
 }
 
 template <class IO>
@@ -957,18 +959,19 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
         TrioPtP acc;
         trio_set_inf_sm2(acc);
         trio_add_digit_sm2(acc, L, tl, static_cast<int>(k.v[7] >> 31), T);  // digit 64 = bit 255
+        fp26 D;  // delta = Z^2 of acc on lane 0 (an affine table point or infinity here)
+        fp26_set(D, p26::ONE_R);
 #pragma unroll 1
         for (int w = 63; w >= 0; --w) {
-            fp26 zz;
-            trio_dbl_sm2(acc, T);
-            trio_dbl_sm2(acc, T);
-            trio_dbl_sm2(acc, T);
-            trio_dbl_sm2_zz(acc, zz, T);  // + Z^2 for the addition
+            trio_dbl_sm2_d(acc, D, T);  // three product levels each (delta carried)
+            trio_dbl_sm2_d(acc, D, T);
+            trio_dbl_sm2_d(acc, D, T);
+            trio_dbl_sm2_d(acc, D, T);
             const uint32_t top = k.v[7];
             const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
             const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
             shl4(k);
-            trio_add_digit_sm2_zz(acc, L, tl, d, zz, T);
+            trio_add_digit_sm2_d(acc, D, L, tl, d, T);
         }
         JacP26 J;
         trio_to_jac_sm2(J, acc, T);

@@ -207,6 +207,110 @@ F26_HD void trio_madd_sm2_zz(TrioPtP& R, const TrioPtP& P, const fp26& ZZ, const
     R = O;
 }
 
+// ---- the delta-carrying chain (the SM2 trio kernel's window): the point travels with D = delta = Z^2
+// on lane 0, so a doubling needs no level for delta and takes THREE product levels:
+//   L1  alpha / 3 = (X - D)(X + D) | gamma = Y^2     | Y Z
+//   L2  alpha^2                    | beta = X gamma  | D' = (2 Y Z)^2  (the next delta = Z3^2)
+//   L3  alpha (4 beta - X3)        | gamma^2         | --              (X3 = alpha^2 - 8 beta on lane 0)
+// (CurveSM2x::dbl's products and magnitudes: X <= 5, Y, Z <= 8, D <= 1 -> (2, 2, 2), D' m 1)
+F26_HD void trio_dbl_sm2_d(TrioPtP& P, fp26& D, const TrioLane& T) {
+    using namespace trio;
+    fp26 t, u, A1, B1, o1, al, Z3, A2, B2, o2, be, b8, X3, t4, A3, B3, o3, g2, Y3, Dn;
+    fp26_sub<2>(t, P.Xr, D);             // lane 0: X - delta          m X + 3
+    fp26_add(u, P.Xr, D);                // lane 0: X + delta          m X + 1
+    sel(A1, T.r0, t, P.P1);              // (X - d | Y | Y)
+    sel(B1, T.r0, u, P.Q1);              // (X + d | Y | Z)
+    mul(o1, A1, B1);                     // (alpha / 3 | gamma | Y Z)
+    fp26_mul_int<3>(al, o1);             // lane 0: alpha              m 3
+    fp26_mul_int<2>(Z3, o1);             // lane 2: Z3 = 2 Y Z         m 2
+    sel(A2, T.r1, P.Xr, Z3);
+    sel(A2, T.r0, al, A2);               // (alpha | X | Z3)
+    sel(B2, T.r1, o1, Z3);
+    sel(B2, T.r0, al, B2);               // (alpha | gamma | Z3)
+    mul(o2, A2, B2);                     // (alpha^2 | beta | Z3^2)
+    fdpp<kR1>(be, o2);                   // lane 0: beta
+    fp26_mul_int<8>(b8, be);             //                            m 8
+    fp26_sub<9>(X3, o2, b8);             //                            m 11
+    fp26_normalize_weak(X3);             // X3 = alpha^2 - 8 beta      m 2
+    fp26_mul_int<4>(t4, be);             //                            m 4
+    fp26_sub<3>(t4, t4, X3);             // 4 beta - X3                m 8
+    sel(A3, T.r0, al, o1);               // (alpha | gamma | -)
+    sel(B3, T.r0, t4, o1);               // (4 beta - X3 | gamma | -)
+    mul(o3, A3, B3);                     // (alpha (4 beta - X3) | gamma^2 | -)
+    fdpp<kR1>(g2, o3);                   // lane 0: gamma^2
+    fp26_mul_int<8>(g2, g2);             //                            m 8
+    fp26_sub<9>(Y3, o3, g2);             //                            m 11
+    fp26_normalize_weak(Y3);             // Y3                         m 2
+    fdpp<kR2>(Dn, o2);                   // lane 0: Z3^2 of lane 2
+    trio_state_sm2(P, X3, Y3, Z3, T);
+    fp26_copy(D, Dn);
+}
+
+// R <- P + Q, Q affine, given D = Z1^2 on lane 0 (trio_dbl_sm2_d): CurveSM2x::madd in 4 product levels,
+// without the P = +-Q tests (the t P chain's additions), returning the sum's D = Z3^2 on lane 0 from
+// the last level's idle lane 2; P = infinity gives Q (D = 1).  X, Y <= 2, Z <= 8, D <= 1, Q <= 2 ->
+// (2, 2, 2), D m 1.
+//   L1  U2 = x2 D        | T = y2 Z        | --
+//   L2  HH = H^2         | S2 = T D        | Z H          (H = U2 - X on lane 0)
+//   L3  J = H I          | rr^2            | V = X I      (I = 4 HH, rr = S2 - Y on lane 1)
+//   L4  rr (V - X3)      | Y J             | Z3^2         (X3 = 4 rr^2 - J - 2V on lane 0, Z3 = 2 Z H)
+F26_HD void trio_madd_sm2_d(TrioPtP& R, fp26& Dout, const TrioPtP& P, const fp26& D, const AffP26& Q,
+                            const TrioLane& T) {
+    using namespace trio;
+    fp26 a, b, A1, B1, o1, h, A2, B2, o2, I, rr, A3, B3, o3, R2, V, X3, t, W, Z3, A4, B4, o4, Y3, Dn;
+    fdpp<kR1>(b, P.Q1);                  // lane 1: Z of lane 2
+    sel(A1, T.r1, Q.y, Q.x);             // (x2 | y2 | x2)
+    sel(B1, T.r0, D, b);                 // (D | Z | -)
+    mul(o1, A1, B1);                     // (U2 | T | -)
+    fp26_sub<3>(h, o1, P.Xr);            // lane 0: H = U2 - X         m 5
+    sel(A2, T.r1, o1, P.Q1);
+    sel(A2, T.r0, h, A2);                // (H | T | Z)
+    fdpp<kL1>(a, D);                     // lane 1: D of lane 0
+    fdpp<kL2>(b, h);                     // lane 2: H of lane 0
+    sel(B2, T.r1, a, b);
+    sel(B2, T.r0, h, B2);                // (H | D | H)
+    mul(o2, A2, B2);                     // (HH | S2 | Z H)
+    fp26_mul_int<4>(I, o2);              // lane 0: I = 4 HH           m 4
+    fp26_sub<3>(rr, o2, P.P1);           // lane 1: rr = S2 - Y        m 5
+    fp26_mul_int<2>(Z3, o2);             // lane 2: Z3 = 2 Z H         m 2
+    fdpp<kL1>(a, P.Xr);                  // lane 2: X of lane 1
+    sel(A3, T.r1, rr, a);
+    sel(A3, T.r0, h, A3);                // (H | rr | X)
+    fdpp<kL2>(b, I);                     // lane 2: I of lane 0
+    sel(B3, T.r1, rr, b);
+    sel(B3, T.r0, I, B3);                // (I | rr | I)
+    mul(o3, A3, B3);                     // (J | rr^2 | V)
+    fdpp<kR1>(R2, o3);
+    fp26_mul_int<4>(R2, R2);             // lane 0: r^2 = 4 rr^2       m 4
+    fdpp<kR2>(V, o3);                    // lane 0: V
+    fp26_sub<2>(X3, R2, o3);             //                            m 7
+    fp26_mul_int<2>(t, V);               //                            m 2
+    fp26_sub<3>(X3, X3, t);              //                            m 11
+    fp26_normalize_weak(X3);             // X3 = r^2 - J - 2V          m 2
+    fp26_sub<3>(W, V, X3);               // V - X3                     m 5
+    fdpp<kR1>(a, rr);                    // lane 0: rr of lane 1       m 5
+    sel(A4, T.r1, P.P1, Z3);
+    sel(A4, T.r0, a, A4);                // (rr | Y | Z3)
+    fdpp<kL1>(b, o3);                    // lane 1: J of lane 0
+    sel(B4, T.r1, b, Z3);
+    sel(B4, T.r0, W, B4);                // (V - X3 | J | Z3)
+    mul(o4, A4, B4);                     // (rr (V - X3) | Y J | Z3^2)
+    fdpp<kR1>(t, o4);
+    fp26_sub<2>(Y3, o4, t);              //                            m 4
+    fp26_mul_int<2>(Y3, Y3);             //                            m 8
+    fp26_normalize_weak(Y3);             // Y3 = r (V - X3) - 2 Y J    m 2
+    fdpp<kR2>(Dn, o4);                   // lane 0: Z3^2 of lane 2
+    TrioPtP O;
+    trio_state_sm2(O, X3, Y3, Z3, T);
+    O.inf = false;
+    if (P.inf) {
+        trio_from_aff_sm2(O, Q, T);
+        fp26_set(Dn, p26::ONE_R);
+    }
+    R = O;
+    fp26_copy(Dout, Dn);
+}
+
 // R <- P + Q (Q affine, never infinity); exceptional cases as CurveSM2x::madd, EXC = false drops the
 // P = +-Q tests for callers that exclude them (see the SM2 trio kernel in ecc_pair.hip)
 template <bool EXC = true>

@@ -277,6 +277,44 @@ void lane_main_sm2(int lane, int round) {
     trio_to_jac_sm2(J, P, T);
     if (t < 5 && !same_point_p(J, R)) pbad[c] = 1;
 }
+// the delta-carrying SM2 window: 4 trio_dbl_sm2_d + trio_madd_sm2_d (D = Z^2 travels with the point)
+std::vector<int> pdbad;
+void lane_main_sm2_d(int lane, int round) {
+    my_lane = lane;
+    const TrioLane T(lane);
+    const int t = (lane % 16) / 3;
+    const int c = round * cases_per_round + (t < 5 ? t : 4);
+    const CaseP& K = pcases[c];
+    TrioPtP P;
+    trio::sel(P.P1, T.r0, K.P.Z, K.P.Y);
+    trio::sel(P.Q1, T.r1, K.P.Y, K.P.Z);
+    P.Xr = K.P.X;
+    P.inf = K.P.inf;
+    fp26 D;
+    fp26_sqr(D, K.P.Z);
+    JacP26 R = K.P;
+    for (int rep = 0; rep < K.reps; ++rep) {
+        for (int d = 0; d < 4; ++d) {
+            trio_dbl_sm2_d(P, D, T);
+            CurveSM2x::dbl(R, R);
+        }
+        fp26 Dn;
+        trio_madd_sm2_d(P, Dn, P, D, K.Q, T);
+        D = Dn;
+        JacP26 S;
+        CurveSM2x::madd(S, R, K.Q);
+        R = S;
+    }
+    JacP26 J;
+    trio_to_jac_sm2(J, P, T);
+    bool ok = t >= 5 || same_point_p(J, R);
+    if (t < 5 && ok && !R.inf) {  // D on lane 0 = Z^2 of the result (Z on lane 2 -> every lane of J)
+        fp26 z2;
+        fp26_sqr(z2, J.Z);
+        ok = (T.r0 ? same_p(D, z2) : true);
+    }
+    if (t < 5 && !ok) pdbad[c] = 1;
+}
 // the SM2 chain's window as the kernel runs it: 3 trio_dbl_sm2 + trio_dbl_sm2_zz + trio_madd_sm2_zz
 std::vector<int> pzbad;
 void lane_main_sm2_zz(int lane, int round) {
@@ -460,6 +498,28 @@ int main() {
         for (int l = 0; l < kLanes; ++l) th.emplace_back(lane_main_sm2, l, r);
         for (auto& x : th) x.join();
     }
+    {  // the delta-carrying window over the same inputs, minus the P = +-Q cases
+        std::vector<CaseP> saved = pcases;
+        for (size_t k = 0; k < pcases.size(); ++k)
+            if (k % 10 == 1 || k % 10 == 2) rand_fp(pcases[k].P.Z, 3, 0);
+        pdbad.assign(pcases.size(), 0);
+        for (int r = 0; r < static_cast<int>(pcases.size()) / cases_per_round; ++r) {
+            std::vector<std::thread> th;
+            for (int l = 0; l < kLanes; ++l) th.emplace_back(lane_main_sm2_d, l, r);
+            for (auto& x : th) x.join();
+        }
+        int nd = 0;
+        for (size_t i = 0; i < pdbad.size(); ++i)
+            if (pdbad[i]) {
+                if (!nd) printf("sm2 delta window mismatch in case %zu (reps %d)\n", i, pcases[i].reps);
+                ++nd;
+            }
+        if (nd) {
+            printf("trio sm2 delta mismatches %d of %zu\n", nd, pcases.size());
+            return 1;
+        }
+        pcases = saved;
+    }
     {  // the zz window over the same inputs, minus the P = +-Q cases
         std::vector<CaseP> saved = pcases;
         for (size_t k = 0; k < pcases.size(); ++k)
@@ -502,7 +562,7 @@ int main() {
         printf("trio mismatches %d of %zu\n", nbad, cases.size());
         return 1;
     }
-    printf("trio ok %zu secp256k1 + %zu zz windows + %zu secp256k1 add + %zu sm2 + %zu sm2 zz windows\n", cases.size(),
+    printf("trio ok %zu secp256k1 + %zu zz windows + %zu secp256k1 add + %zu sm2 + %zu sm2 zz / delta windows\n", cases.size(),
            cases.size(), acases.size(), pcases.size(), pcases.size());
     return 0;
 }
