@@ -10,9 +10,11 @@
 //   madd (5 levels): the secp256k1 split (Z^2 | y2 Z | Z^2 -> U2 | S2 | U2 -> H^2 | rr^2 | Z H ->
 //                   J | - | V -> rr (V - X3) | Y J), with CurveSM2x's weak normalisations
 //
-// a = -3 makes alpha^3 a degree-12 term, so the doubling keeps four product levels (secp256k1's has
-// three).  A point lives in the trio as TrioPtP: P1 = (Z | Y | Y) and Q1 = (Z | Y | Z) (the first
-// doubling level's operands), Xr = (X | X | -); inf on every lane.  dbl: X <= 5, Y, Z <= 8 ->
+// a = -3 makes alpha^3 a degree-12 term, so the doubling above keeps four product levels (secp256k1's
+// has three) -- unless delta = Z^2 travels with the point: the SM2 trio kernel's chain uses
+// trio_dbl_sm2_d / trio_madd_sm2_d below (three levels per doubling, four per addition).  A point
+// lives in the trio as TrioPtP: P1 = (Z | Y | Y) and Q1 = (Z | Y | Z) (the first doubling level's
+// operands), Xr = (X | X | -); inf on every lane.  dbl: X <= 5, Y, Z <= 8 ->
 // (2, 2, 2); madd: X, Y <= 2, Z <= 8, Q <= 2 -> (2, 2, 2).
 #pragma once
 #include "ec26_trio.h"
@@ -114,97 +116,6 @@ F26_HD void trio_dbl_sm2(TrioPtP& P, const TrioLane& T) {
     fp26_normalize_weak(Y3);             // Y3                         m 2
     fp26_mul_int<2>(Z3, o1);             // lane 2: Z3 = 2 Y Z         m 2
     trio_state_sm2(P, X3, Y3, Z3, T);
-}
-
-// P <- 2P as trio_dbl_sm2, and ZZ = Z3^2 on lane 2 for the mixed addition that follows
-// (trio_madd_sm2_zz): the third level squares alpha on lane 0 only, so lane 2 squares Z3 = 2 Y Z there.
-// (X <= 5, Y, Z <= 8 -> (2, 2, 2), ZZ m 1)
-F26_HD void trio_dbl_sm2_zz(TrioPtP& P, fp26& ZZ, const TrioLane& T) {
-    using namespace trio;
-    fp26 o1, t, u, g, P2, Q2, o2, al, S3, o3, be, g2, b8, X3, t4, Y3p, Y3, Z3;
-    mul(o1, P.P1, P.Q1);                 // (delta | gamma | Y Z)
-    fp26_sub<2>(t, P.Xr, o1);            // lane 0: X - delta          m X + 3
-    fp26_add(u, P.Xr, o1);               // lane 0: X + delta          m X + 1
-    fdpp<kL1>(g, o1);                    // lane 2: gamma of lane 1
-    sel(P2, T.r0, t, P.Xr);
-    sel(P2, T.r2, g, P2);                // (X - d | X | gamma)
-    sel(Q2, T.r0, u, o1);
-    sel(Q2, T.r2, g, Q2);                // (X + d | gamma | gamma)
-    mul(o2, P2, Q2);                     // (alpha / 3 | beta | gamma^2)
-    fp26_mul_int<3>(al, o2);             // lane 0: alpha              m 3
-    fp26_mul_int<2>(Z3, o1);             // lane 2: Z3 = 2 Y Z         m 2
-    sel(S3, T.r2, Z3, al);
-    sqr(o3, S3);                         // (alpha^2 | - | Z3^2)
-    fp26_copy(ZZ, o3);                   // lane 2: Z3^2               m 1
-    fdpp<kR1>(be, o2);                   // lane 0: beta
-    fdpp<kR2>(g2, o2);                   // lane 0: gamma^2
-    fp26_mul_int<8>(b8, be);             //                            m 8
-    fp26_sub<9>(X3, o3, b8);             //                            m 11
-    fp26_normalize_weak(X3);             // X3 = alpha^2 - 8 beta      m 2
-    fp26_mul_int<4>(t4, be);             //                            m 4
-    fp26_sub<3>(t4, t4, X3);             // 4 beta - X3                m 8
-    mul(Y3p, al, t4);
-    fp26_mul_int<8>(g2, g2);             //                            m 8
-    fp26_sub<9>(Y3, Y3p, g2);            //                            m 11
-    fp26_normalize_weak(Y3);             // Y3                         m 2
-    trio_state_sm2(P, X3, Y3, Z3, T);
-}
-
-// R <- P + Q, Q affine, given ZZ = Z1^2 on lane 2 (trio_dbl_sm2_zz): CurveSM2x::madd in 4 product
-// levels, without the P = +-Q tests (the t P chain's additions, see the SM2 trio kernel); P = infinity
-// gives Q.  X, Y <= 2, Z <= 8, ZZ <= 1, Q <= 2 -> (2, 2, 2).
-//   L1  U2 = x2 ZZ       | T = y2 Z        | --
-//   L2  HH = H^2         | S2 = T ZZ       | Z H          (H = U2 - X on lane 0)
-//   L3  J = H I          | rr^2            | V = X I      (I = 4 HH, rr = S2 - Y on lane 1)
-//   L4  rr (V - X3)      | Y J             | --           (X3 = 4 rr^2 - J - 2V on lane 0)
-F26_HD void trio_madd_sm2_zz(TrioPtP& R, const TrioPtP& P, const fp26& ZZ, const AffP26& Q, const TrioLane& T) {
-    using namespace trio;
-    fp26 a, b, A1, B1, o1, h, A2, B2, o2, I, rr, A3, B3, o3, R2, V, X3, t, W, A4, B4, o4, Y3, Z3;
-    fdpp<kR2>(a, ZZ);                    // lane 0: ZZ of lane 2
-    fdpp<kR1>(b, P.Q1);                  // lane 1: Z of lane 2
-    sel(A1, T.r1, Q.y, Q.x);             // (x2 | y2 | x2)
-    sel(B1, T.r0, a, b);                 // (ZZ | Z | -)
-    mul(o1, A1, B1);                     // (U2 | T | -)
-    fp26_sub<3>(h, o1, P.Xr);            // lane 0: H = U2 - X         m 5
-    sel(A2, T.r1, o1, P.Q1);
-    sel(A2, T.r0, h, A2);                // (H | T | Z)
-    fdpp<kR1>(a, ZZ);                    // lane 1: ZZ of lane 2
-    fdpp<kL2>(b, h);                     // lane 2: H of lane 0
-    sel(B2, T.r1, a, b);
-    sel(B2, T.r0, h, B2);                // (H | ZZ | H)
-    mul(o2, A2, B2);                     // (HH | S2 | Z H)
-    fp26_mul_int<4>(I, o2);              // lane 0: I = 4 HH           m 4
-    fp26_sub<3>(rr, o2, P.P1);           // lane 1: rr = S2 - Y        m 5
-    fdpp<kL1>(a, P.Xr);                  // lane 2: X of lane 1
-    sel(A3, T.r1, rr, a);
-    sel(A3, T.r0, h, A3);                // (H | rr | X)
-    fdpp<kL2>(b, I);                     // lane 2: I of lane 0
-    sel(B3, T.r1, rr, b);
-    sel(B3, T.r0, I, B3);                // (I | rr | I)
-    mul(o3, A3, B3);                     // (J | rr^2 | V)
-    fdpp<kR1>(R2, o3);
-    fp26_mul_int<4>(R2, R2);             // lane 0: r^2 = 4 rr^2       m 4
-    fdpp<kR2>(V, o3);                    // lane 0: V
-    fp26_sub<2>(X3, R2, o3);             //                            m 7
-    fp26_mul_int<2>(t, V);               //                            m 2
-    fp26_sub<3>(X3, X3, t);              //                            m 11
-    fp26_normalize_weak(X3);             // X3 = r^2 - J - 2V          m 2
-    fp26_sub<3>(W, V, X3);               // V - X3                     m 5
-    fdpp<kR1>(a, rr);                    // lane 0: rr of lane 1       m 5
-    sel(A4, T.r0, a, P.P1);              // (rr | Y | -)
-    fdpp<kL1>(b, o3);                    // lane 1: J of lane 0
-    sel(B4, T.r0, W, b);                 // (V - X3 | J | -)
-    mul(o4, A4, B4);                     // (rr (V - X3) | Y J | -)
-    fdpp<kR1>(t, o4);
-    fp26_sub<2>(Y3, o4, t);              //                            m 4
-    fp26_mul_int<2>(Y3, Y3);             //                            m 8
-    fp26_normalize_weak(Y3);             // Y3 = r (V - X3) - 2 Y J    m 2
-    fp26_mul_int<2>(Z3, o2);             // lane 2: Z3 = 2 Z H         m 2
-    TrioPtP O;
-    trio_state_sm2(O, X3, Y3, Z3, T);
-    O.inf = false;
-    if (P.inf) trio_from_aff_sm2(O, Q, T);
-    R = O;
 }
 
 // ---- the delta-carrying chain (the SM2 trio kernel's window): the point travels with D = delta = Z^2

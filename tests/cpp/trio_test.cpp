@@ -315,36 +315,6 @@ void lane_main_sm2_d(int lane, int round) {
     }
     if (t < 5 && !ok) pdbad[c] = 1;
 }
-// the SM2 chain's window as the kernel runs it: 3 trio_dbl_sm2 + trio_dbl_sm2_zz + trio_madd_sm2_zz
-std::vector<int> pzbad;
-void lane_main_sm2_zz(int lane, int round) {
-    my_lane = lane;
-    const TrioLane T(lane);
-    const int t = (lane % 16) / 3;
-    const int c = round * cases_per_round + (t < 5 ? t : 4);
-    const CaseP& K = pcases[c];
-    TrioPtP P;
-    trio::sel(P.P1, T.r0, K.P.Z, K.P.Y);
-    trio::sel(P.Q1, T.r1, K.P.Y, K.P.Z);
-    P.Xr = K.P.X;
-    P.inf = K.P.inf;
-    JacP26 R = K.P;
-    for (int rep = 0; rep < K.reps; ++rep) {
-        fp26 ZZ;
-        trio_dbl_sm2(P, T);
-        trio_dbl_sm2(P, T);
-        trio_dbl_sm2(P, T);
-        trio_dbl_sm2_zz(P, ZZ, T);
-        trio_madd_sm2_zz(P, P, ZZ, K.Q, T);
-        for (int d = 0; d < 4; ++d) CurveSM2x::dbl(R, R);
-        JacP26 S;
-        CurveSM2x::madd(S, R, K.Q);
-        R = S;
-    }
-    JacP26 J;
-    trio_to_jac_sm2(J, P, T);
-    if (t < 5 && !same_point_p(J, R)) pzbad[c] = 1;
-}
 }  // namespace
 
 int main() {
@@ -520,28 +490,6 @@ int main() {
         }
         pcases = saved;
     }
-    {  // the zz window over the same inputs, minus the P = +-Q cases
-        std::vector<CaseP> saved = pcases;
-        for (size_t k = 0; k < pcases.size(); ++k)
-            if (k % 10 == 1 || k % 10 == 2) rand_fp(pcases[k].P.Z, 3, 0);
-        pzbad.assign(pcases.size(), 0);
-        for (int r = 0; r < static_cast<int>(pcases.size()) / cases_per_round; ++r) {
-            std::vector<std::thread> th;
-            for (int l = 0; l < kLanes; ++l) th.emplace_back(lane_main_sm2_zz, l, r);
-            for (auto& x : th) x.join();
-        }
-        int nz = 0;
-        for (size_t i = 0; i < pzbad.size(); ++i)
-            if (pzbad[i]) {
-                if (!nz) printf("sm2 zz window mismatch in case %zu (reps %d)\n", i, pcases[i].reps);
-                ++nz;
-            }
-        if (nz) {
-            printf("trio sm2 zz mismatches %d of %zu\n", nz, pcases.size());
-            return 1;
-        }
-        pcases = saved;
-    }
     int npbad = 0;
     for (size_t i = 0; i < pbad.size(); ++i)
         if (pbad[i]) {
@@ -562,7 +510,7 @@ int main() {
         printf("trio mismatches %d of %zu\n", nbad, cases.size());
         return 1;
     }
-    printf("trio ok %zu secp256k1 + %zu zz windows + %zu secp256k1 add + %zu sm2 + %zu sm2 zz / delta windows\n", cases.size(),
+    printf("trio ok %zu secp256k1 + %zu zz windows + %zu secp256k1 add + %zu sm2 + %zu sm2 delta windows\n", cases.size(),
            cases.size(), acases.size(), pcases.size(), pcases.size());
     return 0;
 }
