@@ -823,8 +823,18 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(IO io, uin
 // |K| >= 16 before each addition of |d| P, |d| <= 8, and |K| < n, so K = +-d (mod n) cannot occur for
 // a P of order n (SM2's cofactor is 1; a P off the curve fails its verdict).  Bit-identical to
 // tx_verify_kernel<1, *>.
+#ifdef BCOSGPU_SM2_TIMING  // tools/sm2bench.hip: phase timestamps of workgroup 0
+__device__ uint64_t g_sm2_t[4][8];
+#define SM2_T(k) \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_sm2_t[threadIdx.x >> 6][k] = clock64()
+#else
+#define SM2_T(k) \
+    do {         \
+    } while (0)
+#endif
 struct Sm2Trio26Lds {
     uint32_t tab[8][20][64];         // affine 1P..8P in the R' domain as fp26 limbs: [entry][x, y][tx]
+    uint32_t jtab[8][50][40];        // Jacobian 1P..8P: [entry][X, Y, Z, Z^2, Z^3][tx]
     uint32_t kt[8][64];              // t = r + s mod n
     uint32_t acc[25][64];            // the chains' results (canonical X, Y, Z, inf)
     uint32_t g[25][64];
@@ -880,8 +890,69 @@ __device__ __forceinline__ void trio_add_digit_sm2_d(TrioPtP& acc, fp26& D, cons
     fp26_cmov(D, Dn, d != 0);
 }
 
+// the window's addition before the affine table is ready: the Jacobian entry (trio_add_sm2_jd)
+__device__ __forceinline__ void trio_add_digit_sm2_jd(TrioPtP& acc, fp26& D, const Sm2Trio26Lds& L, int tl, int d,
+                                                      const TrioLane& T) {
+    const uint32_t m = static_cast<uint32_t>((d < 0 ? -d : d) - 1) & 7u;
+    const uint32_t* base = &L.jtab[0][0][0] + m * (50 * 40) + tl;
+    JacEntP26 E;
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+        E.X.v[q] = base[q * 40];
+        E.Y.v[q] = base[(10 + q) * 40];
+        E.Z.v[q] = base[(20 + q) * 40];
+        E.ZZ.v[q] = base[(30 + q) * 40];
+        E.ZZZ.v[q] = base[(40 + q) * 40];
+    }
+    F26_SETM(E.X, 1);
+    F26_SETM(E.Y, 1);
+    F26_SETM(E.Z, 1);
+    F26_SETM(E.ZZ, 1);
+    F26_SETM(E.ZZZ, 1);
+    fp26 ny;
+    fp26_neg<2>(ny, E.Y);
+    fp26_cmov(E.Y, ny, d < 0);
+    fp26_normalize_weak(E.Y);
+    TrioPtP R;
+    fp26 Dn;
+    trio_add_sm2_jd(R, Dn, acc, D, E, T);
+    trio_cmov_sm2(acc, R, d != 0);
+    fp26_cmov(D, Dn, d != 0);
+}
+
+// entry j of the Jacobian table from a trio's point (X, Z, D on lane 0, Y on lane 1), m 1
+__device__ __forceinline__ void trio_store_jent(Sm2Trio26Lds& L, int j, const TrioPtP& P, const fp26& D, int tl,
+                                                bool real, const TrioLane& T) {
+    fp26 a, b, c;
+    fp26_copy(a, P.Xr);
+    fp26_copy(b, P.P1);  // lane 0: Z, lane 1: Y
+    fp26_copy(c, D);
+    fp26_normalize(a);
+    fp26_normalize(b);
+    fp26_normalize(c);
+    if (real && T.r0) {
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+            L.jtab[j][q][tl] = a.v[q];
+            L.jtab[j][20 + q][tl] = b.v[q];
+            L.jtab[j][30 + q][tl] = c.v[q];
+        }
+    }
+    if (real && T.r1) {
+#pragma unroll
+        for (int q = 0; q < 10; ++q) L.jtab[j][10 + q][tl] = b.v[q];
+    }
+}
+
+__device__ __forceinline__ void lds_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 template <class IO>
-__global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab) {
+__global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab,
+                                                                        int affine) {
     constexpr int TPW = 40;
     __shared__ Sm2Trio26Lds L;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -889,6 +960,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
     const bool active = lane < TPW && i < n;
     if (threadIdx.x < 4) L.seq[threadIdx.x] = 0u;
     __syncthreads();
+    SM2_T(0);
     const uint8_t* sp = nullptr;
     const bool len_ok = active && io.sig_span(i, sp) == 128u;
     fe r, s, px, py;
@@ -927,40 +999,104 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
     fp26_from_plain(P.x, px);
     fp26_from_plain(P.y, py);
     if (wave <= 1) {
+        // entry 0 of both tables is P itself (one lane per tx; waves 0 and 1 write the same values)
         {
-            AffP26 A[8];
-            sm2_affine_table26(A, P);
-            Unroll<0, 8>::run([&](auto J) {
-                constexpr int j = decltype(J)::value;
-                fp26 x, y;
-                fp26_copy(x, A[j].x);
-                fp26_copy(y, A[j].y);
-                fp26_normalize(x);
-                fp26_normalize(y);
+            fp26 x, y, one;
+            fp26_copy(x, P.x);
+            fp26_copy(y, P.y);
+            fp26_normalize(x);
+            fp26_normalize(y);
+            fp26_set(one, p26::ONE_R);
+            fp26_normalize(one);
+#pragma unroll
+            for (int q = 0; q < 10; ++q) {
+                L.tab[0][q][lane] = x.v[q];
+                L.tab[0][10 + q][lane] = y.v[q];
+            }
+            if (lane < TPW) {
 #pragma unroll
                 for (int q = 0; q < 10; ++q) {
-                    L.tab[j][q][lane] = x.v[q];
-                    L.tab[j][10 + q][lane] = y.v[q];
+                    L.jtab[0][q][lane] = x.v[q];
+                    L.jtab[0][10 + q][lane] = y.v[q];
+                    L.jtab[0][20 + q][lane] = one.v[q];
+                    L.jtab[0][30 + q][lane] = one.v[q];
+                    L.jtab[0][40 + q][lane] = one.v[q];
                 }
-            });
+            }
 #pragma unroll
             for (int q = 0; q < 8; ++q) L.kt[q][lane] = t.v[q];
         }
-        // this wave's own LDS writes before its trio lanes read them (waves 0 and 1 write the same values)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        lds_wave_sync();  // this wave's own LDS writes before its trio lanes read them
         const TrioLane T(lane);
         const int pos = lane & 15, trio_idx = pos / 3;
-        const int tl = wave * 20 + (lane >> 4) * 5 + (trio_idx < 5 ? trio_idx : 4);
+        const bool real = trio_idx < 5;
+        const int tl = wave * 20 + (lane >> 4) * 5 + (real ? trio_idx : 4);
+        // 2P .. 8P of this wave's 20 txs as Jacobian points on the trios (three / four product levels
+        // each), then Z^3 of every entry, one product per lane
+        {
+            AffP26 P0;
+#pragma unroll
+            for (int q = 0; q < 10; ++q) {
+                P0.x.v[q] = L.tab[0][q][tl];
+                P0.y.v[q] = L.tab[0][10 + q][tl];
+            }
+            F26_SETM(P0.x, 1);
+            F26_SETM(P0.y, 1);
+            TrioPtP M1, M2, M3, M;
+            fp26 D1, D2, D3, Dm;
+            trio_from_aff_sm2(M1, P0, T);
+            fp26_set(D1, p26::ONE_R);
+            trio_dbl_sm2_d(M1, D1, T);  // 2P
+            trio_store_jent(L, 1, M1, D1, tl, real, T);
+            trio_madd_sm2_d(M2, D2, M1, D1, P0, T);  // 3P
+            trio_store_jent(L, 2, M2, D2, tl, real, T);
+            M3 = M1;
+            fp26_copy(D3, D1);
+            trio_dbl_sm2_d(M3, D3, T);  // 4P
+            trio_store_jent(L, 3, M3, D3, tl, real, T);
+            trio_madd_sm2_d(M, Dm, M3, D3, P0, T);  // 5P
+            trio_store_jent(L, 4, M, Dm, tl, real, T);
+            trio_dbl_sm2_d(M2, D2, T);  // 6P
+            trio_store_jent(L, 5, M2, D2, tl, real, T);
+            trio_madd_sm2_d(M, Dm, M2, D2, P0, T);  // 7P
+            trio_store_jent(L, 6, M, Dm, tl, real, T);
+            trio_dbl_sm2_d(M3, D3, T);  // 8P
+            trio_store_jent(L, 7, M3, D3, tl, real, T);
+            lds_wave_sync();
+            const int role = T.r0 ? 0 : T.r1 ? 1 : 2;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const int j = 1 + role + 3 * r;
+                const int jj = j <= 7 ? j : 7;
+                fp26 z, zz, zzz;
+#pragma unroll
+                for (int q = 0; q < 10; ++q) {
+                    z.v[q] = L.jtab[jj][20 + q][tl];
+                    zz.v[q] = L.jtab[jj][30 + q][tl];
+                }
+                F26_SETM(z, 1);
+                F26_SETM(zz, 1);
+                fp26_mul(zzz, zz, z);
+                fp26_normalize(zzz);
+                if (real && j <= 7) {
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) L.jtab[jj][40 + q][tl] = zzz.v[q];
+                }
+            }
+            lds_wave_sync();
+            // this wave's 20 Jacobian tables are complete: wave 3 may build their affine forms
+            if (lane == 0) __hip_atomic_store(&L.seq[wave], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        SM2_T(1);
         fe k;
 #pragma unroll
         for (int q = 0; q < 8; ++q) k.v[q] = L.kt[q][tl];
         TrioPtP acc;
         trio_set_inf_sm2(acc);
-        trio_add_digit_sm2(acc, L, tl, static_cast<int>(k.v[7] >> 31), T);  // digit 64 = bit 255
+        trio_add_digit_sm2(acc, L, tl, static_cast<int>(k.v[7] >> 31), T);  // digit 64 = bit 255 (entry 0)
         fp26 D;  // delta = Z^2 of acc on lane 0 (an affine table point or infinity here)
         fp26_set(D, p26::ONE_R);
+        bool aff = false;  // wave-uniform: the affine table (wave 3) is ready
 #pragma unroll 1
         for (int w = 63; w >= 0; --w) {
             trio_dbl_sm2_d(acc, D, T);  // three product levels each (delta carried)
@@ -971,11 +1107,18 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
             const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
             shl4(k);
-            trio_add_digit_sm2_d(acc, D, L, tl, d, T);
+            if (!aff && affine)
+                aff = __builtin_amdgcn_readfirstlane(
+                          __hip_atomic_load(&L.seq[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0u;
+            if (aff)
+                trio_add_digit_sm2_d(acc, D, L, tl, d, T);  // four product levels
+            else
+                trio_add_digit_sm2_jd(acc, D, L, tl, d, T);  // five
         }
         JacP26 J;
         trio_to_jac_sm2(J, acc, T);
-        if (T.r0 && trio_idx < 5) pair26_store_jac(L.acc, J, tl);
+        if (T.r0 && real) pair26_store_jac(L.acc, J, tl);
+        SM2_T(2);
     } else if (wave == 2) {
         fe h;
         fe_zero(h);
@@ -994,7 +1137,9 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
 #pragma unroll
         for (int k = 0; k < 5; ++k) L.addr[k][lane] = ad[k];
         JacP26 G0, G1, G;
+        SM2_T(1);
         comb_range_sm2_26(G0, s, tab, 0, 16);
+        SM2_T(2);
         while (__hip_atomic_load(&L.seq[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
             __builtin_amdgcn_s_sleep(1);
         }
@@ -1002,12 +1147,65 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
         CurveSM2x::add(G, G0, G1);
         pair26_store_jac(L.g, G, lane);
     } else {
+        // the affine table of all 40 txs (one lane per tx) from the Jacobian entries of waves 0 and 1:
+        // one inversion of Z1 .. Z7, then x = X / Z^2, y = Y / Z^3; the chains switch to it when ready
+        while (__hip_atomic_load(&L.seq[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u ||
+               __hip_atomic_load(&L.seq[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+            __builtin_amdgcn_s_sleep(1);
+        }
+        {
+            const int c = lane < TPW ? lane : TPW - 1;
+            fp26 pre[8], inv;
+            fp26_set(pre[0], p26::ONE_R);
+            Unroll<1, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                fp26 z;
+#pragma unroll
+                for (int q = 0; q < 10; ++q) z.v[q] = L.jtab[j][20 + q][c];
+                F26_SETM(z, 1);
+                fp26_mul(pre[j], pre[j - 1], z);
+            });
+            fp26_inv(inv, pre[7]);  // (Z1 ... Z7)^-1
+            Unroll<0, 7>::run([&](auto J) {
+                constexpr int j = 7 - decltype(J)::value;
+                fp26 z, X, Y, zi, zi2, zi3, x, y;
+#pragma unroll
+                for (int q = 0; q < 10; ++q) {
+                    X.v[q] = L.jtab[j][q][c];
+                    Y.v[q] = L.jtab[j][10 + q][c];
+                    z.v[q] = L.jtab[j][20 + q][c];
+                }
+                F26_SETM(X, 1);
+                F26_SETM(Y, 1);
+                F26_SETM(z, 1);
+                fp26_mul(zi, inv, pre[j - 1]);  // Z_j^-1
+                fp26_mul(inv, inv, z);          // (Z1 .. Z(j-1))^-1
+                fp26_sqr(zi2, zi);
+                fp26_mul(zi3, zi2, zi);
+                fp26_mul(x, X, zi2);
+                fp26_mul(y, Y, zi3);
+                fp26_normalize(x);
+                fp26_normalize(y);
+                if (lane < TPW) {
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) {
+                        L.tab[j][q][lane] = x.v[q];
+                        L.tab[j][10 + q][lane] = y.v[q];
+                    }
+                }
+            });
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&L.seq[3], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         JacP26 G1;
+        SM2_T(1);
         comb_range_sm2_26(G1, s, tab, 16, 32);
+        SM2_T(2);
         pair26_store_jac(L.gh, G1, lane);
         __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
+    SM2_T(3);
     if (wave == 0 && active) {
         JacP26 G, A, Q;
         pair26_load_jac(G, L.g, lane);
@@ -1034,6 +1232,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
 #pragma unroll
         for (int k = 0; k < 5; ++k) ad[k] = ok ? L.addr[k][lane] : 0u;
         io.finish(i, ok, ad, nullptr, nullptr);
+        SM2_T(4);
     }
 }
 
@@ -1044,9 +1243,13 @@ int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n,
         const uint32_t* t26;
         const int rc = tables8_sm2_26(&t26);
         if (rc) return rc;
-        if (pol.coop == 2)
+        if (pol.coop == 2) {
+            // BCOSGPU_SM2_JAC_ONLY=1 (tests): every window adds the Jacobian entry (the affine table unused)
+            const char* jo = getenv("BCOSGPU_SM2_JAC_ONLY");
+            const int affine = jo && atoi(jo) != 0 ? 0 : 1;
             hipLaunchKernelGGL(tx_verify_sm2_trio26_kernel<IO>, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0,
-                               st, io, n, t26);
+                               st, io, n, t26, affine);
+        }
         else
             hipLaunchKernelGGL(tx_verify_sm2_pair26_kernel<IO>, grid, dim3(256), 0, st, io, n, t26);
     } else if constexpr (std::is_same_v<IO, TxIO>) {

@@ -222,6 +222,88 @@ F26_HD void trio_madd_sm2_d(TrioPtP& R, fp26& Dout, const TrioPtP& P, const fp26
     fp26_copy(Dout, Dn);
 }
 
+// a Jacobian table entry with its Z powers (the SM2 trio kernel's chain adds these while the affine
+// table is still being built): every element m 1
+struct JacEntP26 {
+    fp26 X, Y, Z, ZZ, ZZZ;
+};
+
+// R <- P + Q, Q a Jacobian table entry (never infinity), given D = Z1^2 on lane 0: CurveSM2x::add's
+// point in 5 product levels, without the P = +-Q tests (as trio_madd_sm2_d), returning the sum's
+// D = Z3^2 on lane 0; P = infinity gives Q (D = ZZ2).  X, Y <= 2, Z <= 8, D <= 1 -> (2, 2, 2), D m 1.
+//   L1  U2 = X2 D        | T = Y2 Z1       | U1 = X1 ZZ2
+//   L2  Z1 Z2            | S2 = T D        | S1 = Y1 ZZZ2   (H = U2 - U1 on lane 0)
+//   L3  HH = H^2         | rr^2            | Z1 Z2 H        (rr = S2 - S1 on lane 1)
+//   L4  J = H I          | Z3^2            | V = U1 I       (I = 4 HH, Z3 = 2 Z1 Z2 H)
+//   L5  rr (V - X3)      | S1 J            | --             (X3 = 4 rr^2 - J - 2V on lane 0)
+F26_HD void trio_add_sm2_jd(TrioPtP& R, fp26& Dout, const TrioPtP& P, const fp26& D, const JacEntP26& Q,
+                            const TrioLane& T) {
+    using namespace trio;
+    fp26 a, b, A1, B1, o1, h, A2, B2, o2, rr, A3, B3, o3, I, Z3, R2, A4, B4, o4, V, X3, t, W, A5, B5, o5, Y3, Dn;
+    fdpp<kR1>(a, P.Q1);                  // lane 1: Z of lane 2
+    fdpp<kL1>(b, P.Xr);                  // lane 2: X of lane 1
+    sel(A1, T.r1, Q.Y, Q.X);
+    sel(A1, T.r2, b, A1);                // (X2 | Y2 | X1)
+    sel(B1, T.r1, a, Q.ZZ);
+    sel(B1, T.r0, D, B1);                // (D | Z1 | ZZ2)
+    mul(o1, A1, B1);                     // (U2 | T | U1)
+    fdpp<kR2>(a, o1);                    // lane 0: U1 of lane 2
+    fp26_sub<2>(h, o1, a);               // lane 0: H = U2 - U1        m 4
+    fdpp<kL1>(b, D);                     // lane 1: D of lane 0
+    sel(B2, T.r1, b, Q.ZZZ);
+    sel(B2, T.r0, Q.Z, B2);              // (Z2 | D | ZZZ2)
+    sel(A2, T.r1, o1, P.P1);             // (Z1 | T | Y1)
+    mul(o2, A2, B2);                     // (Z1 Z2 | S2 | S1)
+    fdpp<kR1>(a, o2);                    // lane 1: S1 of lane 2
+    fp26_sub<2>(rr, o2, a);              // lane 1: rr = S2 - S1       m 4
+    fdpp<kL2>(a, o2);                    // lane 2: Z1 Z2 of lane 0
+    fdpp<kL2>(b, h);                     // lane 2: H of lane 0
+    sel(A3, T.r1, rr, a);
+    sel(A3, T.r0, h, A3);                // (H | rr | Z1 Z2)
+    sel(B3, T.r1, rr, b);
+    sel(B3, T.r0, h, B3);                // (H | rr | H)
+    mul(o3, A3, B3);                     // (HH | rr^2 | Z1 Z2 H)
+    fp26_mul_int<4>(I, o3);              // lane 0: I = 4 HH           m 4
+    fp26_mul_int<2>(Z3, o3);             // lane 2: Z3 = 2 Z1 Z2 H     m 2
+    fdpp<kR1>(R2, o3);
+    fp26_mul_int<4>(R2, R2);             // lane 0: r^2 = 4 rr^2       m 4
+    fdpp<kR1>(a, Z3);                    // lane 1: Z3 of lane 2
+    fdpp<kL2>(b, I);                     // lane 2: I of lane 0
+    sel(A4, T.r1, a, o1);
+    sel(A4, T.r0, h, A4);                // (H | Z3 | U1)
+    sel(B4, T.r1, a, b);
+    sel(B4, T.r0, I, B4);                // (I | Z3 | I)
+    mul(o4, A4, B4);                     // (J | Z3^2 | V)
+    fdpp<kR2>(V, o4);                    // lane 0: V
+    fp26_sub<2>(X3, R2, o4);             //                            m 7
+    fp26_mul_int<2>(t, V);               //                            m 2
+    fp26_sub<3>(X3, X3, t);              //                            m 11
+    fp26_normalize_weak(X3);             // X3 = r^2 - J - 2V          m 2
+    fp26_sub<3>(W, V, X3);               // V - X3                     m 5
+    fdpp<kR1>(a, rr);                    // lane 0: rr of lane 1       m 4
+    fdpp<kR1>(b, o2);                    // lane 1: S1 of lane 2
+    sel(A5, T.r0, a, b);                 // (rr | S1 | -)
+    fdpp<kL1>(b, o4);                    // lane 1: J of lane 0
+    sel(B5, T.r0, W, b);                 // (V - X3 | J | -)
+    mul(o5, A5, B5);                     // (rr (V - X3) | S1 J | -)
+    fdpp<kR1>(t, o5);
+    fp26_sub<2>(Y3, o5, t);              //                            m 4
+    fp26_mul_int<2>(Y3, Y3);             //                            m 8
+    fp26_normalize_weak(Y3);             // Y3 = r (V - X3) - 2 S1 J   m 2
+    fdpp<kR1>(Dn, o4);                   // lane 0: Z3^2 of lane 1
+    TrioPtP O;
+    trio_state_sm2(O, X3, Y3, Z3, T);
+    O.inf = false;
+    if (P.inf) {
+        trio::sel(O.P1, T.r0, Q.Z, Q.Y);
+        trio::sel(O.Q1, T.r1, Q.Y, Q.Z);
+        fp26_copy(O.Xr, Q.X);
+        fp26_copy(Dn, Q.ZZ);
+    }
+    R = O;
+    fp26_copy(Dout, Dn);
+}
+
 // R <- P + Q (Q affine, never infinity); exceptional cases as CurveSM2x::madd, EXC = false drops the
 // P = +-Q tests for callers that exclude them (see the SM2 trio kernel in ecc_pair.hip)
 template <bool EXC = true>

@@ -315,6 +315,52 @@ void lane_main_sm2_d(int lane, int round) {
     }
     if (t < 5 && !ok) pdbad[c] = 1;
 }
+
+// the window with a Jacobian table entry (trio_add_sm2_jd) against CurveSM2x::dbl / add, and D = Z^2
+std::vector<JacEntP26> pqj;
+std::vector<int> pjbad;
+void lane_main_sm2_jd(int lane, int round) {
+    my_lane = lane;
+    const TrioLane T(lane);
+    const int t = (lane % 16) / 3;
+    const int c = round * cases_per_round + (t < 5 ? t : 4);
+    const CaseP& K = pcases[c];
+    const JacEntP26& Q = pqj[c];
+    JacP26 QJ;
+    QJ.X = Q.X;
+    QJ.Y = Q.Y;
+    QJ.Z = Q.Z;
+    QJ.inf = false;
+    TrioPtP P;
+    trio::sel(P.P1, T.r0, K.P.Z, K.P.Y);
+    trio::sel(P.Q1, T.r1, K.P.Y, K.P.Z);
+    P.Xr = K.P.X;
+    P.inf = K.P.inf;
+    fp26 D;
+    fp26_sqr(D, K.P.Z);
+    JacP26 R = K.P;
+    for (int rep = 0; rep < K.reps; ++rep) {
+        for (int d = 0; d < 4; ++d) {
+            trio_dbl_sm2_d(P, D, T);
+            CurveSM2x::dbl(R, R);
+        }
+        fp26 Dn;
+        trio_add_sm2_jd(P, Dn, P, D, Q, T);
+        D = Dn;
+        JacP26 S;
+        CurveSM2x::add(S, R, QJ);
+        R = S;
+    }
+    JacP26 J;
+    trio_to_jac_sm2(J, P, T);
+    bool ok = t >= 5 || same_point_p(J, R);
+    if (t < 5 && ok && !R.inf) {
+        fp26 z2;
+        fp26_sqr(z2, J.Z);
+        ok = (T.r0 ? same_p(D, z2) : true);
+    }
+    if (t < 5 && !ok) pjbad[c] = 1;
+}
 }  // namespace
 
 int main() {
@@ -488,6 +534,33 @@ int main() {
             printf("trio sm2 delta mismatches %d of %zu\n", nd, pcases.size());
             return 1;
         }
+        // the Jacobian-entry window over the same inputs (Q: random X, Y, Z with its Z powers)
+        pqj.clear();
+        for (size_t k = 0; k < pcases.size(); ++k) {
+            JacEntP26 E;
+            rand_fp(E.X, 1, k % 7 == 6 ? 1 : 0);
+            rand_fp(E.Y, 1, 0);
+            rand_fp(E.Z, 1, 0);
+            fp26_sqr(E.ZZ, E.Z);
+            fp26_mul(E.ZZZ, E.ZZ, E.Z);
+            pqj.push_back(E);
+        }
+        pjbad.assign(pcases.size(), 0);
+        for (int r = 0; r < static_cast<int>(pcases.size()) / cases_per_round; ++r) {
+            std::vector<std::thread> th;
+            for (int l = 0; l < kLanes; ++l) th.emplace_back(lane_main_sm2_jd, l, r);
+            for (auto& x : th) x.join();
+        }
+        int nj = 0;
+        for (size_t i = 0; i < pjbad.size(); ++i)
+            if (pjbad[i]) {
+                if (!nj) printf("sm2 jacobian-entry window mismatch in case %zu (reps %d)\n", i, pcases[i].reps);
+                ++nj;
+            }
+        if (nj) {
+            printf("trio sm2 jacobian-entry mismatches %d of %zu\n", nj, pcases.size());
+            return 1;
+        }
         pcases = saved;
     }
     int npbad = 0;
@@ -510,7 +583,8 @@ int main() {
         printf("trio mismatches %d of %zu\n", nbad, cases.size());
         return 1;
     }
-    printf("trio ok %zu secp256k1 + %zu zz windows + %zu secp256k1 add + %zu sm2 + %zu sm2 delta windows\n", cases.size(),
-           cases.size(), acases.size(), pcases.size(), pcases.size());
+    printf("trio ok %zu secp256k1 + %zu zz windows + %zu secp256k1 add + %zu sm2 + %zu sm2 delta windows + %zu sm2 "
+           "jacobian-entry windows\n",
+           cases.size(), cases.size(), acases.size(), pcases.size(), pcases.size(), pcases.size());
     return 0;
 }

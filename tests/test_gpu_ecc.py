@@ -6,6 +6,8 @@ throws, wrong-hash cases), bcos-txpool/test/unittests/txpool/TxPoolTest.cpp:469-
 over another hash is accepted with a different sender; SM2 rejects it) and
 bcos-executor/test/old/EVMPrecompiledTest.cpp:58-72 (ecrecover vector).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -265,21 +267,29 @@ def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
     wh, ws, wst = oracle.tx_verify_packed(suite, pre, po.astype(np.uint64), sg, so.astype(np.uint64), nthreads=16)
     # secp256k1: lane-trio, cooperative-pair, 4-wave split, one-lane occ 1 / 2 on the 10 x 26-bit and on the
     # 8 x 32-bit point arithmetic; SM2: lane-trio and pair kernels and one-lane occ 1 / 2, each on fp26 and 8 x 32
+    # (the SM2 lane-trio kernel once more with every window on the Jacobian table entries:
+    # BCOSGPU_SM2_JAC_ONLY, read at each launch)
     variants = ([(1, 1, 2, 1), (1, 1, 1, 1), (1, 1, 0, 1), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)]
                 if suite == 0
-                else [(1, 1, 2, 1), (1, 1, 1, 1), (1, 1, 1, 0), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)])
+                else [(1, 1, 2, 1), (1, 1, 2, 1, "jac"), (1, 1, 1, 1), (1, 1, 1, 0), (0, 1, 0, 1), (0, 2, 0, 1),
+                      (0, 1, 0, 0), (0, 2, 0, 0)])
     try:
-        for split, occ, coop, field in variants:
+        for split, occ, coop, field, *jac in variants:
+            if jac:
+                os.environ["BCOSGPU_SM2_JAC_ONLY"] = "1"
+            else:
+                os.environ.pop("BCOSGPU_SM2_JAC_ONLY", None)
             gpu.set_tx_kernel_policy(split, occ, coop, field)
             th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
             snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
             st = torch.empty(n, dtype=torch.uint8, device="cuda")
             device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
             torch.cuda.synchronize()
-            assert np.array_equal(th.cpu().numpy(), wh), (split, occ, field)
-            assert np.array_equal(st.cpu().numpy(), wst), (split, occ, field)
-            assert np.array_equal(snd.cpu().numpy(), ws), (split, occ, field)
+            assert np.array_equal(th.cpu().numpy(), wh), (split, occ, field, jac)
+            assert np.array_equal(st.cpu().numpy(), wst), (split, occ, field, jac)
+            assert np.array_equal(snd.cpu().numpy(), ws), (split, occ, field, jac)
     finally:
+        os.environ.pop("BCOSGPU_SM2_JAC_ONLY", None)
         gpu.set_tx_kernel_policy()
 
 
