@@ -998,95 +998,39 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
     AffP26 P;
     fp26_from_plain(P.x, px);
     fp26_from_plain(P.y, py);
-    if (wave <= 1) {
-        // entry 0 of both tables is P itself (one lane per tx; waves 0 and 1 write the same values)
-        {
-            fp26 x, y, one;
-            fp26_copy(x, P.x);
-            fp26_copy(y, P.y);
-            fp26_normalize(x);
-            fp26_normalize(y);
+    // entry 0 of both tables is P itself (one lane per tx; every wave writes the same values)
+    {
+        fp26 x, y, one;
+        fp26_copy(x, P.x);
+        fp26_copy(y, P.y);
+        fp26_normalize(x);
+        fp26_normalize(y);
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+            L.tab[0][q][lane] = x.v[q];
+            L.tab[0][10 + q][lane] = y.v[q];
+        }
+        if (wave >= 2 && lane < TPW) {
             fp26_set(one, p26::ONE_R);
             fp26_normalize(one);
 #pragma unroll
             for (int q = 0; q < 10; ++q) {
-                L.tab[0][q][lane] = x.v[q];
-                L.tab[0][10 + q][lane] = y.v[q];
+                L.jtab[0][q][lane] = x.v[q];
+                L.jtab[0][10 + q][lane] = y.v[q];
+                L.jtab[0][20 + q][lane] = one.v[q];
+                L.jtab[0][30 + q][lane] = one.v[q];
+                L.jtab[0][40 + q][lane] = one.v[q];
             }
-            if (lane < TPW) {
-#pragma unroll
-                for (int q = 0; q < 10; ++q) {
-                    L.jtab[0][q][lane] = x.v[q];
-                    L.jtab[0][10 + q][lane] = y.v[q];
-                    L.jtab[0][20 + q][lane] = one.v[q];
-                    L.jtab[0][30 + q][lane] = one.v[q];
-                    L.jtab[0][40 + q][lane] = one.v[q];
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) L.kt[q][lane] = t.v[q];
         }
+    }
+    if (wave <= 1) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) L.kt[q][lane] = t.v[q];
         lds_wave_sync();  // this wave's own LDS writes before its trio lanes read them
         const TrioLane T(lane);
         const int pos = lane & 15, trio_idx = pos / 3;
         const bool real = trio_idx < 5;
         const int tl = wave * 20 + (lane >> 4) * 5 + (real ? trio_idx : 4);
-        // 2P .. 8P of this wave's 20 txs as Jacobian points on the trios (three / four product levels
-        // each), then Z^3 of every entry, one product per lane
-        {
-            AffP26 P0;
-#pragma unroll
-            for (int q = 0; q < 10; ++q) {
-                P0.x.v[q] = L.tab[0][q][tl];
-                P0.y.v[q] = L.tab[0][10 + q][tl];
-            }
-            F26_SETM(P0.x, 1);
-            F26_SETM(P0.y, 1);
-            TrioPtP M1, M2, M3, M;
-            fp26 D1, D2, D3, Dm;
-            trio_from_aff_sm2(M1, P0, T);
-            fp26_set(D1, p26::ONE_R);
-            trio_dbl_sm2_d(M1, D1, T);  // 2P
-            trio_store_jent(L, 1, M1, D1, tl, real, T);
-            trio_madd_sm2_d(M2, D2, M1, D1, P0, T);  // 3P
-            trio_store_jent(L, 2, M2, D2, tl, real, T);
-            M3 = M1;
-            fp26_copy(D3, D1);
-            trio_dbl_sm2_d(M3, D3, T);  // 4P
-            trio_store_jent(L, 3, M3, D3, tl, real, T);
-            trio_madd_sm2_d(M, Dm, M3, D3, P0, T);  // 5P
-            trio_store_jent(L, 4, M, Dm, tl, real, T);
-            trio_dbl_sm2_d(M2, D2, T);  // 6P
-            trio_store_jent(L, 5, M2, D2, tl, real, T);
-            trio_madd_sm2_d(M, Dm, M2, D2, P0, T);  // 7P
-            trio_store_jent(L, 6, M, Dm, tl, real, T);
-            trio_dbl_sm2_d(M3, D3, T);  // 8P
-            trio_store_jent(L, 7, M3, D3, tl, real, T);
-            lds_wave_sync();
-            const int role = T.r0 ? 0 : T.r1 ? 1 : 2;
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const int j = 1 + role + 3 * r;
-                const int jj = j <= 7 ? j : 7;
-                fp26 z, zz, zzz;
-#pragma unroll
-                for (int q = 0; q < 10; ++q) {
-                    z.v[q] = L.jtab[jj][20 + q][tl];
-                    zz.v[q] = L.jtab[jj][30 + q][tl];
-                }
-                F26_SETM(z, 1);
-                F26_SETM(zz, 1);
-                fp26_mul(zzz, zz, z);
-                fp26_normalize(zzz);
-                if (real && j <= 7) {
-#pragma unroll
-                    for (int q = 0; q < 10; ++q) L.jtab[jj][40 + q][tl] = zzz.v[q];
-                }
-            }
-            lds_wave_sync();
-            // this wave's 20 Jacobian tables are complete: wave 3 may build their affine forms
-            if (lane == 0) __hip_atomic_store(&L.seq[wave], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
         SM2_T(1);
         fe k;
 #pragma unroll
@@ -1107,6 +1051,11 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
             const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
             shl4(k);
+            if (w == 63) {  // this wave's Jacobian table (built by wave 2 + this wave) before the first addition
+                while (__hip_atomic_load(&L.seq[wave], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
             if (!aff && affine)
                 aff = __builtin_amdgcn_readfirstlane(
                           __hip_atomic_load(&L.seq[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0u;
@@ -1119,90 +1068,157 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
         trio_to_jac_sm2(J, acc, T);
         if (T.r0 && real) pair26_store_jac(L.acc, J, tl);
         SM2_T(2);
-    } else if (wave == 2) {
-        fe h;
-        fe_zero(h);
-        if (active) io.template digest<SM3>(i, h);
-        uint32_t eb[8];
-        sm2_e(eb, X, Y, h);
-        fe e, cc;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) e.v[k] = eb[7 - k];
-        reduce_once(e, ParamN2::M);
-        FieldN2::sub(cc, r, e);
-        lds_store_fe(L.c, cc, lane);
-        L.ok2[lane] = sm2_on_curve26(P) ? 1u : 0u;
-        uint32_t ad[5] = {0, 0, 0, 0, 0};
-        if (io.want_addr()) sm3_address(ad, px, py);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) L.addr[k][lane] = ad[k];
-        JacP26 G0, G1, G;
-        SM2_T(1);
-        comb_range_sm2_26(G0, s, tab, 0, 16);
-        SM2_T(2);
-        while (__hip_atomic_load(&L.seq[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
-            __builtin_amdgcn_s_sleep(1);
-        }
-        pair26_load_jac(G1, L.gh, lane);
-        CurveSM2x::add(G, G0, G1);
-        pair26_store_jac(L.g, G, lane);
     } else {
-        // the affine table of all 40 txs (one lane per tx) from the Jacobian entries of waves 0 and 1:
-        // one inversion of Z1 .. Z7, then x = X / Z^2, y = Y / Z^3; the chains switch to it when ready
-        while (__hip_atomic_load(&L.seq[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u ||
-               __hip_atomic_load(&L.seq[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
-            __builtin_amdgcn_s_sleep(1);
-        }
-        {
-            const int c = lane < TPW ? lane : TPW - 1;
-            fp26 pre[8], inv;
-            fp26_set(pre[0], p26::ONE_R);
-            Unroll<1, 8>::run([&](auto J) {
-                constexpr int j = decltype(J)::value;
-                fp26 z;
-#pragma unroll
-                for (int q = 0; q < 10; ++q) z.v[q] = L.jtab[j][20 + q][c];
-                F26_SETM(z, 1);
-                fp26_mul(pre[j], pre[j - 1], z);
-            });
-            fp26_inv(inv, pre[7]);  // (Z1 ... Z7)^-1
-            Unroll<0, 7>::run([&](auto J) {
-                constexpr int j = 7 - decltype(J)::value;
-                fp26 z, X, Y, zi, zi2, zi3, x, y;
+        {  // waves 2 and 3: the Jacobian tables of chain waves 0 and 1
+            lds_wave_sync();
+            const TrioLane T(lane);
+            const int pos = lane & 15, trio_idx = pos / 3;
+            const bool real = trio_idx < 5;
+            const int tl = (wave - 2) * 20 + (lane >> 4) * 5 + (real ? trio_idx : 4);
+            // 2P .. 8P of chain wave (wave - 2)'s 20 txs as Jacobian points on the trios (three / four product
+            // levels each), then Z^3 of every entry, one product per lane
+            {
+                AffP26 P0;
 #pragma unroll
                 for (int q = 0; q < 10; ++q) {
-                    X.v[q] = L.jtab[j][q][c];
-                    Y.v[q] = L.jtab[j][10 + q][c];
-                    z.v[q] = L.jtab[j][20 + q][c];
+                    P0.x.v[q] = L.tab[0][q][tl];
+                    P0.y.v[q] = L.tab[0][10 + q][tl];
                 }
-                F26_SETM(X, 1);
-                F26_SETM(Y, 1);
-                F26_SETM(z, 1);
-                fp26_mul(zi, inv, pre[j - 1]);  // Z_j^-1
-                fp26_mul(inv, inv, z);          // (Z1 .. Z(j-1))^-1
-                fp26_sqr(zi2, zi);
-                fp26_mul(zi3, zi2, zi);
-                fp26_mul(x, X, zi2);
-                fp26_mul(y, Y, zi3);
-                fp26_normalize(x);
-                fp26_normalize(y);
-                if (lane < TPW) {
+                F26_SETM(P0.x, 1);
+                F26_SETM(P0.y, 1);
+                TrioPtP M1, M2, M3, M;
+                fp26 D1, D2, D3, Dm;
+                trio_from_aff_sm2(M1, P0, T);
+                fp26_set(D1, p26::ONE_R);
+                trio_dbl_sm2_d(M1, D1, T);  // 2P
+                trio_store_jent(L, 1, M1, D1, tl, real, T);
+                trio_madd_sm2_d(M2, D2, M1, D1, P0, T);  // 3P
+                trio_store_jent(L, 2, M2, D2, tl, real, T);
+                M3 = M1;
+                fp26_copy(D3, D1);
+                trio_dbl_sm2_d(M3, D3, T);  // 4P
+                trio_store_jent(L, 3, M3, D3, tl, real, T);
+                trio_madd_sm2_d(M, Dm, M3, D3, P0, T);  // 5P
+                trio_store_jent(L, 4, M, Dm, tl, real, T);
+                trio_dbl_sm2_d(M2, D2, T);  // 6P
+                trio_store_jent(L, 5, M2, D2, tl, real, T);
+                trio_madd_sm2_d(M, Dm, M2, D2, P0, T);  // 7P
+                trio_store_jent(L, 6, M, Dm, tl, real, T);
+                trio_dbl_sm2_d(M3, D3, T);  // 8P
+                trio_store_jent(L, 7, M3, D3, tl, real, T);
+                lds_wave_sync();
+                const int role = T.r0 ? 0 : T.r1 ? 1 : 2;
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const int j = 1 + role + 3 * r;
+                    const int jj = j <= 7 ? j : 7;
+                    fp26 z, zz, zzz;
 #pragma unroll
                     for (int q = 0; q < 10; ++q) {
-                        L.tab[j][q][lane] = x.v[q];
-                        L.tab[j][10 + q][lane] = y.v[q];
+                        z.v[q] = L.jtab[jj][20 + q][tl];
+                        zz.v[q] = L.jtab[jj][30 + q][tl];
+                    }
+                    F26_SETM(z, 1);
+                    F26_SETM(zz, 1);
+                    fp26_mul(zzz, zz, z);
+                    fp26_normalize(zzz);
+                    if (real && j <= 7) {
+#pragma unroll
+                        for (int q = 0; q < 10; ++q) L.jtab[jj][40 + q][tl] = zzz.v[q];
                     }
                 }
-            });
+                lds_wave_sync();
+                // these 20 Jacobian tables are complete: chain wave (wave - 2) may add them and wave 3 build
+                // their affine forms
+                if (lane == 0)
+                    __hip_atomic_store(&L.seq[wave - 2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_store(&L.seq[3], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        JacP26 G1;
-        SM2_T(1);
-        comb_range_sm2_26(G1, s, tab, 16, 32);
-        SM2_T(2);
-        pair26_store_jac(L.gh, G1, lane);
-        __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (wave == 2) {
+            fe h;
+            fe_zero(h);
+            if (active) io.template digest<SM3>(i, h);
+            uint32_t eb[8];
+            sm2_e(eb, X, Y, h);
+            fe e, cc;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) e.v[k] = eb[7 - k];
+            reduce_once(e, ParamN2::M);
+            FieldN2::sub(cc, r, e);
+            lds_store_fe(L.c, cc, lane);
+            L.ok2[lane] = sm2_on_curve26(P) ? 1u : 0u;
+            uint32_t ad[5] = {0, 0, 0, 0, 0};
+            if (io.want_addr()) sm3_address(ad, px, py);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) L.addr[k][lane] = ad[k];
+            JacP26 G0, G1, G;
+            SM2_T(1);
+            comb_range_sm2_26(G0, s, tab, 0, 16);
+            SM2_T(2);
+            while (__hip_atomic_load(&L.seq[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+                __builtin_amdgcn_s_sleep(1);
+            }
+            pair26_load_jac(G1, L.gh, lane);
+            CurveSM2x::add(G, G0, G1);
+            pair26_store_jac(L.g, G, lane);
+        } else {
+            // the affine table of all 40 txs (one lane per tx) from the Jacobian entries (waves 2 and 3):
+            // one inversion of Z1 .. Z7, then x = X / Z^2, y = Y / Z^3; the chains switch to it when ready
+            while (__hip_atomic_load(&L.seq[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u ||
+                   __hip_atomic_load(&L.seq[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+                __builtin_amdgcn_s_sleep(1);
+            }
+            {
+                const int c = lane < TPW ? lane : TPW - 1;
+                fp26 pre[8], inv;
+                fp26_set(pre[0], p26::ONE_R);
+                Unroll<1, 8>::run([&](auto J) {
+                    constexpr int j = decltype(J)::value;
+                    fp26 z;
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) z.v[q] = L.jtab[j][20 + q][c];
+                    F26_SETM(z, 1);
+                    fp26_mul(pre[j], pre[j - 1], z);
+                });
+                fp26_inv(inv, pre[7]);  // (Z1 ... Z7)^-1
+                Unroll<0, 7>::run([&](auto J) {
+                    constexpr int j = 7 - decltype(J)::value;
+                    fp26 z, X, Y, zi, zi2, zi3, x, y;
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) {
+                        X.v[q] = L.jtab[j][q][c];
+                        Y.v[q] = L.jtab[j][10 + q][c];
+                        z.v[q] = L.jtab[j][20 + q][c];
+                    }
+                    F26_SETM(X, 1);
+                    F26_SETM(Y, 1);
+                    F26_SETM(z, 1);
+                    fp26_mul(zi, inv, pre[j - 1]);  // Z_j^-1
+                    fp26_mul(inv, inv, z);          // (Z1 .. Z(j-1))^-1
+                    fp26_sqr(zi2, zi);
+                    fp26_mul(zi3, zi2, zi);
+                    fp26_mul(x, X, zi2);
+                    fp26_mul(y, Y, zi3);
+                    fp26_normalize(x);
+                    fp26_normalize(y);
+                    if (lane < TPW) {
+#pragma unroll
+                        for (int q = 0; q < 10; ++q) {
+                            L.tab[j][q][lane] = x.v[q];
+                            L.tab[j][10 + q][lane] = y.v[q];
+                        }
+                    }
+                });
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&L.seq[3], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            JacP26 G1;
+            SM2_T(1);
+            comb_range_sm2_26(G1, s, tab, 16, 32);
+            SM2_T(2);
+            pair26_store_jac(L.gh, G1, lane);
+            __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
     }
     __syncthreads();
     SM2_T(3);
