@@ -371,6 +371,15 @@ __device__ __forceinline__ void fused_level(const uint8_t* in, uint64_t nin, uin
     }
 }
 
+#ifdef BCOSGPU_MERKLE_PROBE  // tools/fusedprobe.hip: per-wave global timestamps (s_memrealtime, 100 MHz)
+__device__ uint64_t g_mp[4096][12];
+#define MP(k) \
+    if (threadIdx.x == 0 && blockIdx.x < 4096 && (k) < 12) g_mp[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define MP(k) \
+    do {      \
+    } while (0)
+#endif
 template <int H, int W>
 __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w,
                                                           uint8_t* __restrict__ tree, const FusedTree f,
@@ -387,12 +396,14 @@ __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restr
     }
     // ---- level 0 (from the leaves, global memory) and levels 1 .. a inside the wave (from LDS); the
     // two kinds of source stay separate so every load has a known address space (no flat loads)
+    MP(0);
     uint64_t base = static_cast<uint64_t>(blockIdx.x) * f.S;  // first level-0 node of this wave
     uint32_t nodes = static_cast<uint32_t>(t.cnt[0] - base < f.S ? t.cnt[0] - base : f.S);
     const int inner = f.a + 1 < t.nlev ? f.a + 1 : t.nlev;  // levels this wave computes before climbing
     fused_level<H, W>(leaves + 32ull * base * width, n - base * width, width, f.S, nodes,
                       tree + 32ull * (t.pos[0] + 1 + base), reinterpret_cast<uint8_t*>(&lds[0][0][0]));
     __syncthreads();
+    MP(1);
     int cur = 0;
     uint32_t full = f.S;  // nodes of the level under a full wave
     for (int l = 1; l < inner; ++l) {
@@ -405,6 +416,7 @@ __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restr
         cur ^= 1;
         __syncthreads();
     }
+    MP(2);
     // ---- climb: the wave completing a parent's group of children hashes the parent
     uint64_t j = base;  // this wave's node at level inner - 1 (lds[cur][0])
     if (inner < t.nlev && lane < 8)  // publish it (device-coherent)
@@ -422,8 +434,10 @@ __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restr
         }
         arrived = __shfl(arrived, 0);
         if (arrived != kids) return;  // a sibling's wave finishes the parent
+        MP(3 + 2 * (l - inner));
         fused_one_node<H>(tree + 32ull * (t.pos[l - 1] + 1), t.cnt[l - 1], width, p, tree + 32ull * (t.pos[l] + 1 + p),
                           reinterpret_cast<uint8_t*>(&lds[0][0][0]));
+        MP(4 + 2 * (l - inner));
         j = p;
     }
     if (root && lane < 8 && j == 0) {  // this wave wrote the root node (or the whole tree fit in it)
