@@ -48,6 +48,20 @@ struct AlignedReader {
     __device__ __forceinline__ uint32_t word(uint32_t i) const { return i < nw ? q[i] : 0u; }
 };
 
+// AlignedReader for messages of at least 4 bytes (Merkle nodes: 32 B per child): every word is loaded
+// from a clamped index (the last message word past the end) and selected, so a block's sixteen loads
+// carry no branches and issue back to back under one wait, where AlignedReader's guarded loads each
+// sit in their own branch behind their own s_waitcnt.
+struct NodeReader {
+    const uint32_t* q;
+    uint32_t nw;  // >= 1
+    __device__ NodeReader(const uint8_t* p, uint32_t n) : q(reinterpret_cast<const uint32_t*>(p)), nw(n >> 2) {}
+    __device__ __forceinline__ uint32_t word(uint32_t i) const {
+        const uint32_t w = q[i < nw ? i : nw - 1u];
+        return i < nw ? w : 0u;
+    }
+};
+
 // ------------------------------------------------------------------ Keccak-256
 __device__ __constant__ static const uint64_t kKeccakRC[24] = {
     0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,

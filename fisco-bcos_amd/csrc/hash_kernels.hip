@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void merkle_level_kernel(const uint8_t* __rest
     const uint64_t first = i * width;
     const uint64_t cnt = (nin - first) < width ? (nin - first) : width;
     const uint32_t len = static_cast<uint32_t>(cnt * 32u);
-    AlignedReader rd(in + first * 32, len);
+    NodeReader rd(in + first * 32, len);
     uint32_t d[8];
     if (H == KECCAK256) keccak256_msg(rd, len, d);
     else sm3_msg(rd, len, d);
@@ -132,7 +132,7 @@ struct TreeLevels {
 template <int H>
 __device__ __forceinline__ void hash_nodes(const uint8_t* src, uint32_t cnt, uint32_t d[8]) {
     const uint32_t len = cnt * 32u;
-    AlignedReader rd(src, len);
+    NodeReader rd(src, len);  // cnt >= 1
     if (H == KECCAK256) keccak256_msg(rd, len, d);
     else sm3_msg(rd, len, d);
 }
@@ -685,7 +685,7 @@ __global__ __launch_bounds__(256) void merkle_seg_level_kernel(const uint8_t* __
     const uint32_t first = j * width;
     const uint32_t cnt = (nin - first) < width ? (nin - first) : width;
     const uint32_t len = cnt * 32u;
-    AlignedReader rd(in + 32ull * (t.in_off[lo] + first), len);
+    NodeReader rd(in + 32ull * (t.in_off[lo] + first), len);
     uint32_t d[8];
     if (H == KECCAK256) keccak256_msg(rd, len, d);
     else sm3_msg(rd, len, d);
