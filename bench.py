@@ -52,11 +52,38 @@ F_SECP_RECOVER = 3240
 F_SM2_VERIFY = 3210
 # Field multiplications the kernels actually execute per unit (counted from their schedules,
 # DESIGN.md §9; the safegcd inversions are ALU work outside the F count): GLV recover with the
-# 16-bit comb (throughput kernels) / the 8-bit comb (small-batch kernels); SM2 radix-16 Booth.
+# 16-bit comb / the 8-bit comb for u1 G; SM2 radix-16 Booth with the 16-bit / 8-bit comb for s G.
 F_SECP_EXEC_WIDE = 2255
 F_SECP_EXEC_COMB8 = 2431
 F_SM2_EXEC = 3092
 F_SM2_EXEC_COMB8 = 3268
+# kernel (name without template arguments; the one-lane kernel by suite) -> (F with the 16-bit comb
+# tables present, F on the 8-bit tables): which comb each kernel's launcher hands it (ecc_coop.hip
+# launch_verify_small_secp: the trio kernel takes the wide tables, the pair / split kernels the 8-bit
+# ones; ecc_pair.hip launch_verify_small_sm2: every SM2 small-batch kernel the 8-bit R'-domain table;
+# ecc_txv.hip launch_verify: the one-lane kernels the wide ones)
+KERNEL_F_EXEC = {
+    "tx_verify_trio26_kernel": (F_SECP_EXEC_WIDE, F_SECP_EXEC_COMB8),
+    "tx_verify_coop26_kernel": (F_SECP_EXEC_COMB8, F_SECP_EXEC_COMB8),
+    "tx_verify_coop_kernel": (F_SECP_EXEC_COMB8, F_SECP_EXEC_COMB8),
+    "tx_verify_split_kernel": (F_SECP_EXEC_COMB8, F_SECP_EXEC_COMB8),
+    "tx_verify_kernel/0": (F_SECP_EXEC_WIDE, F_SECP_EXEC_COMB8),
+    "tx_verify_sm2_trio26_kernel": (F_SM2_EXEC_COMB8, F_SM2_EXEC_COMB8),
+    "tx_verify_sm2_pair26_kernel": (F_SM2_EXEC_COMB8, F_SM2_EXEC_COMB8),
+    "tx_verify_sm2_pair_kernel": (F_SM2_EXEC_COMB8, F_SM2_EXEC_COMB8),
+    "tx_verify_kernel/1": (F_SM2_EXEC, F_SM2_EXEC_COMB8),
+}
+
+
+def kernel_f_exec(kname, wide_tables=None):
+    """Executed F per unit of the launched kernel `kname` (as _kernel_name returns it)."""
+    base = kname.split("<")[0]
+    if base == "tx_verify_kernel":
+        base += "/" + kname.split("<")[1].split(",")[0]
+    if wide_tables is None:
+        wide_tables = os.environ.get("BCOSGPU_TABLES") != "small"
+    wide, comb8 = KERNEL_F_EXEC[base]
+    return wide if wide_tables else comb8
 # measured gfx950 lane-op peaks (fisco-bcos_amd/tools/intbench.hip on MI355X, profiles/r01_intbench.json)
 PEAK_MAC_PER_S = 3.0785e13      # v_mad_u64_u32
 PEAK_ALU_PER_S = 3.7497e13      # full-rate 32-bit VALU (v_alignbit_b32)
@@ -300,11 +327,7 @@ def run_leg(ctx, wl_name, steps=None, warmup=3, warm_seconds=0.0, min_seconds=2.
     ok_frac = float((status[:n] == 0).float().mean().item()) if n else 1.0
     kname = _kernel_name(suite, n)
     f_alg = F_SECP_RECOVER if suite == 0 else F_SM2_VERIFY
-    if suite == 0:
-        wide = kname.startswith("tx_verify_kernel") or kname == "tx_verify_trio26_kernel"  # 16-bit comb for u1 G
-        f_exec = F_SECP_EXEC_WIDE if wide and os.environ.get("BCOSGPU_TABLES") != "small" else F_SECP_EXEC_COMB8
-    else:
-        f_exec = F_SM2_EXEC if kname.startswith("tx_verify_kernel") else F_SM2_EXEC_COMB8
+    f_exec = kernel_f_exec(kname)
     ex = n * f_exec * MAC_PER_F / (kernel_ms * 1e-3)
     alg = n * f_alg * MAC_PER_F / (kernel_ms * 1e-3)
     traffic, traffic_src, same_src = _traffic(wl_name, kname)
@@ -475,6 +498,23 @@ def _cpu_info():
     return model
 
 
+def _physical_cores():
+    """Distinct (package, core) pairs in sysfs -- SMT siblings counted once; os.cpu_count() without sysfs."""
+    cores = set()
+    base = "/sys/devices/system/cpu"
+    try:
+        for d in os.listdir(base):
+            if d.startswith("cpu") and d[3:].isdigit():
+                try:
+                    with open(os.path.join(base, d, "topology", "thread_siblings_list")) as f:
+                        cores.add(f.read().strip())
+                except OSError:
+                    pass
+    except OSError:
+        pass
+    return len(cores) or os.cpu_count() or 1
+
+
 def cpu_threads():
     """Threads for the CPU legs: the box's CPU share (OMP_NUM_THREADS is set to it on the GPU box;
     nproc / the affinity mask show the whole machine there), else the affinity mask."""
@@ -510,16 +550,19 @@ def cpu_baseline(batches, threads):
     best_name = [k for k, v in legs.items() if v is best][0]
     logical = os.cpu_count()
     openssl = best_name.endswith("openssl")
-    return {"value": best["value"], "unit": "tx/s", "cores": threads, "kind": "reference" if openssl else "port",
-            "kind_detail": ("the reference's per-tx path with its third-party ECC replaced by the reference-class "
-                            "library in this image (OpenSSL 1.1.1 libcrypto EC for wedpr's libsecp256k1 / TASSL)"
-                            if openssl else "the oracle's portable C restatement of the path"),
+    return {"value": best["value"], "unit": "tx/s", "cores": threads, "kind": "standin-openssl" if openssl else "port",
+            "kind_detail": ("NOT the reference's ECC: the reference's per-tx path with its third-party ECC (wedpr's "
+                            "libsecp256k1 / TASSL, absent here) replaced by OpenSSL 1.1.1 libcrypto EC, the "
+                            "reference-class library in this image" if openssl
+                            else "the oracle's portable C restatement of the path"),
             "impl": best_name, "sample": best["sample"],
             "host": {"cpu_model": _cpu_info(), "nproc": logical, "affinity": len(os.sched_getaffinity(0)),
                      "threads_used": threads, "libcrypto": oracle.standin_version()},
-            "full_host_estimate": {"value": best["per_thread"] * logical, "unit": "tx/s",
-                                   "note": "per-thread rate x logical CPUs (linear upper bound, SMT counted); "
-                                           "the legs ran on the box's CPU share"},
+            "full_host_estimate": {"value": best["per_thread"] * _physical_cores(), "unit": "tx/s",
+                                   "physical_cores": _physical_cores(), "logical_cpus": logical,
+                                   "smt_upper_bound": best["per_thread"] * logical,
+                                   "note": "per-thread rate (measured on the box's CPU share, one thread per core) x "
+                                           "physical cores; smt_upper_bound counts SMT siblings as cores too"},
             "legs": legs,
             "note": "stand-ins for the reference's third-party ECC (wedpr libsecp256k1 / TASSL, absent and "
                     "unbuildable here, BASELINE.md 3): OpenSSL libcrypto EC and the oracle's 4x64 Montgomery port"}
@@ -545,15 +588,16 @@ def host_api_rate(b, suite, n, reps=5):
             "path": "bcosgpu_tx_verify_batch (host buffers: H2D + kernel + D2H + sync)"}
 
 
-def interface_legs(batches, threads=64, calls=1000, reps=20):
+def interface_legs(batches, threads=(16, 64, 256), calls=1000, reps=20):
     """The reference-interface entry points on the C2-size batches (rank 0, N = 1), per suite:
       recover_batch: SignatureCrypto::recover for a whole batch -- bcosgpu_secp256k1_recover_batch_dev /
                      bcosgpu_sm2_verify_batch_dev (HIP events, the same rounds x latency kernel choice as
                      the tx path) and the host-pointer ABI (bcosgpu_*_batch: H2D + kernel + D2H);
-      single_call:   `threads` host threads x `calls` single calls each (bcosgpu_secp256k1_recover /
-                     bcosgpu_sm2_verify, the per-tx SignatureCrypto::recover of TxPool's submitter pool,
-                     TxPool.h:48-49), coalesced by the engine -- fisco-bcos_amd/lib/callbench, every
-                     result checked against the batch path's."""
+      single_call:   for each T in `threads` (16 = the box's CPU share, 256 = hardware_concurrency here, the
+                     reference's submitter pool size, NodeConfig.cpp:486 / TxPool.h:48-49): T host threads x
+                     `calls` single calls each (bcosgpu_secp256k1_recover / bcosgpu_sm2_verify, the per-tx
+                     SignatureCrypto::recover), coalesced by the engine -- fisco-bcos_amd/lib/callbench,
+                     every result checked against the batch path's -- beside the CPU stand-in at T threads."""
     import struct
     import tempfile
     import numpy as np
@@ -610,14 +654,35 @@ def interface_legs(batches, threads=64, calls=1000, reps=20):
                     f.write(np.ascontiguousarray(arr, dtype=np.uint8).tobytes())
                 path = f.name
             try:
-                r = subprocess.run([exe, path, str(threads), str(calls)], capture_output=True, text=True, timeout=300)
-                line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else "{}"
-                res = json.loads(line)
-                res["rc"] = r.returncode
-                out["single_call_%dt_%s" % (threads, name)] = res
+                for t in threads:
+                    r = subprocess.run([exe, path, str(t), str(calls)], capture_output=True, text=True, timeout=300)
+                    line = r.stdout.strip().splitlines()[-1] if r.stdout.strip() else "{}"
+                    res = json.loads(line)
+                    res["rc"] = r.returncode
+                    res["cpu_standin"] = single_call_cpu(b, suite, t)
+                    out["single_call_%dt_%s" % (t, name)] = res
             finally:
                 os.unlink(path)
     return out
+
+
+def single_call_cpu(b, suite, threads, sample=4000):
+    """The CPU counterpart of `threads` submitter threads each verifying one tx per call: the OpenSSL EC
+    stand-in (else the oracle's port) over `threads` threads on a bounded sample; calls/s and the mean
+    per-call latency of that closed loop (threads / rate, Little's law)."""
+    import numpy as np
+    from oracle import oracle
+    n = min(sample, b.n)
+    pre = b.pre.cpu().numpy()
+    pre_off = np.ascontiguousarray(b.pre_off[: n + 1].cpu().numpy().astype(np.uint64))
+    sig = b.sig.cpu().numpy()
+    sig_off = np.ascontiguousarray(b.sig_off[: n + 1].cpu().numpy().astype(np.uint64))
+    ossl = oracle.standin() is not None
+    fn = oracle.standin_tx_verify_packed if ossl else oracle.tx_verify_packed
+    med, _ = _median_time(lambda: fn(suite, pre, pre_off, sig, sig_off, nthreads=threads), reps=3)
+    rate = n / med
+    return {"calls_per_s": rate, "mean_latency_us": threads / rate * 1e6, "threads": threads,
+            "cores": cpu_threads(), "kind": "standin-openssl" if ossl else "port", "sample": n}
 
 
 def create_transaction_leg(b, suite, n, want_status, reps=20):
@@ -653,6 +718,59 @@ def create_transaction_leg(b, suite, n, want_status, reps=20):
     return {"value": n / (full * 1e-3), "unit": "tx/s", "ms_per_batch": full, "decode_ms": dec,
             "bytes_per_tx": enc.numel() // n, "status_matches_packed_path": same,
             "path": "bcosgpu_tars_tx_verify_batch_dev (decode + pack + verify + dataHash check)"}
+
+
+def _g(x, k=4):
+    return float("%.*g" % (k, x)) if isinstance(x, (int, float)) and not isinstance(x, bool) else x
+
+
+def summarize(line, head_name, head):
+    """A compact digest of every leg, emitted as the LAST key of the line so a reader holding only the
+    line's tail (the driver keeps ~2 kB) still sees all of them: per tx leg tx/s, ms/step, kernel ms, the
+    executed and SURVEY-8d roofline fractions, HBM traffic over algorithmic bytes and the VALU issue
+    fraction; the single-call rates (GPU calls/s, p50 / p99 us, CPU stand-in calls/s at the same thread
+    count); sealer verify; Merkle; the CPU baseline."""
+    out = {}
+
+    def leg(rec):
+        rf = rec["roofline"]
+        alg = rf["algorithmic_bytes_per_unit"] * max(rf["units_per_launch"], 1)
+        return {"tx_s": _g(rec["value"]), "ms_step": _g(rec["ms_per_step"]), "kernel_ms": _g(rf["kernel_ms"]),
+                "frac": _g(rf["frac"], 3), "frac_8d": _g(rf["algorithmic"]["frac"], 3),
+                "traffic_x": _g(rf["traffic"] / alg, 3) if rf.get("traffic") else None,
+                "valu_issue": _g(rf["valu_issue"]["frac"], 3) if rf.get("valu_issue") else None}
+    out[head_name] = leg(head)
+    for k, rec in (line.get("legs") or {}).items():
+        out[k] = leg(rec)
+    itf = line.get("interface") or {}
+    sc = {}
+    for k, v in itf.items():
+        if k.startswith("single_call_") and isinstance(v, dict) and "calls_per_s" in v:
+            t, suite = k[len("single_call_"):].split("_", 1)
+            sc.setdefault(suite, {})[t] = [_g(v["calls_per_s"]), _g(v["latency_us"]["p50"]), _g(v["latency_us"]["p99"]),
+                                           _g((v.get("cpu_standin") or {}).get("calls_per_s"))]
+    if sc:
+        out["single_call[gpu/s,p50us,p99us,cpu/s]"] = sc
+    rb = {k[len("recover_batch_"):]: _g(v["kernel_ms_median"]) for k, v in itf.items() if k.startswith("recover_batch_")}
+    if rb:
+        out["recover_batch_10k_ms"] = rb
+    sv = line.get("sealer_verify")
+    if sv:
+        out["sealer_verify"] = sv.get("summary")
+    mk = line.get("merkle") or {}
+    if mk:
+        out["merkle_ms"] = {k: _g(mk[k]["ms"]) for k in ("keccak256_w16_100k", "sm3_w16_100k", "keccak256_w2_100k",
+                                                          "sm3_w2_100k", "keccak256_w2_1M", "keccak256_w16_16M")
+                            if k in mk}
+    for k in ("pcie_inclusive", "create_transaction"):
+        if line.get(k):
+            out[k + "_tx_s"] = _g(line[k]["value"])
+    cb = line.get("cpu_baseline")
+    if cb:
+        out["cpu"] = {"kind": cb["kind"], "threads": cb["cores"],
+                      "tx_s": {k: _g(v["value"]) for k, v in cb["legs"].items()},
+                      "full_host_est": _g(cb["full_host_estimate"]["value"])}
+    return out
 
 
 def main():
@@ -753,6 +871,7 @@ def main():
             line["cpu_baseline"] = cpu_baseline(batches, threads)
             line["cpu_baseline"]["merkle"] = line.get("merkle", {}).pop("cpu_baseline", None)
     if rank == 0:
+        line["summary"] = summarize(line, args.workload, head)  # last key: survives a tail-only record
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

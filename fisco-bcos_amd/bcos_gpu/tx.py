@@ -145,6 +145,46 @@ def verify_packed(suite: CryptoSuite, pre, pre_off, sig, sig_off):
     return txhash, sender, status
 
 
+def _devices(devices):
+    d = np.ascontiguousarray(devices, dtype=np.int32)
+    assert d.ndim == 1 and 1 <= d.size <= 64, "device list: 1 to 64 entries"
+    return d
+
+
+def verify_packed_multi(devices, suite: CryptoSuite, pre, pre_off, sig, sig_off, width=None):
+    """verify_packed over a device set in ONE process (bcosgpu_tx_verify_batch_multi): the batch split by
+    index over `devices` (an index may repeat: two shards on one GPU, distinct streams).  With `width`,
+    also the block's tx root (bcosgpu_block_verify_multi: per-GPU frontiers gathered on devices[0]).
+    Returns (txhash, sender, status) or (txhash, sender, status, root)."""
+    d = _devices(devices)
+    n = len(pre_off) - 1
+    txhash = np.zeros((n, 32), dtype=np.uint8)
+    sender = np.zeros((n, 20), dtype=np.uint8)
+    status = np.zeros(n, dtype=np.uint8)
+    p = pre if len(pre) else np.zeros(1, dtype=np.uint8)
+    s = sig if len(sig) else np.zeros(1, dtype=np.uint8)
+    po = np.ascontiguousarray(pre_off, dtype=np.uint64)
+    so = np.ascontiguousarray(sig_off, dtype=np.uint64)
+    if width is None:
+        check(lib().bcosgpu_tx_verify_batch_multi(_ptr(d), d.size, suite.suite, _ptr(p), _ptr(po), _ptr(s), _ptr(so), n,
+                                                  _ptr(txhash), _ptr(sender), _ptr(status)))
+        return txhash, sender, status
+    root = np.zeros(32, dtype=np.uint8)
+    check(lib().bcosgpu_block_verify_multi(_ptr(d), d.size, suite.suite, _ptr(p), _ptr(po), _ptr(s), _ptr(so), n,
+                                           width, _ptr(txhash), _ptr(sender), _ptr(status), _ptr(root)))
+    return txhash, sender, status, root.tobytes()
+
+
+def merkle_root_multi(devices, hasher, width, leaves):
+    """Merkle<H, width> root over a device set (bcosgpu_merkle_root_multi); leaves uint8[n, 32]."""
+    d = _devices(devices)
+    lv = np.ascontiguousarray(leaves, dtype=np.uint8).reshape(-1, 32)
+    root = np.zeros(32, dtype=np.uint8)
+    check(lib().bcosgpu_merkle_root_multi(_ptr(d), d.size, hasher, width, _ptr(lv if lv.size else np.zeros(32, np.uint8)),
+                                          lv.shape[0], _ptr(root)))
+    return root.tobytes()
+
+
 def verify_transactions(suite: CryptoSuite, txs):
     """importDownloadedTxs' parallel loop (TransactionSync.cpp:516-548) on the GPU: every tx whose
     sender is unset is verified; tx.sender is set on success (Transaction.h:70-81).  Returns the

@@ -108,6 +108,13 @@ int calling_device(int* dev) {
 
 }  // namespace
 
+// for the device-set entry points (multi.hip)
+namespace bcosgpu {
+int api_set_err(int code, const std::string& msg) { return set_err(code, msg); }
+int api_ready_device(int device) { return ready_device(device); }
+int api_run_job(int device, SigJob& job) { return run_job(device, job); }
+}  // namespace bcosgpu
+
 extern "C" {
 
 int bcosgpu_version(void) { return BCOSGPU_VERSION; }

@@ -266,7 +266,15 @@ int coalesced_run(int device, SigJob& job) {
         }
         free_slot->busy = true;
         lk.unlock();
-        run_batch(device, job.kind, *free_slot, batch);
+        // a host exception (std::bad_alloc from the staging vectors) fails this batch only: the slot is
+        // released and every job of the batch is completed with the error, so no caller waits forever
+        try {
+            run_batch(device, job.kind, *free_slot, batch);
+        } catch (const std::exception& e) {
+            fail(batch, BCOSGPU_E_HIP, std::string("signature batch failed on the host: ") + e.what());
+        } catch (...) {
+            fail(batch, BCOSGPU_E_HIP, "signature batch failed on the host");
+        }
         lk.lock();
         free_slot->busy = false;
         for (SigJob* j : batch) j->done = true;

@@ -68,6 +68,12 @@ struct SigJob {
 };
 int coalesced_run(int device, SigJob& job);
 
+// api.hip internals the device-set entry points (multi.hip) share: the calling thread's error message,
+// one-time device initialisation without changing the calling thread's device, a coalesced job
+int api_set_err(int code, const std::string& msg);
+int api_ready_device(int device);
+int api_run_job(int device, SigJob& job);
+
 // tars_kernels.hip
 uint64_t tars_decode_work_bytes(uint64_t n);
 int launch_tars_tx_decode(const uint8_t* d_enc, const uint64_t* d_enc_off, uint64_t n, uint8_t* d_pre,

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <utility>
+#include <thread>
 #include <vector>
 #include "hash_device.h"
 #include "engine.h"
@@ -447,39 +448,83 @@ __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restr
     }
 }
 
-// one counter slot (kFusedCounters zeroed counters) per (device, stream): launches on one stream run
-// in order, and each launch leaves its counters at zero
-static constexpr uint32_t kFusedCounters = 16384, kFusedSlots = 64;
+// One counter slot (kFusedCounters counters) per launch queue: launches on one stream run in order and
+// each launch leaves its counters at zero, so a slot is clean for the next launch of its owner.
+//  - The owner is (device of the stream, stream handle), and for the null stream and hipStreamPerThread
+//    -- one handle that names a different stream per thread (per-thread default streams) -- also the
+//    calling thread, so two threads never share a slot through one handle.
+//  - A new slot is zeroed by hipMemsetAsync on the claiming stream (ordered before its first launch; no
+//    device-wide synchronisation), and a stream under capture never claims one (a capture may not
+//    allocate): it takes the multi-launch path.
+//  - Pools of kFusedSlots slots are added on demand up to kFusedPools per device; past that the
+//    multi-launch path runs (bit-identical, slower at latency sizes).
+static constexpr uint32_t kFusedCounters = 16384, kFusedSlots = 64, kFusedPools = 16;
 static uint32_t* fused_counter_slot(hipStream_t st) {
     static std::mutex mu;
+    struct Owner {
+        int device;
+        hipStream_t stream;
+        std::thread::id thread;
+    };
     struct Pool {
         int device;
         uint32_t* base;
-        std::vector<hipStream_t> owners;
+        std::vector<Owner> owners;
     };
     static std::vector<Pool> pools;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const bool shared_handle = st == nullptr || st == hipStreamPerThread;
+    if (!shared_handle) {
+        hipDevice_t sd = 0;
+        if (hipStreamGetDevice(st, &sd) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        dev = sd;
+    }
+    const Owner me{dev, st, shared_handle ? std::this_thread::get_id() : std::thread::id()};
     std::lock_guard<std::mutex> g(mu);
+    for (auto& q : pools) {
+        if (q.device != dev) continue;
+        for (size_t k = 0; k < q.owners.size(); ++k)
+            if (q.owners[k].stream == me.stream && q.owners[k].thread == me.thread) return q.base + k * kFusedCounters;
+    }
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (cap != hipStreamCaptureStatusNone) return nullptr;
     Pool* pool = nullptr;
+    int npools = 0;
     for (auto& q : pools)
-        if (q.device == dev) pool = &q;
+        if (q.device == dev) {
+            ++npools;
+            if (q.owners.size() < kFusedSlots) pool = &q;
+        }
     if (!pool) {
+        if (npools >= static_cast<int>(kFusedPools)) return nullptr;
+        int prev = dev;
+        (void)hipGetDevice(&prev);
+        if (prev != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
         void* b = nullptr;
-        const size_t bytes = sizeof(uint32_t) * kFusedCounters * kFusedSlots;
-        if (hipMalloc(&b, bytes) != hipSuccess) return nullptr;
-        if (hipMemset(b, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-            (void)hipFree(b);
+        const hipError_t e = hipMalloc(&b, sizeof(uint32_t) * kFusedCounters * kFusedSlots);
+        if (prev != dev) (void)hipSetDevice(prev);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
             return nullptr;
         }
         pools.push_back(Pool{dev, static_cast<uint32_t*>(b), {}});
         pool = &pools.back();
     }
-    for (size_t k = 0; k < pool->owners.size(); ++k)
-        if (pool->owners[k] == st) return pool->base + k * kFusedCounters;
-    if (pool->owners.size() >= kFusedSlots) return nullptr;  // caller takes the multi-launch path
-    pool->owners.push_back(st);
-    return pool->base + (pool->owners.size() - 1) * kFusedCounters;
+    uint32_t* slot = pool->base + pool->owners.size() * kFusedCounters;
+    if (hipMemsetAsync(slot, 0, sizeof(uint32_t) * kFusedCounters, st) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    pool->owners.push_back(me);
+    return slot;
 }
 
 static constexpr uint64_t kFusedMaxWaves = 2048;  // level-1 waves (two per SIMD) up to which the one-launch path runs

@@ -1,0 +1,439 @@
+// multi.hip -- the device-set entry points (include/bcos_gpu.h "device sets"): one process drives every
+// GPU of its node through the C ABI it links.  A FISCO node is a single process with one CryptoSuite
+// (libinitializer/ProtocolInitializer.cpp:102-124) and in-process batch sites (TransactionSync.cpp:516-548,
+// BlockImpl.h:111-154), so the multi-GPU split of SURVEY 8(e) has to live behind the ABI, not in a
+// process-per-GPU launcher.
+//
+//  - A batch is split by index into one contiguous shard per entry of the device list; shard k runs on
+//    devices[k] from its own host thread, on its own stream and buffers (a ShardCtx per (device, k-th
+//    occurrence of that device in the list), so {0, 0} is two shards on one GPU on distinct streams).
+//  - Signature batches: each shard is a coalesced job on its device (coalesce.hip), exactly what the
+//    single-device host calls run.
+//  - Block check / Merkle root: shard starts are multiples of width^L (Merkle<H, width> groups every
+//    level from index 0, Merkle.h:243-261), so shard k's level-L nodes ARE the reference tree's level-L
+//    nodes for its range; each GPU reduces its shard to them (launch_merkle_levels), devices[0] gathers
+//    the frontiers (a few KB) with peer copies over xGMI and runs the top levels.  Bit-identical to the
+//    single-device root for every n.
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+#include <cstring>
+#include "engine.h"
+
+using namespace bcosgpu;
+
+namespace {
+
+struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+        const hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// a shard's stream and grow-only device buffers; its mutex is held by the call that uses it
+struct ShardCtx {
+    std::mutex mu;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Buf b[10];
+};
+
+std::mutex g_mmu;
+std::map<std::pair<int, int>, ShardCtx*> g_ctx;  // never freed: no teardown races with the HIP runtime
+
+// slot -1 is the gather context of devices[0]
+ShardCtx* shard_ctx(int device, int slot) {
+    std::lock_guard<std::mutex> g(g_mmu);
+    ShardCtx*& c = g_ctx[{device, slot}];
+    if (!c) {
+        c = new ShardCtx();
+        c->device = device;
+    }
+    return c;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            (void)hipGetLastError();
+            prev = -1;
+        }
+        if (prev != dev) err = hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+std::string hip_msg(hipError_t e, const char* what) { return std::string(what) + ": " + hipGetErrorString(e); }
+
+#define SHARD_HIP(call)                                  \
+    do {                                                 \
+        const hipError_t e_ = (call);                    \
+        if (e_ != hipSuccess) {                          \
+            msg = hip_msg(e_, #call);                    \
+            return BCOSGPU_E_HIP;                        \
+        }                                                \
+    } while (0)
+
+int check_set(const int* devices, int ndev) {
+    if (!devices || ndev < 1 || ndev > 64) return api_set_err(BCOSGPU_E_ARG, "device list: 1 to 64 entries");
+    for (int k = 0; k < ndev; ++k)
+        if (int rc = api_ready_device(devices[k])) return rc;
+    return 0;
+}
+
+// shard k's context: devices[k], numbered by its occurrences among devices[0..k)
+std::vector<ShardCtx*> contexts(const int* devices, int ndev) {
+    std::vector<ShardCtx*> out(ndev);
+    for (int k = 0; k < ndev; ++k) {
+        int occ = 0;
+        for (int j = 0; j < k; ++j) occ += devices[j] == devices[k];
+        out[k] = shard_ctx(devices[k], occ);
+    }
+    return out;
+}
+
+// lock every context a call uses (sorted, so concurrent calls cannot deadlock)
+std::vector<std::unique_lock<std::mutex>> lock_all(std::vector<ShardCtx*> cs) {
+    std::sort(cs.begin(), cs.end());
+    cs.erase(std::unique(cs.begin(), cs.end()), cs.end());
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (ShardCtx* c : cs) locks.emplace_back(c->mu);
+    return locks;
+}
+
+// f(k, msg) for every shard, shards 1.. on their own host threads; the first failing shard's code,
+// with its message set on the calling thread
+template <class F>
+int run_shards(int ndev, F&& f) {
+    std::vector<int> rc(ndev, 0);
+    std::vector<std::string> msg(ndev);
+    auto one = [&](int k) {
+        try {
+            rc[k] = f(k, msg[k]);
+        } catch (const std::exception& e) {
+            rc[k] = BCOSGPU_E_HIP;
+            msg[k] = std::string("shard failed on the host: ") + e.what();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int k = 1; k < ndev; ++k) {
+        try {
+            th.emplace_back(one, k);
+        } catch (const std::exception&) {
+            one(k);  // no thread: run the shard here
+        }
+    }
+    one(0);
+    for (auto& t : th) t.join();
+    for (int k = 0; k < ndev; ++k)
+        if (rc[k]) return api_set_err(rc[k], msg[k]);
+    return 0;
+}
+
+// contiguous shards [lo, hi); with width >= 2 every lo is a multiple of width^L, L chosen so the gathered
+// frontier stays small (<= ~64 nodes per shard) while the tree still has more than L levels
+// (bcos_gpu/parallel.py choose_levels / shard_plan, the same rule)
+struct Plan {
+    std::vector<uint64_t> lo, hi;
+    int levels = 0;
+    uint64_t blk = 1;
+    uint64_t count(int k) const { return hi[k] > lo[k] ? (hi[k] - lo[k] + blk - 1) / blk : 0; }
+};
+Plan make_plan(uint64_t n, int ndev, int width) {
+    Plan p;
+    if (width >= 2) {
+        uint64_t b = 1;
+        while (true) {
+            const uint64_t nb = b * static_cast<uint64_t>(width);
+            if (static_cast<uint64_t>(ndev) * 64u * nb > n || (n + nb - 1) / nb < 2) break;
+            b = nb;
+            ++p.levels;
+        }
+        p.blk = b;
+    }
+    const uint64_t per = (n + static_cast<uint64_t>(ndev) * p.blk - 1) / (static_cast<uint64_t>(ndev) * p.blk) * p.blk;
+    p.lo.resize(ndev);
+    p.hi.resize(ndev);
+    for (int k = 0; k < ndev; ++k) {
+        p.lo[k] = std::min<uint64_t>(k * per, n);
+        p.hi[k] = std::min<uint64_t>((k + 1) * per, n);
+    }
+    return p;
+}
+
+std::mutex g_peer_mu;
+std::vector<std::pair<int, int>> g_peer_done;
+
+// devices[0] reads the other devices' frontiers directly when the platform allows it (xGMI peer access);
+// otherwise hipMemcpyPeerAsync stages through the host
+void enable_peers(const int* devices, int ndev) {
+    std::lock_guard<std::mutex> g(g_peer_mu);
+    for (int k = 1; k < ndev; ++k) {
+        const std::pair<int, int> pr{devices[0], devices[k]};
+        if (pr.first == pr.second || std::find(g_peer_done.begin(), g_peer_done.end(), pr) != g_peer_done.end())
+            continue;
+        g_peer_done.push_back(pr);
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, pr.first, pr.second) == hipSuccess && can) {
+            DeviceGuard dg(pr.first);
+            (void)hipDeviceEnablePeerAccess(pr.second, 0);
+        }
+        (void)hipGetLastError();
+    }
+}
+
+hipError_t ensure_stream(ShardCtx* c) {
+    if (c->stream) return hipSuccess;
+    return hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+}
+
+// the top of the tree on devices[0]: gather the shards' level-L nodes (frontier[k], count(k) nodes on
+// devices[k]) into one vector and run Merkle<H, width> over it
+int gather_root(const int* devices, int ndev, const Plan& p, const std::vector<const uint8_t*>& frontier, int hasher,
+                int width, ShardCtx* r, uint8_t* root32) {
+    std::string msg;
+    const int rc = [&]() -> int {
+        DeviceGuard dg(r->device);
+        SHARD_HIP(dg.err);
+        SHARD_HIP(ensure_stream(r));
+        uint64_t total = 0;
+        for (int k = 0; k < ndev; ++k) total += p.count(k);
+        SHARD_HIP(r->b[0].ensure(total * 32));
+        SHARD_HIP(r->b[1].ensure((merkle_size(total, width) + 1) * 32));
+        SHARD_HIP(r->b[2].ensure(32));
+        uint64_t at = 0;
+        for (int k = 0; k < ndev; ++k) {
+            const uint64_t m = p.count(k);
+            if (!m) continue;
+            uint8_t* dst = r->b[0].as<uint8_t>() + 32 * at;
+            if (devices[k] == r->device)
+                SHARD_HIP(hipMemcpyAsync(dst, frontier[k], 32 * m, hipMemcpyDeviceToDevice, r->stream));
+            else
+                SHARD_HIP(hipMemcpyPeerAsync(dst, r->device, frontier[k], devices[k], 32 * m, r->stream));
+            at += m;
+        }
+        const int lrc = launch_merkle(hasher, width, r->b[0].as<uint8_t>(), total, r->b[1].as<uint8_t>(),
+                                      r->b[2].as<uint8_t>(), r->stream);
+        if (lrc) {
+            msg = hip_msg(hipGetLastError(), "merkle top levels launch");
+            return lrc;
+        }
+        SHARD_HIP(hipMemcpyAsync(root32, r->b[2].p, 32, hipMemcpyDeviceToHost, r->stream));
+        SHARD_HIP(hipStreamSynchronize(r->stream));
+        return 0;
+    }();
+    return rc ? api_set_err(rc, msg) : 0;
+}
+
+int sig_multi(const int* devices, int ndev, int kind, size_t n, const uint8_t* hash32, const uint8_t* sig,
+              size_t sig_stride, const uint8_t* pub64, uint8_t* out_pub64, uint8_t* out_addr20, uint8_t* ok) {
+    if (int rc = check_set(devices, ndev)) return rc;
+    const Plan p = make_plan(n, ndev, 0);
+    return run_shards(ndev, [&](int k, std::string& msg) -> int {
+        const uint64_t lo = p.lo[k], m = p.hi[k] - p.lo[k];
+        if (!m) return 0;
+        SigJob job;
+        job.kind = kind;
+        job.n = m;
+        job.hash32 = hash32 + 32 * lo;
+        job.sig = sig + sig_stride * lo;
+        job.sig_stride = sig_stride;
+        job.pub64 = pub64 ? pub64 + 64 * lo : nullptr;
+        job.out_pub64 = out_pub64 ? out_pub64 + 64 * lo : nullptr;
+        job.out_addr20 = out_addr20 ? out_addr20 + 20 * lo : nullptr;
+        job.out_ok = ok + lo;
+        const int rc = coalesced_run(devices[k], job);
+        if (rc) msg = job.err;
+        return rc;
+    });
+}
+
+int tx_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off, const uint8_t* sig,
+             const uint64_t* sig_off, size_t n, int width, uint8_t* txhash32, uint8_t* sender20, uint8_t* status,
+             uint8_t* root32) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return api_set_err(BCOSGPU_E_ARG, "bad suite");
+    if (root32 && (width < 2 || width > 64)) return api_set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
+    if (n == 0) {  // BlockImpl.h:114-119: a block without transactions has the zero root
+        if (root32) std::memset(root32, 0, 32);
+        return check_set(devices, ndev);
+    }
+    if (!pre || !pre_off || !sig || !sig_off || !txhash32 || !sender20 || !status)
+        return api_set_err(BCOSGPU_E_ARG, "null pointer");
+    for (size_t i = 0; i < n; ++i)
+        if (pre_off[i + 1] < pre_off[i] || sig_off[i + 1] < sig_off[i] || pre_off[i + 1] - pre_off[i] > 0xFFFFFFFFull)
+            return api_set_err(BCOSGPU_E_ARG, "offsets must be non-decreasing");
+    if (int rc = check_set(devices, ndev)) return rc;
+    if (root32) enable_peers(devices, ndev);
+    const int hasher = suite == BCOSGPU_SUITE_SM2 ? BCOSGPU_SM3 : BCOSGPU_KECCAK256;
+    const Plan p = make_plan(n, ndev, root32 ? width : 0);
+    std::vector<ShardCtx*> ctx = contexts(devices, ndev);
+    ShardCtx* top = root32 ? shard_ctx(devices[0], -1) : nullptr;
+    std::vector<ShardCtx*> all = ctx;
+    if (top) all.push_back(top);
+    auto locks = lock_all(all);
+    std::vector<const uint8_t*> frontier(ndev, nullptr);
+    int rc = run_shards(ndev, [&](int k, std::string& msg) -> int {
+        const uint64_t lo = p.lo[k], hi = p.hi[k], m = hi - lo;
+        if (!m) return 0;
+        ShardCtx* c = ctx[k];
+        DeviceGuard dg(c->device);
+        SHARD_HIP(dg.err);
+        SHARD_HIP(ensure_stream(c));
+        const uint64_t pb = pre_off[lo], pbytes = pre_off[hi] - pb, sb = sig_off[lo], sbytes = sig_off[hi] - sb;
+        SHARD_HIP(c->b[0].ensure(pbytes + 8));
+        SHARD_HIP(c->b[1].ensure((m + 1) * 8));
+        SHARD_HIP(c->b[2].ensure(sbytes + 8));
+        SHARD_HIP(c->b[3].ensure((m + 1) * 8));
+        SHARD_HIP(c->b[4].ensure(m * 32));
+        SHARD_HIP(c->b[5].ensure(m * 20));
+        SHARD_HIP(c->b[6].ensure(m));
+        std::vector<uint64_t> po(m + 1), so(m + 1);
+        for (uint64_t i = 0; i <= m; ++i) {
+            po[i] = pre_off[lo + i] - pb;
+            so[i] = sig_off[lo + i] - sb;
+        }
+        SHARD_HIP(hipMemcpyAsync(c->b[0].p, pre + pb, pbytes, hipMemcpyHostToDevice, c->stream));
+        SHARD_HIP(hipMemcpyAsync(c->b[1].p, po.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
+        SHARD_HIP(hipMemcpyAsync(c->b[2].p, sig + sb, sbytes, hipMemcpyHostToDevice, c->stream));
+        SHARD_HIP(hipMemcpyAsync(c->b[3].p, so.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
+        int lrc = launch_tx_verify(suite, c->b[0].as<uint8_t>(), c->b[1].as<uint64_t>(), c->b[2].as<uint8_t>(),
+                                   c->b[3].as<uint64_t>(), m, c->b[4].as<uint8_t>(), c->b[5].as<uint8_t>(),
+                                   c->b[6].as<uint8_t>(), c->stream);
+        if (lrc) {
+            msg = hip_msg(hipGetLastError(), "tx verify launch");
+            return lrc;
+        }
+        if (root32 && p.levels > 0) {
+            SHARD_HIP(c->b[7].ensure(64 * ((m + width - 1) / width)));
+            SHARD_HIP(c->b[8].ensure(32 * p.count(k)));
+            lrc = launch_merkle_levels(hasher, width, c->b[4].as<uint8_t>(), m, p.levels, c->b[7].as<uint8_t>(),
+                                       c->b[8].as<uint8_t>(), c->stream);
+            if (lrc) {
+                msg = hip_msg(hipGetLastError(), "merkle frontier launch");
+                return lrc;
+            }
+            frontier[k] = c->b[8].as<uint8_t>();
+        } else if (root32) {
+            frontier[k] = c->b[4].as<uint8_t>();  // L = 0: the tx hashes are the frontier
+        }
+        SHARD_HIP(hipMemcpyAsync(txhash32 + 32 * lo, c->b[4].p, m * 32, hipMemcpyDeviceToHost, c->stream));
+        SHARD_HIP(hipMemcpyAsync(sender20 + 20 * lo, c->b[5].p, m * 20, hipMemcpyDeviceToHost, c->stream));
+        SHARD_HIP(hipMemcpyAsync(status + lo, c->b[6].p, m, hipMemcpyDeviceToHost, c->stream));
+        SHARD_HIP(hipStreamSynchronize(c->stream));
+        return 0;
+    });
+    if (rc || !root32) return rc;
+    return gather_root(devices, ndev, p, frontier, hasher, width, top, root32);
+}
+
+}  // namespace
+
+extern "C" {
+
+int bcosgpu_init_devices(const int* devices, int ndev) { return check_set(devices, ndev); }
+
+int bcosgpu_secp256k1_recover_batch_multi(const int* devices, int ndev, const uint8_t* hash32, const uint8_t* sig65,
+                                          size_t n, uint8_t* pub64, uint8_t* addr20, uint8_t* ok) {
+    if (n == 0) return check_set(devices, ndev);
+    if (!hash32 || !sig65 || !ok) return api_set_err(BCOSGPU_E_ARG, "null pointer");
+    return sig_multi(devices, ndev, kSigJobRecoverK1, n, hash32, sig65, 65, nullptr, pub64, addr20, ok);
+}
+
+int bcosgpu_sm2_verify_batch_multi(const int* devices, int ndev, const uint8_t* hash32, const uint8_t* sig128,
+                                   size_t n, uint8_t* addr20, uint8_t* ok) {
+    if (n == 0) return check_set(devices, ndev);
+    if (!hash32 || !sig128 || !ok) return api_set_err(BCOSGPU_E_ARG, "null pointer");
+    return sig_multi(devices, ndev, kSigJobVerifySM2, n, hash32, sig128, 128, nullptr, nullptr, addr20, ok);
+}
+
+int bcosgpu_verify_batch_multi(const int* devices, int ndev, int suite, const uint8_t* pub64, const uint8_t* hash32,
+                               const uint8_t* sig, size_t sig_stride, size_t n, uint8_t* ok) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return api_set_err(BCOSGPU_E_ARG, "bad suite");
+    if (sig_stride < 64 || sig_stride > 0xFFFFFFFFull) return api_set_err(BCOSGPU_E_ARG, "signature stride must be >= 64");
+    if (n == 0) return check_set(devices, ndev);
+    if (!pub64 || !hash32 || !sig || !ok) return api_set_err(BCOSGPU_E_ARG, "null pointer");
+    return sig_multi(devices, ndev, suite == BCOSGPU_SUITE_SM2 ? kSigJobVerifySM2 : kSigJobVerifyK1, n, hash32, sig,
+                     sig_stride, pub64, nullptr, nullptr, ok);
+}
+
+int bcosgpu_tx_verify_batch_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off,
+                                  const uint8_t* sig, const uint64_t* sig_off, size_t n, uint8_t* txhash32,
+                                  uint8_t* sender20, uint8_t* status) {
+    return tx_multi(devices, ndev, suite, pre, pre_off, sig, sig_off, n, 2, txhash32, sender20, status, nullptr);
+}
+
+int bcosgpu_block_verify_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off,
+                               const uint8_t* sig, const uint64_t* sig_off, size_t n, int width, uint8_t* txhash32,
+                               uint8_t* sender20, uint8_t* status, uint8_t* root32) {
+    if (!root32) return api_set_err(BCOSGPU_E_ARG, "null root pointer");
+    return tx_multi(devices, ndev, suite, pre, pre_off, sig, sig_off, n, width, txhash32, sender20, status, root32);
+}
+
+int bcosgpu_merkle_root_multi(const int* devices, int ndev, int hasher, int width, const uint8_t* leaves32, size_t n,
+                              uint8_t* root32) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return api_set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (width < 2 || width > 64) return api_set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
+    if (n == 0) return api_set_err(BCOSGPU_E_EMPTY, "Empty input");  // Merkle.h:172-175
+    if (!leaves32 || !root32) return api_set_err(BCOSGPU_E_ARG, "null pointer");
+    if (int rc = check_set(devices, ndev)) return rc;
+    if (n == 1) {  // Merkle.h:177-182: the single leaf
+        std::memcpy(root32, leaves32, 32);
+        return 0;
+    }
+    enable_peers(devices, ndev);
+    const Plan p = make_plan(n, ndev, width);
+    std::vector<ShardCtx*> ctx = contexts(devices, ndev);
+    ShardCtx* top = shard_ctx(devices[0], -1);
+    std::vector<ShardCtx*> all = ctx;
+    all.push_back(top);
+    auto locks = lock_all(all);
+    std::vector<const uint8_t*> frontier(ndev, nullptr);
+    int rc = run_shards(ndev, [&](int k, std::string& msg) -> int {
+        const uint64_t lo = p.lo[k], m = p.hi[k] - p.lo[k];
+        if (!m) return 0;
+        ShardCtx* c = ctx[k];
+        DeviceGuard dg(c->device);
+        SHARD_HIP(dg.err);
+        SHARD_HIP(ensure_stream(c));
+        SHARD_HIP(c->b[0].ensure(m * 32));
+        SHARD_HIP(hipMemcpyAsync(c->b[0].p, leaves32 + 32 * lo, m * 32, hipMemcpyHostToDevice, c->stream));
+        if (p.levels > 0) {
+            SHARD_HIP(c->b[7].ensure(64 * ((m + width - 1) / width)));
+            SHARD_HIP(c->b[8].ensure(32 * p.count(k)));
+            const int lrc = launch_merkle_levels(hasher, width, c->b[0].as<uint8_t>(), m, p.levels,
+                                                 c->b[7].as<uint8_t>(), c->b[8].as<uint8_t>(), c->stream);
+            if (lrc) {
+                msg = hip_msg(hipGetLastError(), "merkle frontier launch");
+                return lrc;
+            }
+            frontier[k] = c->b[8].as<uint8_t>();
+        } else {
+            frontier[k] = c->b[0].as<uint8_t>();
+        }
+        SHARD_HIP(hipStreamSynchronize(c->stream));
+        return 0;
+    });
+    if (rc) return rc;
+    return gather_root(devices, ndev, p, frontier, hasher, width, top, root32);
+}
+
+}  // extern "C"

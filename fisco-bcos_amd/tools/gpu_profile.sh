@@ -9,7 +9,11 @@ OUT=gpurun_out/prof/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --warm-seconds 0 --legs= --no-cpu-baseline --no-merkle --no-extras"
-timeout -k 10 $LIM rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 && \
+# the trace pass at steady state: >= 2 s of warm-up launches and >= 2 s of timed ones, so the kernel's
+# average duration is the clock-settled one the bench line reports (the PMC passes serialise dispatches
+# and only count, so they stay short)
+BT="python3 bench.py --workload $WL --steps $((STEPS * 100)) --warmup 2 --warm-seconds 2 --legs= --no-cpu-baseline --no-merkle --no-extras"
+timeout -k 10 $LIM rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BT > $OUT/trace.log 2>&1 && \
 timeout -s KILL $LIM rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B > $OUT/fetch.log 2>&1 && \
 timeout -s KILL $LIM rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B > $OUT/write.log 2>&1 && \
 timeout -s KILL $LIM rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS --output-format csv -d $OUT/sq -o run -- $B > $OUT/sq.log 2>&1 && \

@@ -344,6 +344,45 @@ def check_file(path, quiet=False):
     return total, len(funcs)
 
 
+def _vmem_store(mn):
+    return mn.startswith(("global_store", "buffer_store", "flat_store", "scratch_store"))
+
+
+def fused_publish_order(path, kernel="merkle_fused_kernel"):
+    """The ISA facts the one-launch Merkle kernel's cross-wave hand-off rests on (hash_kernels.hip,
+    merkle_fused_kernel: relaxed agent-scope atomics, no cache-wide fence), per instance of `kernel`:
+      (1) every counter atomic (global_atomic_*) is reached from the preceding node stores only through an
+          `s_waitcnt vmcnt(0)`: scanning back from the atomic, that wait comes before any vector store, so
+          the published node's write-through stores have been acknowledged before the counter moves;
+      (2) the published nodes are written with sc1 stores (write-through past the XCD's L2) and the
+          children are gathered with sc1 loads (missing the non-coherent L2), so the reader of a completed
+          group sees memory, not a stale line.
+    Returns (instances checked, list of (function, offset, problem))."""
+    bad, seen = [], 0
+    for name, start, insts in functions(path):
+        if kernel not in name:
+            continue
+        seen += 1
+        atomics = [i for i, (_, mn, _) in enumerate(insts) if mn.startswith("global_atomic")]
+        if not atomics:
+            bad.append((name, 0, "no counter atomic"))
+        for i in atomics:
+            j = i - 1
+            while j >= 0 and not (insts[j][1] == "s_waitcnt" and "vmcnt(0)" in insts[j][2]):
+                if _vmem_store(insts[j][1]):
+                    bad.append((name, insts[i][0], "vector store %s at 0x%x reaches the atomic without "
+                                "s_waitcnt vmcnt(0)" % (insts[j][1], insts[j][0])))
+                    break
+                j -= 1
+            if j < 0:
+                bad.append((name, insts[i][0], "no s_waitcnt vmcnt(0) before the atomic"))
+        if not any(_vmem_store(mn) and "sc1" in ops for _, mn, ops in insts):
+            bad.append((name, 0, "no sc1 (write-through) node store"))
+        if not any(mn.startswith("global_load") and "sc1" in ops for _, mn, ops in insts):
+            bad.append((name, 0, "no sc1 (coherent) child load"))
+    return seen, bad
+
+
 def main(argv):
     quiet = "--quiet" in argv
     files = [a for a in argv if not a.startswith("--")]

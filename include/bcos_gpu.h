@@ -282,6 +282,41 @@ int bcosgpu_secp256k1_verify(int device, const uint8_t* pub64, const uint8_t* ha
 /* SM2Crypto::verify (SM2Crypto.cpp:66-79) -> fast_sm2_verify: sig64 = r||s, with the given key. */
 int bcosgpu_sm2_verify(int device, const uint8_t* pub64, const uint8_t* hash32, const uint8_t* sig64);
 
+/* ---------------------------------------------------------------- device sets (one process, several GPUs) */
+/* A FISCO node is ONE process with one CryptoSuite (libinitializer/ProtocolInitializer.cpp:102-124) whose
+ * batch sites run in-process (TransactionSync.cpp:516-548, BlockImpl.h:111-154); these entry points let
+ * that process use all the GPUs of its node (SURVEY 8(b) "one context per GPU", 8(e)).  `devices` lists
+ * ndev device indices (1 <= ndev <= 64); a batch is split by index into ndev contiguous shards, shard k
+ * running on devices[k] on its own stream with its own buffers -- an index may repeat (two shards on one
+ * GPU, distinct streams).  Results are identical to the single-device calls for every n.  Host pointers;
+ * the calling thread's current device is left unchanged.
+ * Initialise every device of the set (tables, streams); idempotent. */
+int bcosgpu_init_devices(const int* devices, int ndev);
+/* The signature batches above, sharded over the set (each shard a coalesced job on its device). */
+int bcosgpu_secp256k1_recover_batch_multi(const int* devices, int ndev, const uint8_t* hash32, const uint8_t* sig65,
+                                          size_t n, uint8_t* pub64, uint8_t* addr20, uint8_t* ok);
+int bcosgpu_sm2_verify_batch_multi(const int* devices, int ndev, const uint8_t* hash32, const uint8_t* sig128,
+                                   size_t n, uint8_t* addr20, uint8_t* ok);
+int bcosgpu_verify_batch_multi(const int* devices, int ndev, int suite, const uint8_t* pub64, const uint8_t* hash32,
+                               const uint8_t* sig, size_t sig_stride, size_t n, uint8_t* ok);
+/* bcosgpu_tx_verify_batch over the set: TransactionSync::importDownloadedTxs' verify loop
+ * (TransactionSync.cpp:516-548) for a whole download on every GPU of the node. */
+int bcosgpu_tx_verify_batch_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off,
+                                  const uint8_t* sig, const uint64_t* sig_off, size_t n, uint8_t* txhash32,
+                                  uint8_t* sender20, uint8_t* status);
+/* Block check in one call: bcosgpu_tx_verify_batch_multi plus the block's tx root
+ * (BlockImpl::calculateTransactionRoot, BlockImpl.h:111-154: Merkle<H, width> over the tx hashes, H =
+ * Keccak256 / SM3 by suite; zero hash for an empty block).  Shard starts are multiples of width^L, each
+ * GPU reduces its shard's hashes to the reference tree's level-L nodes, the frontiers (a few KB) are
+ * gathered on devices[0] with peer copies over xGMI, and the top levels run there. */
+int bcosgpu_block_verify_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off,
+                               const uint8_t* sig, const uint64_t* sig_off, size_t n, int width, uint8_t* txhash32,
+                               uint8_t* sender20, uint8_t* status, uint8_t* root32);
+/* Merkle<H, width>::generateMerkle's root (Merkle.h:170-208) over the set, by the same frontier scheme;
+ * n == 0 is BCOSGPU_E_EMPTY, n == 1 returns the leaf. */
+int bcosgpu_merkle_root_multi(const int* devices, int ndev, int hasher, int width, const uint8_t* leaves32, size_t n,
+                              uint8_t* root32);
+
 /* ---------------------------------------------------------------- wedpr-ABI single-call shims */
 /* Same layout as wedpr-crypto's CInputBuffer / COutputBuffer; on the calling thread's current device.
  * Return 0 (WEDPR_SUCCESS), -1 (WEDPR_ERROR: invalid input or signature) or

@@ -11,11 +11,16 @@
  *       verify(PublicPtr) (SM2Crypto.cpp:66-79) is overridden, so SM2Crypto::recover (:81-92), the bytes
  *       overload (:29-34) and recoverAddress (:94-122) -- all of which call it -- run on the GPU;
  *       m_verifier is a wedpr-shaped lambda over the same call; m_signer stays wedpr's.
- *   Both take the device at construction and use it from every thread (TBB workers included).
- *   recoverBatch(hashes, signatures) on both: one device call for a whole batch -- the hook the
- *       batch sites (TransactionSync::importDownloadedTxs' parallel_for, TransactionSync.cpp:516-548)
- *       are rewired to; entry i is the recovered key or nullptr where SignatureCrypto::recover would
- *       throw InvalidSignature.
+ *       recoverAddress (:94-122) is overridden as well: all 160 input bytes are read (the reference copies
+ *       16 and reads the rest uninitialised) and an engine error throws, as on secp256k1.
+ *   Both take a device, or a device SET (all GPUs of the node, one process), at construction and use it
+ *   from every thread (TBB workers included); the calling thread's current device is never changed.
+ *   Single calls go to the set's devices in turn (each device coalesces its own callers).
+ *   recoverBatch(hashes, signatures) on both: one engine call for a whole batch, sharded by index over
+ *       the device set (bcosgpu_*_batch_multi) -- the hook the batch sites (TransactionSync::
+ *       importDownloadedTxs' parallel_for, TransactionSync.cpp:516-548) are rewired to; entry i is the
+ *       recovered key or nullptr where SignatureCrypto::recover would throw (InvalidSignature, or for an
+ *       SM2 signature shorter than 128 bytes InvalidKey).
  *
  * Failures throw what the reference throws: InvalidSignature via BOOST_THROW_EXCEPTION with an
  * errinfo_comment (Secp256k1Crypto.cpp:86-91, SM2Crypto.cpp:89-91); an engine error (no gfx950 device,
@@ -35,6 +40,7 @@
 #include <bcos-crypto/signature/sm2/SM2KeyPair.h>
 #include <wedpr-crypto/WedprCrypto.h>
 
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -57,6 +63,26 @@ inline void engineCheck(int rc, const char* what)
     }
 }
 
+// a device set: single calls take its devices in turn
+class DeviceSet
+{
+public:
+    explicit DeviceSet(std::vector<int> _devices)
+      : m_devices(_devices.empty() ? std::vector<int>{0} : std::move(_devices))
+    {}
+    int next() const
+    {
+        return m_devices[m_next.fetch_add(1, std::memory_order_relaxed) % m_devices.size()];
+    }
+    const int* data() const { return m_devices.data(); }
+    int size() const { return (int)m_devices.size(); }
+    const std::vector<int>& devices() const { return m_devices; }
+
+private:
+    std::vector<int> m_devices;
+    mutable std::atomic<size_t> m_next{0};
+};
+
 // calculateAddress (bcos-crypto/interfaces/crypto/KeyPair.h): right160(H(pub))
 inline bcos::bytes rightAddress(bcos::crypto::Hash::Ptr _hashImpl, const bcos::crypto::KeyInterface& _pub)
 {
@@ -69,7 +95,9 @@ class GpuSecp256k1Crypto : public bcos::crypto::Secp256k1Crypto
 public:
     using Ptr = std::shared_ptr<GpuSecp256k1Crypto>;
     // every call runs on `_device` (initialised on first use), whichever thread makes it
-    explicit GpuSecp256k1Crypto(int _device = 0) : m_device(_device) {}
+    explicit GpuSecp256k1Crypto(int _device = 0) : m_set({_device}) {}
+    // every GPU of the node: single calls spread over the set, batches sharded over it
+    explicit GpuSecp256k1Crypto(std::vector<int> _devices) : m_set(std::move(_devices)) {}
     ~GpuSecp256k1Crypto() override = default;
 
     // Secp256k1Crypto::recover -> secp256k1Recover (Secp256k1Crypto.cpp:79-93); concurrent calls are
@@ -78,7 +106,7 @@ public:
         const bcos::crypto::HashType& _hash, bcos::bytesConstRef _signatureData) const override
     {
         auto pub = std::make_shared<bcos::crypto::KeyImpl>(bcos::crypto::SECP256K1_PUBLIC_LEN);
-        const int rc = bcosgpu_secp256k1_recover(m_device, _hash.data(), _signatureData.data(),
+        const int rc = bcosgpu_secp256k1_recover(m_set.next(), _hash.data(), _signatureData.data(),
             _signatureData.size(), (uint8_t*)pub->mutableData());
         engineCheck(rc, "bcosgpu_secp256k1_recover");
         if (rc != 1)
@@ -100,7 +128,7 @@ public:
         {
             return false;
         }
-        const int rc = bcosgpu_secp256k1_verify(m_device, (const uint8_t*)_pubKey->constData(),
+        const int rc = bcosgpu_secp256k1_verify(m_set.next(), (const uint8_t*)_pubKey->constData(),
             _hash.data(), _signatureData.data(), _signatureData.size());
         engineCheck(rc, "bcosgpu_secp256k1_verify");
         return rc == 1;
@@ -138,7 +166,7 @@ public:
         std::memcpy(sig, in + 64, 64);
         sig[64] = (uint8_t)(in[63] - 27);
         bcos::crypto::KeyImpl pub(bcos::crypto::SECP256K1_PUBLIC_LEN);
-        const int rc = bcosgpu_secp256k1_recover(m_device, in, sig, 65, (uint8_t*)pub.mutableData());
+        const int rc = bcosgpu_secp256k1_recover(m_set.next(), in, sig, 65, (uint8_t*)pub.mutableData());
         engineCheck(rc, "bcosgpu_secp256k1_recover");
         if (rc != 1)
         {
@@ -147,7 +175,7 @@ public:
         return {true, rightAddress(_hashImpl, pub)};
     }
 
-    // batch hook: recover every signature of a batch in one engine call
+    // batch hook: recover every signature of a batch in one engine call, sharded over the device set
     std::vector<bcos::crypto::PublicPtr> recoverBatch(const std::vector<bcos::crypto::HashType>& _hashes,
         const std::vector<bcos::bytesConstRef>& _signatures) const
     {
@@ -168,10 +196,9 @@ public:
                 std::memcpy(s.data() + 65 * i, _signatures[i].data(), 65);
             }
         }
-        engineCheck(bcosgpu_init(m_device), "bcosgpu_init");  // the batch ABI runs on the current device
-        engineCheck(
-            bcosgpu_secp256k1_recover_batch(h.data(), s.data(), n, pub.data(), nullptr, ok.data()),
-            "bcosgpu_secp256k1_recover_batch");
+        engineCheck(bcosgpu_secp256k1_recover_batch_multi(
+                        m_set.data(), m_set.size(), h.data(), s.data(), n, pub.data(), nullptr, ok.data()),
+            "bcosgpu_secp256k1_recover_batch_multi");
         for (size_t i = 0; i < n; ++i)
         {
             if (ok[i] && wellFormed[i])
@@ -184,29 +211,31 @@ public:
         return out;
     }
 
-    int device() const { return m_device; }
+    int device() const { return m_set.devices()[0]; }
+    const std::vector<int>& devices() const { return m_set.devices(); }
 
 private:
-    int m_device;
+    DeviceSet m_set;
 };
 
 class GpuSM2Crypto : public bcos::crypto::SM2Crypto
 {
 public:
     using Ptr = std::shared_ptr<GpuSM2Crypto>;
-    explicit GpuSM2Crypto(int _device = 0) : m_device(_device)
+    explicit GpuSM2Crypto(int _device = 0) : GpuSM2Crypto(std::vector<int>{_device}) {}
+    explicit GpuSM2Crypto(std::vector<int> _devices) : m_set(std::move(_devices))
     {
         // SM2Crypto.h:64-65: the wedpr-shaped verifier, for any code that calls m_verifier directly;
         // an engine failure comes back as BCOSGPU_WEDPR_ENGINE_ERROR, which verify() below turns into
         // SignException
-        const int dev = _device;
-        m_verifier = [dev](const CInputBuffer* _pub, const CInputBuffer* _hash,
+        const DeviceSet* set = &m_set;
+        m_verifier = [set](const CInputBuffer* _pub, const CInputBuffer* _hash,
                          const CInputBuffer* _sig) -> int8_t {
             if (!_pub || !_hash || !_sig || _pub->len != 64 || _hash->len != 32 || _sig->len != 64)
             {
                 return WEDPR_ERROR;
             }
-            const int rc = bcosgpu_sm2_verify(dev, (const uint8_t*)_pub->data,
+            const int rc = bcosgpu_sm2_verify(set->next(), (const uint8_t*)_pub->data,
                 (const uint8_t*)_hash->data, (const uint8_t*)_sig->data);
             return rc < 0 ? (int8_t)BCOSGPU_WEDPR_ENGINE_ERROR : rc == 1 ? WEDPR_SUCCESS : WEDPR_ERROR;
         };
@@ -223,11 +252,34 @@ public:
             return false;
         }
         const int rc = bcosgpu_sm2_verify(
-            m_device, (const uint8_t*)_pubKey->constData(), _hash.data(), _signatureData.data());
+            m_set.next(), (const uint8_t*)_pubKey->constData(), _hash.data(), _signatureData.data());
         engineCheck(rc, "bcosgpu_sm2_verify");
         return rc == 1;
     }
     using bcos::crypto::SM2Crypto::verify;
+
+    // SM2Crypto::recoverAddress (SM2Crypto.cpp:94-122): input = hash || pub || r || s (32 / 64 / 32 / 32
+    // bytes, zero-padded); verify against pub, then {true, right160(H(pub))}, else {false, {}}.  All 160
+    // bytes are read (the reference copies min(size, sizeof(bytesConstRef)) = 16 into its struct and reads
+    // the rest uninitialised); an engine error throws SignException, as GpuSecp256k1Crypto's does (the
+    // inherited body would swallow it into {false, {}}).
+    std::pair<bool, bcos::bytes> recoverAddress(
+        bcos::crypto::Hash::Ptr _hashImpl, bcos::bytesConstRef _in) const override
+    {
+        uint8_t in[160] = {0};
+        std::memcpy(in, _in.data(), _in.size() < 160 ? _in.size() : 160);
+        uint8_t rs[64];
+        std::memcpy(rs, in + 96, 64);
+        const int rc = bcosgpu_sm2_verify(m_set.next(), in + 32, in, rs);
+        engineCheck(rc, "bcosgpu_sm2_verify");
+        if (rc != 1)
+        {
+            return {false, {}};
+        }
+        bcos::crypto::KeyImpl pub(bcos::crypto::SM2_PUBLIC_KEY_LEN);
+        std::memcpy(pub.mutableData(), in + 32, 64);
+        return {true, rightAddress(_hashImpl, pub)};
+    }
 
     // batch hook: SM2Crypto::recover (verify against the embedded key) for a whole batch
     std::vector<bcos::crypto::PublicPtr> recoverBatch(const std::vector<bcos::crypto::HashType>& _hashes,
@@ -244,16 +296,18 @@ public:
         for (size_t i = 0; i < n; ++i)
         {
             std::memcpy(h.data() + 32 * i, _hashes[i].data(), 32);
-            // SignatureDataWithPub needs r || s || pub (128 B); SM2Crypto::recover reads pub from it
-            wellFormed[i] = _signatures[i].size() >= 128;
+            // SM2Crypto::recover takes pub = every byte after r || s (SignatureDataWithPub.h:55-64) and
+            // fast_sm2_verify accepts only a 64-byte key (hex2point of "04" || pub, fast_sm2.cpp:142-160):
+            // shorter signatures throw InvalidKey (KeyImpl.h:36-46), longer ones InvalidSignature
+            wellFormed[i] = _signatures[i].size() == 128;
             if (wellFormed[i])
             {
                 std::memcpy(s.data() + 128 * i, _signatures[i].data(), 128);
             }
         }
-        engineCheck(bcosgpu_init(m_device), "bcosgpu_init");  // the batch ABI runs on the current device
-        engineCheck(bcosgpu_sm2_verify_batch(h.data(), s.data(), n, nullptr, ok.data()),
-            "bcosgpu_sm2_verify_batch");
+        engineCheck(bcosgpu_sm2_verify_batch_multi(m_set.data(), m_set.size(), h.data(), s.data(), n, nullptr,
+                        ok.data()),
+            "bcosgpu_sm2_verify_batch_multi");
         for (size_t i = 0; i < n; ++i)
         {
             if (ok[i] && wellFormed[i])
@@ -266,10 +320,11 @@ public:
         return out;
     }
 
-    int device() const { return m_device; }
+    int device() const { return m_set.devices()[0]; }
+    const std::vector<int>& devices() const { return m_set.devices(); }
 
 private:
-    int m_device;
+    DeviceSet m_set;
 };
 }  // namespace ref
 }  // namespace bcosgpu

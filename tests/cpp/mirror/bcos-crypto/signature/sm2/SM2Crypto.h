@@ -5,6 +5,7 @@
 #include <bcos-crypto/signature/key/KeyImpl.h>
 #include <bcos-crypto/signature/sm2/SM2KeyPair.h>
 #include <wedpr-crypto/WedprCrypto.h>
+#include <algorithm>
 #include <functional>
 namespace bcos
 {
@@ -32,14 +33,17 @@ public:
     {
         return verify(std::make_shared<KeyImpl>(64, _pubKeyBytes), _hash, _signatureData);
     }
+    // SM2Crypto.cpp:81-92: pub = every byte after r || s (SignatureDataWithPub::decode,
+    // SignatureDataWithPub.h:55-64), KeyImpl(64, pub) throws InvalidKey when shorter than 64
+    // (KeyImpl.h:36-46) and keeps all of them otherwise; then the virtual verify
     PublicPtr recover(const HashType& _hash, bytesConstRef _signData) const override
     {
-        if (_signData.size() < 128)
+        auto pubBytes = std::make_shared<bytes>();
+        if (_signData.size() > (size_t)SM2_SIGNATURE_LEN)
         {
-            BOOST_THROW_EXCEPTION(InvalidSignature() << errinfo_comment("invalid signature data"));
+            pubBytes->assign(_signData.data() + SM2_SIGNATURE_LEN, _signData.data() + _signData.size());
         }
-        auto pub = std::make_shared<KeyImpl>(
-            64, std::make_shared<const bytes>(_signData.data() + 64, _signData.data() + 128));
+        auto pub = std::make_shared<KeyImpl>(64, pubBytes);
         if (verify(pub, _hash, _signData))
         {
             return pub;
@@ -51,12 +55,14 @@ public:
     {
         throw SignException() << errinfo_comment("host-side (wedpr) in the reference");
     }
-    // SM2Crypto.cpp:94-122: input = hash || pub || r || s; verify (the virtual) against pub, then
-    // calculateAddress = right160(H(pub)); any exception -> {false, {}}
+    // SM2Crypto.cpp:94-122: input = hash || pub || r || s, of which the reference copies only
+    // min(size, sizeof(bytesConstRef)) = 16 bytes into its struct (the rest is indeterminate there, zero
+    // here); verify (the virtual) against pub, then calculateAddress = right160(H(pub)); any exception
+    // -> {false, {}}.  GpuSM2Crypto overrides this (all 160 bytes, engine errors throw).
     std::pair<bool, bytes> recoverAddress(Hash::Ptr _hashImpl, bytesConstRef _input) const override
     {
         byte in[160] = {0};
-        std::memcpy(in, _input.data(), _input.size() < 160 ? _input.size() : 160);
+        std::memcpy(in, _input.data(), std::min(_input.size(), sizeof(_input)));
         HashType h;
         std::memcpy(h.data(), in, 32);
         bytes sig(in + 96, in + 160);
@@ -70,7 +76,7 @@ public:
                 return {true, bytes(d.data() + 12, d.data() + 32)};
             }
         }
-        catch (const std::exception&)
+        catch (...)
         {
         }
         return {false, {}};

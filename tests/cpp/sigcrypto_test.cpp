@@ -167,6 +167,66 @@ int main() {
         in[100] ^= 1;
         CHECK(!s2.recoverAddress(keccak, bytesConstRef(in)).first);
     }
+    // SM2 signature lengths (oracle/ec.c oracle_sm2_recover: only exactly 128 bytes recover).  The reference:
+    // SM2Crypto::recover takes pub = every byte after r || s (SignatureDataWithPub.h:55-64); KeyImpl(64, pub)
+    // throws InvalidKey below 64 bytes (KeyImpl.h:36-46) and keeps a longer one whole, which fast_sm2_verify's
+    // hex2point("04" || pub) rejects (fast_sm2.cpp:142-160) -> InvalidSignature.  recoverBatch: nullptr for all.
+    // verify with a KNOWN 64-byte key reads r || s only (SM2Crypto.cpp:71), so the length does not matter there.
+    {
+        bytes s127(sm2sig.begin(), sm2sig.begin() + 127);
+        bytes s129 = sm2sig;
+        s129.push_back(0);
+        bytes s192 = sm2sig;
+        s192.insert(s192.end(), 64, 0x11);
+        bool invalidKey = false;
+        try {
+            s2.recover(sm3abcd, bytesConstRef(s127));
+        } catch (const InvalidKey&) {
+            invalidKey = true;
+        }
+        CHECK(invalidKey);
+        CHECK(throws_invalid([&] { s2.recover(sm3abcd, bytesConstRef(s129)); }));
+        CHECK(throws_invalid([&] { s2.recover(sm3abcd, bytesConstRef(s192)); }));
+        CHECK(s2.verify(sp, sm3abcd, bytesConstRef(s127)));
+        CHECK(s2.verify(sp, sm3abcd, bytesConstRef(s129)));
+        CHECK(s2.verify(sp, sm3abcd, bytesConstRef(s192)));
+        auto lb = sm2.recoverBatch({sm3abcd, sm3abcd, sm3abcd, sm3abcd},
+            {bytesConstRef(sm2sig), bytesConstRef(s127), bytesConstRef(s129), bytesConstRef(s192)});
+        CHECK(lb.size() == 4 && lb[0] && !lb[1] && !lb[2] && !lb[3]);
+    }
+    // a device SET in one process ({0, 0}: two shards on the one GPU here): batches sharded over it, single
+    // calls taking its devices in turn -- same results
+    {
+        bcosgpu::ref::GpuSecp256k1Crypto secp2(std::vector<int>{0, 0});
+        bcosgpu::ref::GpuSM2Crypto sm22(std::vector<int>{0, 0});
+        std::vector<HashType> hs;
+        std::vector<bytesConstRef> ss;
+        for (int i = 0; i < 9; ++i) {
+            hs.push_back(i % 3 == 2 ? mh2 : mh);
+            ss.push_back(i % 3 == 1 ? bytesConstRef(bad) : bytesConstRef(sig));
+        }
+        auto b2 = secp2.recoverBatch(hs, ss);
+        CHECK(b2.size() == 9);
+        for (int i = 0; i < 9; ++i)
+            CHECK(i % 3 == 1 ? !b2[i] : (b2[i] && b2[i]->data() == (i % 3 == 2 ? pub2 : pub)->data()));
+        for (int i = 0; i < 4; ++i) CHECK(secp2.recover(mh, bytesConstRef(sig))->data() == pub->data());
+        auto sb2 = sm22.recoverBatch({sm3abcd, sm3abcd, sm3abcd}, {bytesConstRef(sm2sig), bytesConstRef(sm2bad),
+                                                                 bytesConstRef(sm2sig)});
+        CHECK(sb2.size() == 3 && sb2[0] && !sb2[1] && sb2[2]);
+        CHECK(secp2.devices().size() == 2 && sm22.device() == 0);
+    }
+    // SM2 recoverAddress with an engine failure throws SignException (not {false, {}})
+    {
+        bcosgpu::ref::GpuSM2Crypto badSm2(64);
+        bytes in(160, 0);
+        std::memcpy(in.data(), sm3abcd.data(), 32);
+        std::memcpy(in.data() + 32, sm2pub.data(), 64);
+        std::memcpy(in.data() + 96, sm2sig.data(), 64);
+        CHECK(throws_sign_exception([&] { badSm2.recoverAddress(keccak, bytesConstRef(in)); }));
+        // shorter input is zero-padded: no key, no address
+        CHECK(!s2.recoverAddress(keccak, bytesConstRef(in.data(), 100)).first);
+    }
+
     // the wedpr-shaped m_verifier: WEDPR_SUCCESS / WEDPR_ERROR
     SM2Probe probe(0);
     CHECK(probe.callVerifier(sm2pub, sm3abcd, sm2sig) == WEDPR_SUCCESS);

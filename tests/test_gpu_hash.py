@@ -200,3 +200,44 @@ def test_merkle_one_launch_repeat_two_streams(gpu, oracle):
     for (width, _, want), roots in zip(cases, outs):
         got = roots.cpu().numpy()
         assert all(got[r].tobytes() == want for r in range(40)), width
+
+
+def test_merkle_one_launch_per_thread_streams(gpu, oracle):
+    """hipStreamPerThread is ONE handle naming a different stream on each thread: the one-launch path keys
+    its arrival-counter slot by (device, handle, thread) for it (and for the null stream), so two host
+    threads launching through that handle at once never share counters.  Two threads x 30 C1 roots each,
+    every root equal to the oracle's."""
+    import threading
+    import torch
+    from bcos_gpu import _lib, device
+    rng = np.random.default_rng(79)
+    per_thread = 2  # hipStreamPerThread
+    cases, results, errs = [], {}, []
+    for width in (16, 2):
+        leaves = rng.integers(0, 256, size=(100_000, 32), dtype=np.uint8)
+        tree = torch.empty((device.merkle_size(100_000, width), 32), dtype=torch.uint8, device="cuda")
+        roots = torch.zeros((30, 32), dtype=torch.uint8, device="cuda")
+        cases.append((width, torch.from_numpy(leaves).cuda(), tree, roots, oracle.merkle(0, width, leaves, nthreads=16)))
+    torch.cuda.synchronize()
+    lib = _lib.lib()
+
+    def run(k):
+        try:
+            width, d_leaves, tree, roots, _ = cases[k]
+            for r in range(30):
+                rc = lib.bcosgpu_merkle_root_dev(0, width, d_leaves.data_ptr(), 100_000, tree.data_ptr(),
+                                                 roots[r].data_ptr(), per_thread)
+                assert rc == 0, _lib.lib().bcosgpu_last_error()
+            torch.cuda.synchronize()  # before the thread (and its per-thread stream) ends
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for width, _, _, roots, want in cases:
+        got = roots.cpu().numpy()
+        assert all(got[r].tobytes() == want for r in range(30)), width

@@ -1,0 +1,111 @@
+"""Multi-GPU behind the C ABI a FISCO node links (include/bcos_gpu.h "device sets", csrc/multi.hip): one
+process, a device list, batches sharded by index over it (TransactionSync.cpp:516-548) and the block tx
+root from per-GPU frontiers gathered on the first device (BlockImpl.h:111-154).
+
+The box has one GPU, so the device lists repeat device 0 ({0, 0}, {0, 0, 0}): every shard still runs from
+its own host thread on its own stream and buffers, and the frontier gather is the same code (a device-local
+copy where devices differ would take hipMemcpyPeerAsync over xGMI -- that leg is unmeasured on hardware).
+Everything is compared with the oracle."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+from test_cpp_adapter import LIBDIR, ROOT
+
+
+def _build(tmp_path):
+    exe = str(tmp_path / "multi_test")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-o", exe,
+                    os.path.join(ROOT, "tests", "cpp", "multi_test.cpp"), "-L" + LIBDIR, "-lbcosgpu",
+                    "-Wl,-rpath," + LIBDIR], check=True)
+    return exe
+
+
+def test_multi_test_compiles(tmp_path):
+    exe = _build(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2  # usage
+
+
+def test_device_set_argument_errors_without_gpu():
+    """Argument errors come back before any device is touched; without a GPU the set is BCOSGPU_E_NODEV."""
+    import ctypes
+    from bcos_gpu import _lib
+    L = _lib.lib()
+    assert L.bcosgpu_init_devices(None, 0) == _lib.E_ARG
+    devs = (ctypes.c_int * 65)()
+    assert L.bcosgpu_init_devices(devs, 65) == _lib.E_ARG
+    root = ctypes.create_string_buffer(32)
+    assert L.bcosgpu_merkle_root_multi(devs, 1, 0, 2, None, 0, root) == _lib.E_EMPTY
+    assert L.bcosgpu_merkle_root_multi(devs, 1, 0, 1, None, 0, root) == _lib.E_ARG  # width
+    assert L.bcosgpu_block_verify_multi(devs, 1, 0, None, None, None, None, 0, 2, None, None, None, None) == _lib.E_ARG
+    assert L.bcosgpu_block_verify_multi(devs, 1, 5, None, None, None, None, 0, 2, None, None, None, root) == _lib.E_ARG
+    if L.bcosgpu_device_count() == 0:
+        assert L.bcosgpu_init_devices(devs, 1) == _lib.E_NODEV
+
+
+def _threads():
+    env = os.environ.get("OMP_NUM_THREADS")
+    aff = len(os.sched_getaffinity(0))
+    return min(int(env), aff) if env and env.isdigit() and int(env) > 0 else aff
+
+
+def _host(b):
+    return (b.pre.cpu().numpy(), b.pre_off.cpu().numpy().astype(np.uint64), b.sig.cpu().numpy(),
+            b.sig_off.cpu().numpy().astype(np.uint64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("suite", [0, 1])
+def test_device_sets_match_oracle(gpu, oracle, suite):
+    """bcosgpu_block_verify_multi / _tx_verify_batch_multi / _merkle_root_multi over device lists of 1-3
+    entries, sizes from 1 tx to 20,001 (shards empty, ragged, width^L-aligned), widths 2 and 16: every hash,
+    verdict, sender and root equals the oracle's."""
+    from bcos_gpu import synth, tx
+    suite_obj = gpu.sm_suite() if suite else gpu.secp256k1_suite()
+    hasher = oracle.SM3 if suite else oracle.KECCAK256
+    for n in (1, 2, 3, 1000, 20_001):
+        b = synth.make_batch(suite, n, seed=0x3A + n + suite, flip_frac=0.05, bad_v_frac=0.02)
+        pre, po, sg, so = _host(b)
+        wh, ws, wst = oracle.tx_verify_packed(suite, pre, po, sg, so, nthreads=_threads())
+        for devs in ([0], [0, 0], [0, 0, 0]):
+            th, snd, st = tx.verify_packed_multi(devs, suite_obj, pre, po, sg, so)
+            assert np.array_equal(th, wh) and np.array_equal(snd, ws) and np.array_equal(st, wst), (n, devs)
+            for width in (2, 16):
+                th, snd, st, root = tx.verify_packed_multi(devs, suite_obj, pre, po, sg, so, width=width)
+                want_root = oracle.merkle(hasher, width, wh)
+                assert np.array_equal(st, wst) and np.array_equal(th, wh), (n, devs, width)
+                assert root == want_root, (n, devs, width)
+                assert tx.merkle_root_multi(devs, hasher, width, wh) == want_root, (n, devs, width)
+    # BlockImpl.h:114-119: no transactions -> the zero root
+    e8, e64 = np.zeros(1, np.uint8), np.zeros(1, np.uint64)
+    assert tx.verify_packed_multi([0, 0], suite_obj, e8, e64, e8, e64, width=2)[3] == bytes(32)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_c4_1m_block_on_two_shards_through_cpp(gpu, oracle, tmp_path):
+    """configs[3]'s 1M secp256k1 txs as ONE block through the C ABI from a C++ process (tests/cpp/multi_test.cpp)
+    with the device list {0, 0}: two shards on two streams, width-2 Keccak tx root from their frontiers --
+    every tx hash, sender, verdict and the root against the oracle, plus the sharded recover batch."""
+    from bcos_gpu import synth
+    n = 1_000_000
+    b = synth.make_batch(0, n, seed=0xC4)
+    pre, po, sg, so = _host(b)
+    wh, ws, wst = oracle.tx_verify_packed(0, pre, po, sg, so, nthreads=_threads())
+    root = oracle.merkle(oracle.KECCAK256, 2, wh, nthreads=_threads())
+    data = str(tmp_path / "block.bin")
+    with open(data, "wb") as f:
+        f.write(b"BGMT" + struct.pack("<III", 0, n, 2))
+        f.write(struct.pack("<Q", pre.size) + pre.tobytes() + po.tobytes())
+        f.write(struct.pack("<Q", sg.size) + sg.tobytes() + so.tobytes())
+        for a in (wh, ws, wst):
+            f.write(np.ascontiguousarray(a, dtype=np.uint8).tobytes())
+        f.write(root)
+    exe = _build(tmp_path)
+    r = subprocess.run([exe, data, "0,0"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "multi_test: ok" in r.stdout
