@@ -685,6 +685,105 @@ def single_call_cpu(b, suite, threads, sample=4000):
             "cores": cpu_threads(), "kind": "standin-openssl" if ossl else "port", "sample": n}
 
 
+def sealer_verify_leg(threads, reps=100):
+    """PBFT sealer-signature checks: SignatureCrypto::verify(pub, hash, sig) with KNOWN keys
+    (BlockValidator::checkSignatureList, bcos-pbft/.../BlockValidator.cpp:141-182, and
+    PBFTCacheProcessor::checkPrecommitWeight, PBFTCacheProcessor.cpp:795-821 -> Secp256k1Crypto.cpp:51-63 /
+    SM2Crypto.cpp:66-79), per suite:
+      block_{k}:   one block's k in {4, 7, 32} signatures as one bcosgpu_verify_batch call (host buffers, the
+                   engine's coalesced path) -- p50 / p99 latency over `reps` calls;
+      single:      one SignatureCrypto::verify (bcosgpu_secp256k1_verify / bcosgpu_sm2_verify) -- p50;
+      catch_up:    1,000 blocks x 7 signatures (a sync catch-up) in one device-resident call
+                   (bcosgpu_verify_batch_dev, HIP events) -- sigs/s;
+      cpu:         the OpenSSL stand-in on the same 7-signature block (1 thread: the reference verifies a
+                   block's list in one loop) and on the 7,000 signatures over `threads` threads.
+    Every verdict is checked (all signatures valid)."""
+    import numpy as np
+    import torch
+    import bcos_gpu
+    from bcos_gpu import _lib, device
+    from oracle import oracle
+    out, summ = {}, {}
+    L = _lib.lib()
+    n = 7000
+    for suite in (0, 1):
+        name = "secp256k1" if suite == 0 else "sm2"
+        g = torch.Generator(device="cuda")
+        g.manual_seed(0x5EA1 + suite)
+        sk = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
+        sk[:, 0] &= 0x7F
+        sk[:, 31] |= 1
+        h = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
+        okd = torch.empty(n, dtype=torch.uint8, device="cuda")
+        if suite == 0:
+            pub = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
+            sig = torch.empty((n, 65), dtype=torch.uint8, device="cuda")
+            device.secp256k1_sign(sk, h, pub, sig, okd)
+        else:
+            sig = torch.empty((n, 128), dtype=torch.uint8, device="cuda")
+            device.sm2_sign(sk, h, sig, okd)
+            pub = sig[:, 64:128].contiguous()
+        torch.cuda.synchronize()
+        assert bool(okd.all())
+        stride = sig.shape[1]
+        crypto = bcos_gpu.SM2Crypto() if suite else bcos_gpu.Secp256k1Crypto()
+        P, H, S = pub.cpu().numpy(), h.cpu().numpy(), sig.cpu().numpy()
+        rec = {}
+        for k in (4, 7, 32):
+            assert crypto.verify_batch(P[:k], H[:k], S[:k]).all()
+            ts = []
+            for r in range(reps):
+                a = (r * k) % (n - k)
+                t0 = time.perf_counter()
+                crypto.verify_batch(P[a:a + k], H[a:a + k], S[a:a + k])
+                ts.append(time.perf_counter() - t0)
+            ts.sort()
+            rec["block_%d" % k] = {"p50_ms": ts[len(ts) // 2] * 1e3, "p99_ms": ts[len(ts) * 99 // 100] * 1e3}
+        ts = []
+        for r in range(reps):
+            t0 = time.perf_counter()
+            assert crypto.verify(P[r].tobytes(), H[r].tobytes(), S[r].tobytes())
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        rec["single_p50_ms"] = ts[len(ts) // 2] * 1e3
+        stream = torch.cuda.current_stream()
+
+        def launch():
+            _lib.check(L.bcosgpu_verify_batch_dev(suite, pub.data_ptr(), h.data_ptr(), sig.data_ptr(), stride, n,
+                                                  okd.data_ptr(), stream.cuda_stream))
+        for _ in range(3):
+            launch()
+        torch.cuda.synchronize()
+        kt = []
+        for _ in range(20):
+            a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            launch()
+            c.record(stream)
+            c.synchronize()
+            kt.append(a.elapsed_time(c))
+        kt.sort()
+        assert bool(okd.all())
+        rec["catch_up_1000x7"] = {"sigs_per_s": n / (kt[len(kt) // 2] * 1e-3), "kernel_ms": kt[len(kt) // 2]}
+        cpu = {}
+        if oracle.standin() is not None:
+            S64 = np.ascontiguousarray(S[:, :64])
+            med, _ = _median_time(lambda: oracle.standin_verify_batch(suite, P[:7], H[:7], S64[:7], nthreads=1))
+            cpu["block_7_ms"] = med * 1e3
+            med, _ = _median_time(lambda: oracle.standin_verify_batch(suite, P, H, S64, nthreads=threads), reps=3)
+            cpu["catch_up_sigs_per_s"] = n / med
+            cpu.update(threads=threads, kind="standin-openssl")
+            assert oracle.standin_verify_batch(suite, P[:64], H[:64], S64[:64]).all()
+        rec["cpu"] = cpu
+        out[name] = rec
+        summ[name] = {"blk4_p50_ms": _g(rec["block_4"]["p50_ms"]), "blk7_p50_ms": _g(rec["block_7"]["p50_ms"]),
+                      "blk32_p50_ms": _g(rec["block_32"]["p50_ms"]), "single_p50_ms": _g(rec["single_p50_ms"]),
+                      "catchup_sig_s": _g(rec["catch_up_1000x7"]["sigs_per_s"]),
+                      "cpu_blk7_ms": _g(cpu.get("block_7_ms")), "cpu_catchup_sig_s": _g(cpu.get("catch_up_sigs_per_s"))}
+    out["summary"] = summ
+    return out
+
+
 def create_transaction_leg(b, suite, n, want_status, reps=20):
     """The same batch from raw Tars encodings (createTransaction(bytes, checkSig = true, checkHash = true),
     TransactionFactoryImpl.h:46-85): device decode + pack + verify + hash check, HBM-resident."""
@@ -860,6 +959,7 @@ def main():
             from bcos_gpu import synth
             sm2b = synth.make_batch(1, 10_000, seed=0x5A3)
             line["interface"] = interface_legs([(0, b), (1, sm2b)])
+            line["sealer_verify"] = sealer_verify_leg(threads)
         if not args.no_merkle:
             line["merkle"] = merkle_legs(0 if args.no_cpu_baseline else threads)
             line["merkle_c1"] = {h: line["merkle"]["%s_w16_100k" % h] for h in ("keccak256", "sm3")}

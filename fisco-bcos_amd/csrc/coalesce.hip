@@ -53,7 +53,7 @@ struct Slot {
 
 struct DeviceQueue {
     std::mutex mu;
-    std::condition_variable cv;
+    uint64_t next_seq = 0;
     std::deque<SigJob*> pending[kSigJobKinds];
     Slot slots[kMaxSlots];
 };
@@ -230,6 +230,28 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
 
 }  // namespace
 
+// Wake-ups are targeted, never broadcast: a finished batch wakes its own jobs' owners, and for every
+// free slot the owner of the oldest queued job (of any kind) to lead the next batch.  (A broadcast on
+// every completion woke all callers -- 256 submitter threads on the box's 16 cores -- per batch: at
+// 256 threads secp256k1 single calls fell to 30k/s with a p99 of 87 ms, profiles/r04_bench_first.json.)
+static void wake_leaders(DeviceQueue& q) {
+    int free_slots = 0;
+    for (int k = 0; k < slots_in_use(); ++k) free_slots += !q.slots[k].busy;
+    for (int pass = 0; pass < kSigJobKinds && free_slots > 0; ++pass) {
+        // the kind whose front job has waited longest first (jobs carry their arrival order)
+        SigJob* best = nullptr;
+        for (int kd = 0; kd < kSigJobKinds; ++kd) {
+            auto& pend = q.pending[kd];
+            if (pend.empty() || pend.front()->woken) continue;
+            if (!best || pend.front()->seq < best->seq) best = pend.front();
+        }
+        if (!best) return;
+        best->woken = true;
+        best->cv.notify_one();
+        --free_slots;
+    }
+}
+
 int coalesced_run(int device, SigJob& job) {
     if (device < 0 || device >= 64 || job.kind < 0 || job.kind >= kSigJobKinds) {
         job.err = "bad device or job kind";
@@ -240,9 +262,11 @@ int coalesced_run(int device, SigJob& job) {
     std::unique_lock<std::mutex> lk(q.mu);
     job.done = false;
     job.queued = true;
+    job.woken = false;
+    job.seq = q.next_seq++;
     q.pending[job.kind].push_back(&job);
-    // Every queued job's owner is in this loop, so a caller leads only while its own job is still
-    // queued (a caller whose job is in flight just waits for it): each freed slot wakes the owners.
+    // A caller leads only while its own job is still queued (a caller whose job is in flight just waits
+    // for its batch to finish).
     while (!job.done) {
         Slot* free_slot = nullptr;
         for (int k = 0; k < slots_in_use(); ++k)
@@ -251,7 +275,8 @@ int coalesced_run(int device, SigJob& job) {
                 break;
             }
         if (!free_slot || !job.queued) {
-            q.cv.wait(lk);
+            job.cv.wait(lk);
+            job.woken = false;
             continue;
         }
         // lead: take every queued job of this kind, oldest first, up to kMaxBatch items (at least one)
@@ -277,8 +302,11 @@ int coalesced_run(int device, SigJob& job) {
         }
         lk.lock();
         free_slot->busy = false;
-        for (SigJob* j : batch) j->done = true;
-        q.cv.notify_all();
+        for (SigJob* j : batch) {
+            j->done = true;
+            if (j != &job) j->cv.notify_one();
+        }
+        wake_leaders(q);
     }
     return job.rc;
 }

@@ -77,26 +77,6 @@ __device__ __forceinline__ void glv_half_lds(Jac& acc, fe& k, bool neg, bool phi
     }
 }
 
-// parse r, s, v of a 65-byte signature; ok = libsecp256k1 parse_compact + r, s != 0
-__device__ __forceinline__ bool parse_sig65(const uint8_t* sig, uint32_t siglen, fe& r, fe& s, uint32_t& v) {
-    if (siglen != 65u) {
-        fe_zero(r);
-        fe_zero(s);
-        v = 0;
-        return false;
-    }
-    ByteReader rd(sig, 65);
-    uint32_t w[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
-    fe_from_be_words(r, w);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
-    fe_from_be_words(s, w);
-    v = rd.word(16) & 0xffu;
-    return v <= 3u && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, ParamN1::M);
-}
-
 __global__ __launch_bounds__(256, 1) void tx_verify_split_kernel(const uint8_t* __restrict__ pre,
                                                                  const uint64_t* __restrict__ pre_off,
                                                                  const uint8_t* __restrict__ sig,
@@ -1129,16 +1109,21 @@ __device__ __forceinline__ void trio_add_digit_zz(TrioPt& acc, const Trio26Lds& 
 
 // TRIO = false: tx_verify_coop26_kernel (64 txs per workgroup, wave-pair chains); TRIO = true:
 // tx_verify_trio26_kernel (40 txs per workgroup, lane-trio chains).  Phases A and D are the same code.
-template <bool TRIO, class IO>
+// MODE kRecover: public-key recovery (Q = u1 G + u2 R, R from r and v); MODE kVerify (TRIO only):
+// libsecp256k1 ecdsa_verify with a KNOWN key P (sig_verify_trio26_kernel, KeyIO): Q = (e/s) G + (r/s) P,
+// accept iff x(Q) = r mod n -- no square root (P is given), s^-1 instead of r^-1, and the projective
+// x-check instead of the affine inversion and the address hash.
+enum { kRecover = 0, kVerify = 1 };
+template <bool TRIO, int MODE, class IO>
 __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint32_t* __restrict__ tab, int tab_bits) {
+    static_assert(MODE == kRecover || TRIO, "known-key verify runs on the trio kernel only");
+    constexpr bool kVer = MODE == kVerify;
     constexpr int TPW = TRIO ? 40 : 64;  // txs per workgroup
     __shared__ std::conditional_t<TRIO, Trio26Lds, Coop26Lds> L;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * TPW + lane;
     const bool active = lane < TPW && i < n;
     COOP_T(0);
-    const uint8_t* sp = nullptr;
-    const uint32_t slen = active ? io.sig_span(i, sp) : 0u;
     if (threadIdx.x == 0) {
         L.post[0] = 0u;
         L.post[1] = 0u;
@@ -1149,9 +1134,62 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
     fe r, s;
     uint32_t v = 0;
     bool ok = false;
-    if (active) ok = parse_sig65(sp, slen, r, s, v);
-    else { fe_zero(r); fe_zero(s); }
-    if (wave == 1 || wave == 2) {
+    if constexpr (kVer) {
+        // verify: wave 1 checks the key and builds ITS table (P is given: no square root); r kept for the
+        // final x-check (in the LDS slot recovery uses for y)
+        fe kx, ky;
+        if (active) {
+            io.key_rs(i, r, s, kx, ky);
+            ok = fe_lt_k(kx, FieldK1::P) && fe_lt_k(ky, FieldK1::P) && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) &&
+                 fe_lt_k(r, ParamN1::M) && fe_lt_k(s, kN1HalfPlus);  // low-S (secp256k1_ecdsa_verify)
+        } else {
+            fe_zero(r);
+            fe_zero(s);
+            fe_zero(kx);
+            fe_zero(ky);
+        }
+        if (wave == 0) lds_store_fe(L.ys, r, lane);
+        if (wave == 1) {
+            Aff26 P;
+            fe26_from_fe(P.x, kx);
+            fe26_from_fe(P.y, ky);
+            fe26 l, rr, t, seven;
+            fe26_sqr(l, P.y);
+            fe26_sqr(t, P.x);
+            fe26_mul(rr, t, P.x);
+            fe26_set_small(seven, 7u);
+            fe26_add(rr, rr, seven);
+            fe26_sub<3>(l, l, rr);
+            const bool on = fe26_is_zero(l);  // y^2 = x^3 + 7
+            if (!(ok && on)) {  // a valid point for the rejected lanes
+                fe26_const(P.x, kK1Gx);
+                fe26_const(P.y, kK1Gy);
+            }
+            L.rflag[lane] = on ? 2u : 0u;
+            Aff26 A[8];
+            fe26 Zc, beta;
+            {
+                Jac26 T[8];
+                multiples8_26(T, P);
+                coz_table26(A, Zc, T);
+            }
+            fe26_const(beta, kGlvBeta);
+            Unroll<0, 8>::run([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                fe26 bx;
+                fe26_mul(bx, A[j].x, beta);
+                lds_store_limbs26(L.tab[j], A[j].x, lane);
+                lds_store_limbs26(L.tab[j] + 10, A[j].y, lane);
+                lds_store_limbs26(L.tabphx[j], bx, lane);
+            });
+            lds_store_fe26(L.zc, Zc, lane);
+            COOP_T(6);
+        }
+    } else {
+        if (active) ok = io.rsv(i, r, s, v);
+        else { fe_zero(r); fe_zero(s); }
+    }
+    if (!kVer && (wave == 1 || wave == 2)) {
         fe x;
         fe_copy(x, r);
         bool okr = ok;
@@ -1207,10 +1245,11 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             COOP_T(6);
         }
     }
-    if (!ok) {
+    if (!ok) {  // keep the scalar arithmetic well defined on rejected lanes
         fe_zero(r);
         r.v[0] = 1;
         fe_zero(s);
+        if (kVer) s.v[0] = 1;
     }
     if (wave == 3) {
         fe e;
@@ -1221,25 +1260,25 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
         coop_post(&L.post[1]);
         COOP_T(7);
     } else if (wave == 0) {
-        fe rm, rinv;
-        FieldN1::from_plain(rm, r);
+        fe rm, rinv;  // verify: w = s^-1 in this slot
+        FieldN1::from_plain(rm, kVer ? s : r);
         if constexpr (TRIO) FieldInv<FieldN1>::inv_pipe(rinv, rm);  // (pipelined: this kernel has the registers)
         else FieldInv<FieldN1>::inv(rinv, rm);
         lds_store_fe(L.xrinv, rinv, lane);
         coop_post(&L.post[0]);
         COOP_T(7);
     }
-    if (wave != 2) {
+    if (kVer || wave != 2) {
         coop_wait(&L.post[0]);
         coop_wait(&L.post[1]);
         fe e, rinv, u1;
         lds_load_fe(e, L.xe, lane);
         lds_load_fe(rinv, L.xrinv, lane);
-        FieldN1::mul(u1, e, rinv);
-        FieldN1::neg(u1, u1);
+        FieldN1::mul(u1, e, rinv);  // recover: u1 = -e / r; verify: u1 = e / s
+        if (!kVer) FieldN1::neg(u1, u1);
         if (wave == 1) {
             fe u2, k1, k2;
-            FieldN1::mul(u2, s, rinv);
+            FieldN1::mul(u2, kVer ? r : s, rinv);  // recover: s / r; verify: r / s
             bool neg1, neg2;
             glv_split(k1, neg1, k2, neg2, u2);
 #pragma unroll
@@ -1250,13 +1289,15 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             L.flags[lane] = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
         }
         Jac26 G;
-        if (tab_bits == kWideBits) {  // 16 windows of the 16-bit comb: 7 / 7 / 2 (wave 1 also builds the table)
-            const int lo = wave == 0 ? 0 : wave == 3 ? 7 : 14;
-            const int hi = wave == 0 ? 7 : wave == 3 ? 14 : 16;
+        // recover: wave 2 takes the square root, so the comb windows go to waves 0, 3 and 1; verify: wave 2
+        // joins (wave 3 also adds wave 0's partial, wave 1 builds the table first)
+        if (tab_bits == kWideBits) {  // 16 windows of the 16-bit comb: 7 / 7 / 2; verify 6 / 4 / 5 / 1
+            const int lo = kVer ? (wave == 0 ? 0 : wave == 3 ? 6 : wave == 2 ? 10 : 15) : (wave == 0 ? 0 : wave == 3 ? 7 : 14);
+            const int hi = kVer ? (wave == 0 ? 6 : wave == 3 ? 10 : wave == 2 ? 15 : 16) : (wave == 0 ? 7 : wave == 3 ? 14 : 16);
             comb_range26w<kWideBits>(G, u1, tab, lo, hi);
-        } else {  // 32 windows of the 8-bit comb: 12 / 12 / 8
-            const int lo = wave == 0 ? 0 : wave == 3 ? 12 : 24;
-            const int hi = wave == 0 ? 12 : wave == 3 ? 24 : 32;
+        } else {  // 32 windows of the 8-bit comb: 12 / 12 / 8; verify 11 / 8 / 11 / 2
+            const int lo = kVer ? (wave == 0 ? 0 : wave == 3 ? 11 : wave == 2 ? 19 : 30) : (wave == 0 ? 0 : wave == 3 ? 12 : 24);
+            const int hi = kVer ? (wave == 0 ? 11 : wave == 3 ? 19 : wave == 2 ? 30 : 32) : (wave == 0 ? 12 : wave == 3 ? 24 : 32);
             comb_range26w<8>(G, u1, tab, lo, hi);
         }
         // G0 + G3 on wave 3 while phase A waits for wave 1's last window (one addition off phase D)
@@ -1269,8 +1310,10 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             coop26_load_jac(G0, L.pt[2], lane);
             CurveK1x::add(S, G0, G);
             coop26_store_jac(L.pt[3], S, lane);
-        } else {
+        } else if (wave == 1) {
             coop26_store_jac(L.pt[4], G, lane);
+        } else {  // verify: wave 2's windows
+            coop26_store_jac(L.pt[0], G, lane);
         }
     }
     COOP_T(1);
@@ -1320,6 +1363,8 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
         __syncthreads();  // no wave reads the table any more
         if (chain == 1) {
             trio_store(xbuf, acc, lane);
+        } else if constexpr (kVer) {
+            lds_load_fe26(zcy, L.zc, tl);  // the co-Z table of P itself: Z Zc
         } else {
             fe26 zc, y;
             lds_load_fe26(zc, L.zc, tl);
@@ -1327,7 +1372,7 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             fe26_mul(zcy, zc, y);
         }
         __syncthreads();
-        if (chain == 1) {  // G = (G0 + G3) + G1 (phase A's partials)
+        if (chain == 1) {  // G = (G0 + G3) + G1 (+ G2, verify) (phase A's partials)
             Jac26 Ga, Gb;
             TrioPt A, B;
             coop26_load_jac(Ga, L.pt[3], tl);
@@ -1335,6 +1380,11 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             trio_from_jac(A, Ga, T);
             trio_from_jac(B, Gb, T);
             trio_add(A, A, B, T);
+            if constexpr (kVer) {
+                coop26_load_jac(Gb, L.pt[0], tl);
+                trio_from_jac(B, Gb, T);
+                trio_add(A, A, B, T);
+            }
             trio_store(gbuf, A, lane);
         } else {  // R = (k1 R' + k2 phi(R')) on E_w, then (X, Y, Z Zc y) on E
             TrioPt P1;
@@ -1343,7 +1393,28 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             fe26_mul(acc.Zs, acc.Zs, zcy);
         }
         __syncthreads();
-        if (chain == 0) {
+        if (chain == 0 && kVer) {
+            TrioPt G;
+            trio_load(G, gbuf, lane);
+            trio_add(acc, acc, G, T);
+            // x(Q) = X / Z^2 must be r or r + n (when r + n < p): X == c Z^2, projectively, on lane 2
+            fe rr, r2, xw, cw;
+            lds_load_fe(rr, L.ys, tl);
+            fe26 z2, c, rhs;
+            fe26_sqr(z2, acc.Zs);
+            fe26_from_fe(c, rr);
+            fe26_mul(rhs, c, z2);
+            fe26_to_fe(xw, acc.Xs);
+            fe26_to_fe(cw, rhs);
+            bool match = fe_eq_raw(xw, cw);
+            const uint32_t carry = fe_add_k(r2, rr, ParamN1::M);
+            const bool second = carry == 0u && fe_lt_k(r2, FieldK1::P);
+            fe26_from_fe(c, second ? r2 : rr);
+            fe26_mul(rhs, c, z2);
+            fe26_to_fe(cw, rhs);
+            match = match || (second && fe_eq_raw(xw, cw));
+            ok2 = (tflags & 3u) == 3u && !acc.inf && match;
+        } else if (chain == 0) {
             TrioPt G;
             trio_load(G, gbuf, lane);
             trio_add(acc, acc, G, T);
@@ -1478,7 +1549,7 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
 
 template <class IO>
 __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab) {
-    coop26_body<false>(io, n, tab, 8);
+    coop26_body<false, kRecover>(io, n, tab, 8);
 }
 
 // The trio kernel: phase C's doublings and mixed additions cost one multiplication of latency per
@@ -1488,8 +1559,28 @@ __global__ __launch_bounds__(256, 1) void tx_verify_coop26_kernel(IO io, uint64_
 template <class IO>
 __global__ __launch_bounds__(256, 1) void tx_verify_trio26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab,
                                                                   int tab_bits) {
-    coop26_body<true>(io, n, tab, tab_bits);
+    coop26_body<true, kRecover>(io, n, tab, tab_bits);
 }
+
+// SignatureCrypto::verify(pub, hash, sig) with a known key on lane trios (KeyIO): the sealer-signature
+// checks of PBFT (BlockValidator.cpp:141-182, PBFTCacheProcessor.cpp:795-821 -> Secp256k1Crypto.cpp:51-63)
+// verify a block's few signatures per call, so this is the latency path.  Bit-identical verdicts to
+// sig_verify_kernel<secp256k1, *> (secp256k1_verify_lane).
+__global__ __launch_bounds__(256, 1) void sig_verify_trio26_kernel(KeyIO io, uint64_t n, const uint32_t* __restrict__ tab,
+                                                                   int tab_bits) {
+    coop26_body<true, kVerify>(io, n, tab, tab_bits);
+}
+
+int launch_sig_verify_small_secp(const KeyIO& io, uint64_t n, hipStream_t st) {
+    const uint32_t *k1, *sm2;
+    int bits = 8;
+    const int rc = tables(&k1, &sm2, &bits);
+    if (rc) return rc;
+    hipLaunchKernelGGL(sig_verify_trio26_kernel, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0, st, io, n, k1,
+                       bits);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
 
 template <class IO>
 int launch_verify_small_secp(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st) {
@@ -1521,5 +1612,6 @@ int launch_verify_small_secp(const TxKernelPolicy& pol, const IO& io, uint64_t n
 }
 template int launch_verify_small_secp<TxIO>(const TxKernelPolicy&, const TxIO&, uint64_t, hipStream_t);
 template int launch_verify_small_secp<SigIO>(const TxKernelPolicy&, const SigIO&, uint64_t, hipStream_t);
+template int launch_verify_small_secp<EcrecIO>(const TxKernelPolicy&, const EcrecIO&, uint64_t, hipStream_t);
 
 }  // namespace bcosgpu

@@ -552,8 +552,17 @@ int tables8_sm2_26(const uint32_t** tab);
 // SigIO (the I/O policies below); SigIO has the fe26 / fp26 lane-trio and pair kernels only
 struct TxIO;
 struct SigIO;
+struct EcrecIO;
+struct KeyIO;
 template <class IO>
 int launch_verify_small_secp(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st);
+// secp256k1 verify with a known key (KeyIO) on the lane-trio kernel (ecc_coop.hip)
+int launch_sig_verify_small_secp(const KeyIO& io, uint64_t n, hipStream_t st);
+// SM2 verify with a known key over KeyIO (ecc_txv.hip: launch_verify's kernel choice)
+int launch_sm2_verify_key(const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
+                          uint64_t n, uint8_t* d_ok, hipStream_t st);
+// compute units of the current device (cached per device)
+int cu_count();
 template <class IO>
 int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st);
 static inline unsigned grid_of(uint64_t n) { return static_cast<unsigned>((n + 255) / 256); }
@@ -665,6 +674,49 @@ __device__ __forceinline__ void sm3_address(uint32_t a[5], const fe& x, const fe
 }
 
 // ------------------------------------------------------------------ kernel I/O policies
+// parse r, s, v of a 65-byte signature; ok = libsecp256k1 parse_compact + r, s != 0 (r, s zero and
+// v = 0 for any other length, so every later check fails too)
+__device__ __forceinline__ bool parse_sig65(const uint8_t* sig, uint32_t siglen, fe& r, fe& s, uint32_t& v) {
+    if (siglen != 65u) {
+        fe_zero(r);
+        fe_zero(s);
+        v = 0;
+        return false;
+    }
+    ByteReader rd(sig, 65);
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(i);
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = rd.word(8 + i);
+    fe_from_be_words(s, w);
+    v = rd.word(16) & 0xffu;
+    return v <= 3u && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, ParamN1::M);
+}
+// r || s || X || Y of a 128-byte SM2 signature-with-key at p (X, Y as big-endian word arrays)
+__device__ __forceinline__ void parse_sm2_128(const uint8_t* p, fe& r, fe& s, uint32_t X[8], uint32_t Y[8]) {
+    ByteReader rd(p, 128);
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = rd.word(k);
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w[k] = rd.word(8 + k);
+    fe_from_be_words(s, w);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        X[k] = bswap32(rd.word(16 + k));
+        Y[k] = bswap32(rd.word(24 + k));
+    }
+}
+__device__ __forceinline__ void zero_sm2_sig(fe& r, fe& s, uint32_t X[8], uint32_t Y[8]) {
+    fe_zero(r);
+    fe_zero(s);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) X[k] = Y[k] = 0u;
+}
+
 // Every verification kernel body (one-lane, lane-trio, cooperative pair) is written once over one of:
 //   TxIO  -- Transaction::verify (Transaction.h:68-82): the digest is H(preimage) and is an output
 //            (txhash); signature i = sig[sig_off[i] .. sig_off[i+1]); results sender20 and status
@@ -673,6 +725,14 @@ __device__ __forceinline__ void sm3_address(uint32_t a[5], const fe& x, const fe
 //            Secp256k1Crypto.cpp:79-93; SM2Crypto::recover, SM2Crypto.cpp:81-92): 32-byte digests,
 //            signatures at a fixed stride and length; results pub64 (secp256k1 only, nullable), addr20
 //            (nullable) and ok (1 valid / 0 invalid).  Output rows need 4-byte alignment only.
+//   EcrecIO -- the EVM ecRecover precompile (Precompiled.cpp:443-482): input hash || v || r || s (128 B,
+//            recid = (byte)(in[63] - 27)), output 12 zero bytes || address and ok.
+//   KeyIO -- SignatureCrypto::verify(pub, hash, sig) with a KNOWN key (Secp256k1Crypto.cpp:51-63,
+//            SM2Crypto.cpp:66-79): digests given, r || s = the first 64 bytes at a stride, keys pub64;
+//            result ok only.
+// The signature comes out of the policy parsed: rsv (secp256k1 recover: r, s, v and the
+// parse_compact verdict) or sm2_sig (r, s and the key X, Y; false when the signature is not
+// well-formed, e.g. not 128 bytes).
 struct TxIO {
     const uint8_t* pre;
     const uint64_t* pre_off;
@@ -686,6 +746,20 @@ struct TxIO {
         const uint64_t a = sig_off[i], b = sig_off[i + 1];
         p = sig + a;
         return b - a > 0xffffffffull ? 0xffffffffu : static_cast<uint32_t>(b - a);
+    }
+    __device__ __forceinline__ bool rsv(uint64_t i, fe& r, fe& s, uint32_t& v) const {
+        const uint8_t* p;
+        const uint32_t l = sig_span(i, p);
+        return parse_sig65(p, l, r, s, v);
+    }
+    __device__ __forceinline__ bool sm2_sig(uint64_t i, fe& r, fe& s, uint32_t X[8], uint32_t Y[8]) const {
+        const uint8_t* p;
+        if (sig_span(i, p) != 128u) {
+            zero_sm2_sig(r, s, X, Y);
+            return false;
+        }
+        parse_sm2_128(p, r, s, X, Y);
+        return true;
     }
     // the digest as the field element the recover / verify bodies take (hash_be)
     template <int H>
@@ -727,6 +801,17 @@ struct SigIO {
         p = sig + static_cast<uint64_t>(stride) * i;
         return siglen;
     }
+    __device__ __forceinline__ bool rsv(uint64_t i, fe& r, fe& s, uint32_t& v) const {
+        return parse_sig65(sig + static_cast<uint64_t>(stride) * i, siglen, r, s, v);
+    }
+    __device__ __forceinline__ bool sm2_sig(uint64_t i, fe& r, fe& s, uint32_t X[8], uint32_t Y[8]) const {
+        if (siglen != 128u) {
+            zero_sm2_sig(r, s, X, Y);
+            return false;
+        }
+        parse_sm2_128(sig + static_cast<uint64_t>(stride) * i, r, s, X, Y);
+        return true;
+    }
     template <int H>
     __device__ __forceinline__ void digest(uint64_t i, fe& h) const {
         const uint32_t* q = reinterpret_cast<const uint32_t*>(hash + 32 * i);
@@ -749,6 +834,88 @@ struct SigIO {
 #pragma unroll
             for (int k = 0; k < 5; ++k) o[k] = valid ? ad[k] : 0u;
         }
+        ok[i] = valid ? 1 : 0;
+    }
+};
+
+struct EcrecIO {
+    const uint8_t* in;  // n x 128, 16-byte aligned
+    uint8_t* out;       // n x 32
+    uint8_t* ok;
+
+    __device__ __forceinline__ bool rsv(uint64_t i, fe& r, fe& s, uint32_t& v) const {
+        const uint8_t* p = in + 128 * i;
+        load_be256_aligned(r, p + 64);
+        load_be256_aligned(s, p + 96);
+        v = ((reinterpret_cast<const uint32_t*>(p)[15] >> 24) - 27u) & 0xffu;  // (byte)(in[63] - 27)
+        return v <= 3u && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, ParamN1::M);
+    }
+    template <int H>
+    __device__ __forceinline__ void digest(uint64_t i, fe& h) const {
+        load_be256_aligned(h, in + 128 * i);
+    }
+    __device__ __forceinline__ bool want_addr() const { return true; }
+    __device__ __forceinline__ void finish(uint64_t i, bool valid, const uint32_t ad[5], const fe*, const fe*) const {
+        uint32_t* o = reinterpret_cast<uint32_t*>(out + 32 * i);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) o[k] = 0u;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[3 + k] = valid ? ad[k] : 0u;
+        ok[i] = valid ? 1 : 0;
+    }
+};
+
+struct KeyIO {
+    const uint8_t* pub;   // n x 64 (X || Y)
+    const uint8_t* hash;  // n x 32
+    const uint8_t* sig;   // item i at sig + stride i: r || s (only the first 64 bytes are read)
+    uint32_t stride;
+    uint8_t* ok;
+
+    template <int H>
+    __device__ __forceinline__ void digest(uint64_t i, fe& h) const {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(hash + 32 * i);
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = q[k];
+        fe_from_be_words(h, w);
+    }
+    // secp256k1: r, s and the key as plain words (x, y)
+    __device__ __forceinline__ void key_rs(uint64_t i, fe& r, fe& s, fe& x, fe& y) const {
+        ByteReader rs(sig + static_cast<uint64_t>(stride) * i, 64), rp(pub + 64 * i, 64);
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rs.word(k);
+        fe_from_be_words(r, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rs.word(8 + k);
+        fe_from_be_words(s, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rp.word(k);
+        fe_from_be_words(x, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rp.word(8 + k);
+        fe_from_be_words(y, w);
+    }
+    // SM2: r || s from the signature, X || Y from the key array (SM2Crypto::verify, SM2Crypto.cpp:66-79)
+    __device__ __forceinline__ bool sm2_sig(uint64_t i, fe& r, fe& s, uint32_t X[8], uint32_t Y[8]) const {
+        ByteReader rs(sig + static_cast<uint64_t>(stride) * i, 64), rp(pub + 64 * i, 64);
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rs.word(k);
+        fe_from_be_words(r, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) w[k] = rs.word(8 + k);
+        fe_from_be_words(s, w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            X[k] = bswap32(rp.word(k));
+            Y[k] = bswap32(rp.word(8 + k));
+        }
+        return true;
+    }
+    __device__ __forceinline__ bool want_addr() const { return false; }
+    __device__ __forceinline__ void finish(uint64_t i, bool valid, const uint32_t*, const fe*, const fe*) const {
         ok[i] = valid ? 1 : 0;
     }
 };

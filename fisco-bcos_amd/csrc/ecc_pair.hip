@@ -686,30 +686,11 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(IO io, uin
     const bool active = i < n;
     if (threadIdx.x < 4) L.seq[threadIdx.x] = 0u;
     __syncthreads();
-    const uint8_t* sp = nullptr;
-    const bool len_ok = active && io.sig_span(i, sp) == 128u;
     fe r, s, px, py;
     uint32_t X[8], Y[8];
-    if (len_ok) {
-        ByteReader rd(sp, 128);
-        uint32_t w[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w[k] = rd.word(k);
-        fe_from_be_words(r, w);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w[k] = rd.word(8 + k);
-        fe_from_be_words(s, w);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            X[k] = bswap32(rd.word(16 + k));
-            Y[k] = bswap32(rd.word(24 + k));
-        }
-    } else {
-        fe_zero(r);
-        fe_zero(s);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) X[k] = Y[k] = 0u;
-    }
+    bool len_ok = false;  // the signature (and key) as the I/O policy gives them: r || s || pub, or KeyIO's key
+    if (active) len_ok = io.sm2_sig(i, r, s, X, Y);
+    else zero_sm2_sig(r, s, X, Y);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         px.v[k] = X[7 - k];
@@ -961,30 +942,11 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
     if (threadIdx.x < 4) L.seq[threadIdx.x] = 0u;
     __syncthreads();
     SM2_T(0);
-    const uint8_t* sp = nullptr;
-    const bool len_ok = active && io.sig_span(i, sp) == 128u;
     fe r, s, px, py;
     uint32_t X[8], Y[8];
-    if (len_ok) {
-        ByteReader rd(sp, 128);
-        uint32_t w[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w[k] = rd.word(k);
-        fe_from_be_words(r, w);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w[k] = rd.word(8 + k);
-        fe_from_be_words(s, w);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            X[k] = bswap32(rd.word(16 + k));
-            Y[k] = bswap32(rd.word(24 + k));
-        }
-    } else {
-        fe_zero(r);
-        fe_zero(s);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) X[k] = Y[k] = 0u;
-    }
+    bool len_ok = false;  // the signature (and key) as the I/O policy gives them: r || s || pub, or KeyIO's key
+    if (active) len_ok = io.sm2_sig(i, r, s, X, Y);
+    else zero_sm2_sig(r, s, X, Y);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         px.v[k] = X[7 - k];
@@ -1281,5 +1243,6 @@ int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n,
 }
 template int launch_verify_small_sm2<TxIO>(const TxKernelPolicy&, const TxIO&, uint64_t, hipStream_t);
 template int launch_verify_small_sm2<SigIO>(const TxKernelPolicy&, const SigIO&, uint64_t, hipStream_t);
+template int launch_verify_small_sm2<KeyIO>(const TxKernelPolicy&, const KeyIO&, uint64_t, hipStream_t);
 
 }  // namespace bcosgpu

@@ -1,7 +1,7 @@
-// ecc_sig.hip -- one-lane signature kernels: known-key verify, the ecRecover precompile, and the
-// deterministic signing used to build synthetic batches; their launchers.  (Recover and SM2 verify with
-// the digest given run the tx-verify kernels over SigIO: ecc_txv.hip launch_secp256k1_recover /
-// launch_sm2_verify.)
+// ecc_sig.hip -- the one-lane known-key verify kernel and the deterministic signing used to build
+// synthetic batches; the known-key verify launcher.  (Recover, SM2 verify with the digest given and the
+// ecRecover precompile run the tx-verify kernels over SigIO / EcrecIO: ecc_txv.hip; the small-batch
+// known-key verify runs on lane trios: ecc_coop.hip sig_verify_trio26_kernel, ecc_pair.hip over KeyIO.)
 #include "ecc_device.h"
 
 namespace bcosgpu {
@@ -43,34 +43,6 @@ __global__ __launch_bounds__(256) void sig_verify_kernel(const uint8_t* __restri
         if constexpr (F26) ok = secp256k1_verify_lane26(h, sg, pub + 64 * i, CombTab{tab, tbits});
         else ok = secp256k1_verify_lane(h, sg, pub + 64 * i, CombTab{tab, tbits});
     }
-    okout[i] = ok ? 1 : 0;
-}
-
-// EVM ecRecover precompile (bcos-executor/src/vm/Precompiled.cpp:443-482) for a batch: input =
-// hash(32) || v(32) || r(32) || s(32); recid = (byte)(in[63] - 27) (the other 31 bytes of v are not
-// read); on success out = 12 zero bytes || right160(Keccak256(pub)), ok = 1; on failure the
-// precompile returns an empty output: out = zeros, ok = 0.
-template <bool F26>
-__global__ __launch_bounds__(256) void ecrecover_kernel(const uint8_t* __restrict__ in, uint64_t n,
-                                                        const uint32_t* __restrict__ tab, int tbits,
-                                                        uint8_t* __restrict__ out, uint8_t* __restrict__ okout) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint8_t* p = in + 128 * i;
-    fe h, r, s, x, y;
-    load_be256_aligned(h, p);
-    load_be256_aligned(r, p + 64);
-    load_be256_aligned(s, p + 96);
-    const uint32_t v = (reinterpret_cast<const uint32_t*>(p)[15] >> 24) - 27u;
-    const bool ok = F26 ? secp256k1_recover_rsv26(h, r, s, v & 0xffu, CombTab{tab, tbits}, x, y)
-                        : secp256k1_recover_rsv(h, r, s, v & 0xffu, CombTab{tab, tbits}, x, y);
-    uint32_t a[5] = {0, 0, 0, 0, 0};
-    if (ok) keccak_address(a, x, y);
-    uint32_t* o = reinterpret_cast<uint32_t*>(out + 32 * i);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) o[k] = 0u;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) o[3 + k] = a[k];
     okout[i] = ok ? 1 : 0;
 }
 
@@ -255,6 +227,12 @@ int launch_sm2_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
+// The known-key verify batch (bcosgpu_verify_batch*): SM2 runs the SM2 verification kernels over KeyIO
+// (the same rounds x latency choice as recover / tx verify, ecc_txv.hip launch_sm2_verify_key);
+// secp256k1 runs the lane-trio verify kernel for batches of up to two trio rounds (a block's sealer
+// signatures: the latency path) and the one-lane sig_verify_kernel beyond (the trio kernel's round is
+// ~3x shorter than the one-lane kernel's, which fits 6.4x more signatures per round: tools/small_sweep.py
+// verify, profiles/r04_verify_sweep.json).  Policy split 1 / 0 forces the trio / one-lane kernel.
 int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
                       uint64_t n, uint8_t* d_ok, hipStream_t st) {
     if (n == 0) return 0;
@@ -262,35 +240,21 @@ int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, co
     int bits;
     int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    if (suite == BCOSGPU_SUITE_SM2 && tx_policy().f26) {
-        const uint32_t* t26;
-        int b26;
-        rc = tables_sm2_26(&t26, &b26);
-        if (rc) return rc;
-        hipLaunchKernelGGL((sig_verify_kernel<BCOSGPU_SUITE_SM2, true>), dim3(grid_of(n)), dim3(256), 0, st, d_pub,
-                           d_hash, d_sig, stride, n, t26, b26, d_ok);
-    } else if (suite == BCOSGPU_SUITE_SM2)
+    const TxKernelPolicy pol = tx_policy();
+    if (suite == BCOSGPU_SUITE_SM2 && pol.f26) return launch_sm2_verify_key(d_pub, d_hash, d_sig, stride, n, d_ok, st);
+    if (suite == BCOSGPU_SUITE_SECP256K1 && pol.f26 && pol.coop == 2) {
+        const bool small = pol.split >= 0 ? pol.split == 1 : n <= 2ull * 40 * static_cast<uint64_t>(cu_count());
+        if (small) return launch_sig_verify_small_secp(KeyIO{d_pub, d_hash, d_sig, stride, d_ok}, n, st);
+    }
+    if (suite == BCOSGPU_SUITE_SM2)
         hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SM2>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash, d_sig,
                            stride, n, sm2, bits, d_ok);
-    else if (tx_policy().f26)
+    else if (pol.f26)
         hipLaunchKernelGGL((sig_verify_kernel<BCOSGPU_SUITE_SECP256K1, true>), dim3(grid_of(n)), dim3(256), 0, st, d_pub,
                            d_hash, d_sig, stride, n, k1, bits, d_ok);
     else
         hipLaunchKernelGGL(sig_verify_kernel<BCOSGPU_SUITE_SECP256K1>, dim3(grid_of(n)), dim3(256), 0, st, d_pub, d_hash,
                            d_sig, stride, n, k1, bits, d_ok);
-    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
-}
-
-int launch_ecrecover(const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint8_t* d_ok, hipStream_t st) {
-    if (n == 0) return 0;
-    const uint32_t *k1, *sm2;
-    int bits;
-    int rc = tables(&k1, &sm2, &bits);
-    if (rc) return rc;
-    if (tx_policy().f26)
-        hipLaunchKernelGGL(ecrecover_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, d_in, n, k1, bits, d_out, d_ok);
-    else
-        hipLaunchKernelGGL(ecrecover_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, d_in, n, k1, bits, d_out, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 

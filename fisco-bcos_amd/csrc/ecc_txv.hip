@@ -17,9 +17,7 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
     if (i >= n) return;
     fe h;
     io.template digest<SUITE == BCOSGPU_SUITE_SM2 ? SM3 : KECCAK256>(i, h);
-    const uint8_t* sp;
-    const uint32_t slen = io.sig_span(i, sp);
-    fe x, y;
+    fe x, y, r, s;
     uint32_t ad[5] = {0, 0, 0, 0, 0};
     bool ok;
     // OCC 2: the variable-base table's x-coordinates live in LDS (16 KiB per wave, 128 KiB per CU
@@ -27,14 +25,18 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
     constexpr bool kLds = OCC == 2;
     __shared__ uint32_t ldsx_all[kLds ? 4 * 4096 : 1];
     uint32_t* ldsx = kLds ? ldsx_all + (threadIdx.x >> 6) * 4096 + (threadIdx.x & 63) : nullptr;
-    if (SUITE == BCOSGPU_SUITE_SM2) {
-        if constexpr (F26) ok = sm2_verify_lane26<kLds>(h, sp, slen, CombTab{tab, tbits}, x, y, ldsx);
-        else ok = sm2_verify_lane<kLds>(h, sp, slen, CombTab{tab, tbits}, x, y, ldsx);
+    if constexpr (SUITE == BCOSGPU_SUITE_SM2) {
+        uint32_t X[8], Y[8];
+        const bool wf = io.sm2_sig(i, r, s, X, Y);  // a malformed signature fails before any curve work
+        if constexpr (F26) ok = wf && sm2_verify_rs26<kLds>(h, r, s, X, Y, CombTab{tab, tbits}, x, y, ldsx);
+        else ok = wf && sm2_verify_rs<kLds>(h, r, s, X, Y, CombTab{tab, tbits}, x, y, ldsx);
         if (ok && io.want_addr()) sm3_address(ad, x, y);
         io.finish(i, ok, ad, nullptr, nullptr);
     } else {
-        if constexpr (F26) ok = secp256k1_recover_lane26<kLds>(h, sp, slen, CombTab{tab, tbits}, x, y, ldsx);
-        else ok = secp256k1_recover_lane<kLds>(h, sp, slen, CombTab{tab, tbits}, x, y, ldsx);
+        uint32_t v;
+        io.rsv(i, r, s, v);  // r = s = 0 for a malformed signature: the recovery rejects it
+        if constexpr (F26) ok = secp256k1_recover_rsv26<kLds>(h, r, s, v, CombTab{tab, tbits}, x, y, ldsx);
+        else ok = secp256k1_recover_rsv<kLds>(h, r, s, v, CombTab{tab, tbits}, x, y, ldsx);
         if (ok && io.want_addr()) keccak_address(ad, x, y);
         io.finish(i, ok, ad, &x, &y);
     }
@@ -50,7 +52,7 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
 // The trio and pair kernels are candidates up to 2^16 txs (beyond that the one-lane kernel's
 // throughput wins at any rounding).  Returns 2 (trio), 1 (pair), 0 (one-lane, occupancy 1) or -2
 // (one-lane, occupancy 2).
-static int cu_count() {
+int cu_count() {
     static int cus[64] = {0};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
@@ -105,21 +107,35 @@ int launch_verify(int suite, const IO& io, uint64_t n, hipStream_t st) {
     if (!occ) occ = n >= (1ull << 17) ? 2 : 1;  // forced non-automatic policies: >= 2 waves per SIMD of work
     // SigIO has the fe26 / fp26 cooperative kernels only; other policies take the one-lane kernel
     if (small && !kTx && !(pol.f26 && pol.coop)) small = false;
-    if (suite == BCOSGPU_SUITE_SECP256K1 && small) return launch_verify_small_secp(pol, io, n, st);
-    if (suite == BCOSGPU_SUITE_SM2 && small && pol.coop) return launch_verify_small_sm2(pol, io, n, st);
+    // EcrecIO is a secp256k1 recovery only, KeyIO (here) an SM2 verification only
+    constexpr bool kK1 = !std::is_same_v<IO, KeyIO>, kSM2 = !std::is_same_v<IO, EcrecIO>;
+    if constexpr (kK1)
+        if (suite == BCOSGPU_SUITE_SECP256K1 && small) return launch_verify_small_secp(pol, io, n, st);
+    if constexpr (kSM2)
+        if (suite == BCOSGPU_SUITE_SM2 && small && pol.coop) return launch_verify_small_sm2(pol, io, n, st);
 #define TXV(S, O, F, T) \
     hipLaunchKernelGGL((tx_verify_kernel<S, O, F, IO>), dim3(grid_of(n)), dim3(256), 0, st, io, n, T, bits)
-    if (suite == BCOSGPU_SUITE_SM2 && pol.f26) {
-        const uint32_t* t26;
-        rc = tables_sm2_26(&t26, &bits);
-        if (rc) return rc;
-        if (occ == 2) TXV(BCOSGPU_SUITE_SM2, 2, true, t26); else TXV(BCOSGPU_SUITE_SM2, 1, true, t26);
-    } else if (suite == BCOSGPU_SUITE_SM2) {
-        if (occ == 2 && kTx) TXV(BCOSGPU_SUITE_SM2, 2, false, sm2); else TXV(BCOSGPU_SUITE_SM2, 1, false, sm2);
-    } else if (pol.f26) {
-        if (occ == 2) TXV(BCOSGPU_SUITE_SECP256K1, 2, true, k1); else TXV(BCOSGPU_SUITE_SECP256K1, 1, true, k1);
+    if (suite == BCOSGPU_SUITE_SM2) {
+        if constexpr (kSM2) {
+            if (pol.f26) {
+                const uint32_t* t26;
+                rc = tables_sm2_26(&t26, &bits);
+                if (rc) return rc;
+                if (occ == 2) TXV(BCOSGPU_SUITE_SM2, 2, true, t26); else TXV(BCOSGPU_SUITE_SM2, 1, true, t26);
+            } else {
+                if (occ == 2 && kTx) TXV(BCOSGPU_SUITE_SM2, 2, false, sm2); else TXV(BCOSGPU_SUITE_SM2, 1, false, sm2);
+            }
+        } else {
+            return BCOSGPU_E_ARG;
+        }
+    } else if constexpr (kK1) {
+        if (pol.f26) {
+            if (occ == 2) TXV(BCOSGPU_SUITE_SECP256K1, 2, true, k1); else TXV(BCOSGPU_SUITE_SECP256K1, 1, true, k1);
+        } else {
+            if (occ == 2 && kTx) TXV(BCOSGPU_SUITE_SECP256K1, 2, false, k1); else TXV(BCOSGPU_SUITE_SECP256K1, 1, false, k1);
+        }
     } else {
-        if (occ == 2 && kTx) TXV(BCOSGPU_SUITE_SECP256K1, 2, false, k1); else TXV(BCOSGPU_SUITE_SECP256K1, 1, false, k1);
+        return BCOSGPU_E_ARG;
     }
 #undef TXV
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
@@ -145,6 +161,21 @@ int launch_secp256k1_recover(const uint8_t* d_hash, const uint8_t* d_sig, uint32
 int launch_sm2_verify(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride, uint64_t n, uint8_t* d_addr,
                       uint8_t* d_ok, hipStream_t st) {
     const SigIO io{d_hash, d_sig, stride, 128u, nullptr, d_addr, d_ok};
+    return launch_verify(BCOSGPU_SUITE_SM2, io, n, st);
+}
+
+// The EVM ecRecover precompile (Precompiled.cpp:443-482) for a batch: the recovery kernels over EcrecIO,
+// with the same rounds x latency choice (the lane-trio kernel for a block's few calls).
+int launch_ecrecover(const uint8_t* d_in, uint64_t n, uint8_t* d_out, uint8_t* d_ok, hipStream_t st) {
+    const EcrecIO io{d_in, d_out, d_ok};
+    return launch_verify(BCOSGPU_SUITE_SECP256K1, io, n, st);
+}
+
+// SignatureCrypto::verify with a known key, SM2 (SM2Crypto.cpp:66-79): the SM2 verification kernels over
+// KeyIO, the key from pub64 instead of the signature's tail (ecc_sig.hip launch_sig_verify).
+int launch_sm2_verify_key(const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
+                          uint64_t n, uint8_t* d_ok, hipStream_t st) {
+    const KeyIO io{d_pub, d_hash, d_sig, stride, d_ok};
     return launch_verify(BCOSGPU_SUITE_SM2, io, n, st);
 }
 }  // namespace bcosgpu

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <condition_variable>
 #include <string>
 #include "../../include/bcos_gpu.h"
 
@@ -64,7 +65,9 @@ struct SigJob {
     uint8_t* out_ok = nullptr;        // n bytes: 1 valid, 0 invalid
     int rc = 0;                       // filled in by the engine: 0 or BCOSGPU_E_*, with err
     std::string err;
-    bool queued = false, done = false;
+    bool queued = false, done = false, woken = false;
+    uint64_t seq = 0;                 // arrival order in its device queue
+    std::condition_variable cv;       // its owner sleeps on it (under the device queue's mutex)
 };
 int coalesced_run(int device, SigJob& job);
 

@@ -302,6 +302,8 @@ def standin():
         L.standin_hash.argtypes = [I, P, S, P]
         L.standin_merkle_root.restype = I
         L.standin_merkle_root.argtypes = [I, I, P, S, P, I]
+        L.standin_verify_batch.restype = None
+        L.standin_verify_batch.argtypes = [I, P, P, P, S, S, P, I]
         _standin = L
     return _standin
 
@@ -319,6 +321,18 @@ def standin_tx_verify_packed(suite, pre, pre_off, sig, sig_off, nthreads=1):
     standin().standin_tx_verify_batch(suite, _p(pre), _p(pre_off), _p(sig), _p(sig_off), n, _p(txhash),
                                       _p(sender), _p(status), nthreads)
     return txhash, sender, status
+
+
+def standin_verify_batch(suite, pubs, hashes, sigs, nthreads=1):
+    """SignatureCrypto::verify with known keys over OpenSSL (secp256k1: libsecp256k1 verify semantics,
+    low-S; SM2: EVP with the default ID).  pubs [n,64], hashes [n,32], sigs [n, stride >= 64]."""
+    pubs = np.ascontiguousarray(pubs, dtype=np.uint8).reshape(-1, 64)
+    n = pubs.shape[0]
+    hashes = np.ascontiguousarray(hashes, dtype=np.uint8).reshape(n, 32)
+    sigs = np.ascontiguousarray(sigs, dtype=np.uint8).reshape(n, -1)
+    ok = np.zeros(n, dtype=np.uint8)
+    standin().standin_verify_batch(suite, _p(pubs), _p(hashes), _p(sigs), sigs.shape[1], n, _p(ok), nthreads)
+    return ok.astype(bool)
 
 
 def standin_hash(hasher, data):

@@ -186,6 +186,71 @@ void standin_tx_verify_batch(int suite, const uint8_t* pre, const uint64_t* pre_
     oracle_parallel_for(n, nthreads, tx_range, &j);
 }
 
+/* ------------------------------------------------------------------ verify with a known key */
+/* secp256k1Verify -> wedpr_secp256k1_verify (Secp256k1Crypto.cpp:51-63), libsecp256k1 ecdsa_verify
+ * semantics over OpenSSL: key on the curve, r, s in [1, n-1], low-S (s <= n/2), ECDSA_do_verify */
+static int k1_verify(k1_ctx* c, const uint8_t pub[64], const uint8_t h[32], const uint8_t sig[64])
+{
+    int ok = 0;
+    EC_KEY* k = EC_KEY_new();
+    BIGNUM *x = BN_bin2bn(pub, 32, NULL), *y = BN_bin2bn(pub + 32, 32, NULL);
+    BIGNUM *r = BN_bin2bn(sig, 32, NULL), *s = BN_bin2bn(sig + 32, 32, NULL), *half = BN_new();
+    ECDSA_SIG* sg = NULL;
+    BN_rshift1(half, c->n);
+    if (BN_is_zero(r) || BN_is_zero(s) || BN_cmp(r, c->n) >= 0 || BN_cmp(s, half) > 0) goto done;
+    EC_KEY_set_group(k, c->g);
+    if (EC_KEY_set_public_key_affine_coordinates(k, x, y) != 1) goto done;
+    sg = ECDSA_SIG_new();
+    ECDSA_SIG_set0(sg, r, s);
+    r = s = NULL;
+    ok = ECDSA_do_verify(h, 32, sg, k) == 1;
+done:
+    ERR_clear_error();
+    ECDSA_SIG_free(sg);
+    BN_free(r);
+    BN_free(s);
+    BN_free(half);
+    BN_free(x);
+    BN_free(y);
+    EC_KEY_free(k);
+    return ok;
+}
+
+typedef struct {
+    int suite;
+    const uint8_t *pub, *hash, *sig;
+    size_t stride;
+    uint8_t* ok;
+} verify_job;
+
+static void verify_range(void* p, size_t lo, size_t hi)
+{
+    verify_job* j = (verify_job*)p;
+    k1_ctx c = {0};
+    if (j->suite == ORACLE_SUITE_SECP256K1) k1_open(&c);
+    for (size_t i = lo; i < hi; ++i) {
+        const uint8_t* s = j->sig + j->stride * i;
+        if (j->suite == ORACLE_SUITE_SECP256K1) {
+            j->ok[i] = (uint8_t)k1_verify(&c, j->pub + 64 * i, j->hash + 32 * i, s);
+        } else { /* SM2Crypto::verify (SM2Crypto.cpp:66-79): r || s = sig[0..64), the given key */
+            uint8_t rsp[128], out[64];
+            memcpy(rsp, s, 64);
+            memcpy(rsp + 64, j->pub + 64 * i, 64);
+            j->ok[i] = sm2_recover(j->hash + 32 * i, rsp, 128, out) == 0;
+        }
+    }
+    if (j->suite == ORACLE_SUITE_SECP256K1) k1_close(&c);
+}
+
+/* SignatureCrypto::verify(pub, hash, sig) over a batch on nthreads threads (the sealer-signature checks,
+ * BlockValidator.cpp:141-182) */
+void standin_verify_batch(int suite, const uint8_t* pub64, const uint8_t* hash32, const uint8_t* sig, size_t stride,
+                          size_t n, uint8_t* ok, int nthreads)
+{
+    verify_job j = {suite, pub64, hash32, sig, stride, ok};
+    oracle_parallel_for(n, nthreads, verify_range, &j);
+}
+
 /* ------------------------------------------------------------------ the reference's Merkle CPU path */
 /* OpenSSL 1.1.1's KECCAK1600_CTX and EVP_MD_CTX head (the layout OpenSSLHasher.h:51-75 relies on) */
 typedef struct {

@@ -15,6 +15,21 @@ pytestmark = pytest.mark.gpu
 P_SECP = 2**256 - 2**32 - 977
 
 
+# Every kernel a verify / ecRecover batch can take (bcosgpu_set_tx_kernel_policy(split, occupancy, coop,
+# field)): the automatic choice, the lane-trio kernels (sig_verify_trio26_kernel, the SM2 trio kernel over
+# KeyIO, the recovery trio kernel over EcrecIO), the pair kernels, the one-lane kernels at occupancy 1
+# and 2, and the 8 x 32-bit field variants.
+SIG_VARIANTS = {"auto": (-1, 0, 2, 1), "trio": (1, 0, 2, 1), "pair": (1, 0, 1, 1), "onelane_occ1": (0, 1, 2, 1),
+                "onelane_occ2": (0, 2, 2, 1), "fe32": (-1, 0, 2, 0)}
+
+
+@pytest.fixture(params=sorted(SIG_VARIANTS))
+def sig_variant(request, gpu):
+    gpu.set_tx_kernel_policy(*SIG_VARIANTS[request.param])
+    yield request.param
+    gpu.set_tx_kernel_policy()
+
+
 def _keys(rng, n):
     sk = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
     sk[:, 0] &= 0x7F
@@ -48,7 +63,7 @@ def _edit(rng, pub, h, sig, i, kind, order, other_pub):
 
 
 @pytest.mark.parametrize("suite", [0, 1])
-def test_verify_known_key_vs_oracle(gpu, oracle, suite, k1_field):
+def test_verify_known_key_vs_oracle(gpu, oracle, suite, sig_variant):
     rng = np.random.default_rng(31 + suite)
     n = 2000
     sk = _keys(rng, n)
@@ -78,7 +93,7 @@ def test_verify_known_key_vs_oracle(gpu, oracle, suite, k1_field):
     assert not crypto.verify(pub[2].tobytes(), h[2].tobytes(), sig[2].tobytes())
 
 
-def test_ecrecover_precompile_vs_oracle(gpu, oracle, k1_field):
+def test_ecrecover_precompile_vs_oracle(gpu, oracle, sig_variant):
     from bcos_gpu.precompiled import ec_recover, ec_recover_batch
     rng = np.random.default_rng(41)
     n = 1500

@@ -42,3 +42,49 @@ def test_standin_matches_oracle(oracle, suite):
     for w, g in zip(want, got):
         assert np.array_equal(w, g)
     assert 0 < int((want[2] == 0).sum()) < 300
+
+
+@pytest.mark.parametrize("suite", [0, 1])
+def test_standin_known_key_verify_matches_oracle(oracle, suite):
+    """standin_verify_batch (the sealer-verify CPU baseline) gives the oracle's verdicts: valid, high-S
+    (secp256k1 rejects), flipped bits, another key, r = 0."""
+    if oracle.standin() is None:
+        pytest.skip("OpenSSL stand-in not built (no /opt/conda OpenSSL)")
+    rng = np.random.default_rng(21 + suite)
+    n = 200
+    N = (0xFFFFFFFEFFFFFFFFFFFFFFFFFFFFFFFF7203DF6B21C6052B53BBF40939D54123 if suite
+         else 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141)
+    pubs, hs, sigs = [], [], []
+    for i in range(n):
+        h = rng.bytes(32)
+        sk = bytes([rng.integers(1, 0x7F)]) + rng.bytes(31)
+        k = bytes([rng.integers(1, 0x7F)]) + rng.bytes(31)
+        if suite:
+            full = oracle.sm2_sign(sk, h, k)
+            sig, pub = bytearray(full[:64]), full[64:]
+        else:
+            s65 = oracle.secp256k1_sign(sk, h, k)
+            sig, pub = bytearray(s65[:64]), oracle.secp256k1_recover(h, s65)
+        kind = i % 5
+        if kind == 1:
+            s = int.from_bytes(sig[32:], "big")
+            sig[32:] = (N - s).to_bytes(32, "big")
+        elif kind == 2:
+            sig[int(rng.integers(0, 64))] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 3 and pubs:
+            pub = pubs[-1]
+        elif kind == 4:
+            sig[:32] = bytes(32)
+        pubs.append(pub)
+        hs.append(h)
+        sigs.append(bytes(sig))
+    P = np.frombuffer(b"".join(pubs), dtype=np.uint8).reshape(n, 64)
+    H = np.frombuffer(b"".join(hs), dtype=np.uint8).reshape(n, 32)
+    S = np.frombuffer(b"".join(sigs), dtype=np.uint8).reshape(n, 64)
+    got = oracle.standin_verify_batch(suite, P, H, S, nthreads=4)
+    if suite:
+        want = [oracle.sm2_recover(hs[i], sigs[i] + pubs[i]) is not None for i in range(n)]
+    else:
+        want = [oracle.secp256k1_verify(pubs[i], hs[i], sigs[i]) for i in range(n)]
+    assert list(got) == want
+    assert all(want[0::5]) and not any(want[4::5])
