@@ -689,8 +689,15 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(IO io, uin
     fe r, s, px, py;
     uint32_t X[8], Y[8];
     bool len_ok = false;  // the signature (and key) as the I/O policy gives them: r || s || pub, or KeyIO's key
-    if (active) len_ok = io.sm2_sig(i, r, s, X, Y);
-    else zero_sm2_sig(r, s, X, Y);
+    if constexpr (std::is_same_v<IO, KeyIO>) {
+        if (active) len_ok = io.sm2_sig(i, r, s, X, Y);
+        else zero_sm2_sig(r, s, X, Y);
+    } else {  // (kept in this form: the TxIO / SigIO kernels' register allocation depends on it)
+        const uint8_t* sp = nullptr;
+        len_ok = active && io.sig_span(i, sp) == 128u;
+        if (len_ok) parse_sm2_128(sp, r, s, X, Y);
+        else zero_sm2_sig(r, s, X, Y);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         px.v[k] = X[7 - k];
@@ -945,8 +952,15 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
     fe r, s, px, py;
     uint32_t X[8], Y[8];
     bool len_ok = false;  // the signature (and key) as the I/O policy gives them: r || s || pub, or KeyIO's key
-    if (active) len_ok = io.sm2_sig(i, r, s, X, Y);
-    else zero_sm2_sig(r, s, X, Y);
+    if constexpr (std::is_same_v<IO, KeyIO>) {
+        if (active) len_ok = io.sm2_sig(i, r, s, X, Y);
+        else zero_sm2_sig(r, s, X, Y);
+    } else {  // (kept in this form: the TxIO / SigIO kernels' register allocation depends on it)
+        const uint8_t* sp = nullptr;
+        len_ok = active && io.sig_span(i, sp) == 128u;
+        if (len_ok) parse_sm2_128(sp, r, s, X, Y);
+        else zero_sm2_sig(r, s, X, Y);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         px.v[k] = X[7 - k];

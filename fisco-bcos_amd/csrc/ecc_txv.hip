@@ -25,11 +25,19 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
     constexpr bool kLds = OCC == 2;
     __shared__ uint32_t ldsx_all[kLds ? 4 * 4096 : 1];
     uint32_t* ldsx = kLds ? ldsx_all + (threadIdx.x >> 6) * 4096 + (threadIdx.x & 63) : nullptr;
-    if constexpr (SUITE == BCOSGPU_SUITE_SM2) {
+    if constexpr (SUITE == BCOSGPU_SUITE_SM2 && std::is_same_v<IO, KeyIO>) {
         uint32_t X[8], Y[8];
-        const bool wf = io.sm2_sig(i, r, s, X, Y);  // a malformed signature fails before any curve work
-        if constexpr (F26) ok = wf && sm2_verify_rs26<kLds>(h, r, s, X, Y, CombTab{tab, tbits}, x, y, ldsx);
-        else ok = wf && sm2_verify_rs<kLds>(h, r, s, X, Y, CombTab{tab, tbits}, x, y, ldsx);
+        io.sm2_sig(i, r, s, X, Y);  // r || s from the signature, the key from pub64
+        if constexpr (F26) ok = sm2_verify_rs26<kLds>(h, r, s, X, Y, CombTab{tab, tbits}, x, y, ldsx);
+        else ok = sm2_verify_rs<kLds>(h, r, s, X, Y, CombTab{tab, tbits}, x, y, ldsx);
+        io.finish(i, ok, ad, nullptr, nullptr);
+    } else if constexpr (SUITE == BCOSGPU_SUITE_SM2) {
+        // (the r || s || pub parse inside the lane functions: the throughput kernels' register
+        // allocation -- C3's spills -- depends on this form)
+        const uint8_t* sp;
+        const uint32_t slen = io.sig_span(i, sp);
+        if constexpr (F26) ok = sm2_verify_lane26<kLds>(h, sp, slen, CombTab{tab, tbits}, x, y, ldsx);
+        else ok = sm2_verify_lane<kLds>(h, sp, slen, CombTab{tab, tbits}, x, y, ldsx);
         if (ok && io.want_addr()) sm3_address(ad, x, y);
         io.finish(i, ok, ad, nullptr, nullptr);
     } else {

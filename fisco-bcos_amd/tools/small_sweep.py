@@ -22,7 +22,8 @@ VARIANTS = {"trio": (1, 0, 2, 1), "pair": (1, 0, 1, 1), "occ1": (0, 1, 0, 1), "o
             "auto": (-1, 0, 2, 1)}
 args = sys.argv[1:]
 mode = args.pop(0) if args and args[0] == "verify" else "tx"
-sizes = [int(x) for x in (args[0] if args else "10240,12800,16384,20480,24576,32768").split(",")]
+# sizes: one comma-separated argument or several arguments (tools/gpu_run.sh turns commas into spaces)
+sizes = [int(x) for x in (",".join(args) if args else "10240,12800,16384,20480,24576,32768").split(",") if x]
 out = {}
 
 
