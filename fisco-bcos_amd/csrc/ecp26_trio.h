@@ -123,7 +123,9 @@ F26_HD void trio_dbl_sm2(TrioPtP& P, const TrioLane& T) {
 //   L1  alpha / 3 = (X - D)(X + D) | gamma = Y^2     | Y Z
 //   L2  alpha^2                    | beta = X gamma  | D' = (2 Y Z)^2  (the next delta = Z3^2)
 //   L3  alpha (4 beta - X3)        | gamma^2         | --              (X3 = alpha^2 - 8 beta on lane 0)
-// (CurveSM2x::dbl's products and magnitudes: X <= 5, Y, Z <= 8, D <= 1 -> (2, 2, 2), D' m 1)
+// CurveSM2x::dbl's products, with no weak normalisation: fp26_mul takes magnitudes up to 15, so X3 and Y3
+// go on unnormalised (each normalisation was a serial nine-limb carry chain on the critical path) and
+// 4 beta - X3 is formed as 12 beta - alpha^2.  Magnitudes: X <= 12, Y, Z <= 15, D m 1 -> (11, 11, 2), D' m 1.
 F26_HD void trio_dbl_sm2_d(TrioPtP& P, fp26& D, const TrioLane& T) {
     using namespace trio;
     fp26 t, u, A1, B1, o1, al, Z3, A2, B2, o2, be, b8, X3, t4, A3, B3, o3, g2, Y3, Dn;
@@ -141,17 +143,15 @@ F26_HD void trio_dbl_sm2_d(TrioPtP& P, fp26& D, const TrioLane& T) {
     mul(o2, A2, B2);                     // (alpha^2 | beta | Z3^2)
     fdpp<kR1>(be, o2);                   // lane 0: beta
     fp26_mul_int<8>(b8, be);             //                            m 8
-    fp26_sub<9>(X3, o2, b8);             //                            m 11
-    fp26_normalize_weak(X3);             // X3 = alpha^2 - 8 beta      m 2
-    fp26_mul_int<4>(t4, be);             //                            m 4
-    fp26_sub<3>(t4, t4, X3);             // 4 beta - X3                m 8
+    fp26_sub<9>(X3, o2, b8);             // X3 = alpha^2 - 8 beta      m 11
+    fp26_mul_int<12>(t4, be);            //                            m 12
+    fp26_sub<2>(t4, t4, o2);             // 4 beta - X3 = 12 beta - alpha^2   m 15
     sel(A3, T.r0, al, o1);               // (alpha | gamma | -)
     sel(B3, T.r0, t4, o1);               // (4 beta - X3 | gamma | -)
     mul(o3, A3, B3);                     // (alpha (4 beta - X3) | gamma^2 | -)
     fdpp<kR1>(g2, o3);                   // lane 0: gamma^2
     fp26_mul_int<8>(g2, g2);             //                            m 8
-    fp26_sub<9>(Y3, o3, g2);             //                            m 11
-    fp26_normalize_weak(Y3);             // Y3                         m 2
+    fp26_sub<9>(Y3, o3, g2);             // Y3                         m 11
     fdpp<kR2>(Dn, o2);                   // lane 0: Z3^2 of lane 2
     trio_state_sm2(P, X3, Y3, Z3, T);
     fp26_copy(D, Dn);
@@ -159,8 +159,8 @@ F26_HD void trio_dbl_sm2_d(TrioPtP& P, fp26& D, const TrioLane& T) {
 
 // R <- P + Q, Q affine, given D = Z1^2 on lane 0 (trio_dbl_sm2_d): CurveSM2x::madd in 4 product levels,
 // without the P = +-Q tests (the t P chain's additions), returning the sum's D = Z3^2 on lane 0 from
-// the last level's idle lane 2; P = infinity gives Q (D = 1).  X, Y <= 2, Z <= 8, D <= 1, Q <= 2 ->
-// (2, 2, 2), D m 1.
+// the last level's idle lane 2; P = infinity gives Q (D = 1).  No weak normalisations (fp26_mul takes
+// m <= 15): X, Y <= 11, Z <= 15, D m 1, Q <= 2 -> (11, 8, 2), D m 1.
 //   L1  U2 = x2 D        | T = y2 Z        | --
 //   L2  HH = H^2         | S2 = T D        | Z H          (H = U2 - X on lane 0)
 //   L3  J = H I          | rr^2            | V = X I      (I = 4 HH, rr = S2 - Y on lane 1)
@@ -173,7 +173,7 @@ F26_HD void trio_madd_sm2_d(TrioPtP& R, fp26& Dout, const TrioPtP& P, const fp26
     sel(A1, T.r1, Q.y, Q.x);             // (x2 | y2 | x2)
     sel(B1, T.r0, D, b);                 // (D | Z | -)
     mul(o1, A1, B1);                     // (U2 | T | -)
-    fp26_sub<3>(h, o1, P.Xr);            // lane 0: H = U2 - X         m 5
+    fp26_sub<12>(h, o1, P.Xr);           // lane 0: H = U2 - X         m 14
     sel(A2, T.r1, o1, P.Q1);
     sel(A2, T.r0, h, A2);                // (H | T | Z)
     fdpp<kL1>(a, D);                     // lane 1: D of lane 0
@@ -182,7 +182,7 @@ F26_HD void trio_madd_sm2_d(TrioPtP& R, fp26& Dout, const TrioPtP& P, const fp26
     sel(B2, T.r0, h, B2);                // (H | D | H)
     mul(o2, A2, B2);                     // (HH | S2 | Z H)
     fp26_mul_int<4>(I, o2);              // lane 0: I = 4 HH           m 4
-    fp26_sub<3>(rr, o2, P.P1);           // lane 1: rr = S2 - Y        m 5
+    fp26_sub<12>(rr, o2, P.P1);          // lane 1: rr = S2 - Y        m 14
     fp26_mul_int<2>(Z3, o2);             // lane 2: Z3 = 2 Z H         m 2
     fdpp<kL1>(a, P.Xr);                  // lane 2: X of lane 1
     sel(A3, T.r1, rr, a);
@@ -196,10 +196,9 @@ F26_HD void trio_madd_sm2_d(TrioPtP& R, fp26& Dout, const TrioPtP& P, const fp26
     fdpp<kR2>(V, o3);                    // lane 0: V
     fp26_sub<2>(X3, R2, o3);             //                            m 7
     fp26_mul_int<2>(t, V);               //                            m 2
-    fp26_sub<3>(X3, X3, t);              //                            m 11
-    fp26_normalize_weak(X3);             // X3 = r^2 - J - 2V          m 2
-    fp26_sub<3>(W, V, X3);               // V - X3                     m 5
-    fdpp<kR1>(a, rr);                    // lane 0: rr of lane 1       m 5
+    fp26_sub<3>(X3, X3, t);              // X3 = r^2 - J - 2V          m 11
+    fp26_sub<12>(W, V, X3);              // V - X3                     m 14
+    fdpp<kR1>(a, rr);                    // lane 0: rr of lane 1       m 14
     sel(A4, T.r1, P.P1, Z3);
     sel(A4, T.r0, a, A4);                // (rr | Y | Z3)
     fdpp<kL1>(b, o3);                    // lane 1: J of lane 0
@@ -208,8 +207,7 @@ F26_HD void trio_madd_sm2_d(TrioPtP& R, fp26& Dout, const TrioPtP& P, const fp26
     mul(o4, A4, B4);                     // (rr (V - X3) | Y J | Z3^2)
     fdpp<kR1>(t, o4);
     fp26_sub<2>(Y3, o4, t);              //                            m 4
-    fp26_mul_int<2>(Y3, Y3);             //                            m 8
-    fp26_normalize_weak(Y3);             // Y3 = r (V - X3) - 2 Y J    m 2
+    fp26_mul_int<2>(Y3, Y3);             // Y3 = r (V - X3) - 2 Y J    m 8
     fdpp<kR2>(Dn, o4);                   // lane 0: Z3^2 of lane 2
     TrioPtP O;
     trio_state_sm2(O, X3, Y3, Z3, T);
@@ -230,7 +228,8 @@ struct JacEntP26 {
 
 // R <- P + Q, Q a Jacobian table entry (never infinity), given D = Z1^2 on lane 0: CurveSM2x::add's
 // point in 5 product levels, without the P = +-Q tests (as trio_madd_sm2_d), returning the sum's
-// D = Z3^2 on lane 0; P = infinity gives Q (D = ZZ2).  X, Y <= 2, Z <= 8, D <= 1 -> (2, 2, 2), D m 1.
+// D = Z3^2 on lane 0; P = infinity gives Q (D = ZZ2).  No weak normalisations (fp26_mul takes m <= 15):
+// X, Y, Z <= 15, D m 1 -> (11, 8, 2), D m 1.
 //   L1  U2 = X2 D        | T = Y2 Z1       | U1 = X1 ZZ2
 //   L2  Z1 Z2            | S2 = T D        | S1 = Y1 ZZZ2   (H = U2 - U1 on lane 0)
 //   L3  HH = H^2         | rr^2            | Z1 Z2 H        (rr = S2 - S1 on lane 1)
@@ -277,9 +276,8 @@ F26_HD void trio_add_sm2_jd(TrioPtP& R, fp26& Dout, const TrioPtP& P, const fp26
     fdpp<kR2>(V, o4);                    // lane 0: V
     fp26_sub<2>(X3, R2, o4);             //                            m 7
     fp26_mul_int<2>(t, V);               //                            m 2
-    fp26_sub<3>(X3, X3, t);              //                            m 11
-    fp26_normalize_weak(X3);             // X3 = r^2 - J - 2V          m 2
-    fp26_sub<3>(W, V, X3);               // V - X3                     m 5
+    fp26_sub<3>(X3, X3, t);              // X3 = r^2 - J - 2V          m 11
+    fp26_sub<12>(W, V, X3);              // V - X3                     m 14
     fdpp<kR1>(a, rr);                    // lane 0: rr of lane 1       m 4
     fdpp<kR1>(b, o2);                    // lane 1: S1 of lane 2
     sel(A5, T.r0, a, b);                 // (rr | S1 | -)
@@ -288,8 +286,7 @@ F26_HD void trio_add_sm2_jd(TrioPtP& R, fp26& Dout, const TrioPtP& P, const fp26
     mul(o5, A5, B5);                     // (rr (V - X3) | S1 J | -)
     fdpp<kR1>(t, o5);
     fp26_sub<2>(Y3, o5, t);              //                            m 4
-    fp26_mul_int<2>(Y3, Y3);             //                            m 8
-    fp26_normalize_weak(Y3);             // Y3 = r (V - X3) - 2 S1 J   m 2
+    fp26_mul_int<2>(Y3, Y3);             // Y3 = r (V - X3) - 2 S1 J   m 8
     fdpp<kR1>(Dn, o4);                   // lane 0: Z3^2 of lane 1
     TrioPtP O;
     trio_state_sm2(O, X3, Y3, Z3, T);

@@ -9,10 +9,14 @@
 //   -m 2^16 to column i+8 (2^224),                 +m 2^22 to column i+9 (2^256):
 // four multiply-adds by constants per digit, no multiply by p's limbs.  Columns are signed 64-bit
 // accumulators.  Eleven digits (R = 2^286 rather than 2^260) make the output (T + M p) / R < T / R + p
-// < p + 2^232 for inputs of magnitude <= 8, i.e. magnitude 1 whatever the inputs.
+// < p + 2^234 for inputs of magnitude <= 15, i.e. magnitude 1 whatever the inputs (limb 9 <= 2^22).
+// Why 15: the largest column is column 8, nine products of limbs <= m 2^26 (limb 9, <= m 2^22, is not in
+// it; column 9's two limb-9 products are 2^4 smaller): 9 m^2 2^52 = 2025 * 2^52 < 2^63 - 2^56.5 at
+// m = 15, and the redc terms (carry < 2^37, digit terms < 2^49) stay inside that headroom; at m = 16 the
+// column could reach 2^63.2 and wrap.
 //
 // Magnitude (as fe26.h: limbs 0..8 <= m 2^26, limb 9 <= m 2^22):
-//   mul, sqr       : inputs m <= 8 (a column of ten products stays < 2^62 signed) -> m = 1
+//   mul, sqr       : inputs m <= 15 (every column stays < 2^63 signed, see above) -> m = 1
 //   add            : m_a + m_b                 (<= 63)
 //   sub<K>         : m_b <= K - 1              -> m_a + K + 1  (K p in limbs each >= (K-1) 2^26)
 //   neg<K>         : m <= K - 1                -> K + 1
@@ -127,7 +131,7 @@ F26_HD void fp26_redc(fp26& r, int64_t c[21]) {
 }
 
 F26_HD void fp26_mul(fp26& r, const fp26& a, const fp26& b) {
-    F26_REQ(a.m <= 8 && b.m <= 8);
+    F26_REQ(a.m <= 15 && b.m <= 15);
     P26_CHK(a);
     P26_CHK(b);
 #if F26_ASM
@@ -148,7 +152,7 @@ F26_HD void fp26_mul(fp26& r, const fp26& a, const fp26& b) {
 }
 
 F26_HD void fp26_sqr(fp26& r, const fp26& a) {
-    F26_REQ(a.m <= 8);
+    F26_REQ(a.m <= 15);
     P26_CHK(a);
 #if F26_ASM
     fp26_sqr_asm(r.v, a.v);

@@ -373,9 +373,9 @@ __device__ __forceinline__ void fused_level(const uint8_t* in, uint64_t nin, uin
 }
 
 #ifdef BCOSGPU_MERKLE_PROBE  // tools/fusedprobe.hip: per-wave global timestamps (s_memrealtime, 100 MHz)
-__device__ uint64_t g_mp[4096][12];
+__device__ uint64_t g_mp[4096][40];
 #define MP(k) \
-    if (threadIdx.x == 0 && blockIdx.x < 4096 && (k) < 12) g_mp[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime()
+    if (threadIdx.x == 0 && blockIdx.x < 4096 && (k) < 40) g_mp[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime()
 #else
 #define MP(k) \
     do {      \

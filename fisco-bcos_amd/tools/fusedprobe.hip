@@ -1,6 +1,7 @@
 // fusedprobe.hip -- per-wave timelines (s_memrealtime, 10 ns ticks) of merkle_fused_kernel at merkleBench
-// size (100k leaves, width 16) for Keccak and SM3: when level 0, the in-wave levels and each climbed
-// level end, relative to the earliest wave start; to see where SM3's one-launch time goes.
+// size (100k leaves, width 16; or `fusedprobe N WIDTH`) for Keccak and SM3: when level 0, the in-wave
+// levels and each climbed level end (the start and end of each climbed level's hash), relative to the
+// earliest wave start; to see where the one-launch time goes.
 #define BCOSGPU_MERKLE_PROBE 1
 #include "../csrc/hash_kernels.hip"
 #include <cstdio>
@@ -25,9 +26,11 @@ int main(int argc, char** argv) {
     for (int h : {KECCAK256, SM3}) {
         for (int rep = 0; rep < 50; ++rep) launch_merkle(h, width, dl, n, dt, dr, 0);
         (void)hipDeviceSynchronize();
-        static uint64_t mp[4096][12];
+        static uint64_t mp[4096][40];
         (void)hipMemcpyFromSymbol(mp, HIP_SYMBOL(g_mp), sizeof(mp));
-        const uint64_t waves = (n / width + 15) / 16;  // S = 16 at width 16 (one level-1 node per wave)
+        uint64_t S = 1;  // level-1 nodes per wave (launch_merkle_fused: width^a <= 32 for Keccak, <= 64 for SM3)
+        while (S * width <= (h == KECCAK256 ? 32u : 64u)) S *= width;
+        const uint64_t waves = ((n + width - 1) / width + S - 1) / S;
         uint64_t t0 = ~0ull, l0max = 0, innermax = 0, l0sum = 0;
         for (uint64_t b = 0; b < waves && b < 4096; ++b) t0 = mp[b][0] < t0 ? mp[b][0] : t0;
         uint64_t smax = 0;
@@ -41,7 +44,7 @@ int main(int argc, char** argv) {
                "\"inner_end_max_us\": %.2f, \"climb\": [", h, (unsigned long long)waves, smax / 100.0,
                l0sum / 100.0 / waves, l0max / 100.0, innermax / 100.0);
         // the wave that wrote the root: the one with the most climb stamps of this launch
-        for (int k = 3; k < 12; ++k) {
+        for (int k = 3; k < 40; ++k) {
             uint64_t best = 0;
             for (uint64_t b = 0; b < waves && b < 4096; ++b)
                 if (mp[b][k] > mp[b][0] && mp[b][k] >= t0 && mp[b][k] - t0 < 100000 && mp[b][k] - t0 > best) best = mp[b][k] - t0;

@@ -718,8 +718,8 @@ def gen_fp26(square):
     64-bit operand; v0..v47 are declared clobbered."""
     name = "fp26_sqr_asm(uint32_t r[10], const uint32_t a[10])" if square else \
         "fp26_mul_asm(uint32_t r[10], const uint32_t a[10], const uint32_t b[10])"
-    blk = Blk(name, "r = a^2 R^-1 mod p (SM2, fp26: inputs m <= 8, output m = 1)" if square else
-              "r = a b R^-1 mod p (SM2, fp26: inputs m <= 8, output m = 1)",
+    blk = Blk(name, "r = a^2 R^-1 mod p (SM2, fp26: inputs m <= 15, output m = 1)" if square else
+              "r = a b R^-1 mod p (SM2, fp26: inputs m <= 15, output m = 1)",
               ("uint32_t d[9]; " if square else "") + "uint64_t jp, jr; uint32_t k12 = 1u << 12, kn18 = 0xfffc0000u, "
               "kn16 = 0xffff0000u, k22 = 1u << 22;")
     R = blk.vout("r", 10)

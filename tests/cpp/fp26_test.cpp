@@ -59,15 +59,18 @@ int main(int argc, char** argv) {
     for (int it = 0; it < n; ++it) {
         const int mode = it % 3;
         fp26 a, b, r;
-        rand_fp(a, 1 + static_cast<int>(rnd() % 8), mode);
-        rand_fp(b, 1 + static_cast<int>(rnd() % 8), mode == 2 ? 1 : mode);
+        rand_fp(a, 1 + static_cast<int>(rnd() % 15), mode);
+        rand_fp(b, 1 + static_cast<int>(rnd() % 15), mode == 2 ? 1 : mode);
         fp26_mul(r, a, b);
         fcase("mul", a, b, r);
         fp26_sqr(r, a);
         fcase("sqr", a, a, r);
-        rand_fp(a, 8, 1);
+        rand_fp(a, 15, 1);  // every limb at the contract's bound
         fp26_sqr(r, a);
         fcase("sqr", a, a, r);
+        rand_fp(b, 15, 1);
+        fp26_mul(r, a, b);
+        fcase("mul", a, b, r);
         rand_fp(a, 1 + static_cast<int>(rnd() % 30), mode);
         rand_fp(b, 1 + static_cast<int>(rnd() % 30), mode);
         fp26_add(r, a, b);
