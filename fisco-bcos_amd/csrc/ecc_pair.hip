@@ -591,7 +591,11 @@ __device__ __forceinline__ void pair26_madd(JacP26& R, const JacP26& P, const Af
     const bool hz = fp26_is_zero(H) && !P.inf;
     const bool rz = fp26_is_zero(rr);
     JacP26 D;
-    if (hz && rz) CurveSM2x::dbl(D, P);  // P == Q (rare)
+    if (hz && rz) {  // P == Q (rare); back to the pair chain's magnitudes (2, 2, 2)
+        CurveSM2x::dbl(D, P);
+        fp26_normalize_weak(D.X);
+        fp26_normalize_weak(D.Y);
+    }
     const bool pinf = P.inf;
     fp26_copy(R.X, X3);
     fp26_copy(R.Y, Y3);
@@ -786,13 +790,13 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(IO io, uin
         fp26_sqr(z2, Q.Z);
         fp26_from_plain(cm, cc);
         fp26_mul(rhs, cm, z2);
-        fp26_sub<3>(dlt, rhs, Q.X);
+        fp26_sub<13>(dlt, rhs, Q.X);  // Q.X <= 12 (CurveSM2x::add)
         bool match = fp26_is_zero(dlt);
         const uint32_t carry = fe_add_k(c2, cc, ParamN2::M);
         if (carry == 0u && fe_lt_k(c2, ParamP2::M)) {
             fp26_from_plain(cm, c2);
             fp26_mul(rhs, cm, z2);
-            fp26_sub<3>(dlt, rhs, Q.X);
+            fp26_sub<13>(dlt, rhs, Q.X);  // Q.X <= 12 (CurveSM2x::add)
             match = match || fp26_is_zero(dlt);
         }
         ok = ok && match;
@@ -1210,13 +1214,13 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
         fp26_sqr(z2, Q.Z);
         fp26_from_plain(cm, cc);
         fp26_mul(rhs, cm, z2);
-        fp26_sub<3>(dlt, rhs, Q.X);
+        fp26_sub<13>(dlt, rhs, Q.X);  // Q.X <= 12 (CurveSM2x::add)
         bool match = fp26_is_zero(dlt);
         const uint32_t carry = fe_add_k(c2, cc, ParamN2::M);
         if (carry == 0u && fe_lt_k(c2, ParamP2::M)) {
             fp26_from_plain(cm, c2);
             fp26_mul(rhs, cm, z2);
-            fp26_sub<3>(dlt, rhs, Q.X);
+            fp26_sub<13>(dlt, rhs, Q.X);  // Q.X <= 12 (CurveSM2x::add)
             match = match || fp26_is_zero(dlt);
         }
         ok = ok && match;

@@ -1,10 +1,13 @@
 // ecp26.h -- SM2 point arithmetic (a = -3) over fp26 (fp26.h, Montgomery R = 2^286): Jacobian
 // coordinates, the formulas of ec.h's Curve<FieldP2, true> rearranged for fp26's magnitude contracts
-// (mul/sqr inputs <= 8), with a weak normalisation where a coordinate would outgrow them:
-//   dbl  (dbl-2001-b, Z3 = 2 Y Z) : X <= 5, Y, Z <= 8, Y + Z unused -> (2, 2, 2)   4M + 4S
-//   madd (madd-2007-bl, r/2)     : X, Y <= 2, Z <= 8; Q <= 2      -> (2, 2, 2)   8M + 3S
-//   add  (add-2007-bl)           : X, Y, Z <= 2 (both)            -> (2, 2, 2)
-// Complete in the same cases as ec.h.  Checked by the FE26_CHECK host build (tests/cpp/fp26_test.cpp).
+// (mul/sqr inputs <= 15), so that no coordinate needs a weak normalisation (a serial nine-limb carry
+// chain: ten of them per Booth window were ~5 % of the SM2 throughput kernel's instructions):
+//   dbl  (dbl-2001-b, Z3 = 2 Y Z) : X <= 12, Y, Z <= 15                 -> (11, 11, 2)   4M + 4S
+//   madd (madd-2007-bl, r/2)     : X, Y <= 11, Z <= 15; Q <= 11       -> (11, 11, 2)   8M + 3S
+//   add  (add-2007-bl)           : X <= 12, Y, Z <= 15 (both)          -> (12, 15, 15)
+// (madd / add outputs at their largest in the exceptional branches: the doubling, or an input passed
+// through.)  Complete in the same cases as ec.h.  Checked by the FE26_CHECK host build
+// (tests/cpp/fp26_test.cpp).
 #pragma once
 #include "fp26.h"
 
@@ -39,7 +42,7 @@ struct CurveSM2x {
     }
 
     F26_HD static void dbl(JacP26& R, const JacP26& P) {
-        fp26 delta, gamma, beta, t, u, alpha, X3, Y3, Z3, g2;
+        fp26 delta, gamma, beta, t, u, alpha, a2, X3, Y3, Z3, g2;
         fp26_sqr(delta, P.Z);
         fp26_sqr(gamma, P.Y);
         fp26_mul(beta, P.X, gamma);
@@ -47,19 +50,17 @@ struct CurveSM2x {
         fp26_add(u, P.X, delta);         // X + delta                  m X + 1
         fp26_mul(alpha, t, u);
         fp26_mul_int<3>(alpha, alpha);   // alpha = 3 (X - d)(X + d)   m 3
-        fp26_sqr(X3, alpha);
+        fp26_sqr(a2, alpha);
         fp26_mul_int<8>(t, beta);        // 8 beta                     m 8
-        fp26_sub<9>(X3, X3, t);          //                            m 11
-        fp26_normalize_weak(X3);         // X3 = alpha^2 - 8 beta      m 2
+        fp26_sub<9>(X3, a2, t);          // X3 = alpha^2 - 8 beta      m 11
         fp26_mul(Z3, P.Y, P.Z);
         fp26_mul_int<2>(Z3, Z3);         // Z3 = 2 Y Z = (Y + Z)^2 - gamma - delta   m 2
-        fp26_mul_int<4>(t, beta);        // 4 beta                     m 4
-        fp26_sub<3>(t, t, X3);           //                            m 8
+        fp26_mul_int<12>(t, beta);       // 12 beta                    m 12
+        fp26_sub<2>(t, t, a2);           // 4 beta - X3 = 12 beta - alpha^2   m 15
         fp26_mul(Y3, alpha, t);
         fp26_sqr(g2, gamma);
         fp26_mul_int<8>(g2, g2);         // 8 gamma^2                  m 8
-        fp26_sub<9>(Y3, Y3, g2);         //                            m 11
-        fp26_normalize_weak(Y3);         // Y3 = alpha (4 beta - X3) - 8 gamma^2   m 2
+        fp26_sub<9>(Y3, Y3, g2);         // Y3 = alpha (4 beta - X3) - 8 gamma^2   m 11
         fp26_copy(R.X, X3);
         fp26_copy(R.Y, Y3);
         fp26_copy(R.Z, Z3);
@@ -73,24 +74,22 @@ struct CurveSM2x {
         fp26_mul(U2, Q.x, Z1Z1);
         fp26_mul(S2, Q.y, P.Z);
         fp26_mul(S2, S2, Z1Z1);
-        fp26_sub<3>(H, U2, P.X);         // H = U2 - X1                m 5
+        fp26_sub<12>(H, U2, P.X);        // H = U2 - X1                m 14
         fp26_sqr(HH, H);
         fp26_mul_int<4>(I, HH);          // I = 4 HH                   m 4
         fp26_mul(J, H, I);
-        fp26_sub<3>(rr, S2, P.Y);        // rr = S2 - Y1 = r / 2       m 5
+        fp26_sub<12>(rr, S2, P.Y);       // rr = S2 - Y1 = r / 2       m 14
         fp26_mul(V, P.X, I);
         fp26_sqr(X3, rr);
         fp26_mul_int<4>(X3, X3);         // r^2                        m 4
         fp26_sub<2>(X3, X3, J);          //                            m 7
         fp26_mul_int<2>(t, V);           //                            m 2
-        fp26_sub<3>(X3, X3, t);          //                            m 11
-        fp26_normalize_weak(X3);         // X3 = r^2 - J - 2V          m 2
-        fp26_sub<3>(t, V, X3);           // V - X3                     m 5
+        fp26_sub<3>(X3, X3, t);          // X3 = r^2 - J - 2V          m 11
+        fp26_sub<12>(t, V, X3);          // V - X3                     m 14
         fp26_mul(Y3, rr, t);
         fp26_mul(t, P.Y, J);
         fp26_sub<2>(Y3, Y3, t);          //                            m 4
         fp26_mul_int<2>(Y3, Y3);         // Y3 = r (V - X3) - 2 Y1 J   m 8
-        fp26_normalize_weak(Y3);         //                            m 2
         fp26_mul(Z3, P.Z, H);
         fp26_mul_int<2>(Z3, Z3);         // Z3 = 2 Z1 H                m 2
         const bool hz = fp26_is_zero(H) && !P.inf;
@@ -135,14 +134,12 @@ struct CurveSM2x {
         fp26_sqr(X3, rr);
         fp26_sub<2>(X3, X3, J);          // m 4
         fp26_mul_int<2>(t, V);           // m 2
-        fp26_sub<3>(X3, X3, t);          // m 8
-        fp26_normalize_weak(X3);         // X3 = r^2 - J - 2V          m 2
-        fp26_sub<3>(t, V, X3);           // m 5
+        fp26_sub<3>(X3, X3, t);          // X3 = r^2 - J - 2V          m 8
+        fp26_sub<9>(t, V, X3);           // m 11
         fp26_mul(Y3, rr, t);
         fp26_mul(t, S1, J);
         fp26_mul_int<2>(t, t);           // m 2
-        fp26_sub<3>(Y3, Y3, t);          // m 5
-        fp26_normalize_weak(Y3);         // Y3 = r (V - X3) - 2 S1 J   m 2
+        fp26_sub<3>(Y3, Y3, t);          // Y3 = r (V - X3) - 2 S1 J   m 5
         fp26_mul(Z3, P.Z, Q.Z);
         fp26_mul(Z3, Z3, H);
         fp26_mul_int<2>(Z3, Z3);         // Z3 = 2 Z1 Z2 H             m 2

@@ -359,6 +359,8 @@ F26_HD void trio_madd_sm2(TrioPtP& R, const TrioPtP& P, const AffP26& Q, const T
             fp26_copy(A.Z, P.Q1);
             A.inf = P.inf;
             CurveSM2x::dbl(D, A);
+            fp26_normalize_weak(D.X);  // the chain's magnitudes (2, 2, 2)
+            fp26_normalize_weak(D.Y);
             // D on lane 2 -> X3, Y3 on lane 0 and Z3 on lane 2, then the usual state
             fp26 dx, dy;
             fdpp<kR2>(dx, D.X);

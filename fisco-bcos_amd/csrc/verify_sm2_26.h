@@ -132,8 +132,7 @@ __device__ __forceinline__ void add_digit_sm2_26(JacP26& acc, const uint32_t* ld
     fp26_from_fe(S.y, y);
     fp26 ny;
     fp26_neg<2>(ny, S.y);
-    fp26_cmov(S.y, ny, d < 0);
-    fp26_normalize_weak(S.y);  // m 2, as madd's Q requires
+    fp26_cmov(S.y, ny, d < 0);  // m 3 (madd takes Q <= 11)
     JacP26 R;
     CurveSM2x::madd(R, acc, S);
     CurveSM2x::cmov(acc, R, d != 0);
@@ -213,13 +212,13 @@ __device__ __forceinline__ bool sm2_verify_rs26(const fe& hash_be, const fe& r, 
     fp26_sqr(z2, Q.Z);
     fp26_from_plain(cm, c);
     fp26_mul(rhs, cm, z2);
-    fp26_sub<3>(dlt, rhs, Q.X);
+    fp26_sub<13>(dlt, rhs, Q.X);  // Q.X <= 12 (CurveSM2x::add)
     bool match = fp26_is_zero(dlt);
     const uint32_t carry = fe_add_k(c2, c, ParamN2::M);
     if (carry == 0u && fe_lt_k(c2, ParamP2::M)) {
         fp26_from_plain(cm, c2);
         fp26_mul(rhs, cm, z2);
-        fp26_sub<3>(dlt, rhs, Q.X);
+        fp26_sub<13>(dlt, rhs, Q.X);
         match = match || fp26_is_zero(dlt);
     }
     return ok && match;

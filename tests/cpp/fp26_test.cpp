@@ -156,7 +156,7 @@ int main(int argc, char** argv) {
     printf("A add_dbl");
     pr_jac(R);
     JacP26 nGs = Gs;
-    fp26_neg<3>(nGs.Y, Gs.Y);
+    fp26_neg<12>(nGs.Y, Gs.Y);  // Gs.Y <= 11 (madd)
     fp26_normalize_weak(nGs.Y);
     CurveSM2x::add(R, Gj, nGs);  // infinity
     printf("A add_inf");
