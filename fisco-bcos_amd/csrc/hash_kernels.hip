@@ -305,7 +305,14 @@ __global__ __launch_bounds__(1024) void merkle_top_kernel(int w, int l0, uint8_t
 // stores (agent-scope atomic stores: write-through past the per-XCD L2), the wave waits for them
 // (s_waitcnt) before its counter atomic, and the completing wave gathers the children with
 // device-coherent loads into LDS; the last arriver resets the counter, so the slot is clean for the
-// next launch on the stream.
+// next launch on the stream.  The ordering this rests on is the ISA's, not the language's (relaxed
+// atomics order nothing between locations): agent-scope relaxed stores / loads are sc1 accesses,
+// coherent at agent scope; "s_waitcnt vmcnt(0)" returns only once the stores are acknowledged; the
+// counter RMW's return is waited for before the branch that leads to the loads; and compiler barriers
+// ("memory" clobbers) keep the compiler from reordering across either point.  tests/test_hazards.py
+// checks the emitted order on every build (tools/hazard_check.py fused_publish_order).  An acq_rel
+// counter (the language-level form) costs a buffer_wbl2 / buffer_inv of the XCD's L2 per hand-off:
+// 0.175 vs 0.130 ms per 100k-leaf width-2 Keccak root (profiles/r04_merkle_fused_order_ab.log).
 struct FusedTree {
     TreeLevels t;
     uint32_t ctr_off[64];  // first counter of level l (levels a + 1 .. nlev - 1)
@@ -426,7 +433,9 @@ __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restr
         const uint64_t p = j / width;
         const uint32_t kids = static_cast<uint32_t>(t.cnt[l - 1] - p * width < width ? t.cnt[l - 1] - p * width : width);
         uint32_t arrived = 0;
-        __builtin_amdgcn_s_waitcnt(0);  // the published node's stores have completed (whole wave)
+        // the published node's stores have completed (whole wave); the "memory" clobber also keeps the
+        // compiler from moving any memory access across this point (relaxed atomics alone would allow it)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (lane == 0) {
             uint32_t* c = ctr + f.ctr_off[l] + p;
@@ -435,6 +444,7 @@ __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restr
         }
         arrived = __shfl(arrived, 0);
         if (arrived != kids) return;  // a sibling's wave finishes the parent
+        asm volatile("" ::: "memory");  // the children's loads stay after the counter (compiler order)
         MP(3 + 2 * (l - inner));
         fused_one_node<H>(tree + 32ull * (t.pos[l - 1] + 1), t.cnt[l - 1], width, p, tree + 32ull * (t.pos[l] + 1 + p),
                           reinterpret_cast<uint8_t*>(&lds[0][0][0]));

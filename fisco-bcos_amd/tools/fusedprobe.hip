@@ -1,7 +1,8 @@
 // fusedprobe.hip -- per-wave timelines (s_memrealtime, 10 ns ticks) of merkle_fused_kernel at merkleBench
 // size (100k leaves, width 16; or `fusedprobe N WIDTH`) for Keccak and SM3: when level 0, the in-wave
 // levels and each climbed level end (the start and end of each climbed level's hash), relative to the
-// earliest wave start; to see where the one-launch time goes.
+// earliest wave start; to see where the one-launch time goes.  Also the mean per-root time of 400
+// back-to-back launches.
 #define BCOSGPU_MERKLE_PROBE 1
 #include "../csrc/hash_kernels.hip"
 #include <cstdio>
@@ -26,6 +27,18 @@ int main(int argc, char** argv) {
     for (int h : {KECCAK256, SM3}) {
         for (int rep = 0; rep < 50; ++rep) launch_merkle(h, width, dl, n, dt, dr, 0);
         (void)hipDeviceSynchronize();
+        hipEvent_t e0, e1;  // back-to-back launches: the per-root time the bench's Merkle legs report
+        (void)hipEventCreate(&e0);
+        (void)hipEventCreate(&e1);
+        const int reps = 400;
+        (void)hipEventRecord(e0, 0);
+        for (int rep = 0; rep < reps; ++rep) launch_merkle(h, width, dl, n, dt, dr, 0);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        launch_merkle(h, width, dl, n, dt, dr, 0);  // the stamps below are of this lone launch
+        (void)hipDeviceSynchronize();
         static uint64_t mp[4096][40];
         (void)hipMemcpyFromSymbol(mp, HIP_SYMBOL(g_mp), sizeof(mp));
         uint64_t S = 1;  // level-1 nodes per wave (launch_merkle_fused: width^a <= 32 for Keccak, <= 64 for SM3)
@@ -40,8 +53,8 @@ int main(int argc, char** argv) {
             innermax = mp[b][2] - t0 > innermax ? mp[b][2] - t0 : innermax;
             l0sum += mp[b][1] - mp[b][0];
         }
-        printf("{\"hasher\": %d, \"waves\": %llu, \"last_start_us\": %.2f, \"level0_mean_us\": %.2f, \"level0_end_max_us\": %.2f, "
-               "\"inner_end_max_us\": %.2f, \"climb\": [", h, (unsigned long long)waves, smax / 100.0,
+        printf("{\"hasher\": %d, \"n\": %llu, \"width\": %d, \"ms_per_root\": %.4f, \"waves\": %llu, \"last_start_us\": %.2f, \"level0_mean_us\": %.2f, \"level0_end_max_us\": %.2f, "
+               "\"inner_end_max_us\": %.2f, \"climb\": [", h, (unsigned long long)n, width, ms / reps, (unsigned long long)waves, smax / 100.0,
                l0sum / 100.0 / waves, l0max / 100.0, innermax / 100.0);
         // the wave that wrote the root: the one with the most climb stamps of this launch
         for (int k = 3; k < 40; ++k) {
