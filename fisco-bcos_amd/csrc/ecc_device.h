@@ -561,8 +561,6 @@ int launch_sig_verify_small_secp(const KeyIO& io, uint64_t n, hipStream_t st);
 // SM2 verify with a known key over KeyIO (ecc_txv.hip: launch_verify's kernel choice)
 int launch_sm2_verify_key(const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
                           uint64_t n, uint8_t* d_ok, hipStream_t st);
-// compute units of the current device (cached per device)
-int cu_count();
 template <class IO>
 int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st);
 static inline unsigned grid_of(uint64_t n) { return static_cast<unsigned>((n + 255) / 256); }

@@ -834,7 +834,9 @@ struct Sm2Trio26Lds {
     uint32_t c[8][64];
     uint32_t addr[5][64];
     uint32_t ok2[64];
-    uint32_t seq[4];
+    uint32_t kb[8][64];              // t again (waves 2 and 3 write it for their own low-window chains)
+    uint32_t bacc[25][64];           // the low-window chains' results (canonical X, Y, Z, inf)
+    uint32_t seq[8];
 };
 
 __device__ __forceinline__ void trio_add_digit_sm2(TrioPtP& acc, const Sm2Trio26Lds& L, int tl, int d,
@@ -942,15 +944,62 @@ __device__ __forceinline__ void lds_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+// The low `split` Booth windows of t P for the 20 txs of chain wave (wave - 2), run on wave 2 / 3 once
+// their table, hash and comb work is done (they idled for the rest of the kernel before): t's digits
+// split as t = sum_{w >= split} d_w 16^w + sum_{w < split} d_w 16^w, the first sum on waves 0 / 1 (their
+// windows 63 .. split, then 4 split doublings), the second here -- the same window loop on t shifted up
+// by 4 (64 - split) bits, from infinity, on the affine table.  Its first addition is to infinity; after
+// it the accumulator is K P with |K| >= 16 before every addition of |d| P, |d| <= 8, |K| < 2^(4 split + 1)
+// < n, so trio_madd_sm2_d's skipped P = +-Q cases cannot occur (as on the high chain).  Stores the sum
+// as a Jacobian point at L.bacc[.][tx].
+__device__ __forceinline__ void sm2_low_chain(Sm2Trio26Lds& L, int wave, int lane, int split) {
+    lds_wave_sync();
+    const TrioLane T(lane);
+    const int pos = lane & 15, trio_idx = pos / 3;
+    const bool real = trio_idx < 5;
+    const int tl = (wave - 2) * 20 + (lane >> 4) * 5 + (real ? trio_idx : 4);
+    fe k;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) k.v[q] = L.kb[q][tl];
+#pragma unroll 1
+    for (int j = 64 - split; j > 0; --j) shl4(k);  // window split - 1 at the top
+    TrioPtP acc;
+    trio_set_inf_sm2(acc);
+    fp26 D;
+    fp26_set(D, p26::ONE_R);
+    {
+        const uint32_t top = k.v[7];
+        const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
+        const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
+        shl4(k);
+        trio_add_digit_sm2(acc, L, tl, d, T);  // to infinity: the table point (D = 1) or infinity
+    }
+#pragma unroll 1
+    for (int w = split - 2; w >= 0; --w) {
+        trio_dbl_sm2_d(acc, D, T);
+        trio_dbl_sm2_d(acc, D, T);
+        trio_dbl_sm2_d(acc, D, T);
+        trio_dbl_sm2_d(acc, D, T);
+        const uint32_t top = k.v[7];
+        const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
+        const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
+        shl4(k);
+        trio_add_digit_sm2_d(acc, D, L, tl, d, T);
+    }
+    JacP26 J;
+    trio_to_jac_sm2(J, acc, T);
+    if (T.r0 && real) pair26_store_jac(L.bacc, J, tl);
+}
+
 template <class IO>
 __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab,
-                                                                        int affine) {
+                                                                        int affine, int split) {
     constexpr int TPW = 40;
     __shared__ Sm2Trio26Lds L;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * TPW + lane;
     const bool active = lane < TPW && i < n;
-    if (threadIdx.x < 4) L.seq[threadIdx.x] = 0u;
+    if (threadIdx.x < 8) L.seq[threadIdx.x] = 0u;
     __syncthreads();
     SM2_T(0);
     fe r, s, px, py;
@@ -1022,7 +1071,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
         fp26_set(D, p26::ONE_R);
         bool aff = false;  // wave-uniform: the affine table (wave 3) is ready
 #pragma unroll 1
-        for (int w = 63; w >= 0; --w) {
+        for (int w = 63; w >= split; --w) {
             trio_dbl_sm2_d(acc, D, T);  // three product levels each (delta carried)
             trio_dbl_sm2_d(acc, D, T);
             trio_dbl_sm2_d(acc, D, T);
@@ -1044,11 +1093,16 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             else
                 trio_add_digit_sm2_jd(acc, D, L, tl, d, T);  // five
         }
+        // the high windows' sum times 2^(4 split): the low windows run on waves 2 and 3
+#pragma unroll 1
+        for (int j = 4 * split; j > 0; --j) trio_dbl_sm2_d(acc, D, T);
         JacP26 J;
         trio_to_jac_sm2(J, acc, T);
         if (T.r0 && real) pair26_store_jac(L.acc, J, tl);
         SM2_T(2);
     } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) L.kb[q][lane] = t.v[q];  // (both waves write the same values)
         {  // waves 2 and 3: the Jacobian tables of chain waves 0 and 1
             lds_wave_sync();
             const TrioLane T(lane);
@@ -1141,6 +1195,20 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             pair26_load_jac(G1, L.gh, lane);
             CurveSM2x::add(G, G0, G1);
             pair26_store_jac(L.g, G, lane);
+            if (split > 0) {
+                // the low windows of txs 0..19 (the affine table is complete: wave 3 built it before its
+                // comb half, whose result was awaited above), then s G + that sum for all 40 txs
+                sm2_low_chain(L, wave, lane, split);
+                while (__hip_atomic_load(&L.seq[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                lds_wave_sync();
+                JacP26 B;
+                pair26_load_jac(B, L.bacc, lane);
+                CurveSM2x::add(G, G, B);
+                pair26_store_jac(L.g, G, lane);
+            }
+            SM2_T(5);
         } else {
             // the affine table of all 40 txs (one lane per tx) from the Jacobian entries (waves 2 and 3):
             // one inversion of Z1 .. Z7, then x = X / Z^2, y = Y / Z^3; the chains switch to it when ready
@@ -1198,6 +1266,12 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             SM2_T(2);
             pair26_store_jac(L.gh, G1, lane);
             __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (split > 0) {  // the low windows of txs 20..39
+                sm2_low_chain(L, wave, lane, split);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(&L.seq[4], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            SM2_T(5);
         }
     }
     __syncthreads();
@@ -1232,6 +1306,18 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
     }
 }
 
+// low Booth windows of t P run by waves 2 and 3 (sm2_low_chain); BCOSGPU_SM2_SPLIT overrides (0 = all
+// 64 windows on waves 0 and 1, the round-3 schedule), clamped to [0, 63]
+static constexpr int kSm2TrioSplit = 38;
+static int sm2_trio_split() {
+    static const int v = [] {
+        const char* e = getenv("BCOSGPU_SM2_SPLIT");
+        const int x = e ? atoi(e) : kSm2TrioSplit;
+        return x < 0 ? 0 : x > 63 ? 63 : x;
+    }();
+    return v;
+}
+
 template <class IO>
 int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st) {
     const dim3 grid(static_cast<unsigned>((n + 63) / 64));
@@ -1244,7 +1330,7 @@ int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n,
             const char* jo = getenv("BCOSGPU_SM2_JAC_ONLY");
             const int affine = jo && atoi(jo) != 0 ? 0 : 1;
             hipLaunchKernelGGL(tx_verify_sm2_trio26_kernel<IO>, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0,
-                               st, io, n, t26, affine);
+                               st, io, n, t26, affine, sm2_trio_split());
         }
         else
             hipLaunchKernelGGL(tx_verify_sm2_pair26_kernel<IO>, grid, dim3(256), 0, st, io, n, t26);

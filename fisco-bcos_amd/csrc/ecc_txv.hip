@@ -60,17 +60,6 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
 // The trio and pair kernels are candidates up to 2^16 txs (beyond that the one-lane kernel's
 // throughput wins at any rounding).  Returns 2 (trio), 1 (pair), 0 (one-lane, occupancy 1) or -2
 // (one-lane, occupancy 2).
-int cu_count() {
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cus[dev]) {
-        int c = 0;
-        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
-        cus[dev] = c;
-    }
-    return cus[dev];
-}
 static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok) {
     const bool sm2 = suite == BCOSGPU_SUITE_SM2;
     //                    occ 2,              occ 1,              pair,               trio

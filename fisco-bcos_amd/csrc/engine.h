@@ -8,6 +8,19 @@
 
 namespace bcosgpu {
 
+// compute units of the current device (cached per device)
+inline int cu_count() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        cus[dev] = c;
+    }
+    return cus[dev];
+}
+
 // hash_kernels.hip
 int launch_hash_batch(int hasher, const uint8_t* d_data, const uint64_t* d_off, uint64_t n,
                       uint8_t* d_out, hipStream_t st);

@@ -182,24 +182,25 @@ __device__ __forceinline__ void pair_level_pass(const KeccakPair& kp, const uint
 // else one lane per node.
 enum LevelMode : int { kOneLane = 0, kPair = 1, kCoop = 2 };
 template <int H>
-__device__ __forceinline__ int level_mode(uint64_t nout, uint32_t threads, int pair) {
+__device__ __forceinline__ int level_mode(uint64_t nout, uint32_t threads, int pair, uint32_t coop_max = ~0u) {
     if (H != KECCAK256) return kOneLane;
-    if (nout <= threads / 32) return kCoop;
+    if (nout <= threads / 32 && nout <= coop_max) return kCoop;
     if (pair && 2 * nout <= threads) return kPair;
     return kOneLane;
 }
 
+// The workgroup's levels: its B level-1 nodes from the leaves, then every level whose groups lie inside
+// it, through LDS (levels of at most coop_max nodes per full workgroup on 25-lane groups); returns the
+// LDS buffer of the last level (whose first node is the workgroup's node `base` of that level).
 // `pair`: level 1 (from the leaves) and the LDS levels may run on lane pairs (the host sets it when
 // the tree's level 1 leaves most of the GPU idle; a throughput-sized level 1 stays one lane per node,
 // which costs fewer instructions per node)
 template <int H, int W>
-__global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w, int kin,
-                                                        int B, uint8_t* __restrict__ tree, const TreeLevels t,
-                                                        uint8_t* __restrict__ root, int pair) {
-    __shared__ uint4 lds[2][256][2];
-    const uint32_t width = W ? W : static_cast<uint32_t>(w);
+__device__ __forceinline__ int wg_levels(uint4 (*lds)[256][2], const uint8_t* __restrict__ leaves, uint64_t n,
+                                         uint32_t width, int kin, int B, uint8_t* __restrict__ tree, const TreeLevels& t,
+                                         int pair, uint32_t coop_max, uint64_t& base) {
     const uint32_t tid = threadIdx.x;
-    uint64_t base = static_cast<uint64_t>(blockIdx.x) * B;  // first level-1 node of this workgroup
+    base = static_cast<uint64_t>(blockIdx.x) * B;  // first level-1 node of this workgroup
     uint32_t nodes = static_cast<uint32_t>(t.cnt[0] - base < static_cast<uint64_t>(B) ? t.cnt[0] - base : B);
     uint32_t d[8];
     if (level_mode<H>(B, blockDim.x, pair) == kPair) {
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restric
         const uint32_t nn = (nodes + width - 1) / width;
         const uint8_t* in = reinterpret_cast<const uint8_t*>(&lds[cur][0][0]);
         // (the mode is decided on the full group count B / width^l so every workgroup runs alike)
-        const int mode = level_mode<H>((B + width - 1) / width, blockDim.x, pair);
+        const int mode = level_mode<H>((B + width - 1) / width, blockDim.x, pair, coop_max);
         if (mode == kCoop) {  // latency-bound level: 25 lanes per node
             const KeccakCoop kc;
             const uint32_t g = tid / 32;
@@ -242,6 +243,18 @@ __global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restric
         base = nbase;
         B = (B + width - 1) / width;
     }
+    return cur;
+}
+
+template <int H, int W>
+__global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w, int kin,
+                                                        int B, uint8_t* __restrict__ tree, const TreeLevels t,
+                                                        uint8_t* __restrict__ root, int pair) {
+    __shared__ uint4 lds[2][256][2];
+    const uint32_t tid = threadIdx.x;
+    uint64_t base;
+    const int cur = wg_levels<H, W>(lds, leaves, n, W ? W : static_cast<uint32_t>(w), kin, B, tree, t, pair, ~0u, base);
+    const int top = kin + 1 < t.nlev ? kin + 1 : t.nlev;
     if (blockIdx.x == 0 && tid < static_cast<uint32_t>(t.nlev)) {  // count records (Merkle.h:189-204)
         uint32_t* e = reinterpret_cast<uint32_t*>(tree + 32ull * t.pos[tid]);
         e[0] = bswap32(static_cast<uint32_t>(t.cnt[tid]));
@@ -571,6 +584,134 @@ static int launch_merkle_fused(int hasher, int width, const uint8_t* d_leaves, u
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
+// ------------------------------------------------------------------ one launch, four-wave workgroups
+// The one-launch path for narrow Keccak trees (the production width 2, Merkle.h:36 / BlockImpl.h:125).
+// With one wave per workgroup (above) a width-2 tree needs 32 level-1 nodes per wave on lane pairs, i.e.
+// 1,563 waves for 100k leaves -- two waves on many SIMDs -- and then five more lane-pair or 25-lane levels
+// and a cross-wave hand-off for each of the 11 levels above.  Here a workgroup is four waves, one per SIMD
+// of a CU: it hashes B = width^kin <= 256 level-1 nodes one lane each, the levels above them through LDS
+// as merkle_wg_kernel does (lane pairs while a level has more than coop_max nodes, then 25-lane groups,
+// eight per workgroup), and then climbs like merkle_fused_kernel, except that a climb step takes g levels
+// at once: the workgroup completing a group of width^g nodes gathers them and hashes the g levels above
+// with its eight 25-lane groups (width 2: 16 nodes -> 8 -> 4 -> 2 -> 1, one hand-off per four levels).
+// The hand-off is merkle_fused_kernel's: sc1 node stores, s_waitcnt vmcnt(0) + barrier before the counter
+// RMW, sc1 loads after it, compiler barriers at both points (tools/hazard_check.py checks the order).
+struct ClimbTree {
+    TreeLevels t;
+    uint32_t ctr_off[64];  // first arrival counter of level l (the top level of a climb step)
+    int kin;               // levels above level 1 inside a workgroup (B = width^kin)
+    int B;
+    int g;                 // levels per climb step: width^(g - 1) <= 8 first-level nodes
+    uint32_t coop_max;     // in-workgroup levels of at most this many nodes run on 25-lane groups
+    int pair;
+};
+
+template <int H, int W>
+__global__ __launch_bounds__(256) void merkle_climb_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w,
+                                                           uint8_t* __restrict__ tree, const ClimbTree f,
+                                                           uint8_t* __restrict__ root, uint32_t* __restrict__ ctr) {
+    __shared__ uint4 lds[2][256][2];
+    __shared__ uint32_t arrived_s;
+    const TreeLevels& t = f.t;
+    const uint32_t width = W ? W : static_cast<uint32_t>(w);
+    const uint32_t tid = threadIdx.x;
+    if (blockIdx.x == 0 && tid < static_cast<uint32_t>(t.nlev)) {  // count records (Merkle.h:189-204)
+        uint32_t* e = reinterpret_cast<uint32_t*>(tree + 32ull * t.pos[tid]);
+        e[0] = bswap32(static_cast<uint32_t>(t.cnt[tid]));
+#pragma unroll
+        for (int k = 1; k < 8; ++k) e[k] = 0;
+    }
+    uint64_t j;  // this workgroup's node at level l - 1 (LDS buffer cur, entry 0)
+    int cur = wg_levels<H, W>(lds, leaves, n, width, f.kin, f.B, tree, t, f.pair, f.coop_max, j);
+    int l = f.kin + 1 < t.nlev ? f.kin + 1 : t.nlev;  // next level to compute
+    __syncthreads();
+    if (l < t.nlev && tid < 8)  // publish it (device-coherent)
+        st_dev(tree + 32ull * (t.pos[l - 1] + 1 + j) + 4 * tid, reinterpret_cast<const uint32_t*>(&lds[cur][0][0])[tid]);
+    while (l < t.nlev) {
+        const int g = f.g < t.nlev - l ? f.g : t.nlev - l;
+        uint64_t G = 1;
+        for (int q = 0; q < g; ++q) G *= width;
+        const uint64_t P = j / G, first = P * G;  // the step's top node (level l + g - 1), its first child
+        const uint32_t kids = static_cast<uint32_t>(t.cnt[l - 1] - first < G ? t.cnt[l - 1] - first : G);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the published node's stores are acknowledged
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t* c = ctr + f.ctr_off[l + g - 1] + P;
+            const uint32_t a = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+            if (a == kids) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            arrived_s = a;
+        }
+        __syncthreads();
+        if (arrived_s != kids) return;  // a sibling's workgroup climbs on
+        asm volatile("" ::: "memory");  // the children's loads stay after the counter (compiler order)
+        uint32_t* buf = reinterpret_cast<uint32_t*>(&lds[0][0][0]);
+        const uint8_t* src = tree + 32ull * (t.pos[l - 1] + 1 + first);
+        for (uint32_t q = tid; q < 8u * kids; q += 256u) buf[q] = ld_dev(src + 4u * q);
+        __syncthreads();
+        cur = 0;
+        uint32_t nin = kids;
+        uint64_t b = first;
+        const KeccakCoop kc;
+        const uint32_t gq = tid / 32;
+        for (int i = 0; i < g; ++i) {  // nn <= 8 nodes per level: one pass of the eight 32-lane groups
+            const uint32_t nn = (nin + width - 1) / width;
+            b /= width;
+            coop_level_pass<W>(kc, reinterpret_cast<const uint8_t*>(&lds[cur][0][0]), nin, width, gq, nn,
+                               tree + 32ull * (t.pos[l + i] + 1 + b + gq),
+                               reinterpret_cast<uint8_t*>(&lds[cur ^ 1][gq < 8 ? gq : 0][0]));
+            cur ^= 1;
+            nin = nn;
+            __syncthreads();
+        }
+        j = P;
+        l += g;
+        if (l < t.nlev && tid < 8)
+            st_dev(tree + 32ull * (t.pos[l - 1] + 1 + j) + 4 * tid, reinterpret_cast<const uint32_t*>(&lds[cur][0][0])[tid]);
+    }
+    if (root && j == 0 && tid < 8)  // this workgroup produced the root node (or the whole tree fit in it)
+        reinterpret_cast<uint32_t*>(root)[tid] = reinterpret_cast<const uint32_t*>(&lds[cur][0][0])[tid];
+}
+
+static constexpr uint64_t kClimbMaxWgs = 4096;
+static constexpr int kClimbMaxWidth = 4;  // widths the four-wave path takes by default (wider: the one-wave one)  // level-1 workgroups up to which the four-wave path runs
+
+// returns 1 when it does not apply (not Keccak, too wide, too many counters or workgroups, no slot)
+static int launch_merkle_climb(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
+                               uint8_t* d_root, const TreeLevels& t, hipStream_t st) {
+    if (hasher != KECCAK256) return 1;
+    ClimbTree f{};
+    f.t = t;
+    f.B = 1;
+    f.kin = 0;
+    while (f.B * width <= 256) {
+        f.B *= width;
+        ++f.kin;
+    }
+    f.g = 1;
+    for (int q = width; q <= 8; q *= width) ++f.g;  // width^(g - 1) <= 8
+    const uint64_t wgs = (t.cnt[0] + f.B - 1) / f.B;
+    if (wgs > kClimbMaxWgs) return 1;
+    // one workgroup per CU: the latency schedule (25-lane groups from eight nodes down, lane pairs above);
+    // more: every SIMD runs several waves, so the levels take the schedule with the fewest instructions
+    // per node (lane pairs down to two nodes)
+    const bool latency = wgs <= static_cast<uint64_t>(cu_count());
+    f.coop_max = latency ? 8u : 2u;
+    f.pair = 1;
+    uint32_t off = 0;
+    for (int l = 0; l < t.nlev; ++l) {
+        f.ctr_off[l] = off;
+        if (l > f.kin) off += static_cast<uint32_t>(t.cnt[l]);
+    }
+    if (off > kFusedCounters) return 1;
+    uint32_t* ctr = fused_counter_slot(st);
+    if (!ctr) return 1;
+    const dim3 g(static_cast<unsigned>(wgs)), b(256);
+#define CLIMB(WW) hipLaunchKernelGGL((merkle_climb_kernel<KECCAK256, WW>), g, b, 0, st, d_leaves, n, width, d_tree, f, d_root, ctr)
+    if (width == 2) CLIMB(2); else if (width == 16) CLIMB(16); else CLIMB(0);
+#undef CLIMB
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
 static constexpr uint64_t kTopKernelMaxIn = 16384;  // inputs per level the single-workgroup kernel takes
 static constexpr uint64_t kPairMaxNodes = 32768;    // level-1 nodes up to which Keccak levels use lane pairs
 
@@ -606,6 +747,15 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
         const char* e = getenv("BCOSGPU_MERKLE_FUSED");
         return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
     }();
+    // narrow Keccak trees: the four-wave one-launch kernel (BCOSGPU_MERKLE_CLIMB=0/1 forces it off/on)
+    static const int climb_env = [] {
+        const char* e = getenv("BCOSGPU_MERKLE_CLIMB");
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    }();
+    if (fused_env != 1 && (climb_env == 1 || (climb_env < 0 && width <= kClimbMaxWidth))) {
+        const int rc = launch_merkle_climb(hasher, width, d_leaves, n, d_tree, d_root, t, st);
+        if (rc <= 0) return rc;
+    }
     if (fused_env == 1 || (fused_env < 0 && hasher == KECCAK256)) {
         const int rf = launch_merkle_fused(hasher, width, d_leaves, n, d_tree, d_root, t, fused_env == 1, st);
         if (rf <= 0) return rf;

@@ -2,7 +2,7 @@
 # the call (no retries).  Outputs under gpurun_out/.
 #   bash fisco-bcos_amd/tools/gpu_run.sh STEP [STEP ...]
 # steps:
-#   tests[=PYTEST_K]     the -m gpu suite (or the tests whose id matches PYTEST_K), one pytest process
+#   tests[=PYTEST_K]     the -m gpu suite (or the tests PYTEST_K selects, ',' for ' '), one pytest process
 #   file=PATH[::K]       the -m gpu tests of one file (optionally -k K)
 #   smoke                __graft_entry__.smoke()
 #   bench[=ARGS]         bench.py (default arguments = the driver's default run), ARGS with ',' for ' '
@@ -19,11 +19,12 @@ for step in "$@"; do
   log=gpurun_out/step${n}_${name}.log
   case $name in
     tests)
-      k=""; [ -n "$arg" ] && k="-k $arg"
-      timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $k > $log 2>&1 ;;
+      k=(); [ -n "$arg" ] && k=(-k "${arg//,/ }")
+      timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" > $log 2>&1 ;;
     file)
-      f=${arg%%::*}; k=""; [ "$f" != "$arg" ] && k="-k ${arg#*::}"
-      timeout -k 10 900 python3 -u -m pytest $f -m gpu -x -v --timeout 300 --timeout-method thread $k > $log 2>&1 ;;
+      f=${arg%%::*}; k=(); [ "$f" != "$arg" ] && k=(-k "${arg#*::}")
+      k=("${k[@]//,/ }")
+      timeout -k 10 900 python3 -u -m pytest $f -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" > $log 2>&1 ;;
     smoke)
       timeout -k 10 180 python3 -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
     bench)

@@ -1,5 +1,6 @@
 // sm2bench.hip -- phase timestamps (s_memtime cycles) of tx_verify_sm2_trio26_kernel's workgroup 0 on a
 // 10k-tx batch of random inputs (the schedule is input-independent), to see where c2sm2's latency goes.
+//   sm2bench [REPS [SYNTH_DIR | - [SPLIT]]]
 #define BCOSGPU_SM2_TIMING 1
 #include "../csrc/ecc_tables.hip"
 #ifdef SM2BENCH_PAIR_SRC  // A/B builds: another revision of ecc_pair.hip, whose kernel takes no 'affine' flag
@@ -7,7 +8,7 @@
 #define SM2_AFFINE_ARG
 #else
 #include "../csrc/ecc_pair.hip"
-#define SM2_AFFINE_ARG , 1
+#define SM2_AFFINE_ARG , 1, split
 #endif
 #include <cstdio>
 #include <cstdlib>
@@ -16,6 +17,8 @@
 
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 4;
+    // low Booth windows on waves 2 and 3 (sm2_low_chain): argv[3], else the library's default
+    const int split = argc > 3 ? atoi(argv[3]) : bcosgpu::kSm2TrioSplit;
     using namespace bcosgpu;
     if (ecc_init_tables(0, 0)) { printf("no device\n"); return 77; }
     const uint64_t n = 10000;
@@ -24,7 +27,7 @@ int main(int argc, char** argv) {
     uint32_t x = 12345;
     for (auto& b : pre) b = (x = x * 1103515245u + 12345u) >> 24;
     for (auto& b : sig) b = (x = x * 1103515245u + 12345u) >> 24;
-    if (argc > 2) {  // the bench's batch (tools/dump_synth.py <dir>): valid signatures
+    if (argc > 2 && std::string(argv[2]) != "-") {  // the bench's batch (tools/dump_synth.py <dir>): valid signatures
         const std::string d = argv[2];
         FILE* f = fopen((d + "/pre.bin").c_str(), "rb");
         FILE* g = fopen((d + "/sig.bin").c_str(), "rb");
@@ -68,12 +71,13 @@ int main(int argc, char** argv) {
     ms /= static_cast<float>(reps - reps / 2);
     uint64_t t[4][8];
     hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sm2_t), sizeof(t));
-    printf("{\"kernel_ms\": %.4f, \"cycles_since_start\": {", ms);
+    printf("{\"split\": %d, \"kernel_ms\": %.4f, \"cycles_since_start\": {", split, ms);
     for (int w = 0; w < 4; ++w)
-        printf("%s\"wave%d\": [%llu, %llu, %llu]", w ? ", " : "", w, (unsigned long long)(t[w][1] - t[w][0]),
-               (unsigned long long)(t[w][2] - t[w][0]), (unsigned long long)(t[w][3] - t[w][0]));
+        printf("%s\"wave%d\": [%llu, %llu, %llu, %llu]", w ? ", " : "", w, (unsigned long long)(t[w][1] - t[w][0]),
+               (unsigned long long)(t[w][2] - t[w][0]), (unsigned long long)(t[w][3] - t[w][0]),
+               (unsigned long long)(t[w][5] > t[w][0] ? t[w][5] - t[w][0] : 0));
     printf("}, \"wave0_end\": %llu, \"probes\": \"waves 0/1: table built, chain done, after the barrier; waves 2/3: "
-           "hash/e/addr done, comb half done, after the barrier; wave0_end: verdict written\"}\n",
+           "hash/e/addr done, comb half done, after the barrier, low-window chain (+ s G sum) done; wave0_end: verdict written\"}\n",
            (unsigned long long)(t[0][4] - t[0][0]));
     return 0;
 }

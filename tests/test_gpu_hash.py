@@ -162,7 +162,8 @@ def test_merkle_bytes_layout_vs_oracle(gpu, oracle, hasher):
 def test_merkle_one_launch_path_trees(gpu, oracle):
     """The one-launch Keccak path (merkle_fused_kernel: waves publish their subtree roots and the wave that
     completes a group hashes the parent) over widths 2..64 and sizes around its wave boundaries
-    (S = width^a level-1 nodes per wave): every entry of the output vector."""
+    (S = width^a level-1 nodes per wave): every entry of the output vector.  (Widths 2..4 take the
+    four-wave kernel by default, test_merkle_four_wave_climb_trees.)"""
     rng = np.random.default_rng(77)
     H = gpu.Keccak256()
     for width in (2, 3, 4, 5, 7, 16, 17, 31, 32, 33, 64):
@@ -170,6 +171,28 @@ def test_merkle_one_launch_path_trees(gpu, oracle):
         while S * width <= 32:
             S *= width
         for n in sorted({1, 2, width, width + 1, S * width, S * width + 1, 3 * S * width - 1, 40 * S * width + 5}):
+            leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+            got = gpu.Merkle(H, width).generate_merkle([leaves[i].tobytes() for i in range(n)])
+            _, want = oracle.merkle(0, width, leaves, want_tree=True)
+            assert got == [want[i].tobytes() for i in range(want.shape[0])], (width, n)
+
+
+def test_merkle_four_wave_climb_trees(gpu, oracle):
+    """The four-wave one-launch Keccak path for narrow trees (hash_kernels.hip merkle_climb_kernel: B =
+    width^kin <= 256 level-1 nodes per workgroup, then climb steps of g levels) over widths 2..4 and sizes
+    around its workgroup and climb-group boundaries, up to more workgroups than CUs (the throughput
+    schedule): every entry of the output vector."""
+    rng = np.random.default_rng(78)
+    H = gpu.Keccak256()
+    for width in (2, 3, 4):
+        B = 1
+        while B * width <= 256:
+            B *= width
+        G = 1
+        while G <= 8:
+            G *= width  # width^g children per climb step
+        for n in sorted({1, 2, 3, width, width + 1, B * width, B * width + 1, G * B * width, G * B * width + 1,
+                         3 * G * B * width - 1, 300 * B * width + 7}):
             leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
             got = gpu.Merkle(H, width).generate_merkle([leaves[i].tobytes() for i in range(n)])
             _, want = oracle.merkle(0, width, leaves, want_tree=True)
