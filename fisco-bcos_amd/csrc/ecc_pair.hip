@@ -824,6 +824,8 @@ __device__ uint64_t g_sm2_t[4][8];
     do {         \
     } while (0)
 #endif
+// low Booth windows of t P per tx run by waves 2 and 3 (sm2_low_chain)
+static constexpr int kSm2TrioSplit = 38;
 struct Sm2Trio26Lds {
     uint32_t tab[8][20][64];         // affine 1P..8P in the R' domain as fp26 limbs: [entry][x, y][tx]
     uint32_t jtab[8][50][40];        // Jacobian 1P..8P: [entry][X, Y, Z, Z^2, Z^3][tx]
@@ -991,9 +993,10 @@ __device__ __forceinline__ void sm2_low_chain(Sm2Trio26Lds& L, int wave, int lan
     if (T.r0 && real) pair26_store_jac(L.bacc, J, tl);
 }
 
-template <class IO>
+template <class IO, int SPLIT>
 __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab,
-                                                                        int affine, int split) {
+                                                                        int affine) {
+    constexpr int split = SPLIT;  // a compile-time bound: the chain loop's code is allocation-sensitive
     constexpr int TPW = 40;
     __shared__ Sm2Trio26Lds L;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1094,8 +1097,16 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
                 trio_add_digit_sm2_jd(acc, D, L, tl, d, T);  // five
         }
         // the high windows' sum times 2^(4 split): the low windows run on waves 2 and 3
+        if constexpr (split > 0) {  // (four doublings per iteration, as in a window: one per iteration
+                                    // measured 5.2k cycles each against 4.3k inside the window loop)
 #pragma unroll 1
-        for (int j = 4 * split; j > 0; --j) trio_dbl_sm2_d(acc, D, T);
+            for (int j = split; j > 0; --j) {
+                trio_dbl_sm2_d(acc, D, T);
+                trio_dbl_sm2_d(acc, D, T);
+                trio_dbl_sm2_d(acc, D, T);
+                trio_dbl_sm2_d(acc, D, T);
+            }
+        }
         JacP26 J;
         trio_to_jac_sm2(J, acc, T);
         if (T.r0 && real) pair26_store_jac(L.acc, J, tl);
@@ -1195,10 +1206,12 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             pair26_load_jac(G1, L.gh, lane);
             CurveSM2x::add(G, G0, G1);
             pair26_store_jac(L.g, G, lane);
-            if (split > 0) {
+            if constexpr (split > 0) {
                 // the low windows of txs 0..19 (the affine table is complete: wave 3 built it before its
                 // comb half, whose result was awaited above), then s G + that sum for all 40 txs
+                SM2_T(6);
                 sm2_low_chain(L, wave, lane, split);
+                SM2_T(7);
                 while (__hip_atomic_load(&L.seq[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
                     __builtin_amdgcn_s_sleep(1);
                 }
@@ -1266,8 +1279,10 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             SM2_T(2);
             pair26_store_jac(L.gh, G1, lane);
             __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (split > 0) {  // the low windows of txs 20..39
+            if constexpr (split > 0) {  // the low windows of txs 20..39
+                SM2_T(6);
                 sm2_low_chain(L, wave, lane, split);
+                SM2_T(7);
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 if (lane == 0) __hip_atomic_store(&L.seq[4], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
@@ -1306,14 +1321,14 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
     }
 }
 
-// low Booth windows of t P run by waves 2 and 3 (sm2_low_chain); BCOSGPU_SM2_SPLIT overrides (0 = all
-// 64 windows on waves 0 and 1, the round-3 schedule), clamped to [0, 63]
-static constexpr int kSm2TrioSplit = 38;
+// low Booth windows of t P run by waves 2 and 3 (sm2_low_chain): 38 balances the two wave pairs in
+// the phase probe (profiles/r04_sm2_split_sweep.log) and measured best of 30 / 34 / 38 in the library
+// (tools/sm2_split_sweep.py); BCOSGPU_SM2_SPLIT=0 (read once) runs all 64 windows on waves 0 and 1,
+// the round-3 schedule (A/B and tests)
 static int sm2_trio_split() {
     static const int v = [] {
         const char* e = getenv("BCOSGPU_SM2_SPLIT");
-        const int x = e ? atoi(e) : kSm2TrioSplit;
-        return x < 0 ? 0 : x > 63 ? 63 : x;
+        return e ? atoi(e) : kSm2TrioSplit;
     }();
     return v;
 }
@@ -1329,8 +1344,12 @@ int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n,
             // BCOSGPU_SM2_JAC_ONLY=1 (tests): every window adds the Jacobian entry (the affine table unused)
             const char* jo = getenv("BCOSGPU_SM2_JAC_ONLY");
             const int affine = jo && atoi(jo) != 0 ? 0 : 1;
-            hipLaunchKernelGGL(tx_verify_sm2_trio26_kernel<IO>, dim3(static_cast<unsigned>((n + 39) / 40)), dim3(256), 0,
-                               st, io, n, t26, affine, sm2_trio_split());
+            const dim3 g(static_cast<unsigned>((n + 39) / 40));
+            const int sp = sm2_trio_split();
+            if (sp == 0)
+                hipLaunchKernelGGL((tx_verify_sm2_trio26_kernel<IO, 0>), g, dim3(256), 0, st, io, n, t26, affine);
+            else
+                hipLaunchKernelGGL((tx_verify_sm2_trio26_kernel<IO, kSm2TrioSplit>), g, dim3(256), 0, st, io, n, t26, affine);
         }
         else
             hipLaunchKernelGGL(tx_verify_sm2_pair26_kernel<IO>, grid, dim3(256), 0, st, io, n, t26);

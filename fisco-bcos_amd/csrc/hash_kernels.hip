@@ -182,28 +182,30 @@ __device__ __forceinline__ void pair_level_pass(const KeccakPair& kp, const uint
 // else one lane per node.
 enum LevelMode : int { kOneLane = 0, kPair = 1, kCoop = 2 };
 template <int H>
-__device__ __forceinline__ int level_mode(uint64_t nout, uint32_t threads, int pair, uint32_t coop_max = ~0u) {
+__device__ __forceinline__ int level_mode(uint64_t nout, uint32_t threads, int pair, uint32_t coop_max = ~0u,
+                                          uint32_t pair_max = ~0u) {
     if (H != KECCAK256) return kOneLane;
     if (nout <= threads / 32 && nout <= coop_max) return kCoop;
-    if (pair && 2 * nout <= threads) return kPair;
+    if (pair && 2 * nout <= threads && nout <= pair_max) return kPair;
     return kOneLane;
 }
 
 // The workgroup's levels: its B level-1 nodes from the leaves, then every level whose groups lie inside
 // it, through LDS (levels of at most coop_max nodes per full workgroup on 25-lane groups); returns the
-// LDS buffer of the last level (whose first node is the workgroup's node `base` of that level).
+// LDS buffer of the last level (whose first node is the workgroup's node `base` of that level).  Levels of
+// more than pair_max nodes per full workgroup stay one lane per node.
 // `pair`: level 1 (from the leaves) and the LDS levels may run on lane pairs (the host sets it when
 // the tree's level 1 leaves most of the GPU idle; a throughput-sized level 1 stays one lane per node,
 // which costs fewer instructions per node)
 template <int H, int W>
 __device__ __forceinline__ int wg_levels(uint4 (*lds)[256][2], const uint8_t* __restrict__ leaves, uint64_t n,
                                          uint32_t width, int kin, int B, uint8_t* __restrict__ tree, const TreeLevels& t,
-                                         int pair, uint32_t coop_max, uint64_t& base) {
+                                         int pair, uint32_t coop_max, uint32_t pair_max, uint64_t& base) {
     const uint32_t tid = threadIdx.x;
     base = static_cast<uint64_t>(blockIdx.x) * B;  // first level-1 node of this workgroup
     uint32_t nodes = static_cast<uint32_t>(t.cnt[0] - base < static_cast<uint64_t>(B) ? t.cnt[0] - base : B);
     uint32_t d[8];
-    if (level_mode<H>(B, blockDim.x, pair) == kPair) {
+    if (level_mode<H>(B, blockDim.x, pair, ~0u, pair_max) == kPair) {
         const KeccakPair kp;
         pair_level_pass(kp, leaves + 32ull * base * width, n - base * width, width, tid >> 1, nodes,
                         tree + 32ull * (t.pos[0] + 1 + base), reinterpret_cast<uint8_t*>(&lds[0][0][0]));
@@ -222,7 +224,7 @@ __device__ __forceinline__ int wg_levels(uint4 (*lds)[256][2], const uint8_t* __
         const uint32_t nn = (nodes + width - 1) / width;
         const uint8_t* in = reinterpret_cast<const uint8_t*>(&lds[cur][0][0]);
         // (the mode is decided on the full group count B / width^l so every workgroup runs alike)
-        const int mode = level_mode<H>((B + width - 1) / width, blockDim.x, pair, coop_max);
+        const int mode = level_mode<H>((B + width - 1) / width, blockDim.x, pair, coop_max, pair_max);
         if (mode == kCoop) {  // latency-bound level: 25 lanes per node
             const KeccakCoop kc;
             const uint32_t g = tid / 32;
@@ -253,7 +255,8 @@ __global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restric
     __shared__ uint4 lds[2][256][2];
     const uint32_t tid = threadIdx.x;
     uint64_t base;
-    const int cur = wg_levels<H, W>(lds, leaves, n, W ? W : static_cast<uint32_t>(w), kin, B, tree, t, pair, ~0u, base);
+    const int cur = wg_levels<H, W>(lds, leaves, n, W ? W : static_cast<uint32_t>(w), kin, B, tree, t, pair, ~0u, ~0u,
+                                    base);
     const int top = kin + 1 < t.nlev ? kin + 1 : t.nlev;
     if (blockIdx.x == 0 && tid < static_cast<uint32_t>(t.nlev)) {  // count records (Merkle.h:189-204)
         uint32_t* e = reinterpret_cast<uint32_t*>(tree + 32ull * t.pos[tid]);
@@ -601,8 +604,9 @@ struct ClimbTree {
     uint32_t ctr_off[64];  // first arrival counter of level l (the top level of a climb step)
     int kin;               // levels above level 1 inside a workgroup (B = width^kin)
     int B;
-    int g;                 // levels per climb step: width^(g - 1) <= 8 first-level nodes
+    int g;                 // levels per climb step: width^(g - 1) <= 8 first-level nodes (SM3: <= 64)
     uint32_t coop_max;     // in-workgroup levels of at most this many nodes run on 25-lane groups
+    uint32_t pair_max;     // ... of at most this many (and more than coop_max) on lane pairs, else one lane
     int pair;
 };
 
@@ -622,7 +626,7 @@ __global__ __launch_bounds__(256) void merkle_climb_kernel(const uint8_t* __rest
         for (int k = 1; k < 8; ++k) e[k] = 0;
     }
     uint64_t j;  // this workgroup's node at level l - 1 (LDS buffer cur, entry 0)
-    int cur = wg_levels<H, W>(lds, leaves, n, width, f.kin, f.B, tree, t, f.pair, f.coop_max, j);
+    int cur = wg_levels<H, W>(lds, leaves, n, width, f.kin, f.B, tree, t, f.pair, f.coop_max, f.pair_max, j);
     int l = f.kin + 1 < t.nlev ? f.kin + 1 : t.nlev;  // next level to compute
     __syncthreads();
     if (l < t.nlev && tid < 8)  // publish it (device-coherent)
@@ -651,14 +655,22 @@ __global__ __launch_bounds__(256) void merkle_climb_kernel(const uint8_t* __rest
         cur = 0;
         uint32_t nin = kids;
         uint64_t b = first;
-        const KeccakCoop kc;
-        const uint32_t gq = tid / 32;
-        for (int i = 0; i < g; ++i) {  // nn <= 8 nodes per level: one pass of the eight 32-lane groups
+        for (int i = 0; i < g; ++i) {
             const uint32_t nn = (nin + width - 1) / width;
             b /= width;
-            coop_level_pass<W>(kc, reinterpret_cast<const uint8_t*>(&lds[cur][0][0]), nin, width, gq, nn,
-                               tree + 32ull * (t.pos[l + i] + 1 + b + gq),
-                               reinterpret_cast<uint8_t*>(&lds[cur ^ 1][gq < 8 ? gq : 0][0]));
+            const uint8_t* in = reinterpret_cast<const uint8_t*>(&lds[cur][0][0]);
+            if constexpr (H == KECCAK256) {  // nn <= 8 nodes per level: one pass of the eight 32-lane groups
+                const KeccakCoop kc;
+                const uint32_t gq = tid / 32;
+                coop_level_pass<W>(kc, in, nin, width, gq, nn, tree + 32ull * (t.pos[l + i] + 1 + b + gq),
+                                   reinterpret_cast<uint8_t*>(&lds[cur ^ 1][gq < 8 ? gq : 0][0]));
+            } else if (tid < nn) {  // SM3: one lane per node (nn <= 64)
+                uint32_t d[8];
+                const uint32_t c = nin - tid * width < width ? nin - tid * width : width;
+                hash_nodes<H>(in + 32u * tid * width, c, d);
+                store_digest(H, tree + 32ull * (t.pos[l + i] + 1 + b + tid), d);
+                store_digest(H, reinterpret_cast<uint8_t*>(&lds[cur ^ 1][tid][0]), d);
+            }
             cur ^= 1;
             nin = nn;
             __syncthreads();
@@ -672,30 +684,84 @@ __global__ __launch_bounds__(256) void merkle_climb_kernel(const uint8_t* __rest
         reinterpret_cast<uint32_t*>(root)[tid] = reinterpret_cast<const uint32_t*>(&lds[cur][0][0])[tid];
 }
 
-static constexpr uint64_t kClimbMaxWgs = 4096;
-static constexpr int kClimbMaxWidth = 4;  // widths the four-wave path takes by default (wider: the one-wave one)  // level-1 workgroups up to which the four-wave path runs
+// Throughput-sized narrow trees (more climb workgroups than CUs): the bottom k + 1 levels first, one
+// thread per level-k node hashing its whole subtree (width^k + ... + 1 nodes, one lane each, no LDS, no
+// barriers: the fewest instructions per node), then the climb kernel on level k as its leaves, with k
+// the smallest that leaves it one workgroup per CU (1M leaves, width 2: k = 2, 245 workgroups).
+template <int H, int W>
+__global__ __launch_bounds__(256) void merkle_subtree_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w,
+                                                             uint8_t* __restrict__ tree, const TreeLevels t, int k) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t width = W ? W : static_cast<uint64_t>(w);
+    if (blockIdx.x == 0 && threadIdx.x <= static_cast<uint32_t>(k)) {  // count records of levels 0..k
+        uint32_t* e = reinterpret_cast<uint32_t*>(tree + 32ull * t.pos[threadIdx.x]);
+        e[0] = bswap32(static_cast<uint32_t>(t.cnt[threadIdx.x]));
+#pragma unroll
+        for (int q = 1; q < 8; ++q) e[q] = 0;
+    }
+    if (i >= t.cnt[k]) return;
+    uint64_t span = 1;  // level-l nodes under one level-k node
+    for (int l = 0; l < k; ++l) span *= width;
+    for (int l = 0; l <= k; ++l) {
+        const uint8_t* in = l == 0 ? leaves : tree + 32ull * (t.pos[l - 1] + 1);
+        const uint64_t nin = l == 0 ? n : t.cnt[l - 1];
+        const uint64_t lo = i * span, hi = (i + 1) * span < t.cnt[l] ? (i + 1) * span : t.cnt[l];
+        for (uint64_t j = lo; j < hi; ++j) {  // (this thread's own stores of level l - 1 precede these reads)
+            const uint64_t first = j * width;
+            const uint32_t c = static_cast<uint32_t>(nin - first < width ? nin - first : width);
+            uint32_t d[8];
+            hash_nodes<H>(in + 32ull * first, c, d);
+            store_digest(H, tree + 32ull * (t.pos[l] + 1 + j), d);
+        }
+        span /= width;
+    }
+}
 
-// returns 1 when it does not apply (not Keccak, too wide, too many counters or workgroups, no slot)
+static constexpr uint64_t kClimbMaxWgs = 4096;  // level-1 workgroups up to which the four-wave path runs
+static constexpr int kClimbMaxWidth = 4;  // widths the four-wave path takes by default (wider: the one-wave one)
+
+// returns 1 when it does not apply (too many counters or workgroups, no counter slot)
 static int launch_merkle_climb(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
-                               uint8_t* d_root, const TreeLevels& t, hipStream_t st) {
-    if (hasher != KECCAK256) return 1;
+                               uint8_t* d_root, const TreeLevels& t0, hipStream_t st) {
     ClimbTree f{};
-    f.t = t;
     f.B = 1;
     f.kin = 0;
     while (f.B * width <= 256) {
         f.B *= width;
         ++f.kin;
     }
+    // more workgroups than CUs: the subtree kernel first for levels 0..k (width^k <= 64 level-0 nodes per
+    // thread), so that the climb kernel starts with one workgroup per CU
+    const uint64_t cus = static_cast<uint64_t>(cu_count());
+    int k = -1;
+    if ((t0.cnt[0] + f.B - 1) / f.B > cus) {
+        uint64_t span = 1;
+        for (int q = 0; q + 2 < t0.nlev && span <= 64; ++q, span *= width)
+            if ((t0.cnt[q + 1] + f.B - 1) / f.B <= cus) {
+                k = q;
+                break;
+            }
+    }
+    TreeLevels t = t0;  // the climb kernel's levels: those above level k, whose nodes are its leaves
+    if (k >= 0) {
+        t.nlev = t0.nlev - (k + 1);
+        for (int l = 0; l < t.nlev; ++l) {
+            t.pos[l] = t0.pos[l + k + 1];
+            t.cnt[l] = t0.cnt[l + k + 1];
+        }
+    }
+    f.t = t;
     f.g = 1;
-    for (int q = width; q <= 8; q *= width) ++f.g;  // width^(g - 1) <= 8
+    for (int q = width; q <= (hasher == KECCAK256 ? 8 : 64); q *= width) ++f.g;  // width^(g - 1) <= 8 (64)
     const uint64_t wgs = (t.cnt[0] + f.B - 1) / f.B;
     if (wgs > kClimbMaxWgs) return 1;
-    // one workgroup per CU: the latency schedule (25-lane groups from eight nodes down, lane pairs above);
-    // more: every SIMD runs several waves, so the levels take the schedule with the fewest instructions
-    // per node (lane pairs down to two nodes)
+    // one workgroup per CU: the latency schedule (25-lane groups from eight nodes down, lane pairs above,
+    // one lane per node only for level 1's 256); more: every SIMD runs several waves, so each level takes
+    // the fewest wave-cycles -- one lane per node (a wave pass of 64 nodes: 22k cycles) down to 64 nodes,
+    // lane pairs (32 nodes: 15k) down to 4, 25-lane groups (2 nodes: 9.4k) below
     const bool latency = wgs <= static_cast<uint64_t>(cu_count());
     f.coop_max = latency ? 8u : 2u;
+    f.pair_max = latency ? 128u : 32u;
     f.pair = 1;
     uint32_t off = 0;
     for (int l = 0; l < t.nlev; ++l) {
@@ -705,9 +771,25 @@ static int launch_merkle_climb(int hasher, int width, const uint8_t* d_leaves, u
     if (off > kFusedCounters) return 1;
     uint32_t* ctr = fused_counter_slot(st);
     if (!ctr) return 1;
+    if (k >= 0) {
+        const dim3 gs(grid_for(t0.cnt[k], 256)), bs(256);
+#define SUB(HH, WW) hipLaunchKernelGGL((merkle_subtree_kernel<HH, WW>), gs, bs, 0, st, d_leaves, n, width, d_tree, t0, k)
+        if (hasher == SM3) {
+            if (width == 2) SUB(SM3, 2); else if (width == 16) SUB(SM3, 16); else SUB(SM3, 0);
+        } else {
+            if (width == 2) SUB(KECCAK256, 2); else if (width == 16) SUB(KECCAK256, 16); else SUB(KECCAK256, 0);
+        }
+#undef SUB
+        d_leaves = d_tree + 32ull * (t0.pos[k] + 1);
+        n = t0.cnt[k];
+    }
     const dim3 g(static_cast<unsigned>(wgs)), b(256);
-#define CLIMB(WW) hipLaunchKernelGGL((merkle_climb_kernel<KECCAK256, WW>), g, b, 0, st, d_leaves, n, width, d_tree, f, d_root, ctr)
-    if (width == 2) CLIMB(2); else if (width == 16) CLIMB(16); else CLIMB(0);
+#define CLIMB(HH, WW) hipLaunchKernelGGL((merkle_climb_kernel<HH, WW>), g, b, 0, st, d_leaves, n, width, d_tree, f, d_root, ctr)
+    if (hasher == SM3) {
+        if (width == 2) CLIMB(SM3, 2); else if (width == 16) CLIMB(SM3, 16); else CLIMB(SM3, 0);
+    } else {
+        if (width == 2) CLIMB(KECCAK256, 2); else if (width == 16) CLIMB(KECCAK256, 16); else CLIMB(KECCAK256, 0);
+    }
 #undef CLIMB
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
@@ -752,7 +834,11 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
         const char* e = getenv("BCOSGPU_MERKLE_CLIMB");
         return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
     }();
-    if (fused_env != 1 && (climb_env == 1 || (climb_env < 0 && width <= kClimbMaxWidth))) {
+    // (SM3 only for throughput-sized trees, where the subtree kernel runs first: at latency sizes its
+    // one-lane levels measured no faster than the two-launch path, profiles/r04_merkle_paths_ab_sm3.json)
+    const bool climb_sm3 = t.cnt[0] > 256ull * static_cast<uint64_t>(cu_count());
+    if (fused_env != 1 &&
+        (climb_env == 1 || (climb_env < 0 && width <= kClimbMaxWidth && (hasher == KECCAK256 || climb_sm3)))) {
         const int rc = launch_merkle_climb(hasher, width, d_leaves, n, d_tree, d_root, t, st);
         if (rc <= 0) return rc;
     }

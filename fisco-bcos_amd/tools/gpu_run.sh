@@ -9,6 +9,7 @@
 #   profile=WL[,WL...]   rocprofv3 kernel trace + PMC passes per workload (tools/gpu_profile_all.sh)
 #   sweep[=ARGS]         tools/small_sweep.py (ARGS with ',' for ' ')
 #   exe=PATH[,ARGS]      run a built tool from fisco-bcos_amd/lib (ARGS with ',' for ' ')
+#   py=NAME[,ARGS]       run fisco-bcos_amd/tools/NAME.py (ARGS with ',' for ' '), stdout to gpurun_out/NAME_<step>.json
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -35,6 +36,8 @@ for step in "$@"; do
       timeout -k 10 900 python3 -u fisco-bcos_amd/tools/small_sweep.py ${arg//,/ } > gpurun_out/sweep_${n}.json 2> $log ;;
     exe)
       a=${arg//,/ }; timeout -k 10 300 fisco-bcos_amd/lib/$a > $log 2>&1 ;;
+    py)
+      a=${arg//,/ }; timeout -k 10 900 python3 -u fisco-bcos_amd/tools/$a > gpurun_out/${arg%%,*}_${n}.json 2> $log ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -40,20 +40,19 @@ def main():
         notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", f.name], capture_output=True,
                                text=True).stdout
         os.unlink(f.name)
-        cur = {}
+        recs, cur = [], None
         for line in notes.splitlines():
-            m = re.match(r"\s+\.(name|vgpr_count|agpr_count|vgpr_spill_count|sgpr_spill_count|"
+            if re.match(r"^  - \.", line):  # a kernel's record (its fields at 4 spaces, in any order)
+                cur = {}
+                recs.append(cur)
+                line = "    " + line[4:]
+            m = re.match(r"^    \.(name|vgpr_count|agpr_count|vgpr_spill_count|sgpr_spill_count|"
                          r"private_segment_fixed_size|sgpr_count|group_segment_fixed_size):\s+(\S+)", line)
-            if m:
-                k, v = m.groups()
-                if k == "name" and not v.endswith(".kd"):
-                    if cur.get("name") and filt in cur["name"]:
-                        print(cur)
-                    cur = {"name": v}
-                elif k != "name":
-                    cur[k] = v
-        if cur.get("name") and filt in cur["name"]:
-            print(cur)
+            if m and cur is not None:
+                cur[m.group(1)] = m.group(2)
+        for r in recs:
+            if r.get("name") and not r["name"].endswith(".kd") and filt in r["name"]:
+                print(dict(sorted(r.items(), key=lambda kv: kv[0] != "name")))
 
 
 if __name__ == "__main__":

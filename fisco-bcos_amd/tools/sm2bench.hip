@@ -1,6 +1,6 @@
 // sm2bench.hip -- phase timestamps (s_memtime cycles) of tx_verify_sm2_trio26_kernel's workgroup 0 on a
 // 10k-tx batch of random inputs (the schedule is input-independent), to see where c2sm2's latency goes.
-//   sm2bench [REPS [SYNTH_DIR | - [SPLIT]]]
+//   sm2bench [REPS [SYNTH_DIR | - [SPLIT]]]   (SPLIT in 0, 28, 30, 32, 34, 36, 38)
 #define BCOSGPU_SM2_TIMING 1
 #include "../csrc/ecc_tables.hip"
 #ifdef SM2BENCH_PAIR_SRC  // A/B builds: another revision of ecc_pair.hip, whose kernel takes no 'affine' flag
@@ -8,7 +8,11 @@
 #define SM2_AFFINE_ARG
 #else
 #include "../csrc/ecc_pair.hip"
-#define SM2_AFFINE_ARG , 1, split
+#define SM2_AFFINE_ARG , 1
+#define SM2_SPLIT_ARG(S) , S
+#endif
+#ifndef SM2_SPLIT_ARG
+#define SM2_SPLIT_ARG(S)
 #endif
 #include <cstdio>
 #include <cstdlib>
@@ -62,7 +66,13 @@ int main(int argc, char** argv) {
     // reps back-to-back launches (the clock settles under load); the mean over the last half is reported
     for (int rep = 0; rep < reps; ++rep) {
         if (rep == reps / 2) hipEventRecord(e0);
-        hipLaunchKernelGGL(tx_verify_sm2_trio26_kernel<TxIO>, dim3((n + 39) / 40), dim3(256), 0, 0, io, n, t26 SM2_AFFINE_ARG);
+        switch (split) {  // the split is a template parameter of the kernel: the instantiations swept here
+#define SM2_CASE(S) \
+    case S: hipLaunchKernelGGL((tx_verify_sm2_trio26_kernel<TxIO SM2_SPLIT_ARG(S)>), dim3((n + 39) / 40), dim3(256), 0, 0, io, n, t26 SM2_AFFINE_ARG); break;
+            SM2_CASE(0) SM2_CASE(28) SM2_CASE(30) SM2_CASE(32) SM2_CASE(34) SM2_CASE(36) SM2_CASE(38)
+#undef SM2_CASE
+            default: printf("split %d not instantiated\n", split); return 1;
+        }
         if (rep % 64 == 63) hipDeviceSynchronize();
     }
     hipEventRecord(e1);
@@ -73,11 +83,13 @@ int main(int argc, char** argv) {
     hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sm2_t), sizeof(t));
     printf("{\"split\": %d, \"kernel_ms\": %.4f, \"cycles_since_start\": {", split, ms);
     for (int w = 0; w < 4; ++w)
-        printf("%s\"wave%d\": [%llu, %llu, %llu, %llu]", w ? ", " : "", w, (unsigned long long)(t[w][1] - t[w][0]),
-               (unsigned long long)(t[w][2] - t[w][0]), (unsigned long long)(t[w][3] - t[w][0]),
-               (unsigned long long)(t[w][5] > t[w][0] ? t[w][5] - t[w][0] : 0));
+        printf("%s\"wave%d\": [%llu, %llu, %llu, %llu, %llu, %llu]", w ? ", " : "", w,
+               (unsigned long long)(t[w][1] - t[w][0]), (unsigned long long)(t[w][2] - t[w][0]),
+               (unsigned long long)(t[w][3] - t[w][0]), (unsigned long long)(t[w][5] > t[w][0] ? t[w][5] - t[w][0] : 0),
+               (unsigned long long)(t[w][6] > t[w][0] ? t[w][6] - t[w][0] : 0),
+               (unsigned long long)(t[w][7] > t[w][0] ? t[w][7] - t[w][0] : 0));
     printf("}, \"wave0_end\": %llu, \"probes\": \"waves 0/1: table built, chain done, after the barrier; waves 2/3: "
-           "hash/e/addr done, comb half done, after the barrier, low-window chain (+ s G sum) done; wave0_end: verdict written\"}\n",
+           "hash/e/addr done, comb half done, after the barrier, all done, low-window chain start, its end; wave0_end: verdict written\"}\n",
            (unsigned long long)(t[0][4] - t[0][0]));
     return 0;
 }
