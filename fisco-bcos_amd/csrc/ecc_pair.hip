@@ -815,17 +815,17 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_pair26_kernel(IO io, uin
 // |K| >= 16 before each addition of |d| P, |d| <= 8, and |K| < n, so K = +-d (mod n) cannot occur for
 // a P of order n (SM2's cofactor is 1; a P off the curve fails its verdict).  Bit-identical to
 // tx_verify_kernel<1, *>.
-#ifdef BCOSGPU_SM2_TIMING  // tools/sm2bench.hip: phase timestamps of workgroup 0
+// Phase stamps of workgroup 0 (s_memtime; tools/sm2bench.hip reads them): always compiled in.  The
+// chain loops' register allocation is fragile at ~320 VGPRs, and the product kernel is the one the
+// probe measures only if both carry the same stamps (a few scalar-guarded stores per wave).
 __device__ uint64_t g_sm2_t[4][8];
 #define SM2_T(k) \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_sm2_t[threadIdx.x >> 6][k] = clock64()
-#else
-#define SM2_T(k) \
-    do {         \
-    } while (0)
-#endif
 // low Booth windows of t P per tx run by waves 2 and 3 (sm2_low_chain)
 static constexpr int kSm2TrioSplit = 38;
+#ifndef kSm2DblUnroll
+#define kSm2DblUnroll 1  // doublings per window unrolled in the chain loops (1 = rolled)
+#endif
 struct Sm2Trio26Lds {
     uint32_t tab[8][20][64];         // affine 1P..8P in the R' domain as fp26 limbs: [entry][x, y][tx]
     uint32_t jtab[8][50][40];        // Jacobian 1P..8P: [entry][X, Y, Z, Z^2, Z^3][tx]
@@ -978,10 +978,8 @@ __device__ __forceinline__ void sm2_low_chain(Sm2Trio26Lds& L, int wave, int lan
     }
 #pragma unroll 1
     for (int w = split - 2; w >= 0; --w) {
-        trio_dbl_sm2_d(acc, D, T);
-        trio_dbl_sm2_d(acc, D, T);
-        trio_dbl_sm2_d(acc, D, T);
-        trio_dbl_sm2_d(acc, D, T);
+#pragma unroll kSm2DblUnroll
+        for (int q = 0; q < 4; ++q) trio_dbl_sm2_d(acc, D, T);
         const uint32_t top = k.v[7];
         const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
         const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
@@ -1075,10 +1073,10 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
         bool aff = false;  // wave-uniform: the affine table (wave 3) is ready
 #pragma unroll 1
         for (int w = 63; w >= split; --w) {
-            trio_dbl_sm2_d(acc, D, T);  // three product levels each (delta carried)
-            trio_dbl_sm2_d(acc, D, T);
-            trio_dbl_sm2_d(acc, D, T);
-            trio_dbl_sm2_d(acc, D, T);
+            // four doublings, three product levels each (delta carried); rolled: the window's code then
+            // fits the instruction cache far better (kSm2DblRoll)
+#pragma unroll kSm2DblUnroll
+            for (int q = 0; q < 4; ++q) trio_dbl_sm2_d(acc, D, T);
             const uint32_t top = k.v[7];
             const uint32_t W = top >> 28, cb = (top >> 27) & 1u;
             const int d = static_cast<int>(W + cb) - static_cast<int>((W >> 3) << 4);
@@ -1101,10 +1099,8 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
                                     // measured 5.2k cycles each against 4.3k inside the window loop)
 #pragma unroll 1
             for (int j = split; j > 0; --j) {
-                trio_dbl_sm2_d(acc, D, T);
-                trio_dbl_sm2_d(acc, D, T);
-                trio_dbl_sm2_d(acc, D, T);
-                trio_dbl_sm2_d(acc, D, T);
+#pragma unroll kSm2DblUnroll
+                for (int q = 0; q < 4; ++q) trio_dbl_sm2_d(acc, D, T);
             }
         }
         JacP26 J;
