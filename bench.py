@@ -131,8 +131,9 @@ def kernel_source_sha():
 
 def _auto_kernel(suite, n, cus, small_ok=True):
     """Mirror of ecc_txv.hip auto_kernel (rounds x latency): 2 trio, 1 pair, 0 one-lane at occupancy 1,
-    -2 one-lane at occupancy 2 (whose tail round of <= one wave per SIMD costs an occupancy-1 round)."""
-    lat = (3.13, 1.77, 1.15, 1.0) if suite == 1 else (4.13, 2.36, 1.19, 1.0)
+    -2 one-lane at occupancy 2 (whose tail round of <= one wave per SIMD has its own latency)."""
+    lat = (4.315, 2.399, 1.678, 1.0) if suite == 1 else (4.475, 2.643, 1.279, 1.0)
+    occ2_tail = 2.452 if suite == 1 else 2.556
     per = (512 * cus, 256 * cus, 64 * cus, 40 * cus)
     code = (-2, 0, 1, 2)
     best, cost = 0, float("inf")
@@ -140,7 +141,7 @@ def _auto_kernel(suite, n, cus, small_ok=True):
         c = -(-n // per[k]) * lat[k]
         if k == 0:
             tail = n % per[0]
-            c = (n // per[0]) * lat[0] + (0 if tail == 0 else lat[1] if tail <= per[1] else lat[0])
+            c = (n // per[0]) * lat[0] + (0 if tail == 0 else occ2_tail if tail <= per[1] else lat[0])
         if c < cost:
             best, cost = code[k], c
     return best

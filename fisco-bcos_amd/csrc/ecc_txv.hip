@@ -52,27 +52,28 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
 
 // Every kernel runs its batch in rounds of resident workgroups -- the trio kernels take 40 txs per CU,
 // the pair kernels 64, the one-lane kernel 256 at occupancy 1 (one wave per SIMD) and 512 at
-// occupancy 2 -- and a round costs a fixed latency, so a kernel's cost is rounds x latency.  At
-// occupancy 2 a last round that leaves every SIMD with at most one wave costs an occupancy-1 round.
-// The latencies are relative to the trio kernel's round, measured on MI355X (tools/small_sweep.py,
-// profiles/r02_small_sweep.json, profiles/r03_occ_sweep.json): secp256k1 trio 0.415 / pair 0.493 /
-// one-lane 0.99 (occupancy 1) / 1.71 ms (occupancy 2) per round; SM2 0.854 / 0.977 / 1.52 / 2.67 ms.
-// The trio and pair kernels are candidates up to 2^16 txs (beyond that the one-lane kernel's
-// throughput wins at any rounding).  Returns 2 (trio), 1 (pair), 0 (one-lane, occupancy 1) or -2
-// (one-lane, occupancy 2).
+// occupancy 2 -- and a round costs a fixed latency, so a kernel's cost is rounds x latency.  The
+// occupancy-2 kernel's last round, when it leaves every SIMD at most one wave, has its own (shorter)
+// latency.  Latencies relative to the trio kernel's round, fitted from the round-4 sweep on MI355X
+// (tools/small_sweep.py -> tools/fit_auto.py, profiles/r04_small_sweep.json and _fit.json): secp256k1
+// trio 0.379 / pair 0.485 / one-lane 1.00 (occupancy 1) / 1.70 (occupancy 2) / 0.97 ms (its single-wave
+// round); SM2 0.593 / 0.996 / 1.42 / 2.56 / 1.455 ms.  The trio and pair kernels are candidates up to
+// 2^16 txs (beyond that the one-lane kernel's throughput wins at any rounding).  Returns 2 (trio),
+// 1 (pair), 0 (one-lane, occupancy 1) or -2 (one-lane, occupancy 2).
 static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok) {
     const bool sm2 = suite == BCOSGPU_SUITE_SM2;
     //                    occ 2,              occ 1,              pair,               trio
-    const double lat[4] = {sm2 ? 3.13 : 4.13, sm2 ? 1.77 : 2.36, sm2 ? 1.15 : 1.19, 1.0};
+    const double lat[4] = {sm2 ? 4.315 : 4.475, sm2 ? 2.399 : 2.643, sm2 ? 1.678 : 1.279, 1.0};
+    const double occ2_tail = sm2 ? 2.452 : 2.556;  // the occupancy-2 kernel's round of <= one wave per SIMD
     const uint64_t per[4] = {512ull * cus, 256ull * cus, 64ull * cus, 40ull * cus};
     const int code[4] = {-2, 0, 1, 2};
     int best = 0;
     double cost = 1e300;
     for (int k = small_ok ? 3 : 1; k >= 0; --k) {
         double c = static_cast<double>((n + per[k] - 1) / per[k]) * lat[k];
-        if (k == 0) {  // occupancy 2: full rounds, then a tail of at most one wave per SIMD at occupancy-1 cost
+        if (k == 0) {  // occupancy 2: full rounds, then a tail round
             const uint64_t tail = n % per[0];
-            c = static_cast<double>(n / per[0]) * lat[0] + (tail == 0 ? 0.0 : tail <= per[1] ? lat[1] : lat[0]);
+            c = static_cast<double>(n / per[0]) * lat[0] + (tail == 0 ? 0.0 : tail <= per[1] ? occ2_tail : lat[0]);
         }
         if (c < cost) {
             cost = c;

@@ -394,7 +394,8 @@ def test_small_comb_tables_path(gpu):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("suite,n", [(0, 20_480), (0, 196_608), (1, 10_241), (1, 20_480), (1, 196_608)])
+@pytest.mark.parametrize("suite,n", [(0, 10_241), (0, 20_480), (0, 20_481), (0, 196_608), (1, 10_241), (1, 20_480),
+                                     (1, 20_481), (1, 98_304), (1, 196_608)])
 def test_automatic_kernel_choice_within_5_percent(gpu, suite, n):
     """The automatic kernel choice (rounds x measured latency, ecc_txv.hip auto_kernel) at the boundary sizes
     of its rule -- one / two trio rounds, the pair / one-lane crossover, the 8-GPU C4 shard size -- is within
