@@ -399,31 +399,38 @@ def test_small_comb_tables_path(gpu):
 def test_automatic_kernel_choice_within_5_percent(gpu, suite, n):
     """The automatic kernel choice (rounds x measured latency, ecc_txv.hip auto_kernel) at the boundary sizes
     of its rule -- one / two trio rounds, the pair / one-lane crossover, the 8-GPU C4 shard size -- is within
-    5 % of the fastest forced variant (lane-trio, pair, one-lane at occupancy 1 and 2): median of 15 launches
-    each, HIP events."""
+    5 % of the fastest forced variant (lane-trio, pair, one-lane at occupancy 1 and 2): after 1 s of
+    warm-up, the faster of two interleaved medians of 15 launches each, HIP events."""
     import torch
     from bcos_gpu import device, synth
     b = synth.make_batch(suite, n, seed=0xA0 + suite)
     th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
     snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
     st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    import time
     variants = {"auto": (-1, 0, 2, 1), "trio": (1, 0, 2, 1), "pair": (1, 0, 1, 1), "occ1": (0, 1, 0, 1),
                 "occ2": (0, 2, 0, 1)}
     times = {}
     try:
-        for name, pol in variants.items():
-            gpu.set_tx_kernel_policy(*pol)
-            for _ in range(5):
-                device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
-            ts = []
-            for _ in range(15):
-                a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record()
-                device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
-                c.record()
-                c.synchronize()
-                ts.append(a.elapsed_time(c))
-            times[name] = sorted(ts)[len(ts) // 2]
+        t0 = time.time()  # the clock settles under load before anything is timed
+        while time.time() - t0 < 1.0:
+            device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
+            torch.cuda.synchronize()
+        for rnd in range(2):  # two interleaved passes; each variant keeps its faster median
+            for name, pol in variants.items():
+                gpu.set_tx_kernel_policy(*pol)
+                for _ in range(5):
+                    device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
+                ts = []
+                for _ in range(15):
+                    a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record()
+                    device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
+                    c.record()
+                    c.synchronize()
+                    ts.append(a.elapsed_time(c))
+                med = sorted(ts)[len(ts) // 2]
+                times[name] = min(times.get(name, med), med)
     finally:
         gpu.set_tx_kernel_policy()
     best = min(v for k, v in times.items() if k != "auto")
