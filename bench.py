@@ -95,7 +95,7 @@ PEAK_ALU_PER_S = 3.7497e13      # full-rate 32-bit VALU (v_alignbit_b32)
 # SURVEY §8d ALU ops per permutation / compression
 KECCAK_F_OPS = 6240
 SM3_C_OPS = 2100
-PMC_GLOB = "r03_pmc_{}.json"
+PMC_GLOB = "r04_pmc_{}.json"
 KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_device.h", "fisco-bcos_amd/csrc/ecc_tables.hip", "fisco-bcos_amd/csrc/ecc_sig.hip",
               "fisco-bcos_amd/csrc/ecc_txv.hip", "fisco-bcos_amd/csrc/ecc_coop.hip", "fisco-bcos_amd/csrc/ecc_pair.hip",
               "fisco-bcos_amd/csrc/fe_asm.h", "fisco-bcos_amd/csrc/fe.h",
@@ -175,7 +175,8 @@ def _kernel_name(suite, n):
         return "tx_verify_coop26_kernel<TxIO>" if f26 else "tx_verify_coop_kernel"
     if suite == 1 and small and coop:
         if f26:
-            return "tx_verify_sm2_trio26_kernel<TxIO>" if coop == 2 else "tx_verify_sm2_pair26_kernel<TxIO>"
+            return ("tx_verify_sm2_trio26_kernel<TxIO,%d>" % SM2_TRIO_SPLIT if coop == 2
+                    else "tx_verify_sm2_pair26_kernel<TxIO>")
         return "tx_verify_sm2_pair_kernel"
     return "tx_verify_kernel<%d,%d,%s,TxIO>" % (suite, occ, "true" if f26 else "false")
 
