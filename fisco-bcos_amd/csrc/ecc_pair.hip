@@ -655,6 +655,52 @@ __device__ __forceinline__ void comb_range_sm2_26(JacP26& acc, const fe& k_plain
     }
 }
 
+// acc = k * G restricted to the BITS-bit comb windows [lo, hi) of an R'-domain table (8-bit: kCombEntries
+// entries per window; 16-bit: kWideEntries), the next window's entry fetched before the current addition
+// (the 16-bit table's gathers come from HBM, not L2)
+template <int BITS>
+__device__ __forceinline__ void comb_range_sm2_26w(JacP26& acc, const fe& k_plain, const uint32_t* __restrict__ tab,
+                                                   int lo, int hi) {
+    constexpr uint32_t E = 1u << BITS, MASK = E - 1u;
+    fe k;
+    fe_copy(k, k_plain);
+    for (int i = 0; i < lo; ++i) shr_bits<BITS>(k);
+    CurveSM2x::set_inf(acc);
+    uint32_t b = k.v[0] & MASK;
+    shr_bits<BITS>(k);
+    const uint4* e = reinterpret_cast<const uint4*>(tab + (static_cast<size_t>(lo) * E + b) * 16);
+    uint4 q0 = e[0], q1 = e[1], q2 = e[2], q3 = e[3];
+#pragma unroll 1
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t bi = b;
+        AffP26 T;
+        {
+            const uint32_t x[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+            const uint32_t y[8] = {q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+            fp26_from_words(T.x, x);
+            fp26_from_words(T.y, y);
+        }
+        const int in = i + 1 < hi ? i + 1 : i;  // last window: a harmless reload
+        b = k.v[0] & MASK;
+        shr_bits<BITS>(k);
+        e = reinterpret_cast<const uint4*>(tab + (static_cast<size_t>(in) * E + b) * 16);
+        q0 = e[0];
+        q1 = e[1];
+        q2 = e[2];
+        q3 = e[3];
+        JacP26 S;
+        CurveSM2x::madd(S, acc, T);
+        CurveSM2x::cmov(acc, S, bi != 0u);
+    }
+}
+// the comb half of wave 2 (half 0) or 3 (half 1): the 16-bit table's 16 windows split 11 / 5 (wave 3
+// builds the affine table first), the 8-bit table's 32 split 16 / 16
+__device__ __forceinline__ void comb_half_sm2_26(JacP26& acc, const fe& k, const uint32_t* __restrict__ tab, int bits,
+                                                 int half) {
+    if (bits == kWideBits) comb_range_sm2_26w<kWideBits>(acc, k, tab, half ? 11 : 0, half ? 16 : 11);
+    else comb_range_sm2_26w<8>(acc, k, tab, half ? 16 : 0, half ? 32 : 16);
+}
+
 __device__ __forceinline__ void pair26_store_jac(uint32_t (*dst)[64], const JacP26& P, int lane) {
     fe X, Y, Z;
     fp26_to_fe(X, P.X);
@@ -993,7 +1039,8 @@ __device__ __forceinline__ void sm2_low_chain(Sm2Trio26Lds& L, int wave, int lan
 
 template <class IO, int SPLIT>
 __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab,
-                                                                        int affine) {
+                                                                        int affine, const uint32_t* __restrict__ ctab,
+                                                                        int cbits) {
     constexpr int split = SPLIT;  // a compile-time bound: the chain loop's code is allocation-sensitive
     constexpr int TPW = 40;
     __shared__ Sm2Trio26Lds L;
@@ -1194,7 +1241,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             for (int k = 0; k < 5; ++k) L.addr[k][lane] = ad[k];
             JacP26 G0, G1, G;
             SM2_T(1);
-            comb_range_sm2_26(G0, s, tab, 0, 16);
+            comb_half_sm2_26(G0, s, ctab, cbits, 0);
             SM2_T(2);
             while (__hip_atomic_load(&L.seq[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
                 __builtin_amdgcn_s_sleep(1);
@@ -1212,9 +1259,10 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
                     __builtin_amdgcn_s_sleep(1);
                 }
                 lds_wave_sync();
-                JacP26 B;
+                JacP26 B, S;  // (s G reloaded from LDS: kept in registers it cost the chain 3.4k cycles a window)
+                pair26_load_jac(S, L.g, lane);
                 pair26_load_jac(B, L.bacc, lane);
-                CurveSM2x::add(G, G, B);
+                CurveSM2x::add(G, S, B);
                 pair26_store_jac(L.g, G, lane);
             }
             SM2_T(5);
@@ -1271,7 +1319,7 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             if (lane == 0) __hip_atomic_store(&L.seq[3], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             JacP26 G1;
             SM2_T(1);
-            comb_range_sm2_26(G1, s, tab, 16, 32);
+            comb_half_sm2_26(G1, s, ctab, cbits, 1);
             SM2_T(2);
             pair26_store_jac(L.gh, G1, lane);
             __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1340,12 +1388,22 @@ int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n,
             // BCOSGPU_SM2_JAC_ONLY=1 (tests): every window adds the Jacobian entry (the affine table unused)
             const char* jo = getenv("BCOSGPU_SM2_JAC_ONLY");
             const int affine = jo && atoi(jo) != 0 ? 0 : 1;
+            // s G on the 16-bit comb when the wide R'-domain table exists (half the comb windows on waves
+            // 2 and 3, so their low-window chains start earlier)
+            const uint32_t* ctab = t26;
+            int cbits = 8;
+            if (tables_sm2_26(&ctab, &cbits)) {
+                ctab = t26;
+                cbits = 8;
+            }
             const dim3 g(static_cast<unsigned>((n + 39) / 40));
             const int sp = sm2_trio_split();
             if (sp == 0)
-                hipLaunchKernelGGL((tx_verify_sm2_trio26_kernel<IO, 0>), g, dim3(256), 0, st, io, n, t26, affine);
+                hipLaunchKernelGGL((tx_verify_sm2_trio26_kernel<IO, 0>), g, dim3(256), 0, st, io, n, t26, affine, ctab,
+                                   cbits);
             else
-                hipLaunchKernelGGL((tx_verify_sm2_trio26_kernel<IO, kSm2TrioSplit>), g, dim3(256), 0, st, io, n, t26, affine);
+                hipLaunchKernelGGL((tx_verify_sm2_trio26_kernel<IO, kSm2TrioSplit>), g, dim3(256), 0, st, io, n, t26,
+                                   affine, ctab, cbits);
         }
         else
             hipLaunchKernelGGL(tx_verify_sm2_pair26_kernel<IO>, grid, dim3(256), 0, st, io, n, t26);

@@ -9,6 +9,7 @@
 #   profile=WL[,WL...]   rocprofv3 kernel trace + PMC passes per workload (tools/gpu_profile_all.sh)
 #   sweep[=ARGS]         tools/small_sweep.py (ARGS with ',' for ' ')
 #   exe=PATH[,ARGS]      run a built tool from fisco-bcos_amd/lib (ARGS with ',' for ' ')
+#   ab=NAME[,ARGS]       bench.py ARGS with lib_ab/NAME/libbcosgpu.so swapped in (tools/build_ab.sh), then restored
 #   py=NAME[,ARGS]       run fisco-bcos_amd/tools/NAME.py (ARGS with ',' for ' '), stdout to gpurun_out/NAME_<step>.json
 set -o pipefail
 mkdir -p gpurun_out
@@ -36,6 +37,11 @@ for step in "$@"; do
       timeout -k 10 900 python3 -u fisco-bcos_amd/tools/small_sweep.py ${arg//,/ } > gpurun_out/sweep_${n}.json 2> $log ;;
     exe)
       a=${arg//,/ }; timeout -k 10 300 fisco-bcos_amd/lib/$a > $log 2>&1 ;;
+    ab)
+      v=${arg%%,*}; a=""; [ "$v" != "$arg" ] && a=${arg#*,}
+      cp fisco-bcos_amd/lib/libbcosgpu.so /tmp/libbcosgpu.main.so && cp fisco-bcos_amd/lib_ab/$v/libbcosgpu.so fisco-bcos_amd/lib/ && \
+      timeout -k 10 600 python3 -u bench.py ${a//,/ } > gpurun_out/ab_${v}_${n}.json 2> $log
+      rc0=$?; cp /tmp/libbcosgpu.main.so fisco-bcos_amd/lib/libbcosgpu.so; (exit $rc0) ;;
     py)
       a=${arg//,/ }; timeout -k 10 900 python3 -u fisco-bcos_amd/tools/$a > gpurun_out/${arg%%,*}_${n}.json 2> $log ;;
     *)

@@ -1,6 +1,6 @@
 // sm2bench.hip -- phase timestamps (s_memtime cycles) of tx_verify_sm2_trio26_kernel's workgroup 0 on a
 // 10k-tx batch of random inputs (the schedule is input-independent), to see where c2sm2's latency goes.
-//   sm2bench [REPS [SYNTH_DIR | - [SPLIT]]]   (SPLIT in 0, 36, 38, 40, 42, 44)
+//   sm2bench [REPS [SYNTH_DIR | - [SPLIT]]]   (SPLIT in 0, 38, 40, 42, 44, 46)
 #define BCOSGPU_SM2_TIMING 1
 #include "../csrc/ecc_tables.hip"
 #ifdef SM2BENCH_PAIR_SRC  // A/B builds: another revision of ecc_pair.hip, whose kernel takes no 'affine' flag
@@ -8,7 +8,7 @@
 #define SM2_AFFINE_ARG
 #else
 #include "../csrc/ecc_pair.hip"
-#define SM2_AFFINE_ARG , 1
+#define SM2_AFFINE_ARG , 1, ctab, cbits
 #define SM2_SPLIT_ARG(S) , S
 #endif
 #ifndef SM2_SPLIT_ARG
@@ -59,6 +59,9 @@ int main(int argc, char** argv) {
     hipMemcpy(dso, so.data(), 8 * (n + 1), hipMemcpyHostToDevice);
     const uint32_t* t26;
     if (tables8_sm2_26(&t26)) { printf("no table\n"); return 1; }
+    const uint32_t* ctab = t26;  // s G's comb: the 16-bit R'-domain table when present (as the library)
+    int cbits = 8;
+    if (tables_sm2_26(&ctab, &cbits)) { ctab = t26; cbits = 8; }
     const TxIO io{dp, dpo, ds, dso, dh, dsn, dst};
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
@@ -69,7 +72,7 @@ int main(int argc, char** argv) {
         switch (split) {  // the split is a template parameter of the kernel: the instantiations swept here
 #define SM2_CASE(S) \
     case S: hipLaunchKernelGGL((tx_verify_sm2_trio26_kernel<TxIO SM2_SPLIT_ARG(S)>), dim3((n + 39) / 40), dim3(256), 0, 0, io, n, t26 SM2_AFFINE_ARG); break;
-            SM2_CASE(0) SM2_CASE(36) SM2_CASE(38) SM2_CASE(40) SM2_CASE(42) SM2_CASE(44)
+            SM2_CASE(0) SM2_CASE(38) SM2_CASE(40) SM2_CASE(42) SM2_CASE(44) SM2_CASE(46)
 #undef SM2_CASE
             default: printf("split %d not instantiated\n", split); return 1;
         }
@@ -81,7 +84,7 @@ int main(int argc, char** argv) {
     ms /= static_cast<float>(reps - reps / 2);
     uint64_t t[4][8];
     hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sm2_t), sizeof(t));
-    printf("{\"split\": %d, \"kernel_ms\": %.4f, \"cycles_since_start\": {", split, ms);
+    printf("{\"split\": %d, \"comb_bits\": %d, \"kernel_ms\": %.4f, \"cycles_since_start\": {", split, cbits, ms);
     for (int w = 0; w < 4; ++w)
         printf("%s\"wave%d\": [%llu, %llu, %llu, %llu, %llu, %llu]", w ? ", " : "", w,
                (unsigned long long)(t[w][1] - t[w][0]), (unsigned long long)(t[w][2] - t[w][0]),
