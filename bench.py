@@ -60,20 +60,21 @@ F_SM2_EXEC_COMB8 = 3268
 # the SM2 lane-trio kernel's low-window split (ecc_pair.hip kSm2TrioSplit, BCOSGPU_SM2_SPLIT=0 turns it
 # off): the high chain's tail doublings (4 per moved window, 8 F each) and the one extra complete
 # addition (16 F) are executed work the split adds for its shorter critical path
-SM2_TRIO_SPLIT = 0 if os.environ.get("BCOSGPU_SM2_SPLIT") == "0" else 38
-F_SM2_TRIO_EXEC = F_SM2_EXEC_COMB8 + (4 * 8 * SM2_TRIO_SPLIT + 16 if SM2_TRIO_SPLIT else 0)
+SM2_TRIO_SPLIT = 0 if os.environ.get("BCOSGPU_SM2_SPLIT") == "0" else 44
+F_SM2_TRIO_EXTRA = 4 * 8 * SM2_TRIO_SPLIT + 16 if SM2_TRIO_SPLIT else 0
 # kernel (name without template arguments; the one-lane kernel by suite) -> (F with the 16-bit comb
 # tables present, F on the 8-bit tables): which comb each kernel's launcher hands it (ecc_coop.hip
 # launch_verify_small_secp: the trio kernel takes the wide tables, the pair / split kernels the 8-bit
-# ones; ecc_pair.hip launch_verify_small_sm2: every SM2 small-batch kernel the 8-bit R'-domain table;
-# ecc_txv.hip launch_verify: the one-lane kernels the wide ones)
+# ones; ecc_pair.hip launch_verify_small_sm2: the SM2 pair kernels the 8-bit R'-domain table;
+# ecc_txv.hip launch_verify: the one-lane kernels the wide ones; the SM2 trio kernel the wide R'-domain
+# table since round 4)
 KERNEL_F_EXEC = {
     "tx_verify_trio26_kernel": (F_SECP_EXEC_WIDE, F_SECP_EXEC_COMB8),
     "tx_verify_coop26_kernel": (F_SECP_EXEC_COMB8, F_SECP_EXEC_COMB8),
     "tx_verify_coop_kernel": (F_SECP_EXEC_COMB8, F_SECP_EXEC_COMB8),
     "tx_verify_split_kernel": (F_SECP_EXEC_COMB8, F_SECP_EXEC_COMB8),
     "tx_verify_kernel/0": (F_SECP_EXEC_WIDE, F_SECP_EXEC_COMB8),
-    "tx_verify_sm2_trio26_kernel": (F_SM2_TRIO_EXEC, F_SM2_TRIO_EXEC),
+    "tx_verify_sm2_trio26_kernel": (F_SM2_EXEC + F_SM2_TRIO_EXTRA, F_SM2_EXEC_COMB8 + F_SM2_TRIO_EXTRA),
     "tx_verify_sm2_pair26_kernel": (F_SM2_EXEC_COMB8, F_SM2_EXEC_COMB8),
     "tx_verify_sm2_pair_kernel": (F_SM2_EXEC_COMB8, F_SM2_EXEC_COMB8),
     "tx_verify_kernel/1": (F_SM2_EXEC, F_SM2_EXEC_COMB8),

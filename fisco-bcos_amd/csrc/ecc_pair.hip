@@ -868,7 +868,7 @@ __device__ uint64_t g_sm2_t[4][8];
 #define SM2_T(k) \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_sm2_t[threadIdx.x >> 6][k] = clock64()
 // low Booth windows of t P per tx run by waves 2 and 3 (sm2_low_chain)
-static constexpr int kSm2TrioSplit = 38;
+static constexpr int kSm2TrioSplit = 44;
 #ifndef kSm2DblUnroll
 #define kSm2DblUnroll 1  // doublings per window unrolled in the chain loops (1 = rolled)
 #endif
@@ -1249,23 +1249,8 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             pair26_load_jac(G1, L.gh, lane);
             CurveSM2x::add(G, G0, G1);
             pair26_store_jac(L.g, G, lane);
-            if constexpr (split > 0) {
-                // the low windows of txs 0..19 (the affine table is complete: wave 3 built it before its
-                // comb half, whose result was awaited above), then s G + that sum for all 40 txs
-                SM2_T(6);
-                sm2_low_chain(L, wave, lane, split);
-                SM2_T(7);
-                while (__hip_atomic_load(&L.seq[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                lds_wave_sync();
-                JacP26 B, S;  // (s G reloaded from LDS: kept in registers it cost the chain 3.4k cycles a window)
-                pair26_load_jac(S, L.g, lane);
-                pair26_load_jac(B, L.bacc, lane);
-                CurveSM2x::add(G, S, B);
-                pair26_store_jac(L.g, G, lane);
-            }
-            SM2_T(5);
+            // (then the low windows of txs 0..19 below: the affine table is complete, wave 3 built it before
+            // its comb half, whose result was awaited above)
         } else {
             // the affine table of all 40 txs (one lane per tx) from the Jacobian entries (waves 2 and 3):
             // one inversion of Z1 .. Z7, then x = X / Z^2, y = Y / Z^3; the chains switch to it when ready
@@ -1323,15 +1308,30 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
             SM2_T(2);
             pair26_store_jac(L.gh, G1, lane);
             __hip_atomic_store(&L.seq[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if constexpr (split > 0) {  // the low windows of txs 20..39
-                SM2_T(6);
-                sm2_low_chain(L, wave, lane, split);
-                SM2_T(7);
+        }
+        if constexpr (split > 0) {
+            // the low windows of txs 0..19 (wave 2) / 20..39 (wave 3), from ONE call site: inlined into each
+            // wave's branch the two copies took different register allocations (wave 2's ran 25.6k cycles
+            // a window against 22.3k)
+            SM2_T(6);
+            sm2_low_chain(L, wave, lane, split);
+            SM2_T(7);
+            if (wave == 3) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 if (lane == 0) __hip_atomic_store(&L.seq[4], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {  // s G + the low sums for all 40 txs
+                while (__hip_atomic_load(&L.seq[4], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                lds_wave_sync();
+                JacP26 B, S, G;
+                pair26_load_jac(S, L.g, lane);
+                pair26_load_jac(B, L.bacc, lane);
+                CurveSM2x::add(G, S, B);
+                pair26_store_jac(L.g, G, lane);
             }
-            SM2_T(5);
         }
+        SM2_T(5);
     }
     __syncthreads();
     SM2_T(3);
@@ -1365,16 +1365,12 @@ __global__ __launch_bounds__(256, 1) void tx_verify_sm2_trio26_kernel(IO io, uin
     }
 }
 
-// low Booth windows of t P run by waves 2 and 3 (sm2_low_chain): 38 balances the two wave pairs in
-// the phase probe (profiles/r04_sm2_split_sweep.log) and measured best of 30 / 34 / 38 in the library
-// (tools/sm2_split_sweep.py); BCOSGPU_SM2_SPLIT=0 (read once) runs all 64 windows on waves 0 and 1,
-// the round-3 schedule (A/B and tests)
+// low Booth windows of t P run by waves 2 and 3 (sm2_low_chain): kSm2TrioSplit balances the two wave
+// pairs in the phase probe (profiles/r04_sm2_split_sweep.log); BCOSGPU_SM2_SPLIT=0 (read at each launch,
+// as BCOSGPU_SM2_JAC_ONLY) runs all 64 windows on waves 0 and 1, the round-3 schedule (A/B and tests)
 static int sm2_trio_split() {
-    static const int v = [] {
-        const char* e = getenv("BCOSGPU_SM2_SPLIT");
-        return e ? atoi(e) : kSm2TrioSplit;
-    }();
-    return v;
+    const char* e = getenv("BCOSGPU_SM2_SPLIT");
+    return e ? atoi(e) : kSm2TrioSplit;
 }
 
 template <class IO>

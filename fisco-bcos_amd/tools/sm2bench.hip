@@ -1,6 +1,6 @@
 // sm2bench.hip -- phase timestamps (s_memtime cycles) of tx_verify_sm2_trio26_kernel's workgroup 0 on a
 // 10k-tx batch of random inputs (the schedule is input-independent), to see where c2sm2's latency goes.
-//   sm2bench [REPS [SYNTH_DIR | - [SPLIT]]]   (SPLIT in 0, 38, 40, 42, 44, 46)
+//   sm2bench [REPS [SYNTH_DIR | - [SPLIT]]]   (SPLIT in 0, 40, 42, 44, 46, 48)
 #define BCOSGPU_SM2_TIMING 1
 #include "../csrc/ecc_tables.hip"
 #ifdef SM2BENCH_PAIR_SRC  // A/B builds: another revision of ecc_pair.hip, whose kernel takes no 'affine' flag
@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
         switch (split) {  // the split is a template parameter of the kernel: the instantiations swept here
 #define SM2_CASE(S) \
     case S: hipLaunchKernelGGL((tx_verify_sm2_trio26_kernel<TxIO SM2_SPLIT_ARG(S)>), dim3((n + 39) / 40), dim3(256), 0, 0, io, n, t26 SM2_AFFINE_ARG); break;
-            SM2_CASE(0) SM2_CASE(38) SM2_CASE(40) SM2_CASE(42) SM2_CASE(44) SM2_CASE(46)
+            SM2_CASE(0) SM2_CASE(40) SM2_CASE(42) SM2_CASE(44) SM2_CASE(46) SM2_CASE(48)
 #undef SM2_CASE
             default: printf("split %d not instantiated\n", split); return 1;
         }

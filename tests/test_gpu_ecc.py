@@ -267,18 +267,20 @@ def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
     wh, ws, wst = oracle.tx_verify_packed(suite, pre, po.astype(np.uint64), sg, so.astype(np.uint64), nthreads=16)
     # secp256k1: lane-trio, cooperative-pair, 4-wave split, one-lane occ 1 / 2 on the 10 x 26-bit and on the
     # 8 x 32-bit point arithmetic; SM2: lane-trio and pair kernels and one-lane occ 1 / 2, each on fp26 and 8 x 32
-    # (the SM2 lane-trio kernel once more with every window on the Jacobian table entries:
-    # BCOSGPU_SM2_JAC_ONLY, read at each launch)
+    # (the SM2 lane-trio kernel twice more: every window on the Jacobian table entries, BCOSGPU_SM2_JAC_ONLY,
+    # and without the low-window chains, BCOSGPU_SM2_SPLIT=0; both read at each launch)
     variants = ([(1, 1, 2, 1), (1, 1, 1, 1), (1, 1, 0, 1), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)]
                 if suite == 0
-                else [(1, 1, 2, 1), (1, 1, 2, 1, "jac"), (1, 1, 1, 1), (1, 1, 1, 0), (0, 1, 0, 1), (0, 2, 0, 1),
-                      (0, 1, 0, 0), (0, 2, 0, 0)])
+                else [(1, 1, 2, 1), (1, 1, 2, 1, "jac"), (1, 1, 2, 1, "nosplit"), (1, 1, 1, 1), (1, 1, 1, 0),
+                      (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)])
     try:
         for split, occ, coop, field, *jac in variants:
-            if jac:
+            os.environ.pop("BCOSGPU_SM2_JAC_ONLY", None)
+            os.environ.pop("BCOSGPU_SM2_SPLIT", None)
+            if jac == ["jac"]:
                 os.environ["BCOSGPU_SM2_JAC_ONLY"] = "1"
-            else:
-                os.environ.pop("BCOSGPU_SM2_JAC_ONLY", None)
+            elif jac == ["nosplit"]:  # every window on waves 0 / 1 (the low-window chains off)
+                os.environ["BCOSGPU_SM2_SPLIT"] = "0"
             gpu.set_tx_kernel_policy(split, occ, coop, field)
             th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
             snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
@@ -290,6 +292,7 @@ def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
             assert np.array_equal(snd.cpu().numpy(), ws), (split, occ, field, jac)
     finally:
         os.environ.pop("BCOSGPU_SM2_JAC_ONLY", None)
+        os.environ.pop("BCOSGPU_SM2_SPLIT", None)
         gpu.set_tx_kernel_policy()
 
 
@@ -369,20 +372,23 @@ for suite in (0, 1):
     th = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
     snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
     st = torch.empty(n, dtype=torch.uint8, device="cuda")
-    bcos_gpu.check(bcos_gpu.lib().bcosgpu_set_tx_kernel_policy(0, 2, 1, -1))  # the throughput kernel
-    device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
-    torch.cuda.synchronize()
     pre, po, sg, so = (x.cpu().numpy() for x in (b.pre, b.pre_off, b.sig, b.sig_off))
     wh, ws, wst = oracle.tx_verify_packed(suite, pre, po.astype(np.uint64), sg, so.astype(np.uint64), nthreads=16)
-    assert np.array_equal(th.cpu().numpy(), wh) and np.array_equal(st.cpu().numpy(), wst)
-    assert np.array_equal(snd.cpu().numpy(), ws)
+    # the throughput kernel, then the lane-trio kernel (its u1 G / s G comb on the 8-bit table)
+    for pol in ((0, 2, 1, -1), (1, 1, 2, 1)):
+        bcos_gpu.check(bcos_gpu.lib().bcosgpu_set_tx_kernel_policy(*pol))
+        st.fill_(9)
+        device.tx_verify(suite, b.pre, b.pre_off, b.sig, b.sig_off, th, snd, st)
+        torch.cuda.synchronize()
+        assert np.array_equal(th.cpu().numpy(), wh) and np.array_equal(st.cpu().numpy(), wst), (suite, pol)
+        assert np.array_equal(snd.cpu().numpy(), ws), (suite, pol)
 print("small-tables ok")
 """
 
 
 def test_small_comb_tables_path(gpu):
     """bcosgpu_init_ex(dev, BCOSGPU_INIT_SMALL_TABLES) (also the fallback when the 64 MiB tables do not
-    fit): the throughput kernels run the 8-bit comb and stay bit-exact.  Own process: the flag only
+    fit): the throughput and lane-trio kernels run the 8-bit comb and stay bit-exact.  Own process: the flag only
     matters at a device's first initialisation."""
     import os
     import subprocess
