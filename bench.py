@@ -262,6 +262,9 @@ class Ctx:
             self.dist.barrier()
 
 
+EVENT_EVERY = 16  # set from --event-every
+
+
 def run_leg(ctx, wl_name, steps=None, warmup=3, warm_seconds=0.0, min_seconds=2.0):
     """One workload on this rank; returns the leg's record (rank 0's view, times max over ranks)."""
     import numpy as np
@@ -325,8 +328,8 @@ def run_leg(ctx, wl_name, steps=None, warmup=3, warm_seconds=0.0, min_seconds=2.
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step(timed=True)
+    for k in range(steps):  # (kernel duration events on every EVENT_EVERY-th step: each pair adds stream packets)
+        step(timed=k % EVENT_EVERY == 0)
     torch.cuda.synchronize()
     ctx.barrier()
     torch.cuda.synchronize()
@@ -889,12 +892,16 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS), help="the headline leg")
     ap.add_argument("--legs", default="c2sm2,c3,c4,c5", help="comma-separated sub-legs ('' for none)")
     ap.add_argument("--leg-seconds", type=float, default=2.0)
+    ap.add_argument("--event-every", type=int, default=16,
+                    help="record the kernel-duration HIP events on every N-th timed step (1 = every step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the PCIe and createTransaction legs")
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU test of the --gpus launcher path only: spawn, rendezvous (gloo), max over ranks; no GPU work")
     args = ap.parse_args()
+    global EVENT_EVERY
+    EVENT_EVERY = max(1, args.event_every)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args)
