@@ -630,9 +630,11 @@ def interface_legs(batches, threads=(16, 64, 256), calls=1000, reps=20):
                 device.secp256k1_recover(hashes, sigs, pub, None, ok)
             else:
                 device.sm2_verify(hashes, sigs, None, ok)
-        for _ in range(5):
-            launch()
-        torch.cuda.synchronize()
+        t0 = time.perf_counter()  # >= 0.5 s of back-to-back launches first: the clock settles under load
+        while time.perf_counter() - t0 < 0.5:
+            for _ in range(16):
+                launch()
+            torch.cuda.synchronize()
         ts = []
         for _ in range(reps):
             a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -762,9 +764,11 @@ def sealer_verify_leg(threads, reps=100):
         def launch():
             _lib.check(L.bcosgpu_verify_batch_dev(suite, pub.data_ptr(), h.data_ptr(), sig.data_ptr(), stride, n,
                                                   okd.data_ptr(), stream.cuda_stream))
-        for _ in range(3):
-            launch()
-        torch.cuda.synchronize()
+        t0 = time.perf_counter()  # >= 0.5 s of back-to-back launches first (the clock settles under load)
+        while time.perf_counter() - t0 < 0.5:
+            for _ in range(8):
+                launch()
+            torch.cuda.synchronize()
         kt = []
         for _ in range(20):
             a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
