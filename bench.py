@@ -401,6 +401,9 @@ def merkle_legs(cpu_threads):
                                     "work": "%d %s x %d ops (SURVEY.md 8d)" % (
                                         units, "Keccak-f" if h == device.KECCAK256 else "SM3 compressions",
                                         KECCAK_F_OPS if h == device.KECCAK256 else SM3_C_OPS),
+                                    "note": "algorithmic 32-bit op count: the kernels execute fewer instructions "
+                                            "(three-input XORs, 64-bit rotates as v_alignbit pairs), so large "
+                                            "trees can exceed 1",
                                     "hbm_bytes": n * 32 + device.merkle_size(n, width) * 32}}
                 out["%s_w%d_%s" % (hname, width, _count(n))] = rec
         del leaves
