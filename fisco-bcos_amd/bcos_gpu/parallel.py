@@ -149,12 +149,29 @@ def gpu_sharded_tx_root(n, world, rank, hasher, width, dev, group=None):
     from . import device
 
     shard = shard_plan(n, world, width, choose_levels(n, world, width))[rank]
-    work = torch.empty((max(2 * math.ceil(max(shard[1] - shard[0], 1) / width), 1), 32), dtype=torch.uint8,
-                       device=dev)
+    m = max(shard[1] - shard[0], 1)
+    # the shard's whole tree in one call (bcosgpu_merkle_root_dev: the one-launch / subtree + climb
+    # kernels), whose level `levels - 1` is the frontier -- the shard starts on a width^levels boundary, so
+    # its first `levels` levels are exactly the reference tree's nodes over its range; the per-level
+    # frontier launches (bcosgpu_merkle_frontier_dev) took ~0.3 ms of C4's 12.8 ms step
+    shard_tree = torch.empty((max(device.merkle_size(m, width), 1), 32), dtype=torch.uint8, device=dev)
+    shard_root = torch.empty(32, dtype=torch.uint8, device=dev)
+    work = torch.empty((max(2 * math.ceil(m / width), 1), 32), dtype=torch.uint8, device=dev)
     tree = {}
 
     def frontier_fn(leaves, levels, out):
-        device.merkle_frontier(hasher, width, leaves, levels, work, out)
+        k = leaves.shape[0]
+        pos, c, prev = 0, k, k
+        for lv in range(levels):  # entry index of level `levels - 1`'s count record in the shard's tree
+            prev, c = c, -(-c // width)
+            if lv < levels - 1:
+                pos += c + 1
+        if prev <= 1:  # the shard's tree ends below level `levels - 1` (a small last shard, whose nodes
+            # the reference still hashes one child at a time): the per-level path
+            device.merkle_frontier(hasher, width, leaves, levels, work, out)
+            return
+        device.merkle_root(hasher, width, leaves, shard_tree, shard_root)
+        out.copy_(shard_tree[pos + 1:pos + 1 + c])
 
     def root_fn(frontier, root):
         m = frontier.shape[0]

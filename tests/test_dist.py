@@ -166,6 +166,43 @@ def test_sharded_tx_root_sync_free_gloo(oracle, world):
 
 
 @pytest.mark.gpu
+def test_sharded_tx_root_gpu_frontier_ranks(gpu, oracle):
+    """gpu_sharded_tx_root's frontier (the shard's whole tree through bcosgpu_merkle_root_dev, then its
+    level L - 1) for every rank of world 2 / 8, simulated in one process: the gathered frontiers give the
+    oracle root; and a shard whose tree ends below level L - 1 takes the per-level path with the same
+    nodes as bcosgpu_merkle_frontier_dev."""
+    from bcos_gpu import device, parallel
+    for hasher, width, n in ((0, 2, 1_000_003), (1, 2, 300_001), (0, 16, 400_000)):
+        leaves_h = np.random.default_rng(n + 7).integers(0, 256, size=(n, 32), dtype=np.uint8)
+        leaves = torch.from_numpy(leaves_h).cuda()
+        for world in (2, 8):
+            fronts = []
+            for rank in range(world):
+                st = parallel.gpu_sharded_tx_root(n, world, rank, hasher, width, "cuda")
+                lo, hi = st.local_range
+                m = st.counts[rank]
+                if m:
+                    out = torch.empty((m, 32), dtype=torch.uint8, device="cuda")
+                    st.frontier_fn(leaves[lo:hi], st.levels, out)
+                    fronts.append(out)
+            fr = torch.cat(fronts, 0).contiguous()
+            root = parallel.gpu_root_fn(hasher, width)(fr)
+            torch.cuda.synchronize()
+            assert bytes(root.cpu().tolist()) == oracle.merkle(hasher, width, leaves_h, nthreads=16), (n, world)
+    st = parallel.gpu_sharded_tx_root(64, 1, 0, 0, 2, "cuda")
+    for k, levels in ((1, 3), (3, 4), (5, 2), (4, 2)):
+        small = leaves[:k]
+        m = -(-k // 2 ** levels)
+        got = torch.empty((m, 32), dtype=torch.uint8, device="cuda")
+        st.frontier_fn(small, levels, got)
+        want = torch.empty((m, 32), dtype=torch.uint8, device="cuda")
+        work = torch.empty((max(2 * -(-k // 2), 1), 32), dtype=torch.uint8, device="cuda")
+        device.merkle_frontier(0, 2, small, levels, work, want)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), (k, levels)
+
+
+@pytest.mark.gpu
 def test_sharded_tx_root_gpu_world1(gpu, oracle):
     """gpu_sharded_tx_root (bench C4's step) on one GPU equals the oracle root."""
     from bcos_gpu import parallel
