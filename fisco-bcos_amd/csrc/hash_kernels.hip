@@ -12,6 +12,7 @@
 #include <thread>
 #include <vector>
 #include "hash_device.h"
+#include "sm3_x.h"
 #include "engine.h"
 
 namespace bcosgpu {
@@ -135,7 +136,73 @@ __device__ __forceinline__ void hash_nodes(const uint8_t* src, uint32_t cnt, uin
     const uint32_t len = cnt * 32u;
     NodeReader rd(src, len);  // cnt >= 1
     if (H == KECCAK256) keccak256_msg(rd, len, d);
+    else if (cnt == 2) sm3_msg64(rd, d);  // a full width-2 node: constant padding block
     else sm3_msg(rd, len, d);
+}
+
+// SM3 of one node (c children: 32c bytes at buf, in LDS) by a whole wave: lanes 0 .. XB - 1 expand up
+// to XB of its blocks at once into wx (XB * kSm3Exp words of LDS), then every lane runs the compressions
+// from wx (uniform addresses: broadcast reads); the digest ends on every lane.
+template <uint32_t XB>
+__device__ __forceinline__ void sm3_node_lds(const uint8_t* buf, uint32_t c, uint32_t* wx, uint32_t d[8]) {
+    const uint32_t lane = __lane_id();
+    const uint32_t len = 32u * c, nblocks = (len + 8u) / 64u + 1u;
+    sm3_init(d);
+    for (uint32_t b0 = 0; b0 < nblocks; b0 += XB) {
+        const uint32_t nb = nblocks - b0 < XB ? nblocks - b0 : XB;
+        if (lane < nb) {
+            uint32_t W[16];
+            sm3_load_block(reinterpret_cast<const uint32_t*>(buf), len, b0 + lane, W);
+            sm3_expand_block(W, wx + kSm3Exp * lane);
+        }
+        __syncthreads();
+        for (uint32_t b = 0; b < nb; ++b) sm3_compress_x(d, wx + kSm3Exp * b);
+        __syncthreads();  // before the next chunk's expansions overwrite wx
+    }
+}
+
+// One SM3 level of nout nodes (their children at `in`, LDS or global, nin of them) with the message
+// expansions of all its blocks at once -- thread t expands block t % nb of node t / nb into wx (nb = the
+// blocks of a full node) -- then one thread per node runs its compressions from wx and writes the digest
+// to dst + 32 j (and dst2 + 32 j when non-null).  The caller guarantees nout * nb <= blockDim.x and wx of
+// that many blocks (sm3_level_fits), and a barrier between levels.
+__device__ __forceinline__ uint32_t sm3_node_blocks(uint32_t width) { return (32u * width + 8u) / 64u + 1u; }
+__device__ __forceinline__ bool sm3_level_fits(uint64_t nout, uint32_t width, uint32_t cap_blocks) {
+    // (width 2: a full node's second block is the constant padding, which sm3_msg64 takes as literals)
+    const uint32_t lim = blockDim.x < cap_blocks ? blockDim.x : cap_blocks;
+    return width > 2 && nout * sm3_node_blocks(width) <= lim;
+}
+__device__ __forceinline__ void sm3_level_x(const uint8_t* in, uint64_t nin, uint32_t width, uint32_t nout, uint32_t* wx,
+                                            uint8_t* dst, uint8_t* dst2) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t nb = sm3_node_blocks(width);
+    {
+        const uint32_t j = tid / nb, b = tid - j * nb;
+        const uint64_t first = static_cast<uint64_t>(j) * width;
+        const uint32_t c = j < nout ? static_cast<uint32_t>(nin - first < width ? nin - first : width) : 1u;
+        if (j < nout && b < (32u * c + 8u) / 64u + 1u) {
+            uint32_t W[16];
+            sm3_load_block(reinterpret_cast<const uint32_t*>(in + 32ull * first), 32u * c, b, W);
+            sm3_expand_block(W, wx + kSm3Exp * tid);
+        }
+    }
+    __syncthreads();
+    if (tid < nout) {
+        const uint64_t first = static_cast<uint64_t>(tid) * width;
+        const uint32_t c = static_cast<uint32_t>(nin - first < width ? nin - first : width);
+        const uint32_t nblk = (32u * c + 8u) / 64u + 1u;
+        uint32_t V[8];
+        sm3_init(V);
+        for (uint32_t b = 0; b < nblk; ++b) sm3_compress_x(V, wx + kSm3Exp * (tid * nb + b));
+        store_digest(SM3, dst + 32ull * tid, V);
+        if (dst2) store_digest(SM3, dst2 + 32ull * tid, V);
+    }
+}
+
+// blocks of a width-W node's message (32W bytes + padding) expanded at once by sm3_node_lds
+template <int W>
+constexpr uint32_t sm3_node_xb() {
+    return W && (32u * W + 8u) / 64u + 1u < 16u ? (32u * W + 8u) / 64u + 1u : 16u;
 }
 
 // One tree node cooperatively: every 32-lane group of the workgroup hashes node `base + group` of a
@@ -197,10 +264,13 @@ __device__ __forceinline__ int level_mode(uint64_t nout, uint32_t threads, int p
 // `pair`: level 1 (from the leaves) and the LDS levels may run on lane pairs (the host sets it when
 // the tree's level 1 leaves most of the GPU idle; a throughput-sized level 1 stays one lane per node,
 // which costs fewer instructions per node)
-template <int H, int W>
+// X (SM3): levels whose blocks fit kWgXBlocks at once expand them in parallel (sm3_level_x, wx)
+static constexpr uint32_t kWgXBlocks = 256, kTopXBlocks = 448;
+template <int H, int W, bool X = false>
 __device__ __forceinline__ int wg_levels(uint4 (*lds)[256][2], const uint8_t* __restrict__ leaves, uint64_t n,
                                          uint32_t width, int kin, int B, uint8_t* __restrict__ tree, const TreeLevels& t,
-                                         int pair, uint32_t coop_max, uint32_t pair_max, uint64_t& base) {
+                                         int pair, uint32_t coop_max, uint32_t pair_max, uint64_t& base,
+                                         uint32_t* wx = nullptr) {
     const uint32_t tid = threadIdx.x;
     base = static_cast<uint64_t>(blockIdx.x) * B;  // first level-1 node of this workgroup
     uint32_t nodes = static_cast<uint32_t>(t.cnt[0] - base < static_cast<uint64_t>(B) ? t.cnt[0] - base : B);
@@ -234,6 +304,9 @@ __device__ __forceinline__ int wg_levels(uint4 (*lds)[256][2], const uint8_t* __
             const KeccakPair kp;
             pair_level_pass(kp, in, nodes, width, tid >> 1, nn, tree + 32ull * (t.pos[l] + 1 + nbase),
                             reinterpret_cast<uint8_t*>(&lds[cur ^ 1][0][0]));
+        } else if (X && H == SM3 && sm3_level_fits(nn, width, kWgXBlocks)) {
+            sm3_level_x(in, nodes, width, nn, wx, tree + 32ull * (t.pos[l] + 1 + nbase),
+                        reinterpret_cast<uint8_t*>(&lds[cur ^ 1][0][0]));
         } else if (tid < nn) {
             const uint32_t c = nodes - tid * width < width ? nodes - tid * width : width;
             hash_nodes<H>(in + 32u * tid * width, c, d);
@@ -248,15 +321,16 @@ __device__ __forceinline__ int wg_levels(uint4 (*lds)[256][2], const uint8_t* __
     return cur;
 }
 
-template <int H, int W>
+template <int H, int W, bool X>
 __global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w, int kin,
                                                         int B, uint8_t* __restrict__ tree, const TreeLevels t,
                                                         uint8_t* __restrict__ root, int pair) {
     __shared__ uint4 lds[2][256][2];
+    __shared__ uint4 wxs[X ? kWgXBlocks * kSm3Exp / 4 : 1];
     const uint32_t tid = threadIdx.x;
     uint64_t base;
-    const int cur = wg_levels<H, W>(lds, leaves, n, W ? W : static_cast<uint32_t>(w), kin, B, tree, t, pair, ~0u, ~0u,
-                                    base);
+    const int cur = wg_levels<H, W, X>(lds, leaves, n, W ? W : static_cast<uint32_t>(w), kin, B, tree, t, pair, ~0u,
+                                       ~0u, base, reinterpret_cast<uint32_t*>(&wxs[0]));
     const int top = kin + 1 < t.nlev ? kin + 1 : t.nlev;
     if (blockIdx.x == 0 && tid < static_cast<uint32_t>(t.nlev)) {  // count records (Merkle.h:189-204)
         uint32_t* e = reinterpret_cast<uint32_t*>(tree + 32ull * t.pos[tid]);
@@ -275,15 +349,19 @@ __global__ __launch_bounds__(512) void merkle_wg_kernel(const uint8_t* __restric
 }
 
 // levels [l0, t.nlev) (0-based, level l0 - 1 already in the tree) in ONE workgroup; root copy
-template <int H, int W>
+template <int H, int W, bool X>
 __global__ __launch_bounds__(1024) void merkle_top_kernel(int w, int l0, uint8_t* __restrict__ tree, const TreeLevels t,
                                                           uint8_t* __restrict__ root, int pair) {
+    __shared__ uint4 wxs[X ? kTopXBlocks * kSm3Exp / 4 : 1];
     const uint32_t width = W ? W : static_cast<uint32_t>(w);
     for (int l = l0; l < t.nlev; ++l) {
         const uint64_t nin = t.cnt[l - 1];
         const uint8_t* in = tree + 32ull * (t.pos[l - 1] + 1);
         const int mode = level_mode<H>(t.cnt[l], blockDim.x, pair);
-        if (mode == kCoop) {  // latency-bound level: 25 lanes per node
+        if (X && H == SM3 && sm3_level_fits(t.cnt[l], width, kTopXBlocks)) {
+            sm3_level_x(in, nin, width, static_cast<uint32_t>(t.cnt[l]), reinterpret_cast<uint32_t*>(&wxs[0]),
+                        tree + 32ull * (t.pos[l] + 1), nullptr);
+        } else if (mode == kCoop) {  // latency-bound level: 25 lanes per node
             const KeccakCoop kc;
             const uint32_t g = threadIdx.x / 32;
             coop_level_pass<W>(kc, in, nin, width, g, t.cnt[l], tree + 32ull * (t.pos[l] + 1 + g), nullptr);
@@ -344,11 +422,11 @@ __device__ __forceinline__ uint32_t ld_dev(const uint8_t* p) {
 }
 
 // hash node j of a level from its children at `in` (nin of them) -- gathered into LDS `buf` with
-// device-coherent loads -- with one 25-lane group (Keccak; group 1 hashes a dummy copy) or lane 0
-// (SM3); publishes the digest at dst with device-coherent stores
-template <int H>
+// device-coherent loads -- with one 25-lane group (Keccak; group 1 hashes a dummy copy) or the whole
+// wave (SM3, sm3_node_lds over wx); publishes the digest at dst with device-coherent stores
+template <int H, int W>
 __device__ __forceinline__ void fused_one_node(const uint8_t* in, uint64_t nin, uint32_t width, uint64_t j,
-                                               uint8_t* dst, uint8_t* buf) {
+                                               uint8_t* dst, uint8_t* buf, uint32_t* wx) {
     const uint64_t first = j * width;
     const uint32_t c = static_cast<uint32_t>(nin - first < width ? nin - first : width);
     const uint32_t lane = __lane_id();
@@ -364,9 +442,9 @@ __device__ __forceinline__ void fused_one_node(const uint8_t* in, uint64_t nin, 
             st_dev(dst + 8 * kc.gl + 4, hi);
         }
     } else {
+        uint32_t d[8];
+        sm3_node_lds<sm3_node_xb<W>()>(buf, c, wx, d);
         if (lane == 0) {
-            uint32_t d[8];
-            hash_nodes<H>(buf, c, d);
 #pragma unroll
             for (int k = 0; k < 8; ++k) st_dev(dst + 4 * k, bswap32(d[k]));
         }
@@ -409,6 +487,7 @@ __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restr
                                                           uint8_t* __restrict__ tree, const FusedTree f,
                                                           uint8_t* __restrict__ root, uint32_t* __restrict__ ctr) {
     __shared__ uint4 lds[2][64][2];
+    __shared__ uint4 wxs[H == SM3 ? sm3_node_xb<W>() * kSm3Exp / 4 : 1];  // SM3 climb nodes' expanded blocks
     const TreeLevels& t = f.t;
     const uint32_t width = W ? W : static_cast<uint32_t>(w);
     const uint32_t lane = threadIdx.x;
@@ -462,8 +541,8 @@ __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restr
         if (arrived != kids) return;  // a sibling's wave finishes the parent
         asm volatile("" ::: "memory");  // the children's loads stay after the counter (compiler order)
         MP(3 + 2 * (l - inner));
-        fused_one_node<H>(tree + 32ull * (t.pos[l - 1] + 1), t.cnt[l - 1], width, p, tree + 32ull * (t.pos[l] + 1 + p),
-                          reinterpret_cast<uint8_t*>(&lds[0][0][0]));
+        fused_one_node<H, W>(tree + 32ull * (t.pos[l - 1] + 1), t.cnt[l - 1], width, p, tree + 32ull * (t.pos[l] + 1 + p),
+                             reinterpret_cast<uint8_t*>(&lds[0][0][0]), reinterpret_cast<uint32_t*>(&wxs[0]));
         MP(4 + 2 * (l - inner));
         j = p;
     }
@@ -718,7 +797,7 @@ __global__ __launch_bounds__(256) void merkle_subtree_kernel(const uint8_t* __re
 }
 
 static constexpr uint64_t kClimbMaxWgs = 4096;  // level-1 workgroups up to which the four-wave path runs
-static constexpr int kClimbMaxWidth = 4;  // widths the four-wave path takes by default (wider: the one-wave one)
+static constexpr int kClimbMaxWidth = 4;  // widths the four-wave path takes at latency sizes (wider: the one-wave one)
 
 // returns 1 when it does not apply (too many counters or workgroups, no counter slot)
 static int launch_merkle_climb(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
@@ -834,11 +913,15 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
         const char* e = getenv("BCOSGPU_MERKLE_CLIMB");
         return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
     }();
-    // (SM3 only for throughput-sized trees, where the subtree kernel runs first: at latency sizes its
-    // one-lane levels measured no faster than the two-launch path, profiles/r04_merkle_paths_ab_sm3.json)
-    const bool climb_sm3 = t.cnt[0] > 256ull * static_cast<uint64_t>(cu_count());
+    // Throughput-sized trees (more level-1 nodes than 256 per CU), where the subtree kernel runs first,
+    // take it at every width up to 16 and both hashers (16M leaves, width 16: Keccak 0.62 vs 0.94 ms on
+    // the two-launch path, SM3 0.56 vs 0.71, profiles/r04_merkle_paths_ab_w16.json); at latency sizes
+    // only narrow Keccak trees (SM3's one-lane levels measured no faster than the two-launch path,
+    // profiles/r04_merkle_paths_ab_sm3.json; width 16 has the one-wave kernel)
+    const bool big = t.cnt[0] > 256ull * static_cast<uint64_t>(cu_count());
     if (fused_env != 1 &&
-        (climb_env == 1 || (climb_env < 0 && width <= kClimbMaxWidth && (hasher == KECCAK256 || climb_sm3)))) {
+        (climb_env == 1 ||
+         (climb_env < 0 && ((width <= kClimbMaxWidth && (hasher == KECCAK256 || big)) || (width <= 16 && big))))) {
         const int rc = launch_merkle_climb(hasher, width, d_leaves, n, d_tree, d_root, t, st);
         if (rc <= 0) return rc;
     }
@@ -866,11 +949,24 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
     uint32_t threads = pair ? 2u * B : B;
     if (hasher == KECCAK256 && kin >= 1 && 32u * (B / width) > threads && 32u * (B / width) <= 512u) threads = 32u * (B / width);
     const dim3 b1(threads);
-#define WG(HH, WW) hipLaunchKernelGGL((merkle_wg_kernel<HH, WW>), g1, b1, 0, st, d_leaves, n, width, kin, static_cast<int>(B), d_tree, t, d_root, pair)
+    // SM3 at latency sizes (a workgroup per CU at most): the LDS levels' and the top kernel's blocks
+    // expanded in parallel (sm3_level_x; its 70 KB of LDS would cost a throughput-sized level 1 occupancy).
+    // BCOSGPU_MERKLE_SM3X=0/1 forces it off/on (A/B), read once per process.
+    static const int sm3x_env = [] {
+        const char* e = getenv("BCOSGPU_MERKLE_SM3X");
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    }();
+    const bool sm3x = hasher == SM3 && (sm3x_env >= 0 ? sm3x_env == 1 : g1.x <= static_cast<unsigned>(cu_count()));
+    const bool sm3x_top = hasher == SM3 && sm3x_env != 0;
+#define WG(HH, WW, XX) hipLaunchKernelGGL((merkle_wg_kernel<HH, WW, XX>), g1, b1, 0, st, d_leaves, n, width, kin, static_cast<int>(B), d_tree, t, d_root, pair)
     if (hasher == SM3) {
-        if (width == 2) WG(SM3, 2); else if (width == 16) WG(SM3, 16); else WG(SM3, 0);
+        if (sm3x) {
+            if (width == 2) WG(SM3, 2, true); else if (width == 16) WG(SM3, 16, true); else WG(SM3, 0, true);
+        } else {
+            if (width == 2) WG(SM3, 2, false); else if (width == 16) WG(SM3, 16, false); else WG(SM3, 0, false);
+        }
     } else {
-        if (width == 2) WG(KECCAK256, 2); else if (width == 16) WG(KECCAK256, 16); else WG(KECCAK256, 0);
+        if (width == 2) WG(KECCAK256, 2, false); else if (width == 16) WG(KECCAK256, 16, false); else WG(KECCAK256, 0, false);
     }
 #undef WG
     int l = kin + 1;  // next level (0-based) to compute
@@ -880,11 +976,15 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
         ++l;
     }
     if (l < t.nlev) {
-#define TOP(HH, WW) hipLaunchKernelGGL((merkle_top_kernel<HH, WW>), dim3(1), dim3(1024), 0, st, width, l, d_tree, t, d_root, pair)
+#define TOP(HH, WW, XX) hipLaunchKernelGGL((merkle_top_kernel<HH, WW, XX>), dim3(1), dim3(1024), 0, st, width, l, d_tree, t, d_root, pair)
         if (hasher == SM3) {
-            if (width == 2) TOP(SM3, 2); else if (width == 16) TOP(SM3, 16); else TOP(SM3, 0);
+            if (sm3x_top) {
+                if (width == 2) TOP(SM3, 2, true); else if (width == 16) TOP(SM3, 16, true); else TOP(SM3, 0, true);
+            } else {
+                if (width == 2) TOP(SM3, 2, false); else if (width == 16) TOP(SM3, 16, false); else TOP(SM3, 0, false);
+            }
         } else {
-            if (width == 2) TOP(KECCAK256, 2); else if (width == 16) TOP(KECCAK256, 16); else TOP(KECCAK256, 0);
+            if (width == 2) TOP(KECCAK256, 2, false); else if (width == 16) TOP(KECCAK256, 16, false); else TOP(KECCAK256, 0, false);
         }
 #undef TOP
     }

@@ -11,6 +11,7 @@
 #   exe=PATH[,ARGS]      run a built tool from fisco-bcos_amd/lib (ARGS with ',' for ' ')
 #   ab=NAME[,ARGS]       bench.py ARGS with lib_ab/NAME/libbcosgpu.so swapped in (tools/build_ab.sh), then restored
 #   py=NAME[,ARGS]       run fisco-bcos_amd/tools/NAME.py (ARGS with ',' for ' '), stdout to gpurun_out/NAME_<step>.json
+#   abpy=LIB,NAME[,ARGS] the py step with lib_ab/LIB/libbcosgpu.so swapped in, then restored
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -41,6 +42,11 @@ for step in "$@"; do
       v=${arg%%,*}; a=""; [ "$v" != "$arg" ] && a=${arg#*,}
       cp fisco-bcos_amd/lib/libbcosgpu.so /tmp/libbcosgpu.main.so && cp fisco-bcos_amd/lib_ab/$v/libbcosgpu.so fisco-bcos_amd/lib/ && \
       timeout -k 10 600 python3 -u bench.py ${a//,/ } > gpurun_out/ab_${v}_${n}.json 2> $log
+      rc0=$?; cp /tmp/libbcosgpu.main.so fisco-bcos_amd/lib/libbcosgpu.so; (exit $rc0) ;;
+    abpy)
+      v=${arg%%,*}; rest=${arg#*,}; a=${rest//,/ }
+      cp fisco-bcos_amd/lib/libbcosgpu.so /tmp/libbcosgpu.main.so && cp fisco-bcos_amd/lib_ab/$v/libbcosgpu.so fisco-bcos_amd/lib/ && \
+      timeout -k 10 900 python3 -u fisco-bcos_amd/tools/$a > gpurun_out/ab_${v}_${n}.json 2> $log
       rc0=$?; cp /tmp/libbcosgpu.main.so fisco-bcos_amd/lib/libbcosgpu.so; (exit $rc0) ;;
     py)
       a=${arg//,/ }; timeout -k 10 900 python3 -u fisco-bcos_amd/tools/$a > gpurun_out/${arg%%,*}_${n}.json 2> $log ;;

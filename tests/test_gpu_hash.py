@@ -211,17 +211,35 @@ def test_merkle_four_wave_climb_trees(gpu, oracle):
 
 @pytest.mark.parametrize("hasher", [0, 1])
 def test_merkle_subtree_then_climb(gpu, oracle, hasher):
-    """Throughput-sized narrow trees: the subtree kernel hashes levels 0..k one thread per level-k node,
-    then the climb kernel runs on level k (k = 0, 1, 2 at these sizes for width 2 on 256 CUs; SM3 forced
-    through the same kernels is checked where the library takes them); every entry of the output vector."""
+    """Throughput-sized trees (more level-1 nodes than 256 per CU, up to width 16): the subtree kernel hashes
+    levels 0..k one thread per level-k node, then the climb kernel runs on level k (k = 0, 1, 2 at these
+    sizes for width 2 on 256 CUs); every entry of the output vector, both hashers."""
     rng = np.random.default_rng(79 + hasher)
     H = gpu.Keccak256() if hasher == 0 else gpu.SM3()
-    for width, n in ((2, 153_607), (2, 400_005), (2, 1_000_003), (4, 1_000_001), (3, 600_001)):
+    for width, n in ((2, 153_607), (2, 400_005), (2, 1_000_003), (4, 1_000_001), (3, 600_001), (5, 400_001),
+                     (16, 2_000_003)):
         leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
         got = gpu.Merkle(H, width).generate_merkle([leaves[i].tobytes() for i in range(n)])
         _, want = oracle.merkle(hasher, width, leaves, want_tree=True)
         assert len(got) == want.shape[0], (width, n)
         assert b"".join(got) == want.tobytes(), (width, n)
+
+
+def test_merkle_sm3_expanded_levels(gpu, oracle):
+    """SM3 levels whose blocks are all expanded at once (hash_kernels.hip sm3_level_x: the workgroup
+    kernel's LDS levels, up to 256 blocks, and the top kernel's, up to 448) and the one-lane levels past
+    those limits, widths with 2..17 blocks per node, sizes around the limits; every entry of the output
+    vector."""
+    rng = np.random.default_rng(81)
+    H = gpu.SM3()
+    for width in (3, 5, 16, 33):
+        nb = (32 * width + 8) // 64 + 1
+        cap = 448 // nb  # top-kernel nodes per level expanded at once
+        for n in sorted({width * width + 1, cap * width, cap * width + 1, (cap + 1) * width * width - 1, 70_001}):
+            leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+            got = gpu.Merkle(H, width).generate_merkle([leaves[i].tobytes() for i in range(n)])
+            _, want = oracle.merkle(1, width, leaves, want_tree=True)
+            assert b"".join(got) == want.tobytes(), (width, n)
 
 
 def test_merkle_one_launch_repeat_two_streams(gpu, oracle):
