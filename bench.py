@@ -417,7 +417,7 @@ def _count(n):
     return "%dk" % (n // 1000) if n < 1_000_000 else "%dM" % (n // 1_000_000)
 
 
-HASH_LATENCY = "r03_hash_latency.json"  # tools/keccakpair_check.hip on MI355X: cycles per unit, lone wave
+HASH_LATENCY = "r04_hash_latency.json"  # tools/keccakpair_check.hip + sm3probe.hip on MI355X: cycles per unit, lone wave
 CLOCK_HZ = 2.4e9                        # MI355X peak engine clock (MI355X_MICROARCH.md)
 
 
@@ -425,14 +425,15 @@ def merkle_floor(n, width, keccak):
     """Serial-hash floor of Merkle<H,width> over n leaves (Merkle.h:243-261): each level waits for its
     slowest node -- a full group of `width` children, or the level's whole input when smaller -- so the
     critical path is the sum over levels of that node's Keccak-f permutations / SM3 compressions, times
-    the fastest measured per-unit latency of a lone wave (cooperative 25-lane Keccak-f; one-lane SM3)
-    at the peak clock.  No schedule of this hash on this GPU beats it."""
+    the fastest measured per-unit latency of a lone wave (cooperative 25-lane Keccak-f; SM3 from a block
+    expanded beforehand) at the peak clock.  No schedule of this hash on this GPU beats it."""
     try:
         with open(os.path.join(ROOT, "profiles", HASH_LATENCY)) as f:
             lat = json.load(f)
     except (OSError, ValueError):
         return None
-    cyc = min(lat["cycles_per_perm_coop25"], lat["cycles_per_perm_pair"]) if keccak else lat["cycles_per_sm3_compression"]
+    cyc = (min(lat["cycles_per_perm_coop25"], lat["cycles_per_perm_pair"]) if keccak else
+           min(lat["cycles_per_sm3_compression"], lat.get("cycles_per_sm3_compression_expanded", 1 << 30)))
     units, m = 0, n
     while m > 1:
         k = min(width, m)
