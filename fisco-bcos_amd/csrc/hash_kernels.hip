@@ -137,7 +137,7 @@ __device__ __forceinline__ void hash_nodes(const uint8_t* src, uint32_t cnt, uin
     NodeReader rd(src, len);  // cnt >= 1
     if (H == KECCAK256) keccak256_msg(rd, len, d);
     else if (cnt == 2) sm3_msg64(rd, d);  // a full width-2 node: constant padding block
-    else sm3_msg(rd, len, d);
+    else sm3_node_msg(src, len, d);
 }
 
 // SM3 of one node (c children: 32c bytes at buf, in LDS) by a whole wave: lanes 0 .. XB - 1 expand up
