@@ -96,7 +96,9 @@ PEAK_ALU_PER_S = 3.7497e13      # full-rate 32-bit VALU (v_alignbit_b32)
 # SURVEY §8d ALU ops per permutation / compression
 KECCAK_F_OPS = 6240
 SM3_C_OPS = 2100
-PMC_GLOB = "r04_pmc_{}.json"
+PMC_GLOB = "r05_pmc_{}.json"
+# per-leg PMC summary of the Merkle and hash legs (tools/leg_run.py under rocprofv3, tools/leg_prof.py)
+LEG_PMC = "r05_pmc_legs.json"
 KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_device.h", "fisco-bcos_amd/csrc/ecc_tables.hip", "fisco-bcos_amd/csrc/ecc_sig.hip",
               "fisco-bcos_amd/csrc/ecc_txv.hip", "fisco-bcos_amd/csrc/ecc_coop.hip", "fisco-bcos_amd/csrc/ecc_pair.hip",
               "fisco-bcos_amd/csrc/fe_asm.h", "fisco-bcos_amd/csrc/fe.h",
@@ -362,52 +364,154 @@ def run_leg(ctx, wl_name, steps=None, warmup=3, warm_seconds=0.0, min_seconds=2.
     return rec, state
 
 
-def merkle_legs(cpu_threads):
-    """configs[0] (merkleBench: width-16 root, 100k leaves) and the 1M / 16M-leaf roofline legs."""
-    import numpy as np
+MERKLE_SPECS = [(n, hname, width) for n in (100_000, 1_000_000, 16_000_000)
+                for hname in ("keccak256", "sm3") for width in (16, 2)]
+# hashes/s legs (north_star): (name, hasher, messages, length) -- "c2" = configs[1]'s 10k 151-byte tx
+# preimages (synth.preimages, TarsHashable.h:29-40); 1M tx preimages; 1M 64-byte public keys (the
+# address hash, KeyPair.h:30-33)
+HASH_SPECS = [("keccak256_c2", "keccak256", 10_000, 151), ("sm3_c2", "sm3", 10_000, 151),
+              ("keccak256_1M_151B", "keccak256", 1_000_000, 151), ("sm3_1M_151B", "sm3", 1_000_000, 151),
+              ("keccak256_1M_64B", "keccak256", 1_000_000, 64), ("sm3_1M_64B", "sm3", 1_000_000, 64)]
+
+
+def merkle_name(n, hname, width):
+    return "%s_w%d_%s" % (hname, width, _count(n))
+
+
+def merkle_inputs(n):
+    import torch
+    g = torch.Generator(device="cuda")
+    g.manual_seed(n)
+    return torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
+
+
+def hash_inputs(n, length):
+    """Device (data, offsets) of n messages of `length` bytes: the synthetic tx preimages when length is
+    151, else seeded random bytes."""
+    import torch
+    from bcos_gpu import synth
+    if length == synth.PREIMAGE_LEN:
+        data = torch.from_numpy(synth.preimages(n).reshape(-1)).cuda()
+    else:
+        g = torch.Generator(device="cuda")
+        g.manual_seed(n * 7 + length)
+        data = torch.randint(0, 256, (n * length,), dtype=torch.uint8, device="cuda", generator=g)
+    off = torch.arange(0, (n + 1) * length, length, dtype=torch.int64, device="cuda")
+    return data, off
+
+
+def _hasher(hname):
+    from bcos_gpu import device
+    return device.KECCAK256 if hname == "keccak256" else device.SM3
+
+
+def _hash_units(length, keccak):
+    """Keccak-f permutations (rate 136, pad >= 1 byte) / SM3 compressions (64-byte blocks, 9 bytes of
+    padding) for one message of `length` bytes."""
+    return length // 136 + 1 if keccak else (length + 8) // 64 + 1
+
+
+def leg_pmc(name):
+    """Per-root (per-batch) counters of the Merkle / hash leg `name` from the committed PMC summary
+    (tools/leg_prof.py): VALU instructions, GRBM cycles (summed over the 8 XCDs), HBM bytes, and the
+    issue fraction derived from them (wave64 VALU instructions x 4 cycles / 1,024 SIMDs / cycles per
+    XCD, <= 1 by construction)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", LEG_PMC)) as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return None
+    c = pmc.get("legs", {}).get(name)
+    if not c or not c.get("SQ_INSTS_VALU") or not c.get("GRBM_GUI_ACTIVE"):
+        return None
+    out = {"valu_issue": c["SQ_INSTS_VALU"] * 4.0 / 1024.0 / (c["GRBM_GUI_ACTIVE"] / 8.0),
+           "valu_per_unit": c["SQ_INSTS_VALU"], "source": os.path.join("profiles", LEG_PMC),
+           "same_kernel_source": pmc.get("kernel_source_sha") == kernel_source_sha()}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        out["traffic"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+    return out
+
+
+def _event_ms(fn, min_s=0.25, warm=3):
+    """Average device time (ms) of fn() over >= min_s of back-to-back calls, HIP events on torch's stream."""
+    import torch
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    reps = max(5, int(min_s / max(time.perf_counter() - t1, 1e-6)))
+    a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    c.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(c) / reps, reps
+
+
+def _alu_roofline(ms, units, keccak, name):
+    """The executed-instruction roofline of a hash / Merkle leg: frac = the PMC issue fraction (<= 1);
+    useful_frac = SURVEY 8(d)'s op count per second over the v_alignbit peak, a useful-work figure that
+    three-input XORs and paired rotates can push past 1 (not an issue-rate claim)."""
+    ops = units * (KECCAK_F_OPS if keccak else SM3_C_OPS)
+    pmc = leg_pmc(name)
+    return {"bound": "int-valu", "frac": pmc["valu_issue"] if pmc else None,
+            "useful_ops_per_s": ops / (ms * 1e-3), "useful_frac": ops / (ms * 1e-3) / PEAK_ALU_PER_S,
+            "peak_ops_per_s": PEAK_ALU_PER_S, "units": units,
+            "traffic": pmc.get("traffic") if pmc else None, "pmc": pmc}
+
+
+def hash_legs():
+    """hashes/s (north_star): bcosgpu_hash_batch_dev over HBM-resident messages (HASH_SPECS)."""
     import torch
     from bcos_gpu import device
     out = {}
-    for n in (100_000, 1_000_000, 16_000_000):
-        g = torch.Generator(device="cuda")
-        g.manual_seed(n)
-        leaves = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
-        for hname, h in (("keccak256", device.KECCAK256), ("sm3", device.SM3)):
-            for width in (16, 2):
-                tree = torch.empty((device.merkle_size(n, width), 32), dtype=torch.uint8, device="cuda")
-                root = torch.empty(32, dtype=torch.uint8, device="cuda")
-                for _ in range(3):
-                    device.merkle_root(h, width, leaves, tree, root)
-                torch.cuda.synchronize()
-                t1 = time.perf_counter()
-                device.merkle_root(h, width, leaves, tree, root)
-                torch.cuda.synchronize()
-                reps = max(5, int(0.25 / max(time.perf_counter() - t1, 1e-6)))
-                a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record()
-                for _ in range(reps):
-                    device.merkle_root(h, width, leaves, tree, root)
-                c.record()
-                torch.cuda.synchronize()
-                ms = a.elapsed_time(c) / reps
-                units, ops = merkle_work(n, width, h == device.KECCAK256)
-                floor = merkle_floor(n, width, h == device.KECCAK256)
-                rec = {"ms": ms, "GB_per_s": n * 32 / (ms * 1e-3) / 1e9, "reps": reps,
-                       "latency_floor_ms": floor["ms"] if floor else None,
-                       "frac_of_latency_floor": floor["ms"] / ms if floor else None, "latency_floor": floor,
-                       "roofline": {"bound": "int-valu", "achieved": ops / (ms * 1e-3) / 1e12,
-                                    "peak": PEAK_ALU_PER_S / 1e12, "unit": "Tops/s",
-                                    "frac": ops / (ms * 1e-3) / PEAK_ALU_PER_S,
-                                    "work": "%d %s x %d ops (SURVEY.md 8d)" % (
-                                        units, "Keccak-f" if h == device.KECCAK256 else "SM3 compressions",
-                                        KECCAK_F_OPS if h == device.KECCAK256 else SM3_C_OPS),
-                                    "note": "algorithmic 32-bit op count: the kernels execute fewer instructions "
-                                            "(three-input XORs, 64-bit rotates as v_alignbit pairs), so large "
-                                            "trees can exceed 1",
-                                    "hbm_bytes": n * 32 + device.merkle_size(n, width) * 32}}
-                out["%s_w%d_%s" % (hname, width, _count(n))] = rec
-        del leaves
-        torch.cuda.empty_cache()
+    for name, hname, n, length in HASH_SPECS:
+        data, off = hash_inputs(n, length)
+        dig = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+        h = _hasher(hname)
+        ms, reps = _event_ms(lambda: device.hash_batch(h, data, off, dig))
+        keccak = hname == "keccak256"
+        units = n * _hash_units(length, keccak)
+        rf = _alu_roofline(ms, units, keccak, name)
+        rf["algorithmic_bytes"] = n * (length + 8 + 32)
+        out[name] = {"hashes_per_s": n / (ms * 1e-3), "ms": ms, "reps": reps, "messages": n, "bytes_each": length,
+                     "GB_per_s": n * length / (ms * 1e-3) / 1e9, "roofline": rf}
+        del data, off, dig
+    torch.cuda.empty_cache()
+    return out
+
+
+def merkle_legs(cpu_threads):
+    """configs[0] (merkleBench: width-16 root, 100k leaves) and the 1M / 16M-leaf roofline legs."""
+    import torch
+    from bcos_gpu import device
+    out = {}
+    last_n, leaves = None, None
+    for n, hname, width in MERKLE_SPECS:
+        if n != last_n:
+            del leaves
+            torch.cuda.empty_cache()
+            leaves, last_n = merkle_inputs(n), n
+        h = _hasher(hname)
+        keccak = hname == "keccak256"
+        tree = torch.empty((device.merkle_size(n, width), 32), dtype=torch.uint8, device="cuda")
+        root = torch.empty(32, dtype=torch.uint8, device="cuda")
+        ms, reps = _event_ms(lambda: device.merkle_root(h, width, leaves, tree, root))
+        units, _ = merkle_work(n, width, keccak)
+        floor = merkle_floor(n, width, keccak)
+        name = merkle_name(n, hname, width)
+        rf = _alu_roofline(ms, units, keccak, name)
+        rf["algorithmic_bytes"] = n * 32 + device.merkle_size(n, width) * 32
+        out[name] = {"ms": ms, "GB_per_s": n * 32 / (ms * 1e-3) / 1e9, "reps": reps,
+                     "latency_floor_ms": floor["ms"] if floor else None,
+                     "frac_of_latency_floor": floor["ms"] / ms if floor else None, "latency_floor": floor,
+                     "roofline": rf}
+        del tree, root
+    del leaves
+    torch.cuda.empty_cache()
     if cpu_threads:
         out["cpu_baseline"] = merkle_cpu(cpu_threads)
     return out
@@ -493,7 +597,7 @@ def merkle_cpu(threads):
                 med, ts = _median_time(fn)
                 res["%s_w%d_%s" % (hname, width, _count(n))] = {
                     "ms": med * 1e3, "GB_per_s": n * 32 / med / 1e9, "reps_ms": [round(t * 1e3, 3) for t in ts]}
-    return {"legs": res, "threads": threads, "kind": "reference" if use_ossl else "port",
+    return {"legs": res, "threads": threads, "kind": "standin-openssl-restatement" if use_ossl else "port",
             "impl": ("Merkle.h:170-261 over the reference's OpenSSL hashers (OpenSSLHasher.h, EVP_sm3 / EVP_sha3_256 "
                      "with the 0x01 pad poke; OpenSSL %s), level-parallel pthreads" % oracle.standin_version())
             if use_ossl else "oracle/merkle.c restatement of Merkle.h:170-261, level-parallel pthreads",
@@ -838,29 +942,85 @@ def create_transaction_leg(b, suite, n, want_status, reps=20):
             "path": "bcosgpu_tars_tx_verify_batch_dev (decode + pack + verify + dataHash check)"}
 
 
+def devset_legs(devices, min_seconds=1.0):
+    """The topology INTEGRATION.md section 2 prescribes: ONE process drives the device list through the C ABI
+    a node links (csrc/multi.hip): C4 = configs[3]'s 1M secp256k1 txs as one block through
+    bcosgpu_block_verify_multi (index shards, width-2 frontiers gathered on devices[0] by peer copies);
+    C5 = configs[4]'s 64 blocks x 20k txs, one bcosgpu_block_verify_multi call per block in order (a replay).
+    Host buffers in and out (H2D + kernels + D2H per call: the PCIe-inclusive rate, not `value`).  Each
+    leg's root and statuses are checked against the single-device call."""
+    import numpy as np
+    import bcos_gpu
+    from bcos_gpu import synth, tx
+    suite = bcos_gpu.secp256k1_suite()
+    out = {"devices": list(devices)}
+    b = synth.make_batch(0, WORKLOADS["c5"]["n"], seed=0xDE5)
+    pre, po = b.pre.cpu().numpy(), b.pre_off.cpu().numpy().astype(np.uint64)
+    sg, so = b.sig.cpu().numpy(), b.sig_off.cpu().numpy().astype(np.uint64)
+    del b
+    per = WORKLOADS["c5"]["n"] // WORKLOADS["c5"]["blocks"]
+    n4 = WORKLOADS["c4"]["n"]
+
+    def c4(devs):
+        return tx.verify_packed_multi(devs, suite, pre, po[: n4 + 1], sg, so[: n4 + 1], width=2)
+
+    def c5(devs):
+        return [tx.verify_packed_multi(devs, suite, pre, po[k * per: (k + 1) * per + 1], sg,
+                                       so[k * per: (k + 1) * per + 1], width=2)
+                for k in range(WORKLOADS["c5"]["blocks"])]
+
+    for wl, fn in (("c4", c4), ("c5", c5)):
+        want = fn([devices[0]])
+        got = fn(devices)
+        def _same(g, w):
+            return all(np.array_equal(x, y) for x, y in zip(g[:3], w[:3])) and g[3] == w[3]
+        same = _same(got, want) if wl == "c4" else all(_same(g, w) for g, w in zip(got, want))
+        steps, t0 = 0, time.perf_counter()
+        while steps < 2 or time.perf_counter() - t0 < min_seconds:
+            fn(devices)
+            steps += 1
+        dt = (time.perf_counter() - t0) / steps
+        out[wl] = {"tx_s": WORKLOADS[wl]["n"] / dt, "ms_per_step": dt * 1e3, "steps": steps,
+                   "matches_single_device": bool(same)}
+    return out
+
+
 def _g(x, k=4):
     return float("%.*g" % (k, x)) if isinstance(x, (int, float)) and not isinstance(x, bool) else x
 
 
-def summarize(line, head_name, head):
-    """A compact digest of every leg, emitted as the LAST key of the line so a reader holding only the
-    line's tail (the driver keeps ~2 kB) still sees all of them: per tx leg tx/s, ms/step, kernel ms, the
-    executed and SURVEY-8d roofline fractions, HBM traffic over algorithmic bytes and the VALU issue
-    fraction; the single-call rates (GPU calls/s, p50 / p99 us, CPU stand-in calls/s at the same thread
-    count); sealer verify; Merkle; the CPU baseline."""
+def summarize(full, head_name):
+    """A compact digest of every leg of the full record (the line's `summary`, its last key): per tx leg
+    tx/s, ms/step, kernel ms, the executed and SURVEY-8d roofline fractions, HBM traffic over algorithmic
+    bytes and the VALU issue fraction; hashes/s; Merkle; the device-set legs; single-call and sealer-verify
+    latencies; the CPU baseline."""
     out = {}
 
     def leg(rec):
         rf = rec["roofline"]
         alg = rf["algorithmic_bytes_per_unit"] * max(rf["units_per_launch"], 1)
+        vi = rf.get("valu_issue")
         return {"tx_s": _g(rec["value"]), "ms_step": _g(rec["ms_per_step"]), "kernel_ms": _g(rf["kernel_ms"]),
                 "frac": _g(rf["frac"], 3), "frac_8d": _g(rf["algorithmic"]["frac"], 3),
                 "traffic_x": _g(rf["traffic"] / alg, 3) if rf.get("traffic") else None,
-                "valu_issue": _g(rf["valu_issue"]["frac"], 3) if rf.get("valu_issue") else None}
-    out[head_name] = leg(head)
-    for k, rec in (line.get("legs") or {}).items():
+                "valu_issue": _g(vi["frac"] if isinstance(vi, dict) else vi, 3)}
+    out[head_name] = leg(full["head"])
+    for k, rec in (full.get("legs") or {}).items():
         out[k] = leg(rec)
-    itf = line.get("interface") or {}
+    hs = full.get("hashes") or {}
+    if hs:
+        out["hashes[h/s,frac,useful]"] = {k: [_g(v["hashes_per_s"]), _g(v["roofline"]["frac"], 3),
+                                              _g(v["roofline"]["useful_frac"], 3)] for k, v in hs.items()}
+    mk = full.get("merkle") or {}
+    if mk:
+        out["merkle[ms,frac,floor]"] = {k: [_g(v["ms"]), _g(v["roofline"]["frac"], 3), _g(v["frac_of_latency_floor"], 3)]
+                                        for k, v in mk.items() if isinstance(v, dict) and "ms" in v}
+    ds = full.get("devset")
+    if ds:
+        out["devset"] = {"devices": ds["devices"], **{k: {"tx_s": _g(v["tx_s"]), "ms": _g(v["ms_per_step"]),
+                                                          "ok": v["matches_single_device"]}
+                                                      for k, v in ds.items() if k != "devices"}}
+    itf = full.get("interface") or {}
     sc = {}
     for k, v in itf.items():
         if k.startswith("single_call_") and isinstance(v, dict) and "calls_per_s" in v:
@@ -872,23 +1032,57 @@ def summarize(line, head_name, head):
     rb = {k[len("recover_batch_"):]: _g(v["kernel_ms_median"]) for k, v in itf.items() if k.startswith("recover_batch_")}
     if rb:
         out["recover_batch_10k_ms"] = rb
-    sv = line.get("sealer_verify")
+    sv = full.get("sealer_verify")
     if sv:
         out["sealer_verify"] = sv.get("summary")
-    mk = line.get("merkle") or {}
-    if mk:
-        out["merkle_ms"] = {k: _g(mk[k]["ms"]) for k in ("keccak256_w16_100k", "sm3_w16_100k", "keccak256_w2_100k",
-                                                          "sm3_w2_100k", "keccak256_w2_1M", "keccak256_w16_16M")
-                            if k in mk}
     for k in ("pcie_inclusive", "create_transaction"):
-        if line.get(k):
-            out[k + "_tx_s"] = _g(line[k]["value"])
-    cb = line.get("cpu_baseline")
+        if full.get(k):
+            out[k + "_tx_s"] = _g(full[k]["value"])
+    cb = full.get("cpu_baseline")
     if cb:
         out["cpu"] = {"kind": cb["kind"], "threads": cb["cores"],
                       "tx_s": {k: _g(v["value"]) for k, v in cb["legs"].items()},
                       "full_host_est": _g(cb["full_host_estimate"]["value"])}
+        mc = cb.get("merkle")
+        if mc:
+            out["cpu"]["merkle_ms"] = {k: _g(v["ms"]) for k, v in mc["legs"].items() if k.endswith("100k")}
+            out["cpu"]["merkle_kind"] = mc["kind"]
     return out
+
+
+LINE_MAX = 7000  # the driver keeps ~8 kB of stdout and must parse the whole line
+
+
+def compact_line(full):
+    """The ONE line bench.py prints: the contract's head keys, a lean roofline and cpu_baseline and the
+    summary of every leg.  Prose, per-leg notes and nested legs stay in the detail file (--detail-out).
+    Strict JSON (no NaN / Infinity); under LINE_MAX bytes (tests/test_bench_line.py)."""
+    head = full["head"]
+    rf = head["roofline"]
+    vi = rf.get("valu_issue")
+    line = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")}
+    line["roofline"] = {
+        "bound": rf["bound"], "achieved": _g(rf["achieved"], 5), "peak": _g(rf["peak"], 5), "unit": rf["unit"],
+        "frac": _g(rf["frac"], 4), "frac_8d": _g(rf["algorithmic"]["frac"], 4), "kernel": rf["kernel"],
+        "kernel_ms": _g(rf["kernel_ms"], 5), "traffic": _g(rf["traffic"], 5) if rf.get("traffic") else None,
+        "valu_issue": _g(vi["frac"] if isinstance(vi, dict) else vi, 4),
+        "work": "%d txs x %s" % (rf["units_per_launch"], rf["work_per_unit"].split(" (")[0]),
+        "evidence": rf.get("traffic_source")}
+    cb = full.get("cpu_baseline")
+    line["cpu_baseline"] = None if not cb else {
+        "value": _g(cb["value"], 5), "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"],
+        "sample": cb["sample"], "full_host_estimate": _g(cb["full_host_estimate"]["value"], 4),
+        "physical_cores": cb["full_host_estimate"]["physical_cores"]}
+    line["kernel_source_sha"] = full.get("kernel_source_sha")
+    line["detail"] = full.get("detail_path")
+    line["summary"] = summarize(full, full["head_name"])
+    return line
+
+
+def dumps_line(line):
+    """Strict JSON: a NaN or infinity raises instead of printing a line the driver cannot parse."""
+    return json.dumps(line, allow_nan=False, separators=(",", ":"))
 
 
 def main():
@@ -902,8 +1096,14 @@ def main():
     ap.add_argument("--leg-seconds", type=float, default=2.0)
     ap.add_argument("--event-every", type=int, default=16,
                     help="record the kernel-duration HIP events on every N-th timed step (1 = every step)")
+    ap.add_argument("--devset", default="auto",
+                    help="device list for the one-process device-set legs (C4/C5 through bcosgpu_block_verify_multi): "
+                         "'auto' = every rank's GPU when N > 1, {0, 0} at N = 1; 'none' to skip; or e.g. '0,1'")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="where rank 0 writes the full record (every leg, notes, nested objects)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merkle", action="store_true")
+    ap.add_argument("--no-hashes", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the PCIe and createTransaction legs")
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU test of the --gpus launcher path only: spawn, rendezvous (gloo), max over ranks; no GPU work")
@@ -957,45 +1157,71 @@ def main():
             states.pop(wl)
         torch.cuda.empty_cache()
 
-    line = None
+    full = None
     if rank == 0:
         wl = WORKLOADS[args.workload]
-        line = {
+        full = {
             "metric": "sigs_per_sec", "value": head["value"], "unit": "tx/s (hash + recover/verify + sender%s)" % (
                 " + tx root" if args.workload in ("c4", "c5") else ""),
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
             "higher_is_better": True, "scaling": wl["scaling"], "vs_baseline": None,
             "dtype": "u32 (256-bit integer)",
             "data": "synthetic (distinct key per tx, 1%% bit-flipped s, 0.1%% v=4; valid frac %.4f)" % head["valid_frac"],
-            "config": {"workload": wl["name"], "txs_total": head["txs_total"], "txs_rank0": head["txs_rank0"],
+            "config": {"workload": wl["name"].split(":")[0], "txs_total": head["txs_total"],
+                       "txs_rank0": head["txs_rank0"],
                        "parallelism": "dp%d (%s)" % (world, "block shards" if args.workload == "c5" else "tx-index shards"),
-                       "timed_s": head["timed_s"], "warm_seconds": args.warm_seconds},
-            "roofline": head["roofline"], "cpu_baseline": None, "legs": legs,
-            "kernel_source_sha": kernel_source_sha(),
+                       "timed_s": _g(head["timed_s"], 5)},
+            "workload_detail": wl["name"], "warm_seconds": args.warm_seconds,
+            "head_name": args.workload, "head": head, "roofline": head["roofline"], "cpu_baseline": None,
+            "legs": legs, "kernel_source_sha": kernel_source_sha(),
         }
+    # the one-process device-set legs (the node's topology) on rank 0; the other ranks
+    # wait on the rendezvous store, not in a collective, so no RCCL kernel spins on their GPUs meanwhile
+    devset = None
+    if args.devset != "none":
+        if args.devset == "auto":
+            devset = list(range(world)) if world > 1 and torch.cuda.device_count() >= world else [local, local]
+        else:
+            devset = [int(x) for x in args.devset.split(",")]
+    if devset is not None and rank == 0:
+        full["devset"] = devset_legs(devset)
+    if devset is not None and world > 1:
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("bench_devset_done", "1")
+        else:
+            store.wait(["bench_devset_done"])
     if rank == 0 and world == 1:
         threads = cpu_threads()
         if not args.no_extras:
             b = head_state["batch"]
-            line["pcie_inclusive"] = host_api_rate(b, b.suite, head_state["n"])
-            line["create_transaction"] = create_transaction_leg(b, b.suite, head_state["n"], head_state["status"])
+            full["pcie_inclusive"] = host_api_rate(b, b.suite, head_state["n"])
+            full["create_transaction"] = create_transaction_leg(b, b.suite, head_state["n"], head_state["status"])
             from bcos_gpu import synth
             sm2b = synth.make_batch(1, 10_000, seed=0x5A3)
-            line["interface"] = interface_legs([(0, b), (1, sm2b)])
-            line["sealer_verify"] = sealer_verify_leg(threads)
+            full["interface"] = interface_legs([(0, b), (1, sm2b)])
+            full["sealer_verify"] = sealer_verify_leg(threads)
+        if not args.no_hashes:
+            full["hashes"] = hash_legs()
         if not args.no_merkle:
-            line["merkle"] = merkle_legs(0 if args.no_cpu_baseline else threads)
-            line["merkle_c1"] = {h: line["merkle"]["%s_w16_100k" % h] for h in ("keccak256", "sm3")}
+            full["merkle"] = merkle_legs(0 if args.no_cpu_baseline else threads)
         if not args.no_cpu_baseline:
             from bcos_gpu import synth
             batches = [(0, head_state["batch"], min(head_state["n"], 20000))]
             sm2 = states.get("c3", {}).get("batch") or synth.make_batch(1, 20000, seed=0x5A2)
             batches.append((1, sm2, 20000))
-            line["cpu_baseline"] = cpu_baseline(batches, threads)
-            line["cpu_baseline"]["merkle"] = line.get("merkle", {}).pop("cpu_baseline", None)
+            full["cpu_baseline"] = cpu_baseline(batches, threads)
+            full["cpu_baseline"]["merkle"] = (full.get("merkle") or {}).pop("cpu_baseline", None)
     if rank == 0:
-        line["summary"] = summarize(line, args.workload, head)  # last key: survives a tail-only record
-        print(json.dumps(line), flush=True)
+        full["head"] = {k: v for k, v in head.items()}
+        full["detail_path"] = args.detail_out
+        if args.detail_out:
+            d = os.path.dirname(args.detail_out)
+            if d:
+                os.makedirs(d, exist_ok=True)
+            with open(args.detail_out, "w") as f:
+                json.dump(full, f, indent=1, default=str)
+        print(dumps_line(compact_line(full)), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

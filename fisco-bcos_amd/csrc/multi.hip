@@ -21,6 +21,7 @@
 #include <thread>
 #include <utility>
 #include <vector>
+#include <cstdlib>
 #include <cstring>
 #include "engine.h"
 
@@ -183,17 +184,28 @@ Plan make_plan(uint64_t n, int ndev, int width) {
 std::mutex g_peer_mu;
 std::vector<std::pair<int, int>> g_peer_done;
 
+// BCOSGPU_MULTI_PEER=1 (read at each call; a test hook for one-GPU boxes): shards on devices[0] itself
+// also take the cross-device branches -- enable_peers' probe and the hipMemcpyPeerAsync gather (a peer
+// copy whose source and destination device are the same is legal) -- so a one-GPU run executes the code
+// a multi-GPU node runs
+bool force_peer() {
+    const char* v = std::getenv("BCOSGPU_MULTI_PEER");
+    return v && v[0] == '1';
+}
+
 // devices[0] reads the other devices' frontiers directly when the platform allows it (xGMI peer access);
 // otherwise hipMemcpyPeerAsync stages through the host
 void enable_peers(const int* devices, int ndev) {
+    const bool force = force_peer();
     std::lock_guard<std::mutex> g(g_peer_mu);
     for (int k = 1; k < ndev; ++k) {
         const std::pair<int, int> pr{devices[0], devices[k]};
-        if (pr.first == pr.second || std::find(g_peer_done.begin(), g_peer_done.end(), pr) != g_peer_done.end())
+        if ((pr.first == pr.second && !force) ||
+            std::find(g_peer_done.begin(), g_peer_done.end(), pr) != g_peer_done.end())
             continue;
         g_peer_done.push_back(pr);
         int can = 0;
-        if (hipDeviceCanAccessPeer(&can, pr.first, pr.second) == hipSuccess && can) {
+        if (hipDeviceCanAccessPeer(&can, pr.first, pr.second) == hipSuccess && can && pr.first != pr.second) {
             DeviceGuard dg(pr.first);
             (void)hipDeviceEnablePeerAccess(pr.second, 0);
         }
@@ -220,12 +232,13 @@ int gather_root(const int* devices, int ndev, const Plan& p, const std::vector<c
         SHARD_HIP(r->b[0].ensure(total * 32));
         SHARD_HIP(r->b[1].ensure((merkle_size(total, width) + 1) * 32));
         SHARD_HIP(r->b[2].ensure(32));
+        const bool peer_all = force_peer();
         uint64_t at = 0;
         for (int k = 0; k < ndev; ++k) {
             const uint64_t m = p.count(k);
             if (!m) continue;
             uint8_t* dst = r->b[0].as<uint8_t>() + 32 * at;
-            if (devices[k] == r->device)
+            if (devices[k] == r->device && !peer_all)
                 SHARD_HIP(hipMemcpyAsync(dst, frontier[k], 32 * m, hipMemcpyDeviceToDevice, r->stream));
             else
                 SHARD_HIP(hipMemcpyPeerAsync(dst, r->device, frontier[k], devices[k], 32 * m, r->stream));

@@ -8,11 +8,11 @@ WL=${1:-c2}; STEPS=${2:-10}; LIM=${3:-180}; TAG=${4:-$WL}
 OUT=gpurun_out/prof/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --warm-seconds 0 --legs= --no-cpu-baseline --no-merkle --no-extras"
+B="python3 bench.py --workload $WL --steps $STEPS --warmup 2 --warm-seconds 0 --legs= --no-cpu-baseline --no-merkle --no-extras --no-hashes --devset none --detail-out="
 # the trace pass at steady state: >= 2 s of warm-up launches and >= 2 s of timed ones, so the kernel's
 # average duration is the clock-settled one the bench line reports (the PMC passes serialise dispatches
 # and only count, so they stay short)
-BT="python3 bench.py --workload $WL --steps $((STEPS * 100)) --warmup 2 --warm-seconds 2 --legs= --no-cpu-baseline --no-merkle --no-extras"
+BT="python3 bench.py --workload $WL --steps $((STEPS * 100)) --warmup 2 --warm-seconds 2 --legs= --no-cpu-baseline --no-merkle --no-extras --no-hashes --devset none --detail-out="
 timeout -k 10 $LIM rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $BT > $OUT/trace.log 2>&1 && \
 timeout -s KILL $LIM rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B > $OUT/fetch.log 2>&1 && \
 timeout -s KILL $LIM rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B > $OUT/write.log 2>&1 && \

@@ -10,8 +10,8 @@ for tag in $WLS; do
   [ $tag = c4comb8 ] && { wl=c4; envs="BCOSGPU_TABLES=small"; }
   case $wl in c2|c2sm2) st=30;; *) st=3;; esac
   env $envs bash fisco-bcos_amd/tools/gpu_profile.sh $wl $st 240 $tag || exit $?
-  python3 fisco-bcos_amd/tools/prof_summary.py gpurun_out/prof/${R:-r04}_pmc_$tag.json gpurun_out/prof/$tag/trace \
+  python3 fisco-bcos_amd/tools/prof_summary.py gpurun_out/prof/${R:-r05}_pmc_$tag.json gpurun_out/prof/$tag/trace \
     gpurun_out/prof/$tag/fetch gpurun_out/prof/$tag/write gpurun_out/prof/$tag/sq gpurun_out/prof/$tag/valu || exit $?
-  cp $(find gpurun_out/prof/$tag/trace -name '*kernel_stats.csv' | head -1) gpurun_out/prof/${R:-r04}_kernel_stats_$tag.csv
+  cp $(find gpurun_out/prof/$tag/trace -name '*kernel_stats.csv' | head -1) gpurun_out/prof/${R:-r05}_kernel_stats_$tag.csv
 done
 echo done

@@ -7,6 +7,7 @@
 #   smoke                __graft_entry__.smoke()
 #   bench[=ARGS]         bench.py (default arguments = the driver's default run), ARGS with ',' for ' '
 #   profile=WL[,WL...]   rocprofv3 kernel trace + PMC passes per workload (tools/gpu_profile_all.sh)
+#   legprof[=LEGS]       rocprofv3 trace + PMC passes of the bench's Merkle / hash legs (tools/gpu_profile_legs.sh)
 #   sweep[=ARGS]         tools/small_sweep.py (ARGS with ',' for ' ')
 #   exe=PATH[,ARGS]      run a built tool from fisco-bcos_amd/lib (ARGS with ',' for ' ')
 #   ab=NAME[,ARGS]       bench.py ARGS with lib_ab/NAME/libbcosgpu.so swapped in (tools/build_ab.sh), then restored
@@ -33,7 +34,9 @@ for step in "$@"; do
     bench)
       timeout -k 10 600 python3 -u bench.py ${arg//,/ } > gpurun_out/bench_${n}.json 2> $log ;;
     profile)
-      R=${R:-r04} timeout -k 10 1100 bash fisco-bcos_amd/tools/gpu_profile_all.sh ${arg//,/ } > $log 2>&1 ;;
+      R=${R:-r05} timeout -k 10 1100 bash fisco-bcos_amd/tools/gpu_profile_all.sh ${arg//,/ } > $log 2>&1 ;;
+    legprof)
+      R=${R:-r05} timeout -k 10 1200 bash fisco-bcos_amd/tools/gpu_profile_legs.sh ${arg//,/ } > $log 2>&1 ;;
     sweep)
       timeout -k 10 900 python3 -u fisco-bcos_amd/tools/small_sweep.py ${arg//,/ } > gpurun_out/sweep_${n}.json 2> $log ;;
     exe)

@@ -4,8 +4,9 @@ root from per-GPU frontiers gathered on the first device (BlockImpl.h:111-154, S
 
 The box has one GPU, so the device lists repeat device 0 ({0, 0}, {0, 0, 0}): every shard still runs from
 its own host thread on its own stream and buffers, and the frontier gather is the same code (a device-local
-copy where devices differ would take hipMemcpyPeerAsync over xGMI -- that leg is unmeasured on hardware).
-Everything is compared with the oracle."""
+copy; BCOSGPU_MULTI_PEER=1 sends it through the hipMemcpyPeerAsync branch that distinct devices take --
+across two physical GPUs that branch is still unmeasured on hardware).  Everything is compared with the
+oracle."""
 import os
 import struct
 import subprocess
@@ -83,6 +84,31 @@ def test_device_sets_match_oracle(gpu, oracle, suite):
     # BlockImpl.h:114-119: no transactions -> the zero root
     e8, e64 = np.zeros(1, np.uint8), np.zeros(1, np.uint64)
     assert tx.verify_packed_multi([0, 0], suite_obj, e8, e64, e8, e64, width=2)[3] == bytes(32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("suite", [0, 1])
+def test_device_sets_peer_copy_branch(gpu, oracle, suite, monkeypatch):
+    """The cross-device code of the device-set path on a one-GPU box: BCOSGPU_MULTI_PEER=1 (read by
+    multi.hip at each call) sends shards that live on devices[0] itself through enable_peers' probe and
+    the hipMemcpyPeerAsync frontier gather (multi.hip gather_root) -- the branch a node with several GPUs
+    takes.  Every root, hash, verdict and sender against the oracle at sizes whose shards are empty,
+    ragged and width^L-aligned; device lists {0, 0} and {0, 0, 0}."""
+    from bcos_gpu import synth, tx
+    monkeypatch.setenv("BCOSGPU_MULTI_PEER", "1")
+    suite_obj = gpu.sm_suite() if suite else gpu.secp256k1_suite()
+    hasher = oracle.SM3 if suite else oracle.KECCAK256
+    for n in (2, 999, 20_001, 65_537):
+        b = synth.make_batch(suite, n, seed=0x9E + n + suite, flip_frac=0.05, bad_v_frac=0.02)
+        pre, po, sg, so = _host(b)
+        wh, ws, wst = oracle.tx_verify_packed(suite, pre, po, sg, so, nthreads=_threads())
+        for devs in ([0, 0], [0, 0, 0]):
+            for width in (2, 16):
+                th, snd, st, root = tx.verify_packed_multi(devs, suite_obj, pre, po, sg, so, width=width)
+                want_root = oracle.merkle(hasher, width, wh)
+                assert np.array_equal(st, wst) and np.array_equal(th, wh) and np.array_equal(snd, ws), (n, devs)
+                assert root == want_root, (n, devs, width)
+                assert tx.merkle_root_multi(devs, hasher, width, wh) == want_root, (n, devs, width)
 
 
 @pytest.mark.gpu
