@@ -6,6 +6,8 @@
 //   Merkle<Hasher,width>::generateMerkle  bcos-crypto/bcos-crypto/merkle/Merkle.h:170-208
 //     (per-level calculateLevelHashes :243-261 -> merkle_level_kernel, one node per lane)
 //   protocol::calculateMerkleProofRoot    bcos-protocol/bcos-protocol/ParallelMerkleProof.cpp:32-69
+#include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
 #include <utility>
@@ -555,45 +557,73 @@ __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restr
 
 // One counter slot (kFusedCounters counters) per launch queue: launches on one stream run in order and
 // each launch leaves its counters at zero, so a slot is clean for the next launch of its owner.
-//  - The owner is (device of the stream, stream handle), and for the null stream and hipStreamPerThread
-//    -- one handle that names a different stream per thread (per-thread default streams) -- also the
-//    calling thread, so two threads never share a slot through one handle.
+//  - Owners: a created stream by its unique id (hipStreamGetId; a destroyed stream's handle may come back
+//    for a new stream, its id does not, so a new stream never shares a slot with launches of the old one
+//    still in flight); the legacy null stream by its device (one in-order queue for every thread); the
+//    per-thread default stream (hipStreamPerThread) by the calling thread, whose slot goes back to the
+//    pool when that thread exits (after its stream drains).
 //  - A new slot is zeroed by hipMemsetAsync on the claiming stream (ordered before its first launch; no
 //    device-wide synchronisation), and a stream under capture never claims one (a capture may not
 //    allocate): it takes the multi-launch path.
 //  - Pools of kFusedSlots slots are added on demand up to kFusedPools per device; past that the
-//    multi-launch path runs (bit-identical, slower at latency sizes).
+//    multi-launch path runs (bit-identical, slower at latency sizes) and a line on stderr says so once.
 static constexpr uint32_t kFusedCounters = 16384, kFusedSlots = 64, kFusedPools = 16;
+namespace {
+struct SlotOwner {
+    int device;
+    int kind;  // 0 created stream (id), 1 legacy null stream, 2 per-thread default stream (thread), -1 free
+    unsigned long long id;
+    std::thread::id thread;
+};
+struct SlotPool {
+    int device;
+    uint32_t* base;
+    std::vector<SlotOwner> owners;
+};
+std::mutex g_slot_mu;
+std::vector<SlotPool>& slot_pools() {
+    static std::vector<SlotPool>* pools = new std::vector<SlotPool>();  // never destroyed (exit order)
+    return *pools;
+}
+// the calling thread's per-thread-stream slots, returned to their pools when the thread exits
+struct PerThreadSlots {
+    std::vector<std::pair<size_t, size_t>> held;  // (pool, slot)
+    ~PerThreadSlots() {
+        if (held.empty()) return;
+        (void)hipStreamSynchronize(hipStreamPerThread);  // its last launches have reset their counters
+        (void)hipGetLastError();
+        std::lock_guard<std::mutex> g(g_slot_mu);
+        for (auto& h : held) slot_pools()[h.first].owners[h.second].kind = -1;
+    }
+};
+thread_local PerThreadSlots t_slots;
+}  // namespace
+
 static uint32_t* fused_counter_slot(hipStream_t st) {
-    static std::mutex mu;
-    struct Owner {
-        int device;
-        hipStream_t stream;
-        std::thread::id thread;
-    };
-    struct Pool {
-        int device;
-        uint32_t* base;
-        std::vector<Owner> owners;
-    };
-    static std::vector<Pool> pools;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    const bool shared_handle = st == nullptr || st == hipStreamPerThread;
-    if (!shared_handle) {
+    SlotOwner me{dev, 0, 0, std::thread::id()};
+    if (st == nullptr) {
+        me.kind = 1;
+    } else if (st == hipStreamPerThread) {
+        me.kind = 2;
+        me.thread = std::this_thread::get_id();
+    } else {
         hipDevice_t sd = 0;
-        if (hipStreamGetDevice(st, &sd) != hipSuccess) {
+        if (hipStreamGetDevice(st, &sd) != hipSuccess || hipStreamGetId(st, &me.id) != hipSuccess) {
             (void)hipGetLastError();
             return nullptr;
         }
-        dev = sd;
+        me.device = dev = sd;
     }
-    const Owner me{dev, st, shared_handle ? std::this_thread::get_id() : std::thread::id()};
-    std::lock_guard<std::mutex> g(mu);
+    std::lock_guard<std::mutex> g(g_slot_mu);
+    std::vector<SlotPool>& pools = slot_pools();
     for (auto& q : pools) {
         if (q.device != dev) continue;
-        for (size_t k = 0; k < q.owners.size(); ++k)
-            if (q.owners[k].stream == me.stream && q.owners[k].thread == me.thread) return q.base + k * kFusedCounters;
+        for (size_t k = 0; k < q.owners.size(); ++k) {
+            const SlotOwner& o = q.owners[k];
+            if (o.kind == me.kind && o.id == me.id && o.thread == me.thread) return q.base + k * kFusedCounters;
+        }
     }
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(st, &cap) != hipSuccess) {
@@ -601,15 +631,36 @@ static uint32_t* fused_counter_slot(hipStream_t st) {
         return nullptr;
     }
     if (cap != hipStreamCaptureStatusNone) return nullptr;
-    Pool* pool = nullptr;
+    // a returned slot (zero counters: its thread's stream drained), else a new one in a pool with room
+    size_t pi = pools.size(), si = 0;
     int npools = 0;
-    for (auto& q : pools)
-        if (q.device == dev) {
-            ++npools;
-            if (q.owners.size() < kFusedSlots) pool = &q;
+    for (size_t q = 0; q < pools.size() && pi == pools.size(); ++q) {
+        if (pools[q].device != dev) continue;
+        ++npools;
+        for (size_t k = 0; k < pools[q].owners.size(); ++k)
+            if (pools[q].owners[k].kind == -1) {
+                pi = q;
+                si = k;
+                break;
+            }
+    }
+    if (pi == pools.size()) {
+        for (size_t q = 0; q < pools.size(); ++q)
+            if (pools[q].device == dev && pools[q].owners.size() < kFusedSlots) {
+                pi = q;
+                si = pools[q].owners.size();
+                break;
+            }
+    }
+    if (pi == pools.size()) {
+        if (npools >= static_cast<int>(kFusedPools)) {
+            static std::atomic<bool> warned{false};
+            if (!warned.exchange(true))
+                std::fprintf(stderr, "bcosgpu: the one-launch Merkle path's %u counter slots on device %d are all "
+                                     "owned (one per stream); further streams take the multi-launch path\n",
+                             kFusedSlots * kFusedPools, dev);
+            return nullptr;
         }
-    if (!pool) {
-        if (npools >= static_cast<int>(kFusedPools)) return nullptr;
         int prev = dev;
         (void)hipGetDevice(&prev);
         if (prev != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
@@ -620,15 +671,22 @@ static uint32_t* fused_counter_slot(hipStream_t st) {
             (void)hipGetLastError();
             return nullptr;
         }
-        pools.push_back(Pool{dev, static_cast<uint32_t*>(b), {}});
-        pool = &pools.back();
+        pools.push_back(SlotPool{dev, static_cast<uint32_t*>(b), {}});
+        pi = pools.size() - 1;
+        si = 0;
     }
-    uint32_t* slot = pool->base + pool->owners.size() * kFusedCounters;
-    if (hipMemsetAsync(slot, 0, sizeof(uint32_t) * kFusedCounters, st) != hipSuccess) {
+    SlotPool& pool = pools[pi];
+    uint32_t* slot = pool.base + si * kFusedCounters;
+    const bool fresh = si == pool.owners.size();
+    if (fresh && hipMemsetAsync(slot, 0, sizeof(uint32_t) * kFusedCounters, st) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
-    pool->owners.push_back(me);
+    if (fresh)
+        pool.owners.push_back(me);
+    else
+        pool.owners[si] = me;
+    if (me.kind == 2) t_slots.held.emplace_back(pi, si);
     return slot;
 }
 
@@ -830,8 +888,10 @@ static int launch_merkle_climb(int hasher, int width, const uint8_t* d_leaves, u
         }
     }
     f.t = t;
+    // width^(g - 1) <= 8 (SM3: 64) first-level nodes per step, and the step's width^g gathered children
+    // fit one LDS half (lds[0], 256 nodes): the step's first level writes lds[1] while reading them
     f.g = 1;
-    for (int q = width; q <= (hasher == KECCAK256 ? 8 : 64); q *= width) ++f.g;  // width^(g - 1) <= 8 (64)
+    for (int q = width; q <= (hasher == KECCAK256 ? 8 : 64) && q * width <= 256; q *= width) ++f.g;
     const uint64_t wgs = (t.cnt[0] + f.B - 1) / f.B;
     if (wgs > kClimbMaxWgs) return 1;
     // one workgroup per CU: the latency schedule (25-lane groups from eight nodes down, lane pairs above,

@@ -11,8 +11,9 @@
  *       verify(PublicPtr) (SM2Crypto.cpp:66-79) is overridden, so SM2Crypto::recover (:81-92), the bytes
  *       overload (:29-34) and recoverAddress (:94-122) -- all of which call it -- run on the GPU;
  *       m_verifier is a wedpr-shaped lambda over the same call; m_signer stays wedpr's.
- *       recoverAddress (:94-122) is overridden as well: all 160 input bytes are read (the reference copies
- *       16 and reads the rest uninitialised) and an engine error throws, as on secp256k1.
+ *       recoverAddress (:94-122) is overridden as well, with the reference's behaviour (it copies only 16
+ *       input bytes into zero-initialised fields, so it returns {false, {}} for every input), except that
+ *       an engine error throws SignException, as on secp256k1.
  *   Both take a device, or a device SET (all GPUs of the node, one process), at construction and use it
  *   from every thread (TBB workers included); the calling thread's current device is never changed.
  *   Single calls go to the set's devices in turn (each device coalesces its own callers).
@@ -144,15 +145,18 @@ public:
             _hash, _signatureData);
     }
 
-    // Secp256k1Crypto::recoverAddress -> secp256k1Recover(hashImpl, input) (Secp256k1Crypto.cpp:95-124):
-    // input = hash || v || r || s (32 bytes each, zero-padded); v must be 27 or 28 as a 256-bit number;
-    // {true, right160(H(pub))} or {false, {}}.  (The reference copies min(size, sizeof(bytesConstRef))
-    // bytes of the input into its struct -- 16 -- and reads the rest uninitialised; this reads all 128.)
+    // Secp256k1Crypto::recoverAddress -> secp256k1Recover(hashImpl, input) (Secp256k1Crypto.cpp:95-124),
+    // restated as the reference runs it: the input is meant as hash || v || r || s (32 bytes each), but the
+    // reference copies only min(size, sizeof(bytesConstRef)) = 16 bytes of it (:104) into a struct whose
+    // FixedBytes members the constructors zero (FixedBytes.h:94).  So v reads 0, never 27 or 28, and the
+    // result is {false, {}} for every input; kRefCopy keeps that copy length, so the body below is the
+    // reference's logic, not a constant.
     std::pair<bool, bcos::bytes> recoverAddress(
         bcos::crypto::Hash::Ptr _hashImpl, bcos::bytesConstRef _in) const override
     {
+        constexpr size_t kRefCopy = sizeof(bcos::bytesConstRef);
         uint8_t in[128] = {0};
-        std::memcpy(in, _in.data(), _in.size() < 128 ? _in.size() : 128);
+        std::memcpy(in, _in.data(), _in.size() < kRefCopy ? _in.size() : kRefCopy);
         bool vOk = in[63] == 27 || in[63] == 28;
         for (int i = 32; i < 63; ++i)
         {
@@ -258,16 +262,18 @@ public:
     }
     using bcos::crypto::SM2Crypto::verify;
 
-    // SM2Crypto::recoverAddress (SM2Crypto.cpp:94-122): input = hash || pub || r || s (32 / 64 / 32 / 32
-    // bytes, zero-padded); verify against pub, then {true, right160(H(pub))}, else {false, {}}.  All 160
-    // bytes are read (the reference copies min(size, sizeof(bytesConstRef)) = 16 into its struct and reads
-    // the rest uninitialised); an engine error throws SignException, as GpuSecp256k1Crypto's does (the
-    // inherited body would swallow it into {false, {}}).
+    // SM2Crypto::recoverAddress (SM2Crypto.cpp:94-122), restated as the reference runs it: the input is
+    // meant as hash || pub || r || s (32 / 64 / 32 / 32 bytes), but only min(size, sizeof(bytesConstRef))
+    // = 16 bytes are copied (:103) into zero-initialised FixedBytes (FixedBytes.h:94), so pub, r and s are
+    // zero, the verify fails and the result is {false, {}} for every input (kRefCopy keeps that length).
+    // One deliberate difference: an engine error throws SignException, as everywhere in these adapters,
+    // where the reference's catch-all would turn it into {false, {}} (a dead GPU must be visible).
     std::pair<bool, bcos::bytes> recoverAddress(
         bcos::crypto::Hash::Ptr _hashImpl, bcos::bytesConstRef _in) const override
     {
+        constexpr size_t kRefCopy = sizeof(bcos::bytesConstRef);
         uint8_t in[160] = {0};
-        std::memcpy(in, _in.data(), _in.size() < 160 ? _in.size() : 160);
+        std::memcpy(in, _in.data(), _in.size() < kRefCopy ? _in.size() : kRefCopy);
         uint8_t rs[64];
         std::memcpy(rs, in + 96, 64);
         const int rc = bcosgpu_sm2_verify(m_set.next(), in + 32, in, rs);

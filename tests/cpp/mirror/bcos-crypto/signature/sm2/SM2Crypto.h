@@ -56,9 +56,10 @@ public:
         throw SignException() << errinfo_comment("host-side (wedpr) in the reference");
     }
     // SM2Crypto.cpp:94-122: input = hash || pub || r || s, of which the reference copies only
-    // min(size, sizeof(bytesConstRef)) = 16 bytes into its struct (the rest is indeterminate there, zero
-    // here); verify (the virtual) against pub, then calculateAddress = right160(H(pub)); any exception
-    // -> {false, {}}.  GpuSM2Crypto overrides this (all 160 bytes, engine errors throw).
+    // min(size, sizeof(bytesConstRef)) = 16 bytes into its struct (FixedBytes members, zero-initialised
+    // by their constructors, FixedBytes.h:94); verify (the virtual) against pub, then calculateAddress =
+    // right160(H(pub)); any exception -> {false, {}}.  GpuSM2Crypto overrides this with the same copy
+    // (engine errors throw there).
     std::pair<bool, bytes> recoverAddress(Hash::Ptr _hashImpl, bytesConstRef _input) const override
     {
         byte in[160] = {0};

@@ -106,15 +106,18 @@ int main() {
     CHECK(k1.verify(std::make_shared<const bytes>(pub->data()), mh, bytesConstRef(sig)));
     CHECK(!k1.verify(std::make_shared<const bytes>(pub->data()), hash_of(
         "48bed44d1bcd124a28c27f343a817e5f5243190d3c52bf347daf876de1dbbf77"), bytesConstRef(sig)));
-    // recoverAddress (Secp256k1Crypto.cpp:95-124): hash || v || r || s, v = 27 / 28
+    // recoverAddress (Secp256k1Crypto.cpp:95-124): meant as hash || v || r || s, v = 27 / 28 -- but the
+    // reference copies only sizeof(bytesConstRef) = 16 bytes into zeroed fields (:104), so v reads 0 and
+    // even a valid ecrecover input gives {false, {}}; the adapter keeps that behaviour
     auto keccak = std::make_shared<GpuKeccak>();
+    CHECK(sizeof(bytesConstRef) == 16);
     {
         bytes in(128, 0);
         std::memcpy(in.data(), mh.data(), 32);
         in[63] = 27;
         std::memcpy(in.data() + 64, sig.data(), 64);
         auto ra = k1.recoverAddress(keccak, bytesConstRef(in));
-        CHECK(ra.first && ra.second.size() == 20 && std::memcmp(ra.second.data(), want, 20) == 0);
+        CHECK(!ra.first && ra.second.empty());
         in[63] = 29;
         CHECK(!k1.recoverAddress(keccak, bytesConstRef(in)).first);
         in[63] = 27;
@@ -152,7 +155,7 @@ int main() {
     CHECK(throws_invalid([&] { s2.recover(mh, bytesConstRef(sm2sig)); }));  // wrong hash: SM2 rejects
     auto sb = sm2.recoverBatch({sm3abcd, sm3abcd}, {bytesConstRef(sm2sig), bytesConstRef(sm2bad)});
     CHECK(sb.size() == 2 && sb[0] && !sb[1]);
-    // the bytes overload (SM2Crypto.cpp:29-34) and recoverAddress (:94-122) reach the GPU through verify
+    // the bytes overload (SM2Crypto.cpp:29-34) reaches the GPU through verify
     bytes sm2pub(sm2sig.begin() + 64, sm2sig.end());
     CHECK(s2.verify(std::make_shared<const bytes>(sm2pub), sm3abcd, bytesConstRef(sm2sig)));
     CHECK(!s2.verify(std::make_shared<const bytes>(sm2pub), sm3abcd, bytesConstRef(sm2bad)));
@@ -161,9 +164,10 @@ int main() {
         std::memcpy(in.data(), sm3abcd.data(), 32);
         std::memcpy(in.data() + 32, sm2pub.data(), 64);
         std::memcpy(in.data() + 96, sm2sig.data(), 64);
+        // the reference's 16-byte copy (SM2Crypto.cpp:103): pub, r, s read as zero -> {false, {}} even for
+        // the KAT's valid hash || pub || r || s
         auto ra = s2.recoverAddress(keccak, bytesConstRef(in));
-        HashType kp = keccak->hash(bytesConstRef(sm2pub));
-        CHECK(ra.first && ra.second.size() == 20 && std::memcmp(ra.second.data(), kp.data() + 12, 20) == 0);
+        CHECK(!ra.first && ra.second.empty());
         in[100] ^= 1;
         CHECK(!s2.recoverAddress(keccak, bytesConstRef(in)).first);
     }

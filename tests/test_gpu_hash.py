@@ -216,8 +216,9 @@ def test_merkle_subtree_then_climb(gpu, oracle, hasher):
     sizes for width 2 on 256 CUs); every entry of the output vector, both hashers."""
     rng = np.random.default_rng(79 + hasher)
     H = gpu.Keccak256() if hasher == 0 else gpu.SM3()
+    # (widths 7 and 8: the climb step is capped so its width^g gathered children fit one LDS half)
     for width, n in ((2, 153_607), (2, 400_005), (2, 1_000_003), (4, 1_000_001), (3, 600_001), (5, 400_001),
-                     (16, 2_000_003)):
+                     (7, 1_500_001), (8, 1_200_007), (16, 2_000_003)):
         leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
         got = gpu.Merkle(H, width).generate_merkle([leaves[i].tobytes() for i in range(n)])
         _, want = oracle.merkle(hasher, width, leaves, want_tree=True)
