@@ -64,6 +64,10 @@ _SIGS = {
     "bcosgpu_sm2_sign_batch_dev": (_I, [_P, _P, _SZ, _P, _P, _P]),
     "bcosgpu_verify_batch": (_I, [_I, _P, _P, _P, _SZ, _SZ, _P]),
     "bcosgpu_verify_batch_dev": (_I, [_I, _P, _P, _P, _SZ, _SZ, _P, _P]),
+    "bcosgpu_register_keys": (_I, [_I, _I, _P, _SZ, _P]),
+    "bcosgpu_verify_keyed_batch_dev": (_I, [_I, _P, _P, _P, _SZ, _SZ, _P, _P]),
+    "bcosgpu_key_cache_info": (_I, [_I, _I, _P]),
+    "bcosgpu_clear_keys": (_I, [_I, _I]),
     "bcosgpu_ecrecover_batch": (_I, [_P, _SZ, _P, _P]),
     "bcosgpu_ecrecover_batch_dev": (_I, [_P, _SZ, _P, _P, _P]),
     "bcosgpu_tx_verify_batch": (_I, [_I, _P, _P, _P, _P, _SZ, _P, _P, _P]),
@@ -140,3 +144,29 @@ def set_tx_kernel_policy(split=-1, occupancy=0, coop=2, field=1):
     """bcosgpu_set_tx_kernel_policy: force a tx-verify kernel variant (tests / tuning); the defaults
     restore the size-based choice (field 1: the 10 x 26-bit secp256k1 point arithmetic)."""
     check(lib().bcosgpu_set_tx_kernel_policy(split, occupancy, coop, field))
+
+
+def register_keys(suite, pubs, device=0):
+    """bcosgpu_register_keys: comb tables for the keys pubs uint8[n, 64] (the sealer set) on `device`.
+    Returns the int32 slot of each key (-1 where the cache is full)."""
+    import numpy as np
+    ensure_device(device)
+    p = np.ascontiguousarray(pubs, dtype=np.uint8).reshape(-1, 64)
+    slots = np.full(p.shape[0], -1, dtype=np.int32)
+    if p.shape[0]:
+        rc = lib().bcosgpu_register_keys(device, suite, p.ctypes.data, p.shape[0], slots.ctypes.data)
+        if rc < 0:
+            check(rc)
+    return slots
+
+
+def key_cache_info(suite, device=0):
+    """{keys, capacity, keyed (signatures verified on the registered-key kernel), generic, built}."""
+    import numpy as np
+    out = np.zeros(5, dtype=np.int64)
+    check(lib().bcosgpu_key_cache_info(device, suite, out.ctypes.data))
+    return dict(zip(("keys", "capacity", "keyed", "generic", "built"), (int(x) for x in out)))
+
+
+def clear_keys(suite, device=0):
+    check(lib().bcosgpu_clear_keys(device, suite))

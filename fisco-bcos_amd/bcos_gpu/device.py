@@ -71,6 +71,15 @@ def merkle_roots_batch(hasher, width, leaves, block_off, work, roots, stream=Non
                                                _p(work), _p(roots), _s(stream)))
 
 
+def verify_keyed(suite, slots, hashes, sigs, ok, stream=None):
+    """SignatureCrypto::verify against registered keys (bcosgpu_verify_keyed_batch_dev): slots int32[n]
+    (from _lib.register_keys), hashes uint8[n,32], sigs uint8[n, stride >= 64] (r || s read) -> ok uint8[n]."""
+    _dev(ok)
+    n = slots.numel()
+    check(lib().bcosgpu_verify_keyed_batch_dev(suite, _p(slots), _p(hashes), _p(sigs), sigs.shape[1] if n else 64, n,
+                                               _p(ok), _s(stream)))
+
+
 def secp256k1_recover(hashes, sigs, pub, addr, ok, stream=None):
     """hashes uint8[n,32], sigs uint8[n,65] -> pub uint8[n,64] (or None), addr uint8[n,20] (or None), ok uint8[n]."""
     _dev(hashes)

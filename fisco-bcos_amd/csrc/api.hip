@@ -520,6 +520,49 @@ int bcosgpu_verify_batch(int suite, const uint8_t* pub64, const uint8_t* hash32,
     return run_job(dev, job);
 }
 
+// ------------------------------------------------------------------ registered keys (ecc_keyed.hip)
+int bcosgpu_register_keys(int device, int suite, const uint8_t* pub64, size_t n, int32_t* slots) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return set_err(BCOSGPU_E_ARG, "bad suite");
+    if (n && (!pub64 || !slots)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    if (int rc = ready_device(device)) return rc;
+    int prev = -1;
+    if (hipGetDevice(&prev) != hipSuccess) {
+        (void)hipGetLastError();
+        prev = -1;
+    }
+    if (prev != device && hipSetDevice(device) != hipSuccess) return set_err(BCOSGPU_E_HIP, "hipSetDevice failed");
+    bool all = false;
+    const int rc = keyed_slots(suite, pub64, 64, n, slots, true, &all, nullptr);
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    if (rc) return set_err(rc, "key table build failed");
+    int cached = 0;
+    for (size_t i = 0; i < n; ++i) cached += slots[i] >= 0;
+    return cached;
+}
+
+int bcosgpu_verify_keyed_batch_dev(int suite, const int32_t* d_slots, const uint8_t* d_hash32, const uint8_t* d_sig,
+                                   size_t sig_stride, size_t n, uint8_t* d_ok, void* stream) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return set_err(BCOSGPU_E_ARG, "bad suite");
+    if (sig_stride < 64 || sig_stride > 0xFFFFFFFFull) return set_err(BCOSGPU_E_ARG, "signature stride must be >= 64");
+    if (n && (!d_slots || !d_hash32 || !d_sig || !d_ok)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    const int rc = launch_sig_verify_keyed(suite, d_slots, d_hash32, d_sig, static_cast<uint32_t>(sig_stride), n, d_ok,
+                                           nullptr, as_stream(stream));
+    return rc ? set_err(rc, rc == BCOSGPU_E_ARG ? "no key registered on this device" : "keyed verify launch failed") : 0;
+}
+
+int bcosgpu_key_cache_info(int device, int suite, int64_t* out5) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return set_err(BCOSGPU_E_ARG, "bad suite");
+    if (!out5) return set_err(BCOSGPU_E_ARG, "null pointer");
+    const int rc = keyed_cache_info(device, suite, out5);
+    return rc ? set_err(rc, "bad device") : 0;
+}
+
+int bcosgpu_clear_keys(int device, int suite) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return set_err(BCOSGPU_E_ARG, "bad suite");
+    const int rc = keyed_clear(device, suite);
+    return rc ? set_err(rc, "clearing the key cache failed") : 0;
+}
+
 int bcosgpu_ecrecover_batch_dev(const uint8_t* d_in128, size_t n, uint8_t* d_out32, uint8_t* d_ok, void* stream) {
     if (n && (!d_in128 || !d_out32 || !d_ok)) return set_err(BCOSGPU_E_ARG, "null pointer");
     int rc = launch_ecrecover(d_in128, n, d_out32, d_ok, as_stream(stream));

@@ -149,7 +149,10 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
         const int levels = least >= greatest ? least - greatest + 1 : 1;
         BATCH_HIP(hipStreamCreateWithPriority(&slot.stream, hipStreamNonBlocking, least - slot.index % levels));
     }
-    const size_t in_bytes = kInPer[kind] * n, out_bytes = kOutPer[kind] * n;
+    // verify kinds stage the keys' cache slots (int32 per item) after the input (registered-key path)
+    const bool verify = kind == kSigJobVerifyK1 || kind == kSigJobVerifySM2;
+    const size_t slots_at = kInPer[kind] * n;
+    const size_t in_bytes = slots_at + (verify ? 4 * n : 0), out_bytes = kOutPer[kind] * n;
     BATCH_HIP(ensure_pinned(slot.h_in, slot.hd_in, slot.h_in_cap, in_bytes));
     BATCH_HIP(ensure_pinned(slot.h_out, slot.hd_out, slot.h_out_cap, out_bytes));
     static const size_t zero_copy_max = [] {
@@ -190,11 +193,26 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
         }
         at += m;
     }
+    // every key of the batch registered (or promoted now): the registered-key kernel (ecc_keyed.hip)
+    bool keyed = false;
+    if (verify) {
+        const int suite = kind == kSigJobVerifySM2 ? BCOSGPU_SUITE_SM2 : BCOSGPU_SUITE_SECP256K1;
+        const uint8_t* pubs = kind == kSigJobVerifySM2 ? in + 32 * n + 64 : in;
+        const int krc = keyed_slots(suite, pubs, kind == kSigJobVerifySM2 ? 128 : 64, n,
+                                    reinterpret_cast<int32_t*>(in + slots_at), false, &keyed, slot.stream);
+        if (krc) keyed = false;  // a failed table build leaves the generic path
+    }
     if (!zero_copy) BATCH_HIP(hipMemcpyAsync(slot.d_in, slot.h_in, in_bytes, hipMemcpyHostToDevice, slot.stream));
     const uint8_t* di = zero_copy ? slot.hd_in : slot.d_in;
     uint8_t* dout = zero_copy ? slot.hd_out : slot.d_out;
     int rc;
-    if (kind == kSigJobRecoverK1)
+    if (keyed && kind == kSigJobVerifySM2)
+        rc = launch_sig_verify_keyed(BCOSGPU_SUITE_SM2, reinterpret_cast<const int32_t*>(di + slots_at), di, di + 32 * n,
+                                     128, n, dout + 20 * n, want_addr ? dout : nullptr, slot.stream);
+    else if (keyed)
+        rc = launch_sig_verify_keyed(BCOSGPU_SUITE_SECP256K1, reinterpret_cast<const int32_t*>(di + slots_at),
+                                     di + 64 * n, di + 96 * n, 64, n, dout, nullptr, slot.stream);
+    else if (kind == kSigJobRecoverK1)
         rc = launch_secp256k1_recover(di, di + 32 * n, 65, n, want_pub ? dout : nullptr,
                                       want_addr ? dout + 64 * n : nullptr, dout + 84 * n, slot.stream);
     else if (kind == kSigJobVerifySM2)

@@ -1,0 +1,638 @@
+// ecc_keyed.hip -- signature verification against REGISTERED public keys: the sealer path.
+//
+// SignatureCrypto::verify(pub, hash, sig) is called with a small, fixed set of keys on the block-check
+// path: BlockValidator::checkSignatureList verifies one signature per sealer of the block against the
+// consensus node list's keys (bcos-pbft/.../BlockValidator.cpp:141-182), PBFTCacheProcessor::
+// checkPrecommitWeight likewise (PBFTCacheProcessor.cpp:795-821), both through Secp256k1Crypto.cpp:51-63 /
+// SM2Crypto.cpp:66-79.  With the key known in advance, its variable-base multiplication needs no
+// doublings at verify time: the engine keeps an 8-bit comb table per key (32 windows x 256 affine
+// multiples b 2^(8i) P, 512 KiB of HBM, built once by key_table_kernel), so u2 P (secp256k1) / t P (SM2)
+// is 32 table lookups, like u1 G / s G over G's 16-bit comb (16 lookups).
+//
+// The verify kernel spends 16 lanes (one DPP row) on each signature, 4 signatures per wave:
+//   - every lane of the 16 runs the scalar work (range checks, s^-1 mod n and u1, u2 for secp256k1;
+//     t = r + s and e = SM3(Z_A || h) with Z_A cached per key for SM2) -- in lockstep, so it costs the
+//     same as on one lane;
+//   - lane L sums its three table points (windows 2L, 2L+1 of the key's comb, window L of G's 16-bit
+//     comb; the 8-bit G comb adds windows 2L, 2L+1 of it instead) with complete mixed additions;
+//   - four levels of complete Jacobian additions reduce the 16 partial sums inside the row (partners
+//     fetched with ds_bpermute), then the projective x-check (no inversion) gives the verdict.
+// Critical path: secp256k1 ~ s^-1 + 3 madds + 4 adds, SM2 ~ 2 SM3 compressions + 3 madds + 4 adds --
+// against 256 doublings per signature on the generic path.  Same decisions and verdicts as
+// secp256k1_verify_lane26 / sm2_verify_rs26 (libsecp256k1 ecdsa_verify with low-S; sm2_do_verify), for
+// every input: the additions are the complete ones (P = Q, P = -Q, infinity), since a key's owner can
+// pick u1, u2 so that two partial sums coincide.
+//
+// Host side: a per-(device, suite) cache of key tables, filled by bcosgpu_register_keys (the node's
+// consensus list) and by promotion of keys seen in two calls; never evicted while the process runs
+// (bcosgpu_clear_keys drains the device first), so a table is never rewritten under a launch that reads
+// it.  The coalesced host-pointer verify calls take this path when every key of the batch is cached.
+#include <array>
+#include <unordered_map>
+#include "ecc_device.h"
+
+namespace bcosgpu {
+
+// per key slot: a 64-word header, then the comb table [32 windows][256 entries][x[8] y[8]]
+//   header: [0..7] x, [8..15] y (canonical, plain), [16..23] Z_A (SM2: SM3 state words), [24..28] the
+//   address right160(H(pub)) as the kernels store it (Keccak256 secp256k1 / SM3 SM2), [32] 1 = valid key
+//   (coordinates < p, on the curve)
+static constexpr size_t kKeyHdrWords = 64;
+static constexpr size_t kKeySlotWords = kKeyHdrWords + kTabWords;
+static constexpr int kKeyEntriesPerKey = kCombWindows * kCombEntries;  // 8192 table lanes per key
+
+// SM2 Z_A = SM3(ENTL || ID || a || b || xG || yG || xA || yA): the key-independent 128-byte prefix is the
+// constant midstate kZaMid, then two blocks (as sm2_e's first half)
+__device__ __forceinline__ void sm2_za(uint32_t V[8], const uint32_t X[8], const uint32_t Y[8]) {
+    uint32_t W[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) V[i] = kZaMid[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) W[j] = kZaW32[j];
+    W[4] = kZaC36 | (X[0] >> 16);
+#pragma unroll
+    for (int j = 1; j < 8; ++j) W[4 + j] = (X[j - 1] << 16) | (X[j] >> 16);
+    W[12] = (X[7] << 16) | (Y[0] >> 16);
+#pragma unroll
+    for (int j = 1; j < 4; ++j) W[12 + j] = (Y[j - 1] << 16) | (Y[j] >> 16);
+    sm3_compress(V, W);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) W[j] = (Y[j + 3] << 16) | (Y[j + 4] >> 16);
+    W[4] = (Y[7] << 16) | 0x8000u;
+#pragma unroll
+    for (int j = 5; j < 15; ++j) W[j] = 0;
+    W[15] = 210u * 8u;
+    sm3_compress(V, W);
+}
+
+// e = SM3(Z_A || hash) (sm2_e's second half)
+__device__ __forceinline__ void sm2_e_from_za(fe& e, const uint32_t* za, const fe& hash_be) {
+    uint32_t V[8], W[16];
+    sm3_init(V);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) W[j] = za[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) W[8 + j] = hash_be.v[7 - j];
+    sm3_compress(V, W);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) W[j] = 0;
+    W[0] = 0x80000000u;
+    W[15] = 512u;
+    sm3_compress(V, W);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e.v[i] = V[7 - i];
+}
+
+// ------------------------------------------------------------------ table build
+// lane (key k, window i, entry b): b 2^(8i) P by an 8-bit double-and-add of P and 8i doublings, one
+// inversion to affine.  secp256k1 entries are canonical plain words; SM2 entries canonical words of the
+// R' = 2^286 Montgomery form (the layout of the fp26 G tables, tables_sm2_26).  Entry 0 holds 1 2^(8i) P
+// (a valid point the kernels never select).  An invalid key (coordinates >= p or off the curve) gets
+// G's multiples and valid = 0, which makes every verify against it fail, as the reference's does.
+template <int SUITE>
+__global__ __launch_bounds__(256) void key_table_kernel(uint32_t* __restrict__ arena, const int32_t* __restrict__ slots,
+                                                        const uint8_t* __restrict__ pubs, uint32_t nkeys) {
+    const uint64_t idx = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (idx >= static_cast<uint64_t>(nkeys) * kKeyEntriesPerKey) return;
+    const uint32_t k = static_cast<uint32_t>(idx / kKeyEntriesPerKey);
+    const uint32_t ent = static_cast<uint32_t>(idx % kKeyEntriesPerKey);
+    const int win = static_cast<int>(ent / kCombEntries);
+    uint32_t b = ent % kCombEntries;
+    if (b == 0) b = 1;
+    uint32_t* slot = arena + static_cast<size_t>(slots[k]) * kKeySlotWords;
+    uint32_t* out = slot + kKeyHdrWords + static_cast<size_t>(ent) * 16;
+    ByteReader rp(pubs + 64ull * k, 64);
+    uint32_t w[8], X[8], Y[8];
+    fe px, py;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        X[q] = bswap32(rp.word(q));
+        Y[q] = bswap32(rp.word(8 + q));
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w[q] = rp.word(q);
+    fe_from_be_words(px, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w[q] = rp.word(8 + q);
+    fe_from_be_words(py, w);
+    if constexpr (SUITE == BCOSGPU_SUITE_SECP256K1) {
+        bool valid = fe_lt_k(px, FieldK1::P) && fe_lt_k(py, FieldK1::P);
+        Aff26 P;
+        fe26_from_fe(P.x, px);
+        fe26_from_fe(P.y, py);
+        {
+            fe26 l, rr, t, seven;
+            fe26_sqr(l, P.y);
+            fe26_sqr(t, P.x);
+            fe26_mul(rr, t, P.x);
+            fe26_set_small(seven, 7u);
+            fe26_add(rr, rr, seven);
+            fe26_sub<3>(l, l, rr);
+            valid = valid && fe26_is_zero(l);
+        }
+        if (!valid) {
+            fe26_const(P.x, kK1Gx);
+            fe26_const(P.y, kK1Gy);
+        }
+        Jac26 acc, S;
+        CurveK1x::set_inf(acc);
+#pragma unroll 1
+        for (int bit = 7; bit >= 0; --bit) {
+            CurveK1x::dbl(acc, acc);
+            CurveK1x::madd(S, acc, P);
+            CurveK1x::cmov(acc, S, ((b >> bit) & 1u) != 0u);
+        }
+#pragma unroll 1
+        for (int d = 0; d < 8 * win; ++d) CurveK1x::dbl(acc, acc);
+        fe z, zi;
+        fe26_to_fe(z, acc.Z);
+        modinv_safegcd(zi, z, kMod30K1P);
+        fe26 Zi, Zi2, Zi3, ax, ay;
+        fe26_from_fe(Zi, zi);
+        fe26_sqr(Zi2, Zi);
+        fe26_mul(Zi3, Zi2, Zi);
+        fe26_mul(ax, acc.X, Zi2);
+        fe26_mul(ay, acc.Y, Zi3);
+        fe x, y;
+        fe26_to_fe(x, ax);
+        fe26_to_fe(y, ay);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            out[q] = x.v[q];
+            out[8 + q] = y.v[q];
+        }
+        if (ent == 0) {
+            uint32_t a[5];
+            keccak_address(a, px, py);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                slot[q] = px.v[q];
+                slot[8 + q] = py.v[q];
+                slot[16 + q] = 0;
+            }
+#pragma unroll
+            for (int q = 0; q < 5; ++q) slot[24 + q] = a[q];
+            slot[32] = valid ? 1u : 0u;
+        }
+    } else {
+        bool valid = fe_lt_k(px, ParamP2::M) && fe_lt_k(py, ParamP2::M);
+        AffP26 P;
+        fp26_from_plain(P.x, px);
+        fp26_from_plain(P.y, py);
+        valid = valid && sm2_on_curve26(P);
+        if (!valid) {
+            fe gx, gy;
+            fe_set(gx, kSM2Gx);  // Montgomery (R = 2^256) form: back to plain first
+            fe_set(gy, kSM2Gy);
+            FieldP2::to_plain(gx, gx);
+            FieldP2::to_plain(gy, gy);
+            fp26_from_plain(P.x, gx);
+            fp26_from_plain(P.y, gy);
+        }
+        JacP26 acc, S;
+        CurveSM2x::set_inf(acc);
+#pragma unroll 1
+        for (int bit = 7; bit >= 0; --bit) {
+            CurveSM2x::dbl(acc, acc);
+            CurveSM2x::madd(S, acc, P);
+            CurveSM2x::cmov(acc, S, ((b >> bit) & 1u) != 0u);
+        }
+#pragma unroll 1
+        for (int d = 0; d < 8 * win; ++d) CurveSM2x::dbl(acc, acc);
+        fp26 zi, zi2, zi3, ax, ay;
+        fp26_inv(zi, acc.Z);
+        fp26_sqr(zi2, zi);
+        fp26_mul(zi3, zi2, zi);
+        fp26_mul(ax, acc.X, zi2);
+        fp26_mul(ay, acc.Y, zi3);
+        fe x, y;
+        fp26_to_fe(x, ax);
+        fp26_to_fe(y, ay);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            out[q] = x.v[q];
+            out[8 + q] = y.v[q];
+        }
+        if (ent == 0) {
+            uint32_t V[8], a[5];
+            sm2_za(V, X, Y);
+            sm3_address(a, px, py);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                slot[q] = px.v[q];
+                slot[8 + q] = py.v[q];
+                slot[16 + q] = V[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 5; ++q) slot[24 + q] = a[q];
+            slot[32] = valid ? 1u : 0u;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ verify
+// the 16-lane row's partial sums -> lane 0 (lanes of a row are 16-aligned: __shfl_down with width 16)
+template <class J, int LIMBS>
+__device__ __forceinline__ void shfl_down_point(J& o, const J& a, int off) {
+#pragma unroll
+    for (int q = 0; q < LIMBS; ++q) {
+        o.X.v[q] = __shfl_down(a.X.v[q], off, 16);
+        o.Y.v[q] = __shfl_down(a.Y.v[q], off, 16);
+        o.Z.v[q] = __shfl_down(a.Z.v[q], off, 16);
+    }
+    o.inf = __shfl_down(static_cast<int>(a.inf), off, 16) != 0;
+}
+
+// word q of k for a lane-varying q, by selects (a dynamic index would put k in scratch memory)
+__device__ __forceinline__ uint32_t word_of(const fe& k, int q) {
+    uint32_t w = k.v[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) w = q == j ? k.v[j] : w;
+    return w;
+}
+__device__ __forceinline__ uint32_t byte_of(const fe& k, int j) { return (word_of(k, j >> 2) >> ((j & 3) * 8)) & 0xffu; }
+__device__ __forceinline__ uint32_t half_of(const fe& k, int j) { return (word_of(k, j >> 1) >> ((j & 1) * 16)) & 0xffffu; }
+
+// ok[i] = SignatureCrypto::verify(key of slot[i], hash[i], sig[i]); addr (SM2 tx admission: the verified
+// key's SM3 address) may be null.  One 64-thread workgroup = 4 signatures.
+template <int SUITE>
+__global__ __launch_bounds__(64) void sig_verify_keyed_kernel(const uint32_t* __restrict__ arena, uint32_t cap,
+                                                              const int32_t* __restrict__ slots,
+                                                              const uint8_t* __restrict__ hash,
+                                                              const uint8_t* __restrict__ sig, uint32_t stride,
+                                                              uint64_t n, const uint32_t* __restrict__ gtab, int gbits,
+                                                              uint8_t* __restrict__ okout, uint8_t* __restrict__ addr) {
+    const uint32_t lane = threadIdx.x;
+    const int L = static_cast<int>(lane & 15u);
+    const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * 4u + (lane >> 4);
+    const bool live = i0 < n;
+    const uint64_t i = live ? i0 : n - 1;  // a spare row re-runs the last signature (nothing stored)
+    const int32_t sl = slots[i];
+    const bool slot_ok = sl >= 0 && static_cast<uint32_t>(sl) < cap;
+    const uint32_t* key = arena + static_cast<size_t>(slot_ok ? sl : 0) * kKeySlotWords;
+    const uint32_t* ktab = key + kKeyHdrWords;
+    fe h;
+    load_be256(h, hash + 32 * i);
+    ByteReader rs(sig + static_cast<uint64_t>(stride) * i, 64);
+    uint32_t w[8];
+    fe r, s;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w[q] = rs.word(q);
+    fe_from_be_words(r, w);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) w[q] = rs.word(8 + q);
+    fe_from_be_words(s, w);
+    bool ok = slot_ok && key[32] == 1u;
+    bool match = false;
+    if constexpr (SUITE == BCOSGPU_SUITE_SECP256K1) {
+        ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN1::M) && fe_lt_k(s, kN1HalfPlus);
+        fe e;
+        fe_copy(e, h);
+        reduce_once(e, ParamN1::M);
+        fe ss = s;
+        if (!ok) {
+            fe_zero(ss);
+            ss.v[0] = 1;
+        }
+        fe sm, sinv, u1, u2;
+        FieldN1::from_plain(sm, ss);
+        FieldInv<FieldN1>::inv_pipe(sinv, sm);
+        FieldN1::mul(u1, e, sinv);
+        FieldN1::mul(u2, r, sinv);
+        Jac26 acc, S;
+        CurveK1x::set_inf(acc);
+        auto add_entry = [&](const uint32_t* tab, uint32_t d) {
+            Aff26 T;
+            load_aff26(T, tab);
+            CurveK1x::madd(S, acc, T);
+            CurveK1x::cmov(acc, S, d != 0u);
+        };
+        const uint32_t b0 = byte_of(u2, 2 * L), b1 = byte_of(u2, 2 * L + 1);
+        add_entry(ktab + (static_cast<size_t>(2 * L) * kCombEntries + b0) * 16, b0);
+        add_entry(ktab + (static_cast<size_t>(2 * L + 1) * kCombEntries + b1) * 16, b1);
+        if (gbits == kWideBits) {
+            const uint32_t g = half_of(u1, L);
+            add_entry(gtab + (static_cast<size_t>(L) * kWideEntries + g) * 16, g);
+        } else {
+            const uint32_t g0 = byte_of(u1, 2 * L), g1 = byte_of(u1, 2 * L + 1);
+            add_entry(gtab + (static_cast<size_t>(2 * L) * kCombEntries + g0) * 16, g0);
+            add_entry(gtab + (static_cast<size_t>(2 * L + 1) * kCombEntries + g1) * 16, g1);
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            Jac26 o;
+            shfl_down_point<Jac26, 10>(o, acc, off);
+            CurveK1x::add(acc, acc, o);
+        }
+        ok = ok && !acc.inf;
+        fe26 z2, rhs, R, d;
+        fe26_sqr(z2, acc.Z);
+        fe26_from_fe(R, r);
+        fe26_mul(rhs, R, z2);
+        fe26_sub<10>(d, rhs, acc.X);  // acc.X <= 9: an addition may pass a mixed sum through
+        match = fe26_is_zero(d);
+        fe r2;
+        const uint32_t carry = fe_add_k(r2, r, ParamN1::M);
+        if (carry == 0u && fe_lt_k(r2, FieldK1::P)) {
+            fe26_from_fe(R, r2);
+            fe26_mul(rhs, R, z2);
+            fe26_sub<10>(d, rhs, acc.X);
+            match = match || fe26_is_zero(d);
+        }
+    } else {
+        ok = ok && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) && fe_lt_k(r, ParamN2::M) && fe_lt_k(s, ParamN2::M);
+        fe t;
+        FieldN2::add(t, r, s);
+        ok = ok && !fe_is_zero_raw(t);
+        fe e;
+        sm2_e_from_za(e, key + 16, h);
+        reduce_once(e, ParamN2::M);
+        JacP26 acc, S;
+        CurveSM2x::set_inf(acc);
+        auto add_entry = [&](const uint32_t* tab, uint32_t d) {
+            AffP26 T;
+            load_affp26(T, tab);
+            CurveSM2x::madd(S, acc, T);
+            CurveSM2x::cmov(acc, S, d != 0u);
+        };
+        const uint32_t b0 = byte_of(t, 2 * L), b1 = byte_of(t, 2 * L + 1);
+        add_entry(ktab + (static_cast<size_t>(2 * L) * kCombEntries + b0) * 16, b0);
+        add_entry(ktab + (static_cast<size_t>(2 * L + 1) * kCombEntries + b1) * 16, b1);
+        if (gbits == kWideBits) {
+            const uint32_t g = half_of(s, L);
+            add_entry(gtab + (static_cast<size_t>(L) * kWideEntries + g) * 16, g);
+        } else {
+            const uint32_t g0 = byte_of(s, 2 * L), g1 = byte_of(s, 2 * L + 1);
+            add_entry(gtab + (static_cast<size_t>(2 * L) * kCombEntries + g0) * 16, g0);
+            add_entry(gtab + (static_cast<size_t>(2 * L + 1) * kCombEntries + g1) * 16, g1);
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            JacP26 o;
+            shfl_down_point<JacP26, 10>(o, acc, off);
+            CurveSM2x::add(acc, acc, o);
+        }
+        ok = ok && !acc.inf;
+        // x1 = X / Z^2 must be congruent to r - e (mod n): x1 = c or c + n (when c + n < p)
+        fe c, c2;
+        FieldN2::sub(c, r, e);
+        fp26 z2, cm, rhs, dlt;
+        fp26_sqr(z2, acc.Z);
+        fp26_from_plain(cm, c);
+        fp26_mul(rhs, cm, z2);
+        fp26_sub<13>(dlt, rhs, acc.X);
+        match = fp26_is_zero(dlt);
+        const uint32_t carry = fe_add_k(c2, c, ParamN2::M);
+        if (carry == 0u && fe_lt_k(c2, ParamP2::M)) {
+            fp26_from_plain(cm, c2);
+            fp26_mul(rhs, cm, z2);
+            fp26_sub<13>(dlt, rhs, acc.X);
+            match = match || fp26_is_zero(dlt);
+        }
+    }
+    ok = ok && match;
+    if (live && L == 0) {
+        okout[i] = ok ? 1 : 0;
+        if (addr) {
+            uint32_t* a = reinterpret_cast<uint32_t*>(addr + 20 * i);
+#pragma unroll
+            for (int q = 0; q < 5; ++q) a[q] = ok ? key[24 + q] : 0u;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ host: the key cache
+namespace {
+
+using Key64 = std::array<uint8_t, 64>;
+struct Key64Hash {
+    size_t operator()(const Key64& k) const {
+        uint64_t h;
+        std::memcpy(&h, k.data() + 24, 8);  // low bits of x: uniformly distributed for valid keys
+        uint64_t g;
+        std::memcpy(&g, k.data() + 56, 8);
+        return static_cast<size_t>(h ^ (g * 0x9E3779B97F4A7C15ull));
+    }
+};
+
+struct KeyCache {
+    std::mutex mu;
+    uint32_t* arena = nullptr;
+    int cap = 0;
+    bool alloc_failed = false;
+    std::unordered_map<Key64, int32_t, Key64Hash> slot_of;
+    std::unordered_map<Key64, uint32_t, Key64Hash> seen;
+    uint64_t hits = 0, misses = 0, builds = 0;
+};
+
+std::mutex g_kc_mu;
+KeyCache* g_kc[64][2] = {};  // never freed: no teardown races with the HIP runtime at exit
+
+KeyCache* cache_of(int device, int suite) {
+    std::lock_guard<std::mutex> g(g_kc_mu);
+    KeyCache*& c = g_kc[device][suite];
+    if (!c) c = new KeyCache();
+    return c;
+}
+
+int capacity_env() {
+    static const int cap = [] {
+        const char* e = getenv("BCOSGPU_KEY_CACHE");  // keys per (device, suite); 512 KiB each
+        const long v = e ? atol(e) : 256;
+        return static_cast<int>(v < 0 ? 0 : v > 65536 ? 65536 : v);
+    }();
+    return cap;
+}
+
+int promote_after() {
+    static const int k = [] {
+        const char* e = getenv("BCOSGPU_KEY_PROMOTE");  // calls that must see a key before it is cached; 0 = never
+        return e ? atoi(e) : 2;
+    }();
+    return k;
+}
+
+// Under c.mu on the current device: give every key of `todo` a slot and build its table on st,
+// synchronously (a build is rare -- registration, promotion -- and the slots become visible to other
+// threads only after c.mu is released, by which time their tables exist).
+int build_keys(KeyCache& c, int suite, const std::vector<Key64>& todo, std::vector<int32_t>& got, hipStream_t st) {
+    got.assign(todo.size(), -1);
+    if (todo.empty()) return 0;
+    if (!c.arena && !c.alloc_failed) {
+        const int cap = capacity_env();
+        if (cap > 0 && hipMalloc(&c.arena, static_cast<size_t>(cap) * kKeySlotWords * 4) == hipSuccess) {
+            c.cap = cap;
+        } else {
+            (void)hipGetLastError();
+            c.arena = nullptr;
+            c.alloc_failed = true;
+        }
+    }
+    const int32_t old = static_cast<int32_t>(c.slot_of.size());
+    std::vector<Key64> keys;
+    std::vector<int32_t> slots;
+    for (size_t q = 0; q < todo.size(); ++q) {
+        auto it = c.slot_of.find(todo[q]);
+        if (it != c.slot_of.end()) {
+            got[q] = it->second;
+            continue;
+        }
+        const int32_t sl = static_cast<int32_t>(c.slot_of.size());
+        if (!c.arena || sl >= c.cap) continue;  // full: not cached
+        c.slot_of.emplace(todo[q], sl);
+        keys.push_back(todo[q]);
+        slots.push_back(sl);
+        got[q] = sl;
+    }
+    if (keys.empty()) return 0;
+    const size_t kb = 64 * keys.size(), sb = 4 * slots.size();
+    std::vector<uint8_t> host(kb + sb);
+    for (size_t q = 0; q < keys.size(); ++q) std::memcpy(host.data() + 64 * q, keys[q].data(), 64);
+    std::memcpy(host.data() + kb, slots.data(), sb);
+    uint8_t* d = nullptr;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&d), kb + sb);
+    if (e == hipSuccess) e = hipMemcpyAsync(d, host.data(), kb + sb, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+        const uint64_t lanes = static_cast<uint64_t>(keys.size()) * kKeyEntriesPerKey;
+        const dim3 grid(static_cast<unsigned>((lanes + 255) / 256)), block(256);
+        if (suite == BCOSGPU_SUITE_SM2)
+            hipLaunchKernelGGL(key_table_kernel<BCOSGPU_SUITE_SM2>, grid, block, 0, st, c.arena,
+                               reinterpret_cast<const int32_t*>(d + kb), d, static_cast<uint32_t>(keys.size()));
+        else
+            hipLaunchKernelGGL(key_table_kernel<BCOSGPU_SUITE_SECP256K1>, grid, block, 0, st, c.arena,
+                               reinterpret_cast<const int32_t*>(d + kb), d, static_cast<uint32_t>(keys.size()));
+        e = hipGetLastError();
+        const hipError_t e2 = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = e2;
+    }
+    if (d) (void)hipFree(d);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        for (const Key64& k : keys) c.slot_of.erase(k);
+        for (auto& g : got)
+            if (g >= old) g = -1;
+        return BCOSGPU_E_HIP;
+    }
+    c.builds += keys.size();
+    return 0;
+}
+
+}  // namespace
+
+// Slots of n keys (pub i at pubs + pub_stride * i) on the current device; keys not cached are built when
+// `force`, or when seen in promote_after() calls.  Returns 0 and *all = every key has a slot, or < 0.
+int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int32_t* out, bool force, bool* all,
+                hipStream_t st) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BCOSGPU_E_NODEV;
+    *all = false;
+    if (n == 0) {
+        *all = true;
+        return 0;
+    }
+    KeyCache& c = *cache_of(dev, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
+    std::lock_guard<std::mutex> g(c.mu);
+    if (!force && c.slot_of.empty() && promote_after() <= 0) return 0;
+    std::vector<Key64> todo;
+    std::vector<size_t> todo_at;
+    bool every = true;
+    for (size_t i = 0; i < n; ++i) {
+        Key64 k;
+        std::memcpy(k.data(), pubs + pub_stride * i, 64);
+        auto it = c.slot_of.find(k);
+        if (it != c.slot_of.end()) {
+            out[i] = it->second;
+            continue;
+        }
+        out[i] = -1;
+        bool build = force;
+        if (!build && promote_after() > 0) {
+            if (c.seen.size() > (1u << 20)) c.seen.clear();
+            build = ++c.seen[k] >= static_cast<uint32_t>(promote_after());
+        }
+        if (build) {
+            todo.push_back(k);
+            todo_at.push_back(i);
+        } else {
+            every = false;
+        }
+    }
+    if (!todo.empty()) {
+        std::vector<int32_t> got;
+        const int rc = build_keys(c, suite, todo, got, st);
+        if (rc) return rc;
+        for (size_t q = 0; q < todo.size(); ++q) {
+            out[todo_at[q]] = got[q];
+            if (got[q] < 0) every = false;
+            else c.seen.erase(todo[q]);
+        }
+    }
+    if (every) {
+        c.hits += n;
+    } else {
+        c.misses += n;
+    }
+    *all = every;
+    return 0;
+}
+
+int launch_sig_verify_keyed(int suite, const int32_t* d_slots, const uint8_t* d_hash, const uint8_t* d_sig,
+                            uint32_t stride, uint64_t n, uint8_t* d_ok, uint8_t* d_addr, hipStream_t st) {
+    if (n == 0) return 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BCOSGPU_E_NODEV;
+    KeyCache& c = *cache_of(dev, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
+    const uint32_t* arena;
+    uint32_t cap;
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        arena = c.arena;
+        cap = static_cast<uint32_t>(c.slot_of.size());
+    }
+    if (!arena) return BCOSGPU_E_ARG;  // no key registered on this device
+    const dim3 grid(static_cast<unsigned>((n + 3) / 4)), block(64);
+    if (suite == BCOSGPU_SUITE_SM2) {
+        const uint32_t* tab;
+        int bits;
+        if (int rc = tables_sm2_26(&tab, &bits)) return rc;
+        hipLaunchKernelGGL(sig_verify_keyed_kernel<BCOSGPU_SUITE_SM2>, grid, block, 0, st, arena, cap, d_slots, d_hash,
+                           d_sig, stride, n, tab, bits, d_ok, d_addr);
+    } else {
+        const uint32_t *k1, *sm2;
+        int bits;
+        if (int rc = tables(&k1, &sm2, &bits)) return rc;
+        hipLaunchKernelGGL(sig_verify_keyed_kernel<BCOSGPU_SUITE_SECP256K1>, grid, block, 0, st, arena, cap, d_slots,
+                           d_hash, d_sig, stride, n, k1, bits, d_ok, d_addr);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+
+int keyed_cache_info(int device, int suite, int64_t out[5]) {
+    if (device < 0 || device >= 64) return BCOSGPU_E_ARG;
+    KeyCache& c = *cache_of(device, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
+    std::lock_guard<std::mutex> g(c.mu);
+    out[0] = static_cast<int64_t>(c.slot_of.size());
+    out[1] = c.arena ? c.cap : capacity_env();
+    out[2] = static_cast<int64_t>(c.hits);
+    out[3] = static_cast<int64_t>(c.misses);
+    out[4] = static_cast<int64_t>(c.builds);
+    return 0;
+}
+
+// Drop every cached key of (device, suite) after the device has drained (no launch reads a table then).
+int keyed_clear(int device, int suite) {
+    if (device < 0 || device >= 64) return BCOSGPU_E_ARG;
+    KeyCache& c = *cache_of(device, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
+    std::lock_guard<std::mutex> g(c.mu);
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != device && hipSetDevice(device) != hipSuccess) return BCOSGPU_E_HIP;
+    const hipError_t e = hipDeviceSynchronize();
+    if (prev != device) (void)hipSetDevice(prev);
+    if (e != hipSuccess) return BCOSGPU_E_HIP;
+    c.slot_of.clear();
+    c.seen.clear();
+    return 0;
+}
+
+}  // namespace bcosgpu

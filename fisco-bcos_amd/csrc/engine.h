@@ -63,6 +63,14 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
                      const uint8_t* d_sig, const uint64_t* d_sig_off, uint64_t n,
                      uint8_t* d_txhash, uint8_t* d_sender, uint8_t* d_status, hipStream_t st);
 
+// ecc_keyed.hip: verification against registered keys (per-key comb tables in HBM)
+int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int32_t* out, bool force, bool* all,
+                hipStream_t st);
+int launch_sig_verify_keyed(int suite, const int32_t* d_slots, const uint8_t* d_hash, const uint8_t* d_sig,
+                            uint32_t stride, uint64_t n, uint8_t* d_ok, uint8_t* d_addr, hipStream_t st);
+int keyed_cache_info(int device, int suite, int64_t out[5]);
+int keyed_clear(int device, int suite);
+
 // coalesce.hip: the host-pointer signature calls as jobs of a per-device queue, coalesced into shared
 // launches (see the file header).  coalesced_run blocks until the job's results are written.
 enum SigJobKind { kSigJobRecoverK1 = 0, kSigJobVerifySM2 = 1, kSigJobVerifyK1 = 2, kSigJobKinds = 3 };

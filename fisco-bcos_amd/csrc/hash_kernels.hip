@@ -557,9 +557,9 @@ __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restr
 
 // One counter slot (kFusedCounters counters) per launch queue: launches on one stream run in order and
 // each launch leaves its counters at zero, so a slot is clean for the next launch of its owner.
-//  - Owners: a created stream by its unique id (hipStreamGetId; a destroyed stream's handle may come back
-//    for a new stream, its id does not, so a new stream never shares a slot with launches of the old one
-//    still in flight); the legacy null stream by its device (one in-order queue for every thread); the
+//  - Owners: a created stream by its handle (hipStreamDestroy releases the stream object only once its
+//    work has completed, so a handle that comes back for a new stream has no launch of the old one in
+//    flight); the legacy null stream by its device (one in-order queue for every thread); the
 //    per-thread default stream (hipStreamPerThread) by the calling thread, whose slot goes back to the
 //    pool when that thread exits (after its stream drains).
 //  - A new slot is zeroed by hipMemsetAsync on the claiming stream (ordered before its first launch; no
@@ -610,10 +610,11 @@ static uint32_t* fused_counter_slot(hipStream_t st) {
         me.thread = std::this_thread::get_id();
     } else {
         hipDevice_t sd = 0;
-        if (hipStreamGetDevice(st, &sd) != hipSuccess || hipStreamGetId(st, &me.id) != hipSuccess) {
+        if (hipStreamGetDevice(st, &sd) != hipSuccess) {
             (void)hipGetLastError();
             return nullptr;
         }
+        me.id = static_cast<unsigned long long>(reinterpret_cast<uintptr_t>(st));
         me.device = dev = sd;
     }
     std::lock_guard<std::mutex> g(g_slot_mu);

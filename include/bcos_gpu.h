@@ -197,6 +197,28 @@ int bcosgpu_verify_batch(int suite, const uint8_t* pub64, const uint8_t* hash32,
 int bcosgpu_verify_batch_dev(int suite, const uint8_t* d_pub64, const uint8_t* d_hash32, const uint8_t* d_sig,
                              size_t sig_stride, size_t n, uint8_t* d_ok, void* stream);
 
+/* Registered keys: the sealer path.  BlockValidator::checkSignatureList and
+ * PBFTCacheProcessor::checkPrecommitWeight verify against the consensus node list's keys -- a small
+ * set known in advance (ConsensusNode list; PBFTConfig).  A registered key gets an 8-bit comb table of
+ * its multiples in HBM (512 KiB, built once), so verifying against it needs table lookups and ~7 point
+ * additions instead of a variable-base multiplication (~10x shorter per signature; same verdicts).
+ *   bcosgpu_register_keys: tables for n keys (pub64 + 64 i) of `suite` on `device`; slots[i] = the key's
+ *     slot, or -1 when the cache is full (BCOSGPU_KEY_CACHE keys per device and suite, default 256).
+ *     Returns the number of keys cached (< 0 on error).  Registering a cached key is a lookup.
+ *   Host-pointer verify calls (bcosgpu_verify_batch, bcosgpu_secp256k1_verify, bcosgpu_sm2_verify, the
+ *     device-set batches, SM2 recover) take the registered-key kernel when every key of the coalesced
+ *     batch is cached; a key seen in BCOSGPU_KEY_PROMOTE (default 2) calls is cached automatically.
+ *   bcosgpu_verify_keyed_batch_dev: ok[i] = verify(key of d_slots[i], d_hash32 + 32 i, d_sig +
+ *     sig_stride i) on the calling thread's device, stream-ordered; a slot that is not registered fails.
+ *   bcosgpu_key_cache_info: out5 = {keys cached, capacity, verified on the keyed path, verified
+ *     elsewhere, tables built}.  bcosgpu_clear_keys: drains the device, then forgets every key (a
+ *     consensus membership change); slots are reassigned by later registrations. */
+int bcosgpu_register_keys(int device, int suite, const uint8_t* pub64, size_t n, int32_t* slots);
+int bcosgpu_verify_keyed_batch_dev(int suite, const int32_t* d_slots, const uint8_t* d_hash32, const uint8_t* d_sig,
+                                   size_t sig_stride, size_t n, uint8_t* d_ok, void* stream);
+int bcosgpu_key_cache_info(int device, int suite, int64_t* out5);
+int bcosgpu_clear_keys(int device, int suite);
+
 /* EVM ecRecover precompile (bcos-executor/src/vm/Precompiled.cpp:443-482), batched.  Input i =
  * in128 + 128 i = hash(32) || v(32) || r(32) || s(32); the recovery id is (uint8_t)(in[63] - 27).
  * On success out32 = 12 zero bytes || right160(Keccak256(pub)) and ok = 1; on failure the precompile

@@ -28,6 +28,19 @@ def test_library_is_gfx950_code_object():
             assert b"gfx950" in f.read()
 
 
+def test_library_binds_no_hip_symbol_newer_than_torchs_runtime():
+    """libbcosgpu.so is loaded into processes that already hold torch's HIP runtime (torch/lib/libamdhip64.so,
+    ROCm 7.0 -- _lib.lib() imports torch first so both share it); a HIP entry point versioned hip_7.1 or
+    later (hipStreamGetId, say) makes the dlopen fail there.  Every undefined HIP symbol's version <= 7.0."""
+    import re
+    out = subprocess.run(["nm", "-D", "--with-symbol-versions", "--undefined-only", _lib.LIB_PATH],
+                         capture_output=True, text=True, check=True).stdout
+    vers = set(re.findall(r"@+hip_(\d+)\.(\d+)", out))
+    assert vers, "no versioned HIP symbols found"
+    too_new = sorted(v for v in vers if (int(v[0]), int(v[1])) > (7, 0))
+    assert not too_new, too_new
+
+
 def test_cheap_calls_without_gpu():
     L = _lib.lib()
     assert L.bcosgpu_version() == 1
