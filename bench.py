@@ -806,18 +806,22 @@ def single_call_cpu(b, suite, threads, sample=4000):
             "cores": cpu_threads(), "kind": "standin-openssl" if ossl else "port", "sample": n}
 
 
-def sealer_verify_leg(threads, reps=100):
-    """PBFT sealer-signature checks: SignatureCrypto::verify(pub, hash, sig) with KNOWN keys
-    (BlockValidator::checkSignatureList, bcos-pbft/.../BlockValidator.cpp:141-182, and
+def sealer_verify_leg(threads, reps=100, committee=32):
+    """PBFT sealer-signature checks: SignatureCrypto::verify(pub, hash, sig) against the consensus node
+    list's keys (BlockValidator::checkSignatureList, bcos-pbft/.../BlockValidator.cpp:141-182, and
     PBFTCacheProcessor::checkPrecommitWeight, PBFTCacheProcessor.cpp:795-821 -> Secp256k1Crypto.cpp:51-63 /
-    SM2Crypto.cpp:66-79), per suite:
-      block_{k}:   one block's k in {4, 7, 32} signatures as one bcosgpu_verify_batch call (host buffers, the
-                   engine's coalesced path) -- p50 / p99 latency over `reps` calls;
-      single:      one SignatureCrypto::verify (bcosgpu_secp256k1_verify / bcosgpu_sm2_verify) -- p50;
-      catch_up:    1,000 blocks x 7 signatures (a sync catch-up) in one device-resident call
-                   (bcosgpu_verify_batch_dev, HIP events) -- sigs/s;
-      cpu:         the OpenSSL stand-in on the same 7-signature block (1 thread: the reference verifies a
-                   block's list in one loop) and on the 7,000 signatures over `threads` threads.
+    SM2Crypto.cpp:66-79), per suite, with a committee of `committee` sealers registered up front
+    (bcosgpu_register_keys, the node's consensus list):
+      block_{k}:   one block's k in {4, 7, 32} sealer signatures as one bcosgpu_verify_batch call (host
+                   buffers, coalesced; the registered-key kernel) -- p50 / p99 latency over `reps` blocks;
+      unreg_7:     the same call with 7 keys never seen before (the generic verify kernels) -- p50;
+      single:      one SignatureCrypto::verify of a sealer signature (bcosgpu_secp256k1_verify /
+                   bcosgpu_sm2_verify) -- p50;
+      catch_up:    1,000 blocks x 7 sealer signatures (a sync catch-up) in one device-resident call:
+                   registered keys (bcosgpu_verify_keyed_batch_dev) and unregistered (bcosgpu_verify_batch_dev),
+                   HIP events -- sigs/s;
+      cpu:         the OpenSSL stand-in on a 7-signature block (1 thread: the reference verifies a block's
+                   list in one loop) and on the 7,000 signatures over `threads` threads.
     Every verdict is checked (all signatures valid)."""
     import numpy as np
     import torch
@@ -826,82 +830,124 @@ def sealer_verify_leg(threads, reps=100):
     from oracle import oracle
     out, summ = {}, {}
     L = _lib.lib()
-    n = 7000
+    nb = max(reps, 1000)
     for suite in (0, 1):
         name = "secp256k1" if suite == 0 else "sm2"
         g = torch.Generator(device="cuda")
         g.manual_seed(0x5EA1 + suite)
-        sk = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
-        sk[:, 0] &= 0x7F
-        sk[:, 31] |= 1
-        h = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
-        okd = torch.empty(n, dtype=torch.uint8, device="cuda")
-        if suite == 0:
-            pub = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
-            sig = torch.empty((n, 65), dtype=torch.uint8, device="cuda")
-            device.secp256k1_sign(sk, h, pub, sig, okd)
-        else:
-            sig = torch.empty((n, 128), dtype=torch.uint8, device="cuda")
-            device.sm2_sign(sk, h, sig, okd)
-            pub = sig[:, 64:128].contiguous()
-        torch.cuda.synchronize()
-        assert bool(okd.all())
-        stride = sig.shape[1]
+
+        def signed(sk, h):
+            n = sk.shape[0]
+            okd = torch.empty(n, dtype=torch.uint8, device="cuda")
+            if suite == 0:
+                pub = torch.empty((n, 64), dtype=torch.uint8, device="cuda")
+                sig = torch.empty((n, 65), dtype=torch.uint8, device="cuda")
+                device.secp256k1_sign(sk, h, pub, sig, okd)
+            else:
+                sig = torch.empty((n, 128), dtype=torch.uint8, device="cuda")
+                device.sm2_sign(sk, h, sig, okd)
+                pub = sig[:, 64:128].contiguous()
+            torch.cuda.synchronize()
+            assert bool(okd.all())
+            return pub, sig
+
+        def keys(n):
+            sk = torch.randint(0, 256, (n, 32), dtype=torch.uint8, device="cuda", generator=g)
+            sk[:, 0] &= 0x7F
+            sk[:, 31] |= 1
+            return sk
+        # the committee; block b's sealers 0..k-1 sign its hash
+        csk = keys(committee)
+        bh = torch.randint(0, 256, (nb, 32), dtype=torch.uint8, device="cuda", generator=g)
+        who = torch.arange(nb * 7, device="cuda") % 7
+        h7 = bh.repeat_interleave(7, dim=0)
+        pub7, sig7 = signed(csk[who], h7)
         crypto = bcos_gpu.SM2Crypto() if suite else bcos_gpu.Secp256k1Crypto()
-        P, H, S = pub.cpu().numpy(), h.cpu().numpy(), sig.cpu().numpy()
+        cpub, _ = signed(csk, bh[:committee])
+        slots = bcos_gpu.register_keys(suite, cpub.cpu().numpy())
+        assert (slots >= 0).all()
+        P7, H7, S7 = pub7.cpu().numpy(), h7.cpu().numpy(), sig7.cpu().numpy()
         rec = {}
         for k in (4, 7, 32):
-            assert crypto.verify_batch(P[:k], H[:k], S[:k]).all()
+            bk = min(reps, 100)
+            whok = torch.arange(bk * k, device="cuda") % k
+            hk = bh[:bk].repeat_interleave(k, dim=0)
+            pk, sk_ = signed(csk[whok], hk)
+            Pk, Hk, Sk = pk.cpu().numpy(), hk.cpu().numpy(), sk_.cpu().numpy()
+            assert crypto.verify_batch(Pk[:k], Hk[:k], Sk[:k]).all()
             ts = []
-            for r in range(reps):
-                a = (r * k) % (n - k)
+            for r in range(bk):
                 t0 = time.perf_counter()
-                crypto.verify_batch(P[a:a + k], H[a:a + k], S[a:a + k])
+                okb = crypto.verify_batch(Pk[r * k:(r + 1) * k], Hk[r * k:(r + 1) * k], Sk[r * k:(r + 1) * k])
                 ts.append(time.perf_counter() - t0)
+                assert okb.all()
             ts.sort()
             rec["block_%d" % k] = {"p50_ms": ts[len(ts) // 2] * 1e3, "p99_ms": ts[len(ts) * 99 // 100] * 1e3}
+        # unregistered: every block's 7 keys new (each seen once, so never promoted)
+        ts = []
+        for r in range(min(reps, 50)):
+            usk = keys(7)
+            up, us = signed(usk, bh[r:r + 1].repeat(7, 1))
+            UP, US, UH = up.cpu().numpy(), us.cpu().numpy(), bh[r:r + 1].repeat(7, 1).cpu().numpy()
+            t0 = time.perf_counter()
+            okb = crypto.verify_batch(UP, UH, US)
+            ts.append(time.perf_counter() - t0)
+            assert okb.all()
+        ts.sort()
+        rec["unreg_7"] = {"p50_ms": ts[len(ts) // 2] * 1e3}
         ts = []
         for r in range(reps):
             t0 = time.perf_counter()
-            assert crypto.verify(P[r].tobytes(), H[r].tobytes(), S[r].tobytes())
+            assert crypto.verify(P7[r].tobytes(), H7[r].tobytes(), S7[r].tobytes())
             ts.append(time.perf_counter() - t0)
         ts.sort()
         rec["single_p50_ms"] = ts[len(ts) // 2] * 1e3
         stream = torch.cuda.current_stream()
+        n = nb * 7
+        okd = torch.empty(n, dtype=torch.uint8, device="cuda")
+        dslots = torch.from_numpy(slots.astype(np.int32)).cuda()[who]
+        stride = sig7.shape[1]
 
-        def launch():
-            _lib.check(L.bcosgpu_verify_batch_dev(suite, pub.data_ptr(), h.data_ptr(), sig.data_ptr(), stride, n,
+        def keyed():
+            device.verify_keyed(suite, dslots, h7, sig7, okd, stream)
+
+        def generic():
+            _lib.check(L.bcosgpu_verify_batch_dev(suite, pub7.data_ptr(), h7.data_ptr(), sig7.data_ptr(), stride, n,
                                                   okd.data_ptr(), stream.cuda_stream))
-        t0 = time.perf_counter()  # >= 0.5 s of back-to-back launches first (the clock settles under load)
-        while time.perf_counter() - t0 < 0.5:
-            for _ in range(8):
-                launch()
-            torch.cuda.synchronize()
-        kt = []
-        for _ in range(20):
-            a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            launch()
-            c.record(stream)
-            c.synchronize()
-            kt.append(a.elapsed_time(c))
-        kt.sort()
-        assert bool(okd.all())
-        rec["catch_up_1000x7"] = {"sigs_per_s": n / (kt[len(kt) // 2] * 1e-3), "kernel_ms": kt[len(kt) // 2]}
+        for lname, fn in (("catch_up_1000x7", keyed), ("catch_up_1000x7_unreg", generic)):
+            t0 = time.perf_counter()  # >= 0.5 s of back-to-back launches first (the clock settles under load)
+            while time.perf_counter() - t0 < 0.5:
+                for _ in range(8):
+                    fn()
+                torch.cuda.synchronize()
+            kt = []
+            for _ in range(20):
+                a, c = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+                fn()
+                c.record(stream)
+                c.synchronize()
+                kt.append(a.elapsed_time(c))
+            kt.sort()
+            assert bool(okd.all())
+            rec[lname] = {"sigs_per_s": n / (kt[len(kt) // 2] * 1e-3), "kernel_ms": kt[len(kt) // 2]}
         cpu = {}
         if oracle.standin() is not None:
-            S64 = np.ascontiguousarray(S[:, :64])
-            med, _ = _median_time(lambda: oracle.standin_verify_batch(suite, P[:7], H[:7], S64[:7], nthreads=1))
+            S64 = np.ascontiguousarray(S7[:, :64])
+            med, _ = _median_time(lambda: oracle.standin_verify_batch(suite, P7[:7], H7[:7], S64[:7], nthreads=1))
             cpu["block_7_ms"] = med * 1e3
-            med, _ = _median_time(lambda: oracle.standin_verify_batch(suite, P, H, S64, nthreads=threads), reps=3)
+            med, _ = _median_time(lambda: oracle.standin_verify_batch(suite, P7, H7, S64, nthreads=threads), reps=3)
             cpu["catch_up_sigs_per_s"] = n / med
             cpu.update(threads=threads, kind="standin-openssl")
-            assert oracle.standin_verify_batch(suite, P[:64], H[:64], S64[:64]).all()
+            assert oracle.standin_verify_batch(suite, P7[:64], H7[:64], S64[:64]).all()
         rec["cpu"] = cpu
+        rec["key_cache"] = bcos_gpu.key_cache_info(suite)
         out[name] = rec
         summ[name] = {"blk4_p50_ms": _g(rec["block_4"]["p50_ms"]), "blk7_p50_ms": _g(rec["block_7"]["p50_ms"]),
-                      "blk32_p50_ms": _g(rec["block_32"]["p50_ms"]), "single_p50_ms": _g(rec["single_p50_ms"]),
+                      "blk32_p50_ms": _g(rec["block_32"]["p50_ms"]), "unreg7_p50_ms": _g(rec["unreg_7"]["p50_ms"]),
+                      "single_p50_ms": _g(rec["single_p50_ms"]),
                       "catchup_sig_s": _g(rec["catch_up_1000x7"]["sigs_per_s"]),
+                      "catchup_unreg_sig_s": _g(rec["catch_up_1000x7_unreg"]["sigs_per_s"]),
                       "cpu_blk7_ms": _g(cpu.get("block_7_ms")), "cpu_catchup_sig_s": _g(cpu.get("catch_up_sigs_per_s"))}
     out["summary"] = summ
     return out

@@ -24,7 +24,7 @@
 // pick u1, u2 so that two partial sums coincide.
 //
 // Host side: a per-(device, suite) cache of key tables, filled by bcosgpu_register_keys (the node's
-// consensus list) and by promotion of keys seen in two calls; never evicted while the process runs
+// consensus list) and by promotion of keys seen in three calls; never evicted while the process runs
 // (bcosgpu_clear_keys drains the device first), so a table is never rewritten under a launch that reads
 // it.  The coalesced host-pointer verify calls take this path when every key of the batch is cached.
 #include <array>
@@ -253,6 +253,22 @@ __device__ __forceinline__ uint32_t word_of(const fe& k, int q) {
 __device__ __forceinline__ uint32_t byte_of(const fe& k, int j) { return (word_of(k, j >> 2) >> ((j & 3) * 8)) & 0xffu; }
 __device__ __forceinline__ uint32_t half_of(const fe& k, int j) { return (word_of(k, j >> 1) >> ((j & 1) * 16)) & 0xffffu; }
 
+// acc += the comb entry at tab when its digit d != 0 (complete mixed addition)
+__device__ __forceinline__ void keyed_add_entry(Jac26& acc, const uint32_t* tab, uint32_t d) {
+    Aff26 T;
+    load_aff26(T, tab);
+    Jac26 S;
+    CurveK1x::madd(S, acc, T);
+    CurveK1x::cmov(acc, S, d != 0u);
+}
+__device__ __forceinline__ void keyed_add_entry(JacP26& acc, const uint32_t* tab, uint32_t d) {
+    AffP26 T;
+    load_affp26(T, tab);
+    JacP26 S;
+    CurveSM2x::madd(S, acc, T);
+    CurveSM2x::cmov(acc, S, d != 0u);
+}
+
 // ok[i] = SignatureCrypto::verify(key of slot[i], hash[i], sig[i]); addr (SM2 tx admission: the verified
 // key's SM3 address) may be null.  One 64-thread workgroup = 4 signatures.
 template <int SUITE>
@@ -299,24 +315,18 @@ __global__ __launch_bounds__(64) void sig_verify_keyed_kernel(const uint32_t* __
         FieldInv<FieldN1>::inv_pipe(sinv, sm);
         FieldN1::mul(u1, e, sinv);
         FieldN1::mul(u2, r, sinv);
-        Jac26 acc, S;
+        Jac26 acc;
         CurveK1x::set_inf(acc);
-        auto add_entry = [&](const uint32_t* tab, uint32_t d) {
-            Aff26 T;
-            load_aff26(T, tab);
-            CurveK1x::madd(S, acc, T);
-            CurveK1x::cmov(acc, S, d != 0u);
-        };
         const uint32_t b0 = byte_of(u2, 2 * L), b1 = byte_of(u2, 2 * L + 1);
-        add_entry(ktab + (static_cast<size_t>(2 * L) * kCombEntries + b0) * 16, b0);
-        add_entry(ktab + (static_cast<size_t>(2 * L + 1) * kCombEntries + b1) * 16, b1);
+        keyed_add_entry(acc, ktab + (static_cast<size_t>(2 * L) * kCombEntries + b0) * 16, b0);
+        keyed_add_entry(acc, ktab + (static_cast<size_t>(2 * L + 1) * kCombEntries + b1) * 16, b1);
         if (gbits == kWideBits) {
             const uint32_t g = half_of(u1, L);
-            add_entry(gtab + (static_cast<size_t>(L) * kWideEntries + g) * 16, g);
+            keyed_add_entry(acc, gtab + (static_cast<size_t>(L) * kWideEntries + g) * 16, g);
         } else {
             const uint32_t g0 = byte_of(u1, 2 * L), g1 = byte_of(u1, 2 * L + 1);
-            add_entry(gtab + (static_cast<size_t>(2 * L) * kCombEntries + g0) * 16, g0);
-            add_entry(gtab + (static_cast<size_t>(2 * L + 1) * kCombEntries + g1) * 16, g1);
+            keyed_add_entry(acc, gtab + (static_cast<size_t>(2 * L) * kCombEntries + g0) * 16, g0);
+            keyed_add_entry(acc, gtab + (static_cast<size_t>(2 * L + 1) * kCombEntries + g1) * 16, g1);
         }
 #pragma unroll
         for (int off = 1; off < 16; off <<= 1) {
@@ -347,24 +357,18 @@ __global__ __launch_bounds__(64) void sig_verify_keyed_kernel(const uint32_t* __
         fe e;
         sm2_e_from_za(e, key + 16, h);
         reduce_once(e, ParamN2::M);
-        JacP26 acc, S;
+        JacP26 acc;
         CurveSM2x::set_inf(acc);
-        auto add_entry = [&](const uint32_t* tab, uint32_t d) {
-            AffP26 T;
-            load_affp26(T, tab);
-            CurveSM2x::madd(S, acc, T);
-            CurveSM2x::cmov(acc, S, d != 0u);
-        };
         const uint32_t b0 = byte_of(t, 2 * L), b1 = byte_of(t, 2 * L + 1);
-        add_entry(ktab + (static_cast<size_t>(2 * L) * kCombEntries + b0) * 16, b0);
-        add_entry(ktab + (static_cast<size_t>(2 * L + 1) * kCombEntries + b1) * 16, b1);
+        keyed_add_entry(acc, ktab + (static_cast<size_t>(2 * L) * kCombEntries + b0) * 16, b0);
+        keyed_add_entry(acc, ktab + (static_cast<size_t>(2 * L + 1) * kCombEntries + b1) * 16, b1);
         if (gbits == kWideBits) {
             const uint32_t g = half_of(s, L);
-            add_entry(gtab + (static_cast<size_t>(L) * kWideEntries + g) * 16, g);
+            keyed_add_entry(acc, gtab + (static_cast<size_t>(L) * kWideEntries + g) * 16, g);
         } else {
             const uint32_t g0 = byte_of(s, 2 * L), g1 = byte_of(s, 2 * L + 1);
-            add_entry(gtab + (static_cast<size_t>(2 * L) * kCombEntries + g0) * 16, g0);
-            add_entry(gtab + (static_cast<size_t>(2 * L + 1) * kCombEntries + g1) * 16, g1);
+            keyed_add_entry(acc, gtab + (static_cast<size_t>(2 * L) * kCombEntries + g0) * 16, g0);
+            keyed_add_entry(acc, gtab + (static_cast<size_t>(2 * L + 1) * kCombEntries + g1) * 16, g1);
         }
 #pragma unroll
         for (int off = 1; off < 16; off <<= 1) {
@@ -446,8 +450,11 @@ int capacity_env() {
 
 int promote_after() {
     static const int k = [] {
-        const char* e = getenv("BCOSGPU_KEY_PROMOTE");  // calls that must see a key before it is cached; 0 = never
-        return e ? atoi(e) : 2;
+        // calls that must see a key before it is cached (0 = never).  3: a sealer's key is cached by its
+        // third block, while admission traffic over many distinct keys (each seen once or twice) does not
+        // fill the cache with one-off keys
+        const char* e = getenv("BCOSGPU_KEY_PROMOTE");
+        return e ? atoi(e) : 3;
     }();
     return k;
 }

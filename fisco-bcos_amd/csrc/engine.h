@@ -44,7 +44,7 @@ uint64_t merkle_levels(uint64_t n, int width);
 // the output vector -> the packed vector<bytes> layout (4-byte count records)
 int launch_merkle_compact(const uint8_t* d_tree, uint64_t n, int width, uint8_t* d_out, hipStream_t st);
 
-// ecc_kernels.hip
+// ecc_tables.hip, ecc_sig.hip, ecc_txv.hip (the ECC kernels: tables, signing, verify / recover launchers)
 int ecc_init_tables(int device, int small_tables);
 void set_tx_kernel_policy(int split, int occ, int coop, int f26);
 int launch_secp256k1_recover(const uint8_t* d_hash, const uint8_t* d_sig, uint32_t sig_stride,

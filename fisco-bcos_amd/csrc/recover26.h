@@ -1,11 +1,11 @@
 // recover26.h -- secp256k1 public-key recovery with the point arithmetic over the 10 x 26-bit field
 // (fe26.h / ec26.h), for the throughput kernels (tx_verify_kernel<secp, *> and the recover / verify
 // kernels).  Same algorithm, same decisions and same outputs as secp256k1_recover_rsv in
-// ecc_kernels.hip (libsecp256k1 secp256k1_ecdsa_recover semantics, as wedpr calls it from
+// ecc_device.h (libsecp256k1 secp256k1_ecdsa_recover semantics, as wedpr calls it from
 // Secp256k1Crypto.cpp:79-93): the scalar work (range checks, r^-1 mod n, u1, u2, the GLV split) stays
 // in the 8 x 32-bit code, the curve work -- sqrt, the GLV double-and-add over the co-Z table, the comb,
 // the final addition -- runs on fe26, and the result is converted back to canonical words once.
-// Included by ecc_kernels.hip after its FieldK1 helpers (constants, glv_split, booth digits, CombTab).
+// Included by ecc_device.h after its FieldK1 helpers (constants, glv_split, booth digits, CombTab).
 #pragma once
 #include "ec26.h"
 

@@ -3,7 +3,7 @@
 // (sm2_do_verify semantics, SM2Crypto.cpp:66-92 -> fast_sm2.cpp:139-227): the scalar work (range
 // checks, t = r + s mod n, e = SM3(Z_A || h)) stays 8 x 32-bit; t*P (table 1P..8P, 65 radix-16 Booth
 // windows), s*G (comb over tables re-expressed in the R' domain at init) and the projective x-check run
-// on fp26.  Included by ecc_kernels.hip after its SM2 helpers.
+// on fp26.  Included by ecc_device.h after its SM2 helpers.
 #pragma once
 #include "ecp26.h"
 

@@ -185,7 +185,7 @@ def test_registered_key_exceptional_additions(gpu, oracle):
 
 
 def test_promotion_single_calls_and_sm2_recover(gpu, oracle):
-    """Keys seen in two calls are promoted (BCOSGPU_KEY_PROMOTE, default 2): the second batch and the single
+    """Keys seen in three calls are promoted (BCOSGPU_KEY_PROMOTE, default 3): the third batch and the single
     SignatureCrypto::verify calls after it run on the registered-key kernel with the oracle's verdicts; SM2
     recover (SM2Crypto::recover, embedded key) over registered keys returns the same addresses as the
     generic path."""
@@ -200,7 +200,9 @@ def test_promotion_single_calls_and_sm2_recover(gpu, oracle):
         want = np.ones(nk, dtype=bool)
         i0 = gpu.key_cache_info(suite)
         assert np.array_equal(crypto.verify_batch(pub, h, sig), want)   # first sighting: generic
-        assert np.array_equal(crypto.verify_batch(pub, h, sig), want)   # promoted: keyed
+        assert np.array_equal(crypto.verify_batch(pub, h, sig), want)   # second: generic
+        assert gpu.key_cache_info(suite)["built"] == i0["built"]
+        assert np.array_equal(crypto.verify_batch(pub, h, sig), want)   # third: promoted, keyed
         i1 = gpu.key_cache_info(suite)
         assert i1["built"] - i0["built"] == nk and i1["keyed"] - i0["keyed"] >= nk
         for i in range(nk):
