@@ -427,6 +427,8 @@ struct KeyCache {
     std::unordered_map<Key64, int32_t, Key64Hash> slot_of;
     std::unordered_map<Key64, uint32_t, Key64Hash> seen;
     uint64_t hits = 0, misses = 0, builds = 0;
+    int promoted = 0;  // slots taken by promotion: at most half the capacity, the rest stays for registrations
+    int registered = 0;
 };
 
 std::mutex g_kc_mu;
@@ -553,7 +555,7 @@ int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int
         }
         out[i] = -1;
         bool build = force;
-        if (!build && promote_after() > 0) {
+        if (!build && promote_after() > 0 && c.promoted + static_cast<int>(todo.size()) < capacity_env() / 2) {
             if (c.seen.size() > (1u << 20)) c.seen.clear();
             build = ++c.seen[k] >= static_cast<uint32_t>(promote_after());
         }
@@ -566,8 +568,10 @@ int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int
     }
     if (!todo.empty()) {
         std::vector<int32_t> got;
+        const int before = static_cast<int>(c.slot_of.size());
         const int rc = build_keys(c, suite, todo, got, st);
         if (rc) return rc;
+        (force ? c.registered : c.promoted) += static_cast<int>(c.slot_of.size()) - before;
         for (size_t q = 0; q < todo.size(); ++q) {
             out[todo_at[q]] = got[q];
             if (got[q] < 0) every = false;
@@ -639,6 +643,7 @@ int keyed_clear(int device, int suite) {
     if (e != hipSuccess) return BCOSGPU_E_HIP;
     c.slot_of.clear();
     c.seen.clear();
+    c.promoted = c.registered = 0;
     return 0;
 }
 

@@ -26,8 +26,12 @@ def _is_sep(name):
 
 
 def _legs(rows, order):
-    """rows: [(dispatch_id, kernel, payload)] -> {leg: [(kernel, payload), ...]} by separator pairs."""
+    """rows: [(dispatch_id, kernel, payload)] -> {leg: [(kernel, payload), ...]} by separator pairs (the last
+    2 x len(order) fills: an earlier fill -- a torch.zeros -- is not a separator)."""
     rows.sort(key=lambda r: r[0])
+    fills = [i for i, r in enumerate(rows) if _is_sep(r[1])]
+    if len(fills) > 2 * len(order):
+        rows = rows[fills[len(fills) - 2 * len(order)]:]
     out, cur, nsep = {}, None, 0
     for _, k, pay in rows:
         if _is_sep(k):

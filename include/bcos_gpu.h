@@ -207,7 +207,8 @@ int bcosgpu_verify_batch_dev(int suite, const uint8_t* d_pub64, const uint8_t* d
  *     Returns the number of keys cached (< 0 on error).  Registering a cached key is a lookup.
  *   Host-pointer verify calls (bcosgpu_verify_batch, bcosgpu_secp256k1_verify, bcosgpu_sm2_verify, the
  *     device-set batches, SM2 recover) take the registered-key kernel when every key of the coalesced
- *     batch is cached; a key seen in BCOSGPU_KEY_PROMOTE (default 3) calls is cached automatically.
+ *     batch is cached; a key seen in BCOSGPU_KEY_PROMOTE (default 3) calls is cached automatically (in at
+ *     most half the capacity: the other half is kept for registrations).
  *   bcosgpu_verify_keyed_batch_dev: ok[i] = verify(key of d_slots[i], d_hash32 + 32 i, d_sig +
  *     sig_stride i) on the calling thread's device, stream-ordered; a slot that is not registered fails.
  *   bcosgpu_key_cache_info: out5 = {keys cached, capacity, verified on the keyed path, verified
