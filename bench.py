@@ -353,8 +353,9 @@ def run_leg(ctx, wl_name, steps=None, warmup=3, warm_seconds=0.0, min_seconds=2.
         "work_per_unit": "%d F x %d MAC executed (kernel schedule, DESIGN.md 9)" % (f_exec, MAC_PER_F),
         "algorithmic": {"work_per_unit": "%d F x %d MAC (SURVEY.md 8d, non-GLV count)" % (f_alg, MAC_PER_F),
                         "achieved": alg / 1e12, "frac": alg / PEAK_MAC_PER_S,
-                        "note": "useful work per second against the MAC peak; exceeds the executed frac "
-                                "because GLV and the comb execute fewer multiplications than 8d counts"},
+                        "note": "USEFUL work per second (SURVEY 8d's non-GLV count) against the MAC peak, not an "
+                                "issue rate: GLV and the comb execute fewer multiplications than 8d counts, so "
+                                "it can exceed 1 (C4/C5); the issue fraction is valu_issue"},
         "algorithmic_bytes_per_unit": 151 + 65 + 53 if suite == 0 else 151 + 128 + 53,
     }
     rec = {"workload": wl["name"], "value": units_total * steps / elapsed, "unit": "tx/s",
@@ -1047,7 +1048,7 @@ def summarize(full, head_name):
         alg = rf["algorithmic_bytes_per_unit"] * max(rf["units_per_launch"], 1)
         vi = rf.get("valu_issue")
         return {"tx_s": _g(rec["value"]), "ms_step": _g(rec["ms_per_step"]), "kernel_ms": _g(rf["kernel_ms"]),
-                "frac": _g(rf["frac"], 3), "frac_8d": _g(rf["algorithmic"]["frac"], 3),
+                "frac": _g(rf["frac"], 3), "useful_8d": _g(rf["algorithmic"]["frac"], 3),
                 "traffic_x": _g(rf["traffic"] / alg, 3) if rf.get("traffic") else None,
                 "valu_issue": _g(vi["frac"] if isinstance(vi, dict) else vi, 3)}
     out[head_name] = leg(full["head"])
@@ -1110,7 +1111,7 @@ def compact_line(full):
                                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")}
     line["roofline"] = {
         "bound": rf["bound"], "achieved": _g(rf["achieved"], 5), "peak": _g(rf["peak"], 5), "unit": rf["unit"],
-        "frac": _g(rf["frac"], 4), "frac_8d": _g(rf["algorithmic"]["frac"], 4), "kernel": rf["kernel"],
+        "frac": _g(rf["frac"], 4), "useful_8d": _g(rf["algorithmic"]["frac"], 4), "kernel": rf["kernel"],
         "kernel_ms": _g(rf["kernel_ms"], 5), "traffic": _g(rf["traffic"], 5) if rf.get("traffic") else None,
         "valu_issue": _g(vi["frac"] if isinstance(vi, dict) else vi, 4),
         "work": "%d txs x %s" % (rf["units_per_launch"], rf["work_per_unit"].split(" (")[0]),

@@ -62,7 +62,7 @@ def test_line_is_strict_json_under_the_limit(which):
         assert k in back, (name, k)
     assert list(back)[-1] == "summary"  # the last key survives a tail-only record
     rf = back["roofline"]
-    for k in ("bound", "achieved", "peak", "unit", "frac", "frac_8d", "kernel", "kernel_ms", "traffic", "valu_issue"):
+    for k in ("bound", "achieved", "peak", "unit", "frac", "useful_8d", "kernel", "kernel_ms", "traffic", "valu_issue"):
         assert k in rf, (name, k)
     assert 0 < rf["frac"] <= 1
     cb = back["cpu_baseline"]
