@@ -993,7 +993,9 @@ def devset_legs(devices, min_seconds=1.0):
     """The topology INTEGRATION.md section 2 prescribes: ONE process drives the device list through the C ABI
     a node links (csrc/multi.hip): C4 = configs[3]'s 1M secp256k1 txs as one block through
     bcosgpu_block_verify_multi (index shards, width-2 frontiers gathered on devices[0] by peer copies);
-    C5 = configs[4]'s 64 blocks x 20k txs, one bcosgpu_block_verify_multi call per block in order (a replay).
+    C5 = configs[4]'s 64 blocks x 20k txs in one bcosgpu_blocks_verify_multi call (whole blocks per device,
+    each device's roots by the many-tree level kernel), and c5_seq = one bcosgpu_block_verify_multi call per
+    block in order (each block sharded over the devices).
     Host buffers in and out (H2D + kernels + D2H per call: the PCIe-inclusive rate, not `value`).  Each
     leg's root and statuses are checked against the single-device call."""
     import numpy as np
@@ -1011,23 +1013,31 @@ def devset_legs(devices, min_seconds=1.0):
     def c4(devs):
         return tx.verify_packed_multi(devs, suite, pre, po[: n4 + 1], sg, so[: n4 + 1], width=2)
 
-    def c5(devs):
+    nblk = WORKLOADS["c5"]["blocks"]
+    bo = np.arange(nblk + 1, dtype=np.uint64) * np.uint64(per)
+
+    def c5(devs):  # the 64 blocks in one call, whole blocks per device (bcosgpu_blocks_verify_multi)
+        return tx.blocks_verify_multi(devs, suite, pre, po, sg, so, bo, width=2)
+
+    def c5_seq(devs):  # one block at a time, each sharded over the devices (bcosgpu_block_verify_multi)
         return [tx.verify_packed_multi(devs, suite, pre, po[k * per: (k + 1) * per + 1], sg,
                                        so[k * per: (k + 1) * per + 1], width=2)
-                for k in range(WORKLOADS["c5"]["blocks"])]
+                for k in range(nblk)]
 
-    for wl, fn in (("c4", c4), ("c5", c5)):
+    def _same(g, w):
+        return all(np.array_equal(x, y) for x, y in zip(g[:3], w[:3])) and (
+            np.array_equal(g[3], w[3]) if isinstance(g[3], np.ndarray) else g[3] == w[3])
+
+    for wl, fn in (("c4", c4), ("c5", c5), ("c5_seq", c5_seq)):
         want = fn([devices[0]])
         got = fn(devices)
-        def _same(g, w):
-            return all(np.array_equal(x, y) for x, y in zip(g[:3], w[:3])) and g[3] == w[3]
-        same = _same(got, want) if wl == "c4" else all(_same(g, w) for g, w in zip(got, want))
+        same = _same(got, want) if wl != "c5_seq" else all(_same(g, w) for g, w in zip(got, want))
         steps, t0 = 0, time.perf_counter()
         while steps < 2 or time.perf_counter() - t0 < min_seconds:
             fn(devices)
             steps += 1
         dt = (time.perf_counter() - t0) / steps
-        out[wl] = {"tx_s": WORKLOADS[wl]["n"] / dt, "ms_per_step": dt * 1e3, "steps": steps,
+        out[wl] = {"tx_s": WORKLOADS[wl.split("_")[0]]["n"] / dt, "ms_per_step": dt * 1e3, "steps": steps,
                    "matches_single_device": bool(same)}
     return out
 

@@ -89,6 +89,7 @@ _SIGS = {
     "bcosgpu_tx_verify_batch_multi": (_I, [_P, _I, _I, _P, _P, _P, _P, _SZ, _P, _P, _P]),
     "bcosgpu_block_verify_multi": (_I, [_P, _I, _I, _P, _P, _P, _P, _SZ, _I, _P, _P, _P, _P]),
     "bcosgpu_merkle_root_multi": (_I, [_P, _I, _I, _I, _P, _SZ, _P]),
+    "bcosgpu_blocks_verify_multi": (_I, [_P, _I, _I, _P, _P, _P, _P, _P, _SZ, _I, _P, _P, _P, _P]),
     "bcosgpu_wedpr_secp256k1_recover_public_key": (ctypes.c_int8, [_P, _P, _P]),
     "bcosgpu_wedpr_sm2_verify": (ctypes.c_int8, [_P, _P, _P]),
     "bcosgpu_wedpr_secp256k1_verify": (ctypes.c_int8, [_P, _P, _P]),

@@ -175,6 +175,26 @@ def verify_packed_multi(devices, suite: CryptoSuite, pre, pre_off, sig, sig_off,
     return txhash, sender, status, root.tobytes()
 
 
+def blocks_verify_multi(devices, suite: CryptoSuite, pre, pre_off, sig, sig_off, block_off, width=2):
+    """Many blocks in one call over a device set (bcosgpu_blocks_verify_multi): block b = txs
+    [block_off[b], block_off[b+1]).  Returns (txhash, sender, status, roots uint8[nblocks, 32])."""
+    d = _devices(devices)
+    bo = np.ascontiguousarray(block_off, dtype=np.uint64)
+    nb = bo.size - 1
+    n = int(bo[-1]) if nb >= 0 else 0
+    txhash = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    sender = np.zeros((max(n, 1), 20), dtype=np.uint8)
+    status = np.zeros(max(n, 1), dtype=np.uint8)
+    roots = np.zeros((max(nb, 1), 32), dtype=np.uint8)
+    p = pre if len(pre) else np.zeros(1, dtype=np.uint8)
+    s = sig if len(sig) else np.zeros(1, dtype=np.uint8)
+    po = np.ascontiguousarray(pre_off, dtype=np.uint64)
+    so = np.ascontiguousarray(sig_off, dtype=np.uint64)
+    check(lib().bcosgpu_blocks_verify_multi(_ptr(d), d.size, suite.suite, _ptr(p), _ptr(po), _ptr(s), _ptr(so), _ptr(bo),
+                                            nb, width, _ptr(txhash), _ptr(sender), _ptr(status), _ptr(roots)))
+    return txhash[:n], sender[:n], status[:n], roots[:nb]
+
+
 def merkle_root_multi(devices, hasher, width, leaves):
     """Merkle<H, width> root over a device set (bcosgpu_merkle_root_multi); leaves uint8[n, 32]."""
     d = _devices(devices)

@@ -358,6 +358,98 @@ int tx_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const 
     return gather_root(devices, ndev, p, frontier, hasher, width, top, root32);
 }
 
+// Many blocks at once over the device set (a sync catch-up or a replay: configs[4]): whole blocks per
+// device, contiguous ranges balanced by tx count; each device verifies its txs and computes its blocks'
+// roots with the many-tree level kernel (launch_merkle_roots_batch); no exchange.
+int blocks_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off, const uint8_t* sig,
+                 const uint64_t* sig_off, const uint64_t* block_off, size_t nblocks, int width, uint8_t* txhash32,
+                 uint8_t* sender20, uint8_t* status, uint8_t* roots32) {
+    if (suite != BCOSGPU_SUITE_SECP256K1 && suite != BCOSGPU_SUITE_SM2) return api_set_err(BCOSGPU_E_ARG, "bad suite");
+    if (width < 2 || width > 64) return api_set_err(BCOSGPU_E_ARG, "width must be in [2, 64]");
+    if (nblocks == 0) return check_set(devices, ndev);
+    if (!block_off || !roots32) return api_set_err(BCOSGPU_E_ARG, "null pointer");
+    if (block_off[0] != 0) return api_set_err(BCOSGPU_E_ARG, "block_off[0] must be 0");
+    for (size_t b = 0; b < nblocks; ++b)
+        if (block_off[b + 1] < block_off[b] || block_off[b + 1] - block_off[b] > 0xFFFFFFFFull)
+            return api_set_err(BCOSGPU_E_ARG, "block offsets must be non-decreasing");
+    const uint64_t n = block_off[nblocks];
+    if (n && (!pre || !pre_off || !sig || !sig_off || !txhash32 || !sender20 || !status))
+        return api_set_err(BCOSGPU_E_ARG, "null pointer");
+    for (uint64_t i = 0; i < n; ++i)
+        if (pre_off[i + 1] < pre_off[i] || sig_off[i + 1] < sig_off[i] || pre_off[i + 1] - pre_off[i] > 0xFFFFFFFFull)
+            return api_set_err(BCOSGPU_E_ARG, "offsets must be non-decreasing");
+    if (int rc = check_set(devices, ndev)) return rc;
+    const int hasher = suite == BCOSGPU_SUITE_SM2 ? BCOSGPU_SM3 : BCOSGPU_KECCAK256;
+    // block ranges [bl[k], bl[k + 1]): device k's share ends at the first block boundary past (k + 1) n / ndev
+    std::vector<size_t> bl(ndev + 1, nblocks);
+    bl[0] = 0;
+    for (int k = 1; k < ndev; ++k) {
+        const uint64_t want = n * static_cast<uint64_t>(k) / static_cast<uint64_t>(ndev);
+        size_t b = bl[k - 1];
+        while (b < nblocks && block_off[b] < want) ++b;
+        bl[k] = b;
+    }
+    std::vector<ShardCtx*> ctx = contexts(devices, ndev);
+    auto locks = lock_all(ctx);
+    return run_shards(ndev, [&](int k, std::string& msg) -> int {
+        const size_t b0 = bl[k], b1 = bl[k + 1];
+        if (b0 == b1) return 0;
+        const uint64_t lo = block_off[b0], hi = block_off[b1], m = hi - lo;
+        ShardCtx* c = ctx[k];
+        DeviceGuard dg(c->device);
+        SHARD_HIP(dg.err);
+        SHARD_HIP(ensure_stream(c));
+        const uint64_t pb = m ? pre_off[lo] : 0, pbytes = m ? pre_off[hi] - pb : 0;
+        const uint64_t sb = m ? sig_off[lo] : 0, sbytes = m ? sig_off[hi] - sb : 0;
+        const size_t nb = b1 - b0;
+        SHARD_HIP(c->b[0].ensure(pbytes + 8));
+        SHARD_HIP(c->b[1].ensure((m + 1) * 8));
+        SHARD_HIP(c->b[2].ensure(sbytes + 8));
+        SHARD_HIP(c->b[3].ensure((m + 1) * 8));
+        SHARD_HIP(c->b[4].ensure(m * 32 + 32));
+        SHARD_HIP(c->b[5].ensure(m * 20 + 4));
+        SHARD_HIP(c->b[6].ensure(m + 4));
+        SHARD_HIP(c->b[7].ensure(merkle_roots_work_bytes(m, nb, width)));
+        SHARD_HIP(c->b[8].ensure(nb * 32));
+        std::vector<uint64_t> boff(nb + 1);
+        for (size_t b = 0; b <= nb; ++b) boff[b] = block_off[b0 + b] - lo;
+        if (m) {
+            std::vector<uint64_t> po(m + 1), so(m + 1);
+            for (uint64_t i = 0; i <= m; ++i) {
+                po[i] = pre_off[lo + i] - pb;
+                so[i] = sig_off[lo + i] - sb;
+            }
+            SHARD_HIP(hipMemcpyAsync(c->b[0].p, pre + pb, pbytes, hipMemcpyHostToDevice, c->stream));
+            SHARD_HIP(hipMemcpyAsync(c->b[1].p, po.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
+            SHARD_HIP(hipMemcpyAsync(c->b[2].p, sig + sb, sbytes, hipMemcpyHostToDevice, c->stream));
+            SHARD_HIP(hipMemcpyAsync(c->b[3].p, so.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
+            const int lrc = launch_tx_verify(suite, c->b[0].as<uint8_t>(), c->b[1].as<uint64_t>(), c->b[2].as<uint8_t>(),
+                                             c->b[3].as<uint64_t>(), m, c->b[4].as<uint8_t>(), c->b[5].as<uint8_t>(),
+                                             c->b[6].as<uint8_t>(), c->stream);
+            if (lrc) {
+                msg = hip_msg(hipGetLastError(), "tx verify launch");
+                return lrc;
+            }
+            // (the pageable po / so must outlive their copies: wait before they go out of scope)
+            SHARD_HIP(hipStreamSynchronize(c->stream));
+        }
+        const int rrc = launch_merkle_roots_batch(hasher, width, c->b[4].as<uint8_t>(), boff.data(), nb,
+                                                  c->b[7].as<uint8_t>(), c->b[8].as<uint8_t>(), c->stream);
+        if (rrc) {
+            msg = hip_msg(hipGetLastError(), "merkle roots launch");
+            return rrc;
+        }
+        if (m) {
+            SHARD_HIP(hipMemcpyAsync(txhash32 + 32 * lo, c->b[4].p, m * 32, hipMemcpyDeviceToHost, c->stream));
+            SHARD_HIP(hipMemcpyAsync(sender20 + 20 * lo, c->b[5].p, m * 20, hipMemcpyDeviceToHost, c->stream));
+            SHARD_HIP(hipMemcpyAsync(status + lo, c->b[6].p, m, hipMemcpyDeviceToHost, c->stream));
+        }
+        SHARD_HIP(hipMemcpyAsync(roots32 + 32 * b0, c->b[8].p, nb * 32, hipMemcpyDeviceToHost, c->stream));
+        SHARD_HIP(hipStreamSynchronize(c->stream));
+        return 0;
+    });
+}
+
 }  // namespace
 
 extern "C" {
@@ -399,6 +491,13 @@ int bcosgpu_block_verify_multi(const int* devices, int ndev, int suite, const ui
                                uint8_t* sender20, uint8_t* status, uint8_t* root32) {
     if (!root32) return api_set_err(BCOSGPU_E_ARG, "null root pointer");
     return tx_multi(devices, ndev, suite, pre, pre_off, sig, sig_off, n, width, txhash32, sender20, status, root32);
+}
+
+int bcosgpu_blocks_verify_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off,
+                                const uint8_t* sig, const uint64_t* sig_off, const uint64_t* block_off, size_t nblocks,
+                                int width, uint8_t* txhash32, uint8_t* sender20, uint8_t* status, uint8_t* roots32) {
+    return blocks_multi(devices, ndev, suite, pre, pre_off, sig, sig_off, block_off, nblocks, width, txhash32, sender20,
+                        status, roots32);
 }
 
 int bcosgpu_merkle_root_multi(const int* devices, int ndev, int hasher, int width, const uint8_t* leaves32, size_t n,

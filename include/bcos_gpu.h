@@ -335,6 +335,13 @@ int bcosgpu_tx_verify_batch_multi(const int* devices, int ndev, int suite, const
 int bcosgpu_block_verify_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off,
                                const uint8_t* sig, const uint64_t* sig_off, size_t n, int width, uint8_t* txhash32,
                                uint8_t* sender20, uint8_t* status, uint8_t* root32);
+/* Many blocks in one call (a sync catch-up / replay of downloaded blocks, configs[4]): block b's txs are
+ * [block_off[b], block_off[b+1]) (block_off[0] = 0, nblocks + 1 entries), every tx verified as
+ * bcosgpu_tx_verify_batch does and roots32 + 32 b = block b's tx root (zero hash for an empty block).
+ * Whole blocks go to the devices in contiguous ranges balanced by tx count; no exchange. */
+int bcosgpu_blocks_verify_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off,
+                                const uint8_t* sig, const uint64_t* sig_off, const uint64_t* block_off, size_t nblocks,
+                                int width, uint8_t* txhash32, uint8_t* sender20, uint8_t* status, uint8_t* roots32);
 /* Merkle<H, width>::generateMerkle's root (Merkle.h:170-208) over the set, by the same frontier scheme;
  * n == 0 is BCOSGPU_E_EMPTY, n == 1 returns the leaf. */
 int bcosgpu_merkle_root_multi(const int* devices, int ndev, int hasher, int width, const uint8_t* leaves32, size_t n,

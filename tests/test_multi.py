@@ -44,6 +44,11 @@ def test_device_set_argument_errors_without_gpu():
     assert L.bcosgpu_merkle_root_multi(devs, 1, 0, 1, None, 0, root) == _lib.E_ARG  # width
     assert L.bcosgpu_block_verify_multi(devs, 1, 0, None, None, None, None, 0, 2, None, None, None, None) == _lib.E_ARG
     assert L.bcosgpu_block_verify_multi(devs, 1, 5, None, None, None, None, 0, 2, None, None, None, root) == _lib.E_ARG
+    bo = (ctypes.c_uint64 * 3)(1, 2, 3)
+    assert L.bcosgpu_blocks_verify_multi(devs, 1, 0, None, None, None, None, bo, 2, 2, None, None, None, root) == _lib.E_ARG
+    bo = (ctypes.c_uint64 * 3)(0, 2, 1)  # decreasing
+    assert L.bcosgpu_blocks_verify_multi(devs, 1, 0, None, None, None, None, bo, 2, 2, None, None, None, root) == _lib.E_ARG
+    assert L.bcosgpu_blocks_verify_multi(devs, 1, 0, None, None, None, None, bo, 2, 1, None, None, None, root) == _lib.E_ARG
     if L.bcosgpu_device_count() == 0:
         assert L.bcosgpu_init_devices(devs, 1) == _lib.E_NODEV
 
@@ -109,6 +114,34 @@ def test_device_sets_peer_copy_branch(gpu, oracle, suite, monkeypatch):
                 assert np.array_equal(st, wst) and np.array_equal(th, wh) and np.array_equal(snd, ws), (n, devs)
                 assert root == want_root, (n, devs, width)
                 assert tx.merkle_root_multi(devs, hasher, width, wh) == want_root, (n, devs, width)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("suite", [0, 1])
+def test_many_blocks_over_device_sets(gpu, oracle, suite):
+    """bcosgpu_blocks_verify_multi (a sync catch-up / configs[4]'s replay in one call): 37 blocks of 0 to
+    3,000 txs (empty and one-tx blocks included) over {0}, {0, 0}, {0, 0, 0}: every hash, sender and
+    verdict, and every block's root (width 2 and 16; the zero hash for an empty block, BlockImpl.h:114-119)
+    against the oracle."""
+    from bcos_gpu import synth, tx
+    rng = np.random.default_rng(0xB10C + suite)
+    sizes = [int(x) for x in rng.integers(0, 3000, size=37)]
+    sizes[3], sizes[4], sizes[20] = 0, 1, 0
+    bo = np.zeros(len(sizes) + 1, dtype=np.uint64)
+    bo[1:] = np.cumsum(sizes)
+    n = int(bo[-1])
+    b = synth.make_batch(suite, n, seed=0x77 + suite, flip_frac=0.05, bad_v_frac=0.02)
+    pre, po, sg, so = _host(b)
+    wh, ws, wst = oracle.tx_verify_packed(suite, pre, po, sg, so, nthreads=_threads())
+    hasher = oracle.SM3 if suite else oracle.KECCAK256
+    suite_obj = gpu.sm_suite() if suite else gpu.secp256k1_suite()
+    for width in (2, 16):
+        want_roots = [oracle.merkle(hasher, width, wh[int(bo[k]):int(bo[k + 1])]) if sizes[k] else bytes(32)
+                      for k in range(len(sizes))]
+        for devs in ([0], [0, 0], [0, 0, 0]):
+            th, snd, st, roots = tx.blocks_verify_multi(devs, suite_obj, pre, po, sg, so, bo, width=width)
+            assert np.array_equal(th, wh) and np.array_equal(snd, ws) and np.array_equal(st, wst), (devs, width)
+            assert [r.tobytes() for r in roots] == want_roots, (devs, width)
 
 
 @pytest.mark.gpu
