@@ -38,6 +38,32 @@ struct ByteReader {
     }
 };
 
+// ByteReader without branches (hash_batch_kernel): both dwords of a word are loaded from clamped
+// indices and selected, so a block's loads issue back to back under one wait instead of one branch
+// and one s_waitcnt each.  Still never reads a dword outside the message: an empty message that
+// overlaps no dword reads a zero constant.
+__device__ __constant__ static const uint32_t kZeroDwords[2] = {0u, 0u};
+struct FlatReader {
+    const uint32_t* q;  // aligned base (kZeroDwords when no dword overlaps the message)
+    uint32_t sh, len, nq, last;
+    __device__ FlatReader(const uint8_t* p, uint32_t n) {
+        uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        sh = static_cast<uint32_t>(a & 3u);
+        nq = (n + sh + 3u) >> 2;
+        q = nq ? reinterpret_cast<const uint32_t*>(a - sh) : kZeroDwords;
+        last = nq ? nq - 1u : 0u;
+        len = n;
+    }
+    __device__ __forceinline__ uint32_t word(uint32_t i) const {
+        const uint32_t l = q[i < last ? i : last], h = q[i + 1u < last ? i + 1u : last];
+        const uint32_t lo = i < nq ? l : 0u, hi = i + 1u < nq ? h : 0u;
+        uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        const uint32_t b = i * 4u;
+        const uint32_t keep = b >= len ? 0u : b + 4u > len ? (1u << ((len - b) * 8u)) - 1u : 0xffffffffu;
+        return w & keep;
+    }
+};
+
 // Reader for 4-byte-aligned messages whose length is a multiple of 4 (Merkle nodes: 32-B children).
 struct AlignedReader {
     const uint32_t* q;

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256) void hash_batch_kernel(const uint8_t* __restri
     if (i >= n) return;
     const uint64_t a = off[i], b = off[i + 1];
     const uint32_t len = static_cast<uint32_t>(b - a);
-    ByteReader rd(data + a, len);
+    FlatReader rd(data + a, len);
     uint32_t d[8];
     if (H == KECCAK256) keccak256_msg(rd, len, d);
     else sm3_msg(rd, len, d);
