@@ -312,7 +312,9 @@ int bcosgpu_sm2_verify(int device, const uint8_t* pub64, const uint8_t* hash32, 
  * ndev device indices (1 <= ndev <= 64); a batch is split by index into ndev contiguous shards, shard k
  * running on devices[k] on its own stream with its own buffers -- an index may repeat (two shards on one
  * GPU, distinct streams).  Results are identical to the single-device calls for every n.  Host pointers;
- * the calling thread's current device is left unchanged.
+ * the calling thread's current device is left unchanged.  Test status: every entry point is checked
+ * against the oracle on repeated-device lists ({0, 0}, {0, 0, 0}), including the cross-device peer-copy
+ * gather (forced by BCOSGPU_MULTI_PEER=1); lists of distinct physical GPUs have not run on hardware yet.
  * Initialise every device of the set (tables, streams); idempotent. */
 int bcosgpu_init_devices(const int* devices, int ndev);
 /* The signature batches above, sharded over the set (each shard a coalesced job on its device). */
