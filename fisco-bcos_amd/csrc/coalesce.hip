@@ -195,36 +195,44 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
     }
     // every key of the batch registered (or promoted now): the registered-key kernel (ecc_keyed.hip)
     bool keyed = false;
+    uint64_t gen = 0;
+    const int vsuite = kind == kSigJobVerifySM2 ? BCOSGPU_SUITE_SM2 : BCOSGPU_SUITE_SECP256K1;
     if (verify) {
-        const int suite = kind == kSigJobVerifySM2 ? BCOSGPU_SUITE_SM2 : BCOSGPU_SUITE_SECP256K1;
         const uint8_t* pubs = kind == kSigJobVerifySM2 ? in + 32 * n + 64 : in;
-        const int krc = keyed_slots(suite, pubs, kind == kSigJobVerifySM2 ? 128 : 64, n,
-                                    reinterpret_cast<int32_t*>(in + slots_at), false, &keyed, slot.stream);
+        const int krc = keyed_slots(vsuite, pubs, kind == kSigJobVerifySM2 ? 128 : 64, n,
+                                    reinterpret_cast<int32_t*>(in + slots_at), false, &keyed, slot.stream, &gen);
         if (krc) keyed = false;  // a failed table build leaves the generic path
     }
     if (!zero_copy) BATCH_HIP(hipMemcpyAsync(slot.d_in, slot.h_in, in_bytes, hipMemcpyHostToDevice, slot.stream));
     const uint8_t* di = zero_copy ? slot.hd_in : slot.d_in;
     uint8_t* dout = zero_copy ? slot.hd_out : slot.d_out;
-    int rc;
-    if (keyed && kind == kSigJobVerifySM2)
-        rc = launch_sig_verify_keyed(BCOSGPU_SUITE_SM2, reinterpret_cast<const int32_t*>(di + slots_at), di, di + 32 * n,
-                                     128, n, dout + 20 * n, want_addr ? dout : nullptr, slot.stream);
-    else if (keyed)
-        rc = launch_sig_verify_keyed(BCOSGPU_SUITE_SECP256K1, reinterpret_cast<const int32_t*>(di + slots_at),
-                                     di + 64 * n, di + 96 * n, 64, n, dout, nullptr, slot.stream);
-    else if (kind == kSigJobRecoverK1)
-        rc = launch_secp256k1_recover(di, di + 32 * n, 65, n, want_pub ? dout : nullptr,
-                                      want_addr ? dout + 64 * n : nullptr, dout + 84 * n, slot.stream);
-    else if (kind == kSigJobVerifySM2)
-        rc = launch_sm2_verify(di, di + 32 * n, 128, n, want_addr ? dout : nullptr, dout + 20 * n, slot.stream);
-    else
-        rc = launch_sig_verify(BCOSGPU_SUITE_SECP256K1, di, di + 64 * n, di + 96 * n, 64, n, dout, slot.stream);
-    if (rc) {
-        hipError_t e = hipGetLastError();
-        return fail(batch, rc, std::string("signature batch launch failed: ") + hipGetErrorString(e));
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        int rc;
+        if (keyed && kind == kSigJobVerifySM2)
+            rc = launch_sig_verify_keyed(BCOSGPU_SUITE_SM2, reinterpret_cast<const int32_t*>(di + slots_at), di,
+                                         di + 32 * n, 128, n, dout + 20 * n, want_addr ? dout : nullptr, slot.stream);
+        else if (keyed)
+            rc = launch_sig_verify_keyed(BCOSGPU_SUITE_SECP256K1, reinterpret_cast<const int32_t*>(di + slots_at),
+                                         di + 64 * n, di + 96 * n, 64, n, dout, nullptr, slot.stream);
+        else if (kind == kSigJobRecoverK1)
+            rc = launch_secp256k1_recover(di, di + 32 * n, 65, n, want_pub ? dout : nullptr,
+                                          want_addr ? dout + 64 * n : nullptr, dout + 84 * n, slot.stream);
+        else if (kind == kSigJobVerifySM2)
+            rc = launch_sm2_verify(di, di + 32 * n, 128, n, want_addr ? dout : nullptr, dout + 20 * n, slot.stream);
+        else
+            rc = launch_sig_verify(BCOSGPU_SUITE_SECP256K1, di, di + 64 * n, di + 96 * n, 64, n, dout, slot.stream);
+        if (rc) {
+            hipError_t e = hipGetLastError();
+            return fail(batch, rc, std::string("signature batch launch failed: ") + hipGetErrorString(e));
+        }
+        if (!zero_copy)
+            BATCH_HIP(hipMemcpyAsync(slot.h_out, slot.d_out, out_bytes, hipMemcpyDeviceToHost, slot.stream));
+        BATCH_HIP(hipStreamSynchronize(slot.stream));
+        // the key cache was cleared (bcosgpu_clear_keys) between the lookup and the launch: its slots may
+        // have been rebuilt for other keys meanwhile, so this batch runs again on the generic kernels
+        if (!keyed || keyed_generation(vsuite) == gen) break;
+        keyed = false;
     }
-    if (!zero_copy) BATCH_HIP(hipMemcpyAsync(slot.h_out, slot.d_out, out_bytes, hipMemcpyDeviceToHost, slot.stream));
-    BATCH_HIP(hipStreamSynchronize(slot.stream));
     // scatter
     const uint8_t* out = slot.h_out;
     at = 0;

@@ -429,6 +429,7 @@ struct KeyCache {
     uint64_t hits = 0, misses = 0, builds = 0;
     int promoted = 0;  // slots taken by promotion: at most half the capacity, the rest stays for registrations
     int registered = 0;
+    uint64_t gen = 0;  // bumped by keyed_clear: a slot looked up under another generation may name another key
 };
 
 std::mutex g_kc_mu;
@@ -531,7 +532,7 @@ int build_keys(KeyCache& c, int suite, const std::vector<Key64>& todo, std::vect
 // Slots of n keys (pub i at pubs + pub_stride * i) on the current device; keys not cached are built when
 // `force`, or when seen in promote_after() calls.  Returns 0 and *all = every key has a slot, or < 0.
 int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int32_t* out, bool force, bool* all,
-                hipStream_t st) {
+                hipStream_t st, uint64_t* gen) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BCOSGPU_E_NODEV;
     *all = false;
@@ -541,6 +542,7 @@ int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int
     }
     KeyCache& c = *cache_of(dev, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
     std::lock_guard<std::mutex> g(c.mu);
+    if (gen) *gen = c.gen;
     if (!force && c.slot_of.empty() && promote_after() <= 0) return 0;
     std::vector<Key64> todo;
     std::vector<size_t> todo_at;
@@ -556,7 +558,7 @@ int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int
         out[i] = -1;
         bool build = force;
         if (!build && promote_after() > 0 && c.promoted + static_cast<int>(todo.size()) < capacity_env() / 2) {
-            if (c.seen.size() > (1u << 20)) c.seen.clear();
+            if (c.seen.size() > (1u << 16)) c.seen.clear();  // a bounded sketch of recent keys
             build = ++c.seen[k] >= static_cast<uint32_t>(promote_after());
         }
         if (build) {
@@ -618,6 +620,14 @@ int launch_sig_verify_keyed(int suite, const int32_t* d_slots, const uint8_t* d_
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
+uint64_t keyed_generation(int suite) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return ~0ull;
+    KeyCache& c = *cache_of(dev, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
+    std::lock_guard<std::mutex> g(c.mu);
+    return c.gen;
+}
+
 int keyed_cache_info(int device, int suite, int64_t out[5]) {
     if (device < 0 || device >= 64) return BCOSGPU_E_ARG;
     KeyCache& c = *cache_of(device, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
@@ -644,6 +654,7 @@ int keyed_clear(int device, int suite) {
     c.slot_of.clear();
     c.seen.clear();
     c.promoted = c.registered = 0;
+    ++c.gen;
     return 0;
 }
 

@@ -213,7 +213,9 @@ int bcosgpu_verify_batch_dev(int suite, const uint8_t* d_pub64, const uint8_t* d
  *     sig_stride i) on the calling thread's device, stream-ordered; a slot that is not registered fails.
  *   bcosgpu_key_cache_info: out5 = {keys cached, capacity, verified on the keyed path, verified
  *     elsewhere, tables built}.  bcosgpu_clear_keys: drains the device, then forgets every key (a
- *     consensus membership change); slots are reassigned by later registrations. */
+ *     consensus membership change); slots are reassigned by later registrations (a coalesced batch that
+ *     looked its keys up before the clear runs again on the generic kernels; callers of
+ *     bcosgpu_verify_keyed_batch_dev must not clear while their launches are in flight). */
 int bcosgpu_register_keys(int device, int suite, const uint8_t* pub64, size_t n, int32_t* slots);
 int bcosgpu_verify_keyed_batch_dev(int suite, const int32_t* d_slots, const uint8_t* d_hash32, const uint8_t* d_sig,
                                    size_t sig_stride, size_t n, uint8_t* d_ok, void* stream);

@@ -228,3 +228,36 @@ def test_promotion_single_calls_and_sm2_recover(gpu, oracle):
     assert np.array_equal(got_ok, want_ok)
     for i in np.nonzero(want_ok)[0]:
         assert got_addr[i].tobytes() == oracle.sm3(pub[i].tobytes())[12:]
+
+
+def test_clear_and_reregister(gpu, oracle):
+    """bcosgpu_clear_keys (a consensus membership change) forgets every key; registering another set reuses
+    the slots; the forgotten keys' signatures then verify on the generic kernels and the new keys' on the
+    registered-key kernel, every verdict equal to the oracle's."""
+    rng = np.random.default_rng(4242)
+    for suite in (0, 1):
+        crypto = gpu.SM2Crypto() if suite else gpu.Secp256k1Crypto()
+        sk_a, sk_b = _keys(rng, 5), _keys(rng, 5)
+        h = rng.integers(0, 256, size=(5, 32), dtype=np.uint8)
+        pa, sa, _ = _dev_sign(gpu, suite, sk_a, h)
+        pb, sb, _ = _dev_sign(gpu, suite, sk_b, h)
+        sa, sb = sa.copy(), sb.copy()
+        sa[0, 7] ^= 1
+        sb[1, 9] ^= 2
+        want_a = np.array([_oracle_verify(oracle, suite, pa[i].tobytes(), h[i].tobytes(), sa[i].tobytes())
+                           for i in range(5)])
+        want_b = np.array([_oracle_verify(oracle, suite, pb[i].tobytes(), h[i].tobytes(), sb[i].tobytes())
+                           for i in range(5)])
+        slots_a = gpu.register_keys(suite, pa)
+        assert np.array_equal(crypto.verify_batch(pa, h, sa), want_a)
+        gpu.clear_keys(suite)
+        assert gpu.key_cache_info(suite)["keys"] == 0
+        slots_b = gpu.register_keys(suite, pb)
+        assert set(slots_b.tolist()) <= set(range(5)) and set(slots_a.tolist()) & set(slots_b.tolist())
+        k0 = gpu.key_cache_info(suite)
+        assert np.array_equal(crypto.verify_batch(pa, h, sa), want_a)   # forgotten: generic
+        k1 = gpu.key_cache_info(suite)
+        assert k1["keyed"] == k0["keyed"]
+        assert np.array_equal(crypto.verify_batch(pb, h, sb), want_b)   # registered: keyed
+        assert gpu.key_cache_info(suite)["keyed"] - k1["keyed"] == 5
+        assert np.array_equal(_keyed_dev(suite, slots_b, h, sb), want_b)
