@@ -253,7 +253,8 @@ def test_clear_and_reregister(gpu, oracle):
         gpu.clear_keys(suite)
         assert gpu.key_cache_info(suite)["keys"] == 0
         slots_b = gpu.register_keys(suite, pb)
-        assert set(slots_b.tolist()) <= set(range(5)) and set(slots_a.tolist()) & set(slots_b.tolist())
+        assert sorted(slots_b.tolist()) == list(range(5))  # numbering restarts: earlier slots are reused
+        assert (slots_a >= 0).all()
         k0 = gpu.key_cache_info(suite)
         assert np.array_equal(crypto.verify_batch(pa, h, sa), want_a)   # forgotten: generic
         k1 = gpu.key_cache_info(suite)
