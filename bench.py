@@ -105,7 +105,8 @@ KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_device.h", "fisco-bcos_amd/csrc/ecc_table
               "fisco-bcos_amd/csrc/ec.h", "fisco-bcos_amd/csrc/hash_device.h", "fisco-bcos_amd/csrc/modinv.h",
               "fisco-bcos_amd/csrc/fe26.h", "fisco-bcos_amd/csrc/ec26.h", "fisco-bcos_amd/csrc/recover26.h",
               "fisco-bcos_amd/csrc/fp26.h", "fisco-bcos_amd/csrc/ecp26.h", "fisco-bcos_amd/csrc/verify_sm2_26.h",
-              "fisco-bcos_amd/csrc/ec26_trio.h", "fisco-bcos_amd/csrc/ecp26_trio.h"]
+              "fisco-bcos_amd/csrc/ec26_trio.h", "fisco-bcos_amd/csrc/ecp26_trio.h", "fisco-bcos_amd/csrc/ecc_row.hip",
+              "fisco-bcos_amd/csrc/fe_row.h", "fisco-bcos_amd/csrc/ec_row.h"]
 
 WORKLOADS = {
     "c2": dict(suite=0, n=10_000, scaling="weak",
@@ -132,9 +133,13 @@ def kernel_source_sha():
     return h.hexdigest()[:16]
 
 
-def _auto_kernel(suite, n, cus, small_ok=True):
-    """Mirror of ecc_txv.hip auto_kernel (rounds x latency): 2 trio, 1 pair, 0 one-lane at occupancy 1,
-    -2 one-lane at occupancy 2 (whose tail round of <= one wave per SIMD has its own latency)."""
+ROW_LAT = 0.55  # ecc_txv.hip kRowLat
+
+
+def _auto_kernel(suite, n, cus, small_ok=True, row_ok=True):
+    """Mirror of ecc_txv.hip auto_kernel (rounds x latency): 3 row (secp256k1 recovery), 2 trio, 1 pair,
+    0 one-lane at occupancy 1, -2 one-lane at occupancy 2 (whose tail round of <= one wave per SIMD has
+    its own latency)."""
     lat = (4.315, 2.399, 1.678, 1.0) if suite == 1 else (4.475, 2.643, 1.279, 1.0)
     occ2_tail = 2.452 if suite == 1 else 2.556
     per = (512 * cus, 256 * cus, 64 * cus, 40 * cus)
@@ -147,6 +152,8 @@ def _auto_kernel(suite, n, cus, small_ok=True):
             c = (n // per[0]) * lat[0] + (0 if tail == 0 else occ2_tail if tail <= per[1] else lat[0])
         if c < cost:
             best, cost = code[k], c
+    if row_ok and suite == 0 and small_ok and -(-n // cus) * ROW_LAT < cost:
+        best = 3
     return best
 
 
@@ -157,12 +164,12 @@ def _kernel_name(suite, n):
     f26 = os.environ.get("BCOSGPU_K1_F26", "1") != "0"
     split = os.environ.get("BCOSGPU_TXV_SPLIT")
     small = (split == "1") if split in ("0", "1") else n <= (1 << 15)
-    coop = {"0": 0, "1": 1}.get(os.environ.get("BCOSGPU_TXV_COOP", "2"), 2)
+    coop = {"0": 0, "1": 1, "3": 3}.get(os.environ.get("BCOSGPU_TXV_COOP", "2"), 2)
     occ = os.environ.get("BCOSGPU_TXV_OCC")
     occ = int(occ) if occ in ("1", "2") else 0
     if split not in ("0", "1") and coop == 2 and f26:
         cus = torch.cuda.get_device_properties(0).multi_processor_count if torch.cuda.is_available() else 256
-        k = _auto_kernel(suite, n, cus, n <= (1 << 16))
+        k = _auto_kernel(suite, n, cus, n <= (1 << 16), os.environ.get("BCOSGPU_TXV_ROW", "1") != "0")
         small = k > 0
         if small:
             coop = k
@@ -171,6 +178,8 @@ def _kernel_name(suite, n):
     if not occ:
         occ = 2 if n >= (1 << 17) else 1
     if suite == 0 and small:
+        if coop == 3 and f26:
+            return "recover_row_kernel<TxIO>"
         if not coop:
             return "tx_verify_split_kernel"
         if coop == 2 and f26:

@@ -1586,6 +1586,7 @@ int launch_sig_verify_small_secp(const KeyIO& io, uint64_t n, hipStream_t st) {
 
 template <class IO>
 int launch_verify_small_secp(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st) {
+    if (pol.coop == 3 && pol.f26) return launch_recover_row(io, n, st);  // ecc_row.hip
     const uint32_t *k1, *sm2;
     const int rc = tables8(&k1, &sm2);
     if (rc) return rc;

@@ -534,7 +534,8 @@ __device__ __forceinline__ void lds_load_fe(fe& a, const uint32_t (*src)[64], in
 struct TxKernelPolicy {
     int split = -1;  // small-batch secp kernels: -1 by size (n <= 2^15), 0 never, 1 always
     int occ = 0;     // tx_verify_kernel occupancy: 0 by size (2 for n >= 2^17), 1 or 2 forced
-    int coop = 2;    // small-batch secp kernel: 2 lane-trio (fe26 only), 1 cooperative-pair, 0 4-wave split
+    int coop = 2;    // small-batch secp kernel: 3 row kernel, 2 lane-trio (fe26 only), 1 cooperative-pair, 0 4-wave split
+                     // (automatic policy: 2 = choose among row / trio / pair / one-lane by rounds x latency)
     int f26 = 1;     // throughput secp kernels: 1 point arithmetic on the 10 x 26-bit field, 0 on FieldK1
 };
 
@@ -558,6 +559,9 @@ template <class IO>
 int launch_verify_small_secp(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st);
 // secp256k1 verify with a known key (KeyIO) on the lane-trio kernel (ecc_coop.hip)
 int launch_sig_verify_small_secp(const KeyIO& io, uint64_t n, hipStream_t st);
+// secp256k1 recovery, one signature per workgroup on row-spread field elements (ecc_row.hip)
+template <class IO>
+int launch_recover_row(const IO& io, uint64_t n, hipStream_t st);
 // SM2 verify with a known key over KeyIO (ecc_txv.hip: launch_verify's kernel choice)
 int launch_sm2_verify_key(const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
                           uint64_t n, uint8_t* d_ok, hipStream_t st);

@@ -1380,7 +1380,7 @@ int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n,
         const uint32_t* t26;
         const int rc = tables8_sm2_26(&t26);
         if (rc) return rc;
-        if (pol.coop == 2) {
+        if (pol.coop >= 2) {  // (3, the secp256k1 row kernel's policy, has no SM2 kernel: the trio)
             // BCOSGPU_SM2_JAC_ONLY=1 (tests): every window adds the Jacobian entry (the affine table unused)
             const char* jo = getenv("BCOSGPU_SM2_JAC_ONLY");
             const int affine = jo && atoi(jo) != 0 ? 0 : 1;

@@ -242,7 +242,7 @@ int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, co
     if (rc) return rc;
     const TxKernelPolicy pol = tx_policy();
     if (suite == BCOSGPU_SUITE_SM2 && pol.f26) return launch_sm2_verify_key(d_pub, d_hash, d_sig, stride, n, d_ok, st);
-    if (suite == BCOSGPU_SUITE_SECP256K1 && pol.f26 && pol.coop == 2) {
+    if (suite == BCOSGPU_SUITE_SECP256K1 && pol.f26 && pol.coop >= 2) {
         const bool small = pol.split >= 0 ? pol.split == 1 : n <= 2ull * 40 * static_cast<uint64_t>(cu_count());
         if (small) return launch_sig_verify_small_secp(KeyIO{d_pub, d_hash, d_sig, stride, d_ok}, n, st);
     }

@@ -92,7 +92,7 @@ static void read_policy_env() {
     g_policy_read = true;
     if (const char* e = getenv("BCOSGPU_TXV_SPLIT")) g_policy.split = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : -1;
     if (const char* e = getenv("BCOSGPU_TXV_OCC")) g_policy.occ = (atoi(e) == 1 || atoi(e) == 2) ? atoi(e) : 0;
-    if (const char* e = getenv("BCOSGPU_TXV_COOP")) g_policy.coop = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : 2;
+    if (const char* e = getenv("BCOSGPU_TXV_COOP")) g_policy.coop = atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : atoi(e) == 3 ? 3 : 2;
     if (const char* e = getenv("BCOSGPU_K1_F26")) g_policy.f26 = atoi(e) != 0;
 }
 
@@ -101,7 +101,7 @@ void set_tx_kernel_policy(int split, int occ, int coop, int f26) {
     read_policy_env();
     g_policy.split = (split == 0 || split == 1) ? split : -1;
     g_policy.occ = (occ == 1 || occ == 2) ? occ : 0;
-    g_policy.coop = coop == 0 ? 0 : coop == 1 ? 1 : 2;
+    g_policy.coop = coop == 0 ? 0 : coop == 1 ? 1 : coop == 3 ? 3 : 2;
     if (f26 == 0 || f26 == 1) g_policy.f26 = f26;
 }
 

@@ -58,9 +58,11 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
 // (tools/small_sweep.py -> tools/fit_auto.py, profiles/r04_small_sweep.json and _fit.json): secp256k1
 // trio 0.379 / pair 0.485 / one-lane 1.00 (occupancy 1) / 1.70 (occupancy 2) / 0.97 ms (its single-wave
 // round); SM2 0.593 / 0.996 / 1.42 / 2.56 / 1.455 ms.  The trio and pair kernels are candidates up to
-// 2^16 txs (beyond that the one-lane kernel's throughput wins at any rounding).  Returns 2 (trio),
-// 1 (pair), 0 (one-lane, occupancy 1) or -2 (one-lane, occupancy 2).
-static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok) {
+// 2^16 txs (beyond that the one-lane kernel's throughput wins at any rounding).  secp256k1 recovery also
+// has the row kernel (ecc_row.hip): one signature per CU per round at kRowLat of the trio's round.
+// Returns 3 (row), 2 (trio), 1 (pair), 0 (one-lane, occupancy 1) or -2 (one-lane, occupancy 2).
+static constexpr double kRowLat = 0.55;
+static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_ok) {
     const bool sm2 = suite == BCOSGPU_SUITE_SM2;
     //                    occ 2,              occ 1,              pair,               trio
     const double lat[4] = {sm2 ? 4.315 : 4.475, sm2 ? 2.399 : 2.643, sm2 ? 1.678 : 1.279, 1.0};
@@ -80,6 +82,10 @@ static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok) {
             best = code[k];
         }
     }
+    if (row_ok && !sm2 && small_ok) {
+        const double c = static_cast<double>((n + cus - 1) / cus) * kRowLat;
+        if (c < cost) best = 3;
+    }
     return best;
 }
 
@@ -97,7 +103,12 @@ int launch_verify(int suite, const IO& io, uint64_t n, hipStream_t st) {
     bool small = pol.split >= 0 ? pol.split == 1 : n <= (1ull << 15);
     int occ = pol.occ;
     if (pol.split < 0 && pol.coop == 2 && pol.f26) {
-        const int k = auto_kernel(suite, n, cu_count(), n <= (1ull << 16));
+        // the row kernel recovers (TxIO, SigIO, EcrecIO); BCOSGPU_TXV_ROW=0 leaves it out of the choice
+        static const bool row_env = [] {
+            const char* e = getenv("BCOSGPU_TXV_ROW");
+            return !(e && atoi(e) == 0);
+        }();
+        const int k = auto_kernel(suite, n, cu_count(), n <= (1ull << 16), row_env && !std::is_same_v<IO, KeyIO>);
         small = k > 0;
         if (small) pol.coop = k;
         else if (!occ) occ = k == -2 ? 2 : 1;

@@ -1,5 +1,5 @@
 """Kernel time of every small-batch variant against the batch size (the data behind the automatic
-choice in ecc_txv.hip): secp256k1 and SM2, lane-trio / wave-pair / one-lane at occupancy 1 and 2, each
+choice in ecc_txv.hip): secp256k1 and SM2, row (secp256k1) / lane-trio / wave-pair / one-lane at occupancy 1 and 2, each
 forced with bcosgpu_set_tx_kernel_policy, and the automatic policy; median of HIP-event-timed launches
 after a warm-up.  One JSON line.
   small_sweep.py [SIZES]          Transaction::verify batches (bcosgpu_tx_verify_batch_dev)
@@ -18,8 +18,8 @@ import bcos_gpu
 from bcos_gpu import device, synth
 
 bcos_gpu.ensure_device(0)
-VARIANTS = {"trio": (1, 0, 2, 1), "pair": (1, 0, 1, 1), "occ1": (0, 1, 0, 1), "occ2": (0, 2, 0, 1),
-            "auto": (-1, 0, 2, 1)}
+VARIANTS = {"trio": (1, 0, 2, 1), "row": (1, 0, 3, 1), "pair": (1, 0, 1, 1), "occ1": (0, 1, 0, 1),
+            "occ2": (0, 2, 0, 1), "auto": (-1, 0, 2, 1)}  # row: secp256k1 only (ecc_row.hip)
 args = sys.argv[1:]
 mode = args.pop(0) if args and args[0] == "verify" else "tx"
 # sizes: one comma-separated argument or several arguments (tools/gpu_run.sh turns commas into spaces)
@@ -87,6 +87,8 @@ for suite in (0, 1):
         snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
         st = torch.empty(n, dtype=torch.uint8, device="cuda")
         for name, pol in VARIANTS.items():
+            if name == "row" and suite == 1:
+                continue
             bcos_gpu.set_tx_kernel_policy(*pol)
             for _ in range(30):
                 device.tx_verify(suite, big.pre, po, big.sig, so, th, snd, st)

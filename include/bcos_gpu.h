@@ -72,8 +72,10 @@ int bcosgpu_init_ex(int device, int flags);
  * read once from BCOSGPU_TXV_SPLIT / _OCC / _COOP and BCOSGPU_K1_F26 at the first init, never per launch):
  * split -1 by size (secp256k1 batches <= 2^15 run the small-batch kernels), 0 never, 1 always;
  * occupancy 0 by size (2 waves/SIMD for n >= 2^17), 1 or 2 forced; coop (secp256k1 small batches)
- * 2 lane-trio (default; needs field 1), 1 cooperative-pair, 0 split (SM2: 2 lane-trio, 1 pair kernel,
- * 0 the one-lane kernel);
+ * 3 the row kernel (recovery: one signature per workgroup on row-spread field elements, ecc_row.hip),
+ * 2 lane-trio (default; needs field 1; with split -1 the automatic choice among row, lane-trio, pair and
+ * one-lane kernels by rounds x latency), 1 cooperative-pair, 0 split (SM2: 3 and 2 lane-trio, 1 pair
+ * kernel, 0 the one-lane kernel);
  * field (secp256k1 throughput kernels) 1 the 10 x 26-bit point arithmetic (default), 0 the 8 x 32-bit
  * one, -1 unchanged.  Every variant returns identical results. */
 int bcosgpu_set_tx_kernel_policy(int split, int occupancy, int coop, int field);

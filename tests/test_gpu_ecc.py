@@ -256,7 +256,7 @@ def test_synthetic_batch_device_path(gpu, oracle, suite):
 
 @pytest.mark.parametrize("suite", [0, 1])
 def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
-    """Every launch variant (secp256k1 lane-trio, cooperative-pair and 4-wave split kernels, the SM2 pair kernel,
+    """Every launch variant (secp256k1 lane-trio, row, cooperative-pair and 4-wave split kernels, the SM2 pair kernel,
     the one-lane kernels at occupancy 1 and 2) gives identical outputs (bcosgpu_set_tx_kernel_policy
     forces each one)."""
     import torch
@@ -269,7 +269,8 @@ def test_tx_verify_kernel_variants_agree(gpu, oracle, suite):
     # 8 x 32-bit point arithmetic; SM2: lane-trio and pair kernels and one-lane occ 1 / 2, each on fp26 and 8 x 32
     # (the SM2 lane-trio kernel twice more: every window on the Jacobian table entries, BCOSGPU_SM2_JAC_ONLY,
     # and without the low-window chains, BCOSGPU_SM2_SPLIT=0; both read at each launch)
-    variants = ([(1, 1, 2, 1), (1, 1, 1, 1), (1, 1, 0, 1), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)]
+    variants = ([(1, 1, 2, 1), (1, 1, 3, 1), (1, 1, 1, 1), (1, 1, 0, 1), (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0),
+                 (0, 2, 0, 0)]
                 if suite == 0
                 else [(1, 1, 2, 1), (1, 1, 2, 1, "jac"), (1, 1, 2, 1, "nosplit"), (1, 1, 1, 1), (1, 1, 1, 0),
                       (0, 1, 0, 1), (0, 2, 0, 1), (0, 1, 0, 0), (0, 2, 0, 0)])
@@ -337,8 +338,8 @@ def test_tx_verify_kernel_variants_edge_signatures(gpu, oracle, suite):
     wh, ws, wst = oracle.tx_verify_packed(suite, pre, po.astype(np.uint64), mutated.reshape(-1),
                                           so.astype(np.uint64), nthreads=16)
     assert (wst == 0).sum() > n // 10 and (wst != 0).sum() > n // 4
-    variants = [None, (1, 1, 2, 1), (1, 1, 1, 1), (1, 1, 0, 1) if suite == 0 else (1, 1, 1, 0), (0, 2, 0, 1),
-                (0, 2, 0, 0)]
+    variants = [None, (1, 1, 2, 1), (1, 1, 3, 1), (1, 1, 1, 1), (1, 1, 0, 1) if suite == 0 else (1, 1, 1, 0),
+                (0, 2, 0, 1), (0, 2, 0, 0)]
     try:
         for v in variants:
             if v is None:
