@@ -25,15 +25,17 @@ namespace bcosgpu {
 namespace {
 
 struct RowLds {
-    uint32_t tab[8][3][16];  // co-Z table of R' on E_w: x, y, beta x as canonical fe26 limbs (10..15 zero)
-    uint32_t res[2][3][16];  // the chains' points (row limbs), phase C -> D
-    uint32_t k[2][4];        // GLV halves of u2
-    uint32_t u1[8], e[8], zc[8], ys[8];
-    uint32_t g[3][8];        // u1 G (canonical words)
-    uint32_t kflags;         // wave 0: bit 0 scalars ok, bit 2 neg1, bit 3 neg2
-    uint32_t rflag;          // wave 2: R on the curve (bit 1)
-    uint32_t ginf, cinf[2];  // u1 G / chain results at infinity
-    uint32_t post[3];        // 0: e, 1: k / u1, 2: table
+    uint32_t tab[2][8][3][16];  // GLV tables of R' and 2^64 R' on E_w: x, y, beta x (row limbs, magnitude 1)
+    uint32_t zc[2][16];         // their co-Z factors Zc, Zc64
+    uint32_t zcy[2][16];        // Zc y, Zc64 y (wave 3)
+    uint32_t pt[8][3][16];      // phase D: the four chains' points, the four comb partials, then the sums
+    uint32_t pinf[8];
+    uint32_t slot[4][16];       // per-wave conversion slot (fe_row -> fe26)
+    uint32_t k[2][4];           // GLV halves of u2
+    uint32_t u1[8], e[8];
+    uint32_t kflags;            // wave 0: bit 0 scalars ok, bit 2 neg1, bit 3 neg2
+    uint32_t rflag;             // wave 3: R on the curve (bit 1)
+    uint32_t post[4];           // 0: e, 1: k / u1, 2: table of R', 3: table of 2^64 R'
 };
 
 __device__ __forceinline__ void row_post(uint32_t* f) {
@@ -49,51 +51,19 @@ __device__ __forceinline__ void get8(fe& a, const uint32_t* d) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) a.v[q] = d[q];
 }
-// a fe26 as canonical limbs into a 16-word row slot
-__device__ __forceinline__ void put_limbs(uint32_t* d, const fe26& a, int lane) {
-    fe26 t;
-    fe26_copy(t, a);
-    fe26_normalize(t);
-    if (lane < 16) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int q = 0; q < 10; ++q) w = lane == q ? t.v[q] : w;
-        d[lane] = w;
-    }
-}
-// ten row limbs (any row magnitude <= 16: limbs < 2^31) -> fe26 of magnitude <= 2
-__device__ __forceinline__ void fe26_from_row(fe26& r, const uint32_t* l) {
-    using namespace f26;
-    uint64_t t = 0;
-#pragma unroll
-    for (int q = 0; q < 10; ++q) {
-        t += l[q];
-        r.v[q] = static_cast<uint32_t>(t) & M26;
-        t >>= 26;
-    }
-    // bits from 2^256 up: x 2^256 = x 977 + x 2^32 (mod p)
-    const uint64_t x = (r.v[9] >> 22) + (t << 4);
-    r.v[9] &= M22;
-    uint64_t u = r.v[0] + x * 977u;
-    r.v[0] = static_cast<uint32_t>(u) & M26;
-    u = (u >> 26) + r.v[1] + (x << 6);
-    r.v[1] = static_cast<uint32_t>(u) & M26;
-#pragma unroll
-    for (int q = 2; q < 9; ++q) {
-        u = (u >> 26) + r.v[q];
-        r.v[q] = static_cast<uint32_t>(u) & M26;
-    }
-    r.v[9] += static_cast<uint32_t>(u >> 26);
-    F26_SETM(r, 2);
-}
-__device__ __forceinline__ void jac_from_row(Jac26& P, const uint32_t (*src)[16], bool inf) {
-    fe26_from_row(P.X, src[0]);
-    fe26_from_row(P.Y, src[1]);
-    fe26_from_row(P.Z, src[2]);
-    P.inf = inf;
-}
+__device__ __forceinline__ uint32_t sgpr(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 }  // namespace
+
+// workgroup-0 phase stamps (s_memtime) per wave for tools/rowphase.hip: 0 start, 1 phase-A work done,
+// 2 chain done, 6 comb partial done, 3 end; wave 0: 4 / 5 around the affine inversion
+#ifdef BCOSGPU_ROW_TIMING
+__device__ uint64_t g_row_t[4][8];
+#define ROW_T(k) \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_row_t[threadIdx.x >> 6][k] = clock64()
+#else
+#define ROW_T(k) ((void)0)
+#endif
 
 template <class IO>
 __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab,
@@ -101,34 +71,20 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
     __shared__ RowLds S;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
+    const frow::Lane L(lane);
+    uint32_t* const slot = S.slot[wave];
     const uint64_t i = blockIdx.x;  // one signature per workgroup (the grid is n)
-    if (threadIdx.x < 3) S.post[threadIdx.x] = 0u;
+    ROW_T(0);
+    if (threadIdx.x < 4) S.post[threadIdx.x] = 0u;
     __syncthreads();
     fe r, s;
     uint32_t v = 0;
-    const bool ok = io.rsv(i, r, s, v);
+    // every lane parses the same signature: the verdict bits are made wave-uniform (SGPRs), so no branch
+    // below depends on a lane's value (a row operation under a partial EXEC would misread its rows)
+    const bool ok = sgpr(io.rsv(i, r, s, v) ? 1u : 0u) != 0u;
+    v = sgpr(v);
     // ---------------------------------------------------------------- phase A
-    if (wave == 3) {
-        fe e;
-        io.template digest<KECCAK256>(i, e);
-        reduce_once(e, ParamN1::M);
-        put8(S.e, e, lane);
-        row_post(&S.post[0]);
-        row_wait(&S.post[1]);
-        fe u1;
-        get8(u1, S.u1);
-        Jac26 G;
-        if (tab_bits == kWideBits) comb_mul26<kWideBits>(G, u1, tab);
-        else comb_mul26<8>(G, u1, tab);
-        fe X, Y, Z;
-        fe26_to_fe(X, G.X);
-        fe26_to_fe(Y, G.Y);
-        fe26_to_fe(Z, G.Z);
-        put8(S.g[0], X, lane);
-        put8(S.g[1], Y, lane);
-        put8(S.g[2], Z, lane);
-        if (lane == 0) S.ginf = G.inf ? 1u : 0u;
-    } else if (wave == 0) {
+    if (wave == 0) {  // r^-1, u1, u2, the GLV split (one lane's work)
         fe rr, ss;
         fe_copy(rr, r);
         fe_copy(ss, s);
@@ -156,6 +112,15 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         if (lane == 0) S.kflags = (ok ? 1u : 0u) | (neg1 ? 4u : 0u) | (neg2 ? 8u : 0u);
         row_post(&S.post[1]);
     } else {
+        if (wave == 1) {
+            fe e;
+            io.template digest<KECCAK256>(i, e);
+            reduce_once(e, ParamN1::M);
+            put8(S.e, e, lane);
+            row_post(&S.post[0]);
+        }
+        // x = r (+ n), w = x^3 + 7 and R' = (w x, w^2) on E_w: Y^2 = X^3 + 7 w^3 (a point (X, Y, Z) of E_w
+        // is (X, Y, Z y) on E, y = sqrt(w))
         fe x;
         fe_copy(x, r);
         bool okr = ok;
@@ -163,101 +128,131 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
             okr = okr && fe_lt_k(r, kK1PminusN);
             fe_add_k(x, r, ParamN1::M);
         }
-        fe26 X, w, t, seven;
-        fe26_from_fe(X, x);
-        fe26_sqr(t, X);
-        fe26_mul(w, t, X);
-        fe26_set_small(seven, 7u);
-        fe26_add(w, w, seven);  // w = x^3 + 7 (m 2)
-        if (wave == 2) {
+        fe26 X26;
+        fe26_from_fe(X26, x);
+        const uint32_t X = frow::from_fe26(X26, L);
+        const uint32_t w = frow::mul(frow::sqr(X, L), X, L) + 7u * L.one;  // m 1 + 7 / 2^26
+        if (wave == 3) {  // y = sqrt(w) with v's parity, then Zc y and Zc64 y
+            const uint32_t yc = frow::sqrt_cand(w, L);
+            const bool square = frow::is_zero(frow::sub<2>(frow::sqr(yc, L), w, L), slot, L);
+            okr = okr && square;
             fe26 y, ny;
-            fe26_sqrt_cand(y, w);
-            fe26_sqr(t, y);
-            fe26_sub<3>(t, t, w);
-            okr = okr && fe26_is_zero(t);
+            frow::to_fe26(y, yc, slot, L);
             fe26_normalize(y);
             fe26_neg<2>(ny, y);
             fe26_normalize(ny);
             fe26_cmov(y, ny, (y.v[0] & 1u) != (v & 1u));
-            fe yw;
-            fe26_to_fe(yw, y);
-            put8(S.ys, yw, lane);
+            const uint32_t yr = frow::from_fe26(y, L);
             if (lane == 0) S.rflag = okr ? 2u : 0u;
-        } else {
-            Aff26 R, A[8];
-            fe26_mul(R.x, w, X);  // w x
-            fe26_sqr(R.y, w);     // w^2
-            fe26 Zc, beta;
-            {
-                Jac26 T[8];
-                multiples8_26(T, R);
-                coz_table26(A, Zc, T);
+            row_wait(&S.post[2]);
+            row_wait(&S.post[3]);
+            uint32_t a, b;
+            frow::gather01(frow::mul(frow::sel4(L, S.zc[0][L.k], S.zc[1][L.k], S.zc[1][L.k], S.zc[1][L.k]), yr, L), a,
+                           b);
+            if (L.row == 0) {
+                S.zcy[0][L.k] = a;
+                S.zcy[1][L.k] = b;
             }
-            fe26_const(beta, kGlvBeta);
+        } else {  // the GLV table of R' (wave 1) or of 2^64 R' (wave 2)
+            uint32_t Rx, Ry;
+            frow::gather01(frow::mul(w, frow::sel4(L, X, w, w, w), L), Rx, Ry);
+            frow::Pt P{Rx, Ry, L.one};
+            if (wave == 2) {
 #pragma unroll 1
-            for (int j = 0; j < 8; ++j) {
-                fe26 bx;
-                fe26_mul(bx, A[j].x, beta);
-                put_limbs(S.tab[j][0], A[j].x, lane);
-                put_limbs(S.tab[j][1], A[j].y, lane);
-                put_limbs(S.tab[j][2], bx, lane);
+                for (int q = 0; q < 64; ++q) frow::dbl(P, L);
             }
-            fe zw;
-            fe26_to_fe(zw, Zc);
-            put8(S.zc, zw, lane);
-            row_post(&S.post[2]);
+            fe26 beta26;
+            fe26_const(beta26, kGlvBeta);
+            frow::build_table(S.tab[wave - 1], S.zc[wave - 1], P, frow::from_fe26(beta26, L), L);
+            row_post(&S.post[wave == 1 ? 2 : 3]);
         }
     }
-    // ---------------------------------------------------------------- phase C: the GLV chains on the rows
-    if (wave < 2) {
-        row_wait(&S.post[1]);
-        row_wait(&S.post[2]);
-        const frow::Lane L(lane);
+    ROW_T(1);
+    // ---------------------------------------------------------------- phase C: four 64-bit GLV chains
+    // wave 0: low half of k1 on R', 1: low half of k2 on phi(R'), 2 / 3: the high halves on 2^64 R'
+    row_wait(&S.post[1]);
+    row_wait(&S.post[2]);
+    row_wait(&S.post[3]);
+    {
+        const int kh = wave & 1, part = wave >> 1;
         fe k;
         fe_zero(k);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) k.v[q] = __builtin_amdgcn_readfirstlane(S.k[wave][q]);
-        const uint32_t kf = __builtin_amdgcn_readfirstlane(S.kflags);
-        const bool neg = (kf & (wave == 0 ? 4u : 8u)) != 0u;
+        k.v[2] = sgpr(S.k[kh][2 * part]);
+        k.v[3] = sgpr(S.k[kh][2 * part + 1]);
+        const uint32_t kf = sgpr(S.kflags);
+        const bool neg = (kf & (kh == 0 ? 4u : 8u)) != 0u;
         frow::Pt acc{0u, 0u, 0u};
-        const bool fin = frow::glv_chain(acc, k, neg, wave == 1, &S.tab[0][0][0], L);
-        if (lane < 16) {
-            S.res[wave][0][lane] = acc.X;
-            S.res[wave][1][lane] = acc.Y;
-            S.res[wave][2][lane] = acc.Z;
+        const bool fin = frow::glv_chain<16>(acc, k, neg, kh == 1, &S.tab[part][0][0][0], L);
+        frow::pt_store(S.pt[wave], acc, L);
+        if (lane == 0) S.pinf[wave] = fin ? 0u : 1u;
+    }
+    ROW_T(2);
+    // ---------------------------------------------------------------- phase D
+    {  // u1 G: this wave's quarter of the comb windows (the additions never meet P = +-Q: a partial sum
+       // is an integer multiple of G below the window's own 2^(bits i) G multiples)
+        constexpr int kW16 = 256 / kWideBits;
+        const int W = tab_bits == kWideBits ? kW16 : 32, bits = tab_bits == kWideBits ? kWideBits : 8;
+        const int lo = wave * (W / 4), hi = lo + W / 4;
+        frow::Pt g{0u, 0u, 0u};
+        bool ginf = true;
+#pragma unroll 1
+        for (int q = lo; q < hi; ++q) {
+            const int bit = q * bits;
+            const uint32_t wd = sgpr(S.u1[bit >> 5]);
+            const uint32_t b = bits == 16 ? (wd >> (bit & 31)) & 0xffffu : (wd >> (bit & 31)) & 0xffu;
+            if (b == 0u) continue;
+            const uint32_t* e = tab + (static_cast<size_t>(q) << bits | b) * 16;
+            const uint32_t ex = frow::from_words(e, L), ey = frow::from_words(e + 8, L);
+            if (ginf) {
+                g = frow::Pt{ex, ey, L.one};
+                ginf = false;
+            } else {
+                frow::madd(g, ex, ey, L);
+            }
         }
-        if (lane == 0) S.cinf[wave] = fin ? 0u : 1u;
+        frow::pt_store(S.pt[4 + wave], g, L);
+        if (lane == 0) S.pinf[4 + wave] = ginf ? 1u : 0u;
+    }
+    ROW_T(6);
+    __syncthreads();
+    {  // wave 0: chains 0 + 1 (co-Z curve of R') -> E; wave 1: chains 2 + 3 (of 2^64 R') -> E;
+       // waves 2, 3: comb partials 0 + 1, 2 + 3
+        frow::Pt P, Q, R;
+        bool rinf;
+        frow::pt_load(P, S.pt[2 * wave], L);
+        frow::pt_load(Q, S.pt[2 * wave + 1], L);
+        frow::add_full(R, rinf, P, sgpr(S.pinf[2 * wave]) != 0u, Q, sgpr(S.pinf[2 * wave + 1]) != 0u, slot, L);
+        if (wave < 2 && !rinf) R.Z = frow::mul(R.Z, S.zcy[wave][L.k], L);  // (X, Y, Z Zc y) on E
+        frow::pt_store(S.pt[2 * wave], R, L);
+        if (lane == 0) S.pinf[2 * wave] = rinf ? 1u : 0u;
     }
     __syncthreads();
-    // ---------------------------------------------------------------- phase D (wave 0, one lane's work)
-    if (wave == 0) {
-        Jac26 P0, P1, Q, G, Rq;
-        jac_from_row(P0, S.res[0], S.cinf[0] != 0u);
-        jac_from_row(P1, S.res[1], S.cinf[1] != 0u);
-        CurveK1x::add(Q, P0, P1);  // on the co-Z curve of E_w
-        fe zw, yw;
-        get8(zw, S.zc);
-        get8(yw, S.ys);
-        fe26 zc, y;
-        fe26_from_fe(zc, zw);
-        fe26_from_fe(y, yw);
-        fe26_mul(zc, zc, y);
-        fe26_mul(Q.Z, Q.Z, zc);  // (X, Y, Z Zc y) on E
-        {
-            fe X, Y, Z;
-            get8(X, S.g[0]);
-            get8(Y, S.g[1]);
-            get8(Z, S.g[2]);
-            fe26_from_fe(G.X, X);
-            fe26_from_fe(G.Y, Y);
-            fe26_from_fe(G.Z, Z);
-            G.inf = S.ginf != 0u;
-        }
-        CurveK1x::add(Rq, Q, G);
-        const bool ok2 = ((S.kflags | S.rflag) & 3u) == 3u && !Rq.inf;
+    if (wave < 2) {  // wave 0: the R part; wave 1: the G part
+        frow::Pt P, Q, R;
+        bool rinf;
+        frow::pt_load(P, S.pt[4 * wave], L);
+        frow::pt_load(Q, S.pt[4 * wave + 2], L);
+        frow::add_full(R, rinf, P, sgpr(S.pinf[4 * wave]) != 0u, Q, sgpr(S.pinf[4 * wave + 2]) != 0u, slot, L);
+        frow::pt_store(S.pt[4 * wave], R, L);
+        if (lane == 0) S.pinf[4 * wave] = rinf ? 1u : 0u;
+    }
+    __syncthreads();
+    if (wave == 0) {  // Q = R part + G part, affine, address
+        frow::Pt P, Q, R;
+        bool rinf;
+        frow::pt_load(P, S.pt[0], L);
+        frow::pt_load(Q, S.pt[4], L);
+        frow::add_full(R, rinf, P, sgpr(S.pinf[0]) != 0u, Q, sgpr(S.pinf[4]) != 0u, slot, L);
+        const bool ok2 = ((sgpr(S.kflags) | sgpr(S.rflag)) & 3u) == 3u && !rinf;
+        Jac26 Rq;
+        frow::to_fe26(Rq.X, R.X, slot, L);
+        frow::to_fe26(Rq.Y, R.Y, slot, L);
+        frow::to_fe26(Rq.Z, R.Z, slot, L);
         fe z, zi, ax, ay;
         fe26_to_fe(z, Rq.Z);
+        ROW_T(4);
         FieldInv<FieldK1>::inv_pipe(zi, z);
+        ROW_T(5);
         fe26 zi26, zi2, zi3, AX, AY;
         fe26_from_fe(zi26, zi);
         fe26_sqr(zi2, zi26);
@@ -270,6 +265,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         if (ok2 && io.want_addr()) keccak_address(ad, ax, ay);
         if (lane == 0) io.finish(i, ok2, ad, &ax, &ay);
     }
+    ROW_T(3);
 }
 
 template <class IO>
