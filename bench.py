@@ -133,7 +133,7 @@ def kernel_source_sha():
     return h.hexdigest()[:16]
 
 
-ROW_LAT = 0.55  # ecc_txv.hip kRowLat
+ROW_LAT, ROW_LAT_N = 0.42, 0.28  # ecc_txv.hip kRowLat, kRowLatN
 
 
 def _auto_kernel(suite, n, cus, small_ok=True, row_ok=True):
@@ -152,7 +152,7 @@ def _auto_kernel(suite, n, cus, small_ok=True, row_ok=True):
             c = (n // per[0]) * lat[0] + (0 if tail == 0 else occ2_tail if tail <= per[1] else lat[0])
         if c < cost:
             best, cost = code[k], c
-    if row_ok and suite == 0 and small_ok and -(-n // cus) * ROW_LAT < cost:
+    if row_ok and suite == 0 and small_ok and ROW_LAT + (-(-n // cus) - 1) * ROW_LAT_N < cost:
         best = 3
     return best
 

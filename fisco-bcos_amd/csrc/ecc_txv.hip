@@ -59,9 +59,12 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
 // trio 0.379 / pair 0.485 / one-lane 1.00 (occupancy 1) / 1.70 (occupancy 2) / 0.97 ms (its single-wave
 // round); SM2 0.593 / 0.996 / 1.42 / 2.56 / 1.455 ms.  The trio and pair kernels are candidates up to
 // 2^16 txs (beyond that the one-lane kernel's throughput wins at any rounding).  secp256k1 recovery also
-// has the row kernel (ecc_row.hip): one signature per CU per round at kRowLat of the trio's round.
+// has the row kernel (ecc_row.hip, one signature per workgroup): its first round of one signature per
+// CU costs kRowLat of the trio's round and each further round kRowLatN (two workgroups share a CU:
+// tools/small_sweep.py, profiles/r05_small_sweep_row.json: 0.149 / 0.176 / 0.275 / 0.365 / 0.428 ms at
+// 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.378).
 // Returns 3 (row), 2 (trio), 1 (pair), 0 (one-lane, occupancy 1) or -2 (one-lane, occupancy 2).
-static constexpr double kRowLat = 0.55;
+static constexpr double kRowLat = 0.42, kRowLatN = 0.28;
 static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_ok) {
     const bool sm2 = suite == BCOSGPU_SUITE_SM2;
     //                    occ 2,              occ 1,              pair,               trio
@@ -83,7 +86,7 @@ static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_o
         }
     }
     if (row_ok && !sm2 && small_ok) {
-        const double c = static_cast<double>((n + cus - 1) / cus) * kRowLat;
+        const double c = kRowLat + static_cast<double>((n + cus - 1) / cus - 1) * kRowLatN;
         if (c < cost) best = 3;
     }
     return best;

@@ -52,14 +52,15 @@ def test_small_batch_choice_mirrors_library():
     mt = re.search(r"occ2_tail = sm2 \? ([\d.]+) : ([\d.]+);", src)
     mbt = re.search(r"occ2_tail = ([\d.]+) if suite == 1 else ([\d.]+)", bsrc)
     assert mt and mbt and (mt.group(1), mt.group(2)) == (mbt.group(1), mbt.group(2))
-    mr = re.search(r"kRowLat = ([\d.]+);", src)
-    mbr = re.search(r"ROW_LAT = ([\d.]+)", bsrc)
-    assert mr and mbr and mr.group(1) == mbr.group(1)
+    mr = re.search(r"kRowLat = ([\d.]+), kRowLatN = ([\d.]+);", src)
+    mbr = re.search(r"ROW_LAT, ROW_LAT_N = ([\d.]+), ([\d.]+)", bsrc)
+    assert mr and mbr and mr.groups() == mbr.groups()
     ns = {"__name__": "bench_mirror", "__file__": os.path.join(ROOT, "bench.py")}
-    exec(bsrc[bsrc.index("def _auto_kernel"):bsrc.index("def _kernel_name")], ns)
+    exec(bsrc[bsrc.index("ROW_LAT, ROW_LAT_N ="):bsrc.index("def _kernel_name")], ns)
     pick = ns["_auto_kernel"]
-    names = {2: "trio", 1: "pair", 0: "occ1", -2: "occ2"}
-    for fname in ("r04_small_sweep.json",):
+    names = {3: "row", 2: "trio", 1: "pair", 0: "occ1", -2: "occ2"}
+    # round 5's sweep adds the row kernel (1 .. 2,048 signatures)
+    for fname, row_ok in (("r04_small_sweep.json", False), ("r05_small_sweep_row.json", True)):
         path = os.path.join(ROOT, "profiles", fname)
         if not os.path.exists(path):
             continue
@@ -69,8 +70,8 @@ def test_small_batch_choice_mirrors_library():
             if variant != "occ1":
                 continue
             suite, n = (1 if suite_name == "sm2" else 0), int(n)
-            cands = [v for v in ("trio", "pair", "occ1", "occ2") if "%s_%d_%s" % (suite_name, n, v) in sweep]
+            cands = [v for v in ("row", "trio", "pair", "occ1", "occ2") if "%s_%d_%s" % (suite_name, n, v) in sweep]
             best = min(sweep["%s_%d_%s" % (suite_name, n, v)] for v in cands)
             # (the round-4 sweep predates the row kernel: the choice among the kernels it timed)
-            chosen = sweep["%s_%d_%s" % (suite_name, n, names[pick(suite, n, 256, n <= (1 << 16), False)])]
+            chosen = sweep["%s_%d_%s" % (suite_name, n, names[pick(suite, n, 256, n <= (1 << 16), row_ok)])]
             assert chosen <= best * 1.05, (key, chosen, best)
