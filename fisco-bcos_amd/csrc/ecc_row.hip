@@ -65,9 +65,15 @@ __device__ uint64_t g_row_t[4][8];
 #define ROW_T(k) ((void)0)
 #endif
 
-template <class IO>
+// MODE kRowRecover: public-key recovery (SigIO, TxIO, EcrecIO).  MODE kRowVerify: libsecp256k1
+// ecdsa_verify with a KNOWN key P (KeyIO, Secp256k1Crypto.cpp:51-63 for a sealer's unregistered key):
+// Q = (e / s) G + (r / s) P, accept iff x(Q) = r (mod n) -- s^-1 instead of r^-1, the tables of P and
+// 2^64 P (no square root, no E_w), and the projective x-check instead of the inversion and the address.
+enum { kRowRecover = 0, kRowVerify = 1 };
+template <int MODE, class IO>
 __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab,
                                                              int tab_bits) {
+    constexpr bool kVer = MODE == kRowVerify;
     __shared__ RowLds S;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
@@ -77,31 +83,40 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
     ROW_T(0);
     if (threadIdx.x < 4) S.post[threadIdx.x] = 0u;
     __syncthreads();
-    fe r, s;
+    fe r, s, kx, ky;
     uint32_t v = 0;
     // every lane parses the same signature: the verdict bits are made wave-uniform (SGPRs), so no branch
     // below depends on a lane's value (a row operation under a partial EXEC would misread its rows)
-    const bool ok = sgpr(io.rsv(i, r, s, v) ? 1u : 0u) != 0u;
+    bool okp;
+    if constexpr (kVer) {
+        io.key_rs(i, r, s, kx, ky);
+        okp = fe_lt_k(kx, FieldK1::P) && fe_lt_k(ky, FieldK1::P) && !fe_is_zero_raw(r) && !fe_is_zero_raw(s) &&
+              fe_lt_k(r, ParamN1::M) && fe_lt_k(s, kN1HalfPlus);  // low-S (secp256k1_ecdsa_verify)
+    } else {
+        okp = io.rsv(i, r, s, v);
+    }
+    const bool ok = sgpr(okp ? 1u : 0u) != 0u;
     v = sgpr(v);
     // ---------------------------------------------------------------- phase A
     if (wave == 0) {  // r^-1, u1, u2, the GLV split (one lane's work)
-        fe rr, ss;
-        fe_copy(rr, r);
-        fe_copy(ss, s);
+        // recover: u1 = -e / r, u2 = s / r; verify: u1 = e / s, u2 = r / s
+        fe inv_of, other;
+        fe_copy(inv_of, kVer ? s : r);
+        fe_copy(other, kVer ? r : s);
         if (!ok) {  // keep the scalar arithmetic well defined (the verdict is already false)
-            fe_zero(rr);
-            rr.v[0] = 1;
-            fe_zero(ss);
+            fe_zero(inv_of);
+            inv_of.v[0] = 1;
+            fe_zero(other);
         }
         fe rm, rinv;
-        FieldN1::from_plain(rm, rr);
+        FieldN1::from_plain(rm, inv_of);
         FieldInv<FieldN1>::inv_pipe(rinv, rm);
         row_wait(&S.post[0]);
         fe e, u1, u2, k1, k2;
         get8(e, S.e);
         FieldN1::mul(u1, e, rinv);
-        FieldN1::neg(u1, u1);
-        FieldN1::mul(u2, ss, rinv);
+        if (!kVer) FieldN1::neg(u1, u1);
+        FieldN1::mul(u2, other, rinv);
         bool neg1, neg2;
         glv_split(k1, neg1, k2, neg2, u2);
         put8(S.u1, u1, lane);
@@ -119,6 +134,40 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
             put8(S.e, e, lane);
             row_post(&S.post[0]);
         }
+        if constexpr (kVer) {
+            if (wave == 3) {  // the chains map to E with Z Zc alone
+                row_wait(&S.post[2]);
+                row_wait(&S.post[3]);
+                if (L.row == 0) {
+                    S.zcy[0][L.k] = S.zc[0][L.k];
+                    S.zcy[1][L.k] = S.zc[1][L.k];
+                }
+            } else {  // the key's table (wave 1: P, with its on-curve check; wave 2: 2^64 P)
+                fe26 X26, Y26;
+                fe26_from_fe(X26, kx);
+                fe26_from_fe(Y26, ky);
+                uint32_t X = frow::from_fe26(X26, L), Y = frow::from_fe26(Y26, L);
+                const uint32_t rhs = frow::mul(frow::sqr(X, L), X, L) + 7u * L.one;
+                const bool on = frow::is_zero(frow::sub<2>(frow::sqr(Y, L), rhs, L), slot, L);
+                if (!(ok && on)) {  // a valid point for a rejected key (its verdict is already false)
+                    fe26 gx, gy;
+                    fe26_const(gx, kK1Gx);
+                    fe26_const(gy, kK1Gy);
+                    X = frow::from_fe26(gx, L);
+                    Y = frow::from_fe26(gy, L);
+                }
+                if (wave == 1 && lane == 0) S.rflag = on ? 2u : 0u;
+                frow::Pt P{X, Y, L.one};
+                if (wave == 2) {
+#pragma unroll 1
+                    for (int q = 0; q < 64; ++q) frow::dbl(P, L);
+                }
+                fe26 beta26;
+                fe26_const(beta26, kGlvBeta);
+                frow::build_table(S.tab[wave - 1], S.zc[wave - 1], P, frow::from_fe26(beta26, L), L);
+                row_post(&S.post[wave == 1 ? 2 : 3]);
+            }
+        } else {
         // x = r (+ n), w = x^3 + 7 and R' = (w x, w^2) on E_w: Y^2 = X^3 + 7 w^3 (a point (X, Y, Z) of E_w
         // is (X, Y, Z y) on E, y = sqrt(w))
         fe x;
@@ -165,6 +214,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
             fe26_const(beta26, kGlvBeta);
             frow::build_table(S.tab[wave - 1], S.zc[wave - 1], P, frow::from_fe26(beta26, L), L);
             row_post(&S.post[wave == 1 ? 2 : 3]);
+        }
         }
     }
     ROW_T(1);
@@ -246,8 +296,26 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         const bool ok2 = ((sgpr(S.kflags) | sgpr(S.rflag)) & 3u) == 3u && !rinf;
         Jac26 Rq;
         frow::to_fe26(Rq.X, R.X, slot, L);
-        frow::to_fe26(Rq.Y, R.Y, slot, L);
+        if constexpr (!kVer) frow::to_fe26(Rq.Y, R.Y, slot, L);
         frow::to_fe26(Rq.Z, R.Z, slot, L);
+        if constexpr (kVer) {  // x(Q) = X / Z^2 is r or r + n (when r + n < p): X == c Z^2, projectively
+            fe26 z2, c, rhs;
+            fe xw, cw, r2;
+            fe26_sqr(z2, Rq.Z);
+            fe26_from_fe(c, r);
+            fe26_mul(rhs, c, z2);
+            fe26_to_fe(xw, Rq.X);
+            fe26_to_fe(cw, rhs);
+            bool match = fe_eq_raw(xw, cw);
+            const uint32_t carry = fe_add_k(r2, r, ParamN1::M);
+            const bool second = carry == 0u && fe_lt_k(r2, FieldK1::P);
+            fe26_from_fe(c, second ? r2 : r);
+            fe26_mul(rhs, c, z2);
+            fe26_to_fe(cw, rhs);
+            match = match || (second && fe_eq_raw(xw, cw));
+            if (lane == 0) io.finish(i, ok2 && match, nullptr, nullptr, nullptr);
+            return;
+        } else {
         fe z, zi, ax, ay;
         fe26_to_fe(z, Rq.Z);
         ROW_T(4);
@@ -264,6 +332,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         uint32_t ad[5] = {0, 0, 0, 0, 0};
         if (ok2 && io.want_addr()) keccak_address(ad, ax, ay);
         if (lane == 0) io.finish(i, ok2, ad, &ax, &ay);
+        }
     }
     ROW_T(3);
 }
@@ -275,7 +344,18 @@ int launch_recover_row(const IO& io, uint64_t n, hipStream_t st) {
     int bits = 8;
     const int rc = tables(&k1, &sm2, &bits);
     if (rc) return rc;
-    hipLaunchKernelGGL(recover_row_kernel<IO>, dim3(static_cast<unsigned>(n)), dim3(256), 0, st, io, n, k1, bits);
+    hipLaunchKernelGGL((recover_row_kernel<kRowRecover, IO>), dim3(static_cast<unsigned>(n)), dim3(256), 0, st, io, n,
+                       k1, bits);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+int launch_sig_verify_row_secp(const KeyIO& io, uint64_t n, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int bits = 8;
+    const int rc = tables(&k1, &sm2, &bits);
+    if (rc) return rc;
+    hipLaunchKernelGGL((recover_row_kernel<kRowVerify, KeyIO>), dim3(static_cast<unsigned>(n)), dim3(256), 0, st, io,
+                       n, k1, bits);
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 template int launch_recover_row<TxIO>(const TxIO&, uint64_t, hipStream_t);

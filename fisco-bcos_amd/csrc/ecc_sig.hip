@@ -233,6 +233,7 @@ int launch_sm2_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint
 // signatures: the latency path) and the one-lane sig_verify_kernel beyond (the trio kernel's round is
 // ~3x shorter than the one-lane kernel's, which fits 6.4x more signatures per round: tools/small_sweep.py
 // verify, profiles/r04_verify_sweep.json).  Policy split 1 / 0 forces the trio / one-lane kernel.
+static constexpr uint64_t kRowVerifyRounds = 2;
 int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
                       uint64_t n, uint8_t* d_ok, hipStream_t st) {
     if (n == 0) return 0;
@@ -243,7 +244,16 @@ int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, co
     const TxKernelPolicy pol = tx_policy();
     if (suite == BCOSGPU_SUITE_SM2 && pol.f26) return launch_sm2_verify_key(d_pub, d_hash, d_sig, stride, n, d_ok, st);
     if (suite == BCOSGPU_SUITE_SECP256K1 && pol.f26 && pol.coop >= 2) {
-        const bool small = pol.split >= 0 ? pol.split == 1 : n <= 2ull * 40 * static_cast<uint64_t>(cu_count());
+        const uint64_t cus = static_cast<uint64_t>(cu_count());
+        const bool small = pol.split >= 0 ? pol.split == 1 : n <= 2ull * 40 * cus;
+        // the row kernel (ecc_row.hip) while its rounds of one signature per CU beat the trio's round
+        // (tools/small_sweep.py verify, profiles/r05_verify_sweep_row.json); coop 3 forces it
+        static const bool row_env = [] {
+            const char* e = getenv("BCOSGPU_TXV_ROW");
+            return !(e && atoi(e) == 0);
+        }();
+        const bool row = pol.coop == 3 || (pol.split < 0 && row_env && n <= kRowVerifyRounds * cus);
+        if (small && row) return launch_sig_verify_row_secp(KeyIO{d_pub, d_hash, d_sig, stride, d_ok}, n, st);
         if (small) return launch_sig_verify_small_secp(KeyIO{d_pub, d_hash, d_sig, stride, d_ok}, n, st);
     }
     if (suite == BCOSGPU_SUITE_SM2)

@@ -58,7 +58,7 @@ if mode == "verify":
             pub = torch.empty((m, 64), dtype=torch.uint8, device="cuda")
             sig = torch.empty((m, 65), dtype=torch.uint8, device="cuda")
             device.secp256k1_sign(sk, h, pub, sig, ok)
-            variants = {"trio": (1, 0, 2, 1), "onelane": (0, 0, 2, 1), "auto": (-1, 0, 2, 1)}
+            variants = {"trio": (1, 0, 2, 1), "row": (1, 0, 3, 1), "onelane": (0, 0, 2, 1), "auto": (-1, 0, 2, 1)}
         else:
             sig = torch.empty((m, 128), dtype=torch.uint8, device="cuda")
             device.sm2_sign(sk, h, sig, ok)
