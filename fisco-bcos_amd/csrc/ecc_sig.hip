@@ -233,7 +233,9 @@ int launch_sm2_sign(const uint8_t* d_sk, const uint8_t* d_hash, uint64_t n, uint
 // signatures: the latency path) and the one-lane sig_verify_kernel beyond (the trio kernel's round is
 // ~3x shorter than the one-lane kernel's, which fits 6.4x more signatures per round: tools/small_sweep.py
 // verify, profiles/r04_verify_sweep.json).  Policy split 1 / 0 forces the trio / one-lane kernel.
-static constexpr uint64_t kRowVerifyRounds = 2;
+// the row verify kernel's rounds of one signature per CU: 0.104 / 0.131 / 0.169 / 0.217 ms at 1 / 256 /
+// 512 / 768 signatures against the trio's 0.338 (profiles/r05_verify_sweep_row.json)
+static constexpr uint64_t kRowVerifyRounds = 4;
 int launch_sig_verify(int suite, const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
                       uint64_t n, uint8_t* d_ok, hipStream_t st) {
     if (n == 0) return 0;
