@@ -134,6 +134,7 @@ def kernel_source_sha():
 
 
 ROW_LAT, ROW_LAT_N = 0.42, 0.28  # ecc_txv.hip kRowLat, kRowLatN
+ROW_LAT_SM2, ROW_LAT_N_SM2 = 0.60, 0.61  # kRowLatSM2, kRowLatNSM2 (rounds of 2 per CU)
 
 
 def _auto_kernel(suite, n, cus, small_ok=True, row_ok=True):
@@ -152,7 +153,9 @@ def _auto_kernel(suite, n, cus, small_ok=True, row_ok=True):
             c = (n // per[0]) * lat[0] + (0 if tail == 0 else occ2_tail if tail <= per[1] else lat[0])
         if c < cost:
             best, cost = code[k], c
-    if row_ok and suite == 0 and small_ok and ROW_LAT + (-(-n // cus) - 1) * ROW_LAT_N < cost:
+    r1, rn = (ROW_LAT_SM2, ROW_LAT_N_SM2) if suite == 1 else (ROW_LAT, ROW_LAT_N)
+    per_round = (2 if suite == 1 else 1) * cus
+    if row_ok and small_ok and r1 + (-(-n // per_round) - 1) * rn < cost:
         best = 3
     return best
 
@@ -186,8 +189,10 @@ def _kernel_name(suite, n):
             return "tx_verify_trio26_kernel<TxIO>"
         return "tx_verify_coop26_kernel<TxIO>" if f26 else "tx_verify_coop_kernel"
     if suite == 1 and small and coop:
+        if coop == 3 and f26:
+            return "sm2_verify_row_kernel<TxIO>"
         if f26:
-            return ("tx_verify_sm2_trio26_kernel<TxIO,%d>" % SM2_TRIO_SPLIT if coop == 2
+            return ("tx_verify_sm2_trio26_kernel<TxIO,%d>" % SM2_TRIO_SPLIT if coop >= 2
                     else "tx_verify_sm2_pair26_kernel<TxIO>")
         return "tx_verify_sm2_pair_kernel"
     return "tx_verify_kernel<%d,%d,%s,TxIO>" % (suite, occ, "true" if f26 else "false")

@@ -564,6 +564,9 @@ template <class IO>
 int launch_recover_row(const IO& io, uint64_t n, hipStream_t st);
 // secp256k1 verify with a known key, one signature per workgroup on the rows (ecc_row.hip)
 int launch_sig_verify_row_secp(const KeyIO& io, uint64_t n, hipStream_t st);
+// SM2 verify (TxIO, SigIO, KeyIO), one signature per workgroup on the rows (ecc_row.hip)
+template <class IO>
+int launch_sm2_verify_row(const IO& io, uint64_t n, hipStream_t st);
 // SM2 verify with a known key over KeyIO (ecc_txv.hip: launch_verify's kernel choice)
 int launch_sm2_verify_key(const uint8_t* d_pub, const uint8_t* d_hash, const uint8_t* d_sig, uint32_t stride,
                           uint64_t n, uint8_t* d_ok, hipStream_t st);

@@ -1375,12 +1375,13 @@ static int sm2_trio_split() {
 
 template <class IO>
 int launch_verify_small_sm2(const TxKernelPolicy& pol, const IO& io, uint64_t n, hipStream_t st) {
+    if (pol.coop == 3 && pol.f26) return launch_sm2_verify_row(io, n, st);  // ecc_row.hip
     const dim3 grid(static_cast<unsigned>((n + 63) / 64));
     if (pol.f26) {  // fp26 point arithmetic over the R'-domain 8-bit table
         const uint32_t* t26;
         const int rc = tables8_sm2_26(&t26);
         if (rc) return rc;
-        if (pol.coop >= 2) {  // (3, the secp256k1 row kernel's policy, has no SM2 kernel: the trio)
+        if (pol.coop >= 2) {
             // BCOSGPU_SM2_JAC_ONLY=1 (tests): every window adds the Jacobian entry (the affine table unused)
             const char* jo = getenv("BCOSGPU_SM2_JAC_ONLY");
             const int affine = jo && atoi(jo) != 0 ? 0 : 1;

@@ -78,6 +78,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
     const frow::Lane L(lane);
+    const frow::FK1 fk{L};
     uint32_t* const slot = S.slot[wave];
     const uint64_t i = blockIdx.x;  // one signature per workgroup (the grid is n)
     ROW_T(0);
@@ -160,11 +161,11 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
                 frow::Pt P{X, Y, L.one};
                 if (wave == 2) {
 #pragma unroll 1
-                    for (int q = 0; q < 64; ++q) frow::dbl(P, L);
+                    for (int q = 0; q < 64; ++q) frow::dbl(P, fk);
                 }
                 fe26 beta26;
                 fe26_const(beta26, kGlvBeta);
-                frow::build_table(S.tab[wave - 1], S.zc[wave - 1], P, frow::from_fe26(beta26, L), L);
+                frow::build_table(S.tab[wave - 1], S.zc[wave - 1], P, frow::from_fe26(beta26, L), fk);
                 row_post(&S.post[wave == 1 ? 2 : 3]);
             }
         } else {
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         const uint32_t X = frow::from_fe26(X26, L);
         const uint32_t w = frow::mul(frow::sqr(X, L), X, L) + 7u * L.one;  // m 1 + 7 / 2^26
         if (wave == 3) {  // y = sqrt(w) with v's parity, then Zc y and Zc64 y
-            const uint32_t yc = frow::sqrt_cand(w, L);
+            const uint32_t yc = frow::sqrt_cand(w, fk);
             const bool square = frow::is_zero(frow::sub<2>(frow::sqr(yc, L), w, L), slot, L);
             okr = okr && square;
             fe26 y, ny;
@@ -208,11 +209,11 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
             frow::Pt P{Rx, Ry, L.one};
             if (wave == 2) {
 #pragma unroll 1
-                for (int q = 0; q < 64; ++q) frow::dbl(P, L);
+                for (int q = 0; q < 64; ++q) frow::dbl(P, fk);
             }
             fe26 beta26;
             fe26_const(beta26, kGlvBeta);
-            frow::build_table(S.tab[wave - 1], S.zc[wave - 1], P, frow::from_fe26(beta26, L), L);
+            frow::build_table(S.tab[wave - 1], S.zc[wave - 1], P, frow::from_fe26(beta26, L), fk);
             row_post(&S.post[wave == 1 ? 2 : 3]);
         }
         }
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         const uint32_t kf = sgpr(S.kflags);
         const bool neg = (kf & (kh == 0 ? 4u : 8u)) != 0u;
         frow::Pt acc{0u, 0u, 0u};
-        const bool fin = frow::glv_chain<16>(acc, k, neg, kh == 1, &S.tab[part][0][0][0], L);
+        const bool fin = frow::glv_chain<16>(acc, k, neg, kh == 1, &S.tab[part][0][0][0], fk);
         frow::pt_store(S.pt[wave], acc, L);
         if (lane == 0) S.pinf[wave] = fin ? 0u : 1u;
     }
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
                 g = frow::Pt{ex, ey, L.one};
                 ginf = false;
             } else {
-                frow::madd(g, ex, ey, L);
+                frow::madd(g, ex, ey, fk);
             }
         }
         frow::pt_store(S.pt[4 + wave], g, L);
@@ -271,7 +272,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         bool rinf;
         frow::pt_load(P, S.pt[2 * wave], L);
         frow::pt_load(Q, S.pt[2 * wave + 1], L);
-        frow::add_full(R, rinf, P, sgpr(S.pinf[2 * wave]) != 0u, Q, sgpr(S.pinf[2 * wave + 1]) != 0u, slot, L);
+        frow::add_full(R, rinf, P, sgpr(S.pinf[2 * wave]) != 0u, Q, sgpr(S.pinf[2 * wave + 1]) != 0u, slot, fk);
         if (wave < 2 && !rinf) R.Z = frow::mul(R.Z, S.zcy[wave][L.k], L);  // (X, Y, Z Zc y) on E
         frow::pt_store(S.pt[2 * wave], R, L);
         if (lane == 0) S.pinf[2 * wave] = rinf ? 1u : 0u;
@@ -282,7 +283,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         bool rinf;
         frow::pt_load(P, S.pt[4 * wave], L);
         frow::pt_load(Q, S.pt[4 * wave + 2], L);
-        frow::add_full(R, rinf, P, sgpr(S.pinf[4 * wave]) != 0u, Q, sgpr(S.pinf[4 * wave + 2]) != 0u, slot, L);
+        frow::add_full(R, rinf, P, sgpr(S.pinf[4 * wave]) != 0u, Q, sgpr(S.pinf[4 * wave + 2]) != 0u, slot, fk);
         frow::pt_store(S.pt[4 * wave], R, L);
         if (lane == 0) S.pinf[4 * wave] = rinf ? 1u : 0u;
     }
@@ -292,7 +293,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         bool rinf;
         frow::pt_load(P, S.pt[0], L);
         frow::pt_load(Q, S.pt[4], L);
-        frow::add_full(R, rinf, P, sgpr(S.pinf[0]) != 0u, Q, sgpr(S.pinf[4]) != 0u, slot, L);
+        frow::add_full(R, rinf, P, sgpr(S.pinf[0]) != 0u, Q, sgpr(S.pinf[4]) != 0u, slot, fk);
         const bool ok2 = ((sgpr(S.kflags) | sgpr(S.rflag)) & 3u) == 3u && !rinf;
         Jac26 Rq;
         frow::to_fe26(Rq.X, R.X, slot, L);
@@ -336,6 +337,198 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
     }
     ROW_T(3);
 }
+
+// ------------------------------------------------------------------ SM2 verify on the rows
+// SM2Crypto::verify / recover with the key (SM2Crypto.cpp:66-92, sm2_do_verify: fast_sm2.cpp:139-227)
+// for the smallest batches: Q = s G + t P (t = r + s mod n), accept iff x(Q) = r - e (mod n), e =
+// SM3(Z_A || hash).  SM2 has no endomorphism, so t P is ONE chain of 64 radix-16 windows (doublings of
+// 4 product levels for a = -3: 19 levels a window) on wave 0; wave 1 builds the key's table (its
+// on-curve check on the rows) while wave 0 hashes Z_A and e, waves 2 and 3 each take half of the s G
+// comb windows (the comb entries are FieldP2 Montgomery words: one row product by R^-1 each).  The
+// x-check is projective (X == c Z^2), so there is no inversion.  Outputs bit-identical to every other
+// SM2 verification kernel (tests/test_gpu_row.py, the kernel-variant tests).
+__device__ __constant__ static const uint32_t kSm2RowRinv[16] = {0x4u, 0x3fffe40u, 0x6fffu, 0x3f40000u, 0x2ffffffu,
+                                                                 0x0u, 0x3ffffc0u, 0x17ffu, 0x3fb0000u, 0x3fffffu,
+                                                                 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u};
+namespace {
+struct Sm2RowLds {
+    uint32_t tab[8][3][16];  // the key's table: x, y (row limbs, magnitude 1; slot 2 unused)
+    uint32_t zc[16];
+    uint32_t pt[3][3][16];   // the chain's point, the two comb halves
+    uint32_t pinf[3];
+    uint32_t slot[4][16];
+    uint32_t c[2][8];        // c = (r - e) mod n and c + n (canonical words)
+    uint32_t cflag, kflag, rflag;
+    uint32_t ad[5];
+    uint32_t post[3];        // 0: table, 1: scalars, 2: comb half of wave 3
+};
+}  // namespace
+
+template <class IO>
+__global__ __launch_bounds__(256, 1) void sm2_verify_row_kernel(IO io, uint64_t n, const uint32_t* __restrict__ tab,
+                                                                int tab_bits) {
+    __shared__ Sm2RowLds S;
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const frow::Lane L(lane);
+    const frow::Sm2Lane C(L);
+    const frow::FSM2 f{L, C};
+    uint32_t* const slot = S.slot[wave];
+    const uint64_t i = blockIdx.x;
+    if (threadIdx.x < 3) S.post[threadIdx.x] = 0u;
+    __syncthreads();
+    fe r, s, px, py, t;
+    uint32_t X[8], Y[8];
+    const bool parsed = io.sm2_sig(i, r, s, X, Y);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        px.v[q] = X[7 - q];
+        py.v[q] = Y[7 - q];
+    }
+    FieldN2::add(t, r, s);
+    const bool okp = parsed && fe_lt_k(px, ParamP2::M) && fe_lt_k(py, ParamP2::M) && !fe_is_zero_raw(r) &&
+                     !fe_is_zero_raw(s) && fe_lt_k(r, ParamN2::M) && fe_lt_k(s, ParamN2::M) && !fe_is_zero_raw(t);
+    const bool ok = sgpr(okp ? 1u : 0u) != 0u;
+    const uint32_t rinv = kSm2RowRinv[L.k];
+    // ---------------------------------------------------------------- phase A
+    if (wave == 0) {  // e, c = r - e (mod n), the address of the key
+        fe h, e, c, c2;
+        io.template digest<SM3>(i, h);
+        uint32_t eb[8];
+        sm2_e(eb, X, Y, h);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) e.v[q] = eb[7 - q];
+        reduce_once(e, ParamN2::M);
+        FieldN2::sub(c, r, e);
+        const uint32_t carry = fe_add_k(c2, c, ParamN2::M);
+        const bool second = carry == 0u && fe_lt_k(c2, ParamP2::M);
+        put8(S.c[0], c, lane);
+        put8(S.c[1], c2, lane);
+        uint32_t ad[5] = {0, 0, 0, 0, 0};
+        if (io.want_addr()) sm3_address(ad, px, py);
+        if (lane < 5) {
+            uint32_t a = 0;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) a = lane == q ? ad[q] : a;
+            S.ad[lane] = a;
+        }
+        if (lane == 0) {
+            S.cflag = second ? 1u : 0u;
+            S.kflag = ok ? 1u : 0u;
+        }
+        row_post(&S.post[1]);
+    } else if (wave == 1) {  // the key on the rows, its curve check and its table
+        fe26 X26, Y26;
+        fe26_from_words(X26, px.v);
+        fe26_from_words(Y26, py.v);
+        uint32_t Xr = frow::from_fe26(X26, L), Yr = frow::from_fe26(Y26, L);
+        const uint32_t b = f.mul(frow::from_words(kSM2B, L), rinv);  // b (FieldP2 words are Montgomery)
+        const uint32_t x3 = f.mul(f.mul(Xr, Xr), Xr);
+        const uint32_t rhs = f.template sub<4>(x3 + b, frow::mul_int<3>(Xr));  // x^3 - 3x + b   m 6
+        const bool on = frow::is_zero_sm2(f.template sub<7>(f.mul(Yr, Yr), rhs), slot, L);
+        if (!(ok && on)) {  // a valid point for a rejected key (its verdict is already false)
+            uint32_t gx, gy;
+            frow::gather01(f.mul(frow::sel4(L, frow::from_words(kSM2Gx, L), frow::from_words(kSM2Gy, L),
+                                            frow::from_words(kSM2Gy, L), frow::from_words(kSM2Gy, L)),
+                                 rinv),
+                           gx, gy);
+            Xr = gx;
+            Yr = gy;
+        }
+        if (lane == 0) S.rflag = on ? 2u : 0u;
+        frow::build_table<frow::FSM2, false>(S.tab, S.zc, frow::Pt{Xr, Yr, L.one}, 0u, f);
+        row_post(&S.post[0]);
+    } else {  // waves 2, 3: s G over half of the comb windows each (no P = +-Q inside a half)
+        const int W = tab_bits == kWideBits ? 256 / kWideBits : 32, bits = tab_bits == kWideBits ? kWideBits : 8;
+        const int lo = (wave - 2) * (W / 2), hi = lo + W / 2;
+        frow::Pt g{0u, 0u, 0u};
+        bool ginf = true;
+#pragma unroll 1
+        for (int q = lo; q < hi; ++q) {
+            const int bit = q * bits;
+            uint32_t wd = 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) wd = (bit >> 5) == u ? s.v[u] : wd;
+            wd = sgpr(wd);
+            const uint32_t b = bits == 16 ? (wd >> (bit & 31)) & 0xffffu : (wd >> (bit & 31)) & 0xffu;
+            if (b == 0u) continue;
+            const uint32_t* e = tab + (static_cast<size_t>(q) << bits | b) * 16;
+            uint32_t ex, ey;  // Montgomery -> plain
+            frow::gather01(f.mul(frow::sel4(L, frow::from_words(e, L), frow::from_words(e + 8, L),
+                                            frow::from_words(e + 8, L), frow::from_words(e + 8, L)),
+                                 rinv),
+                           ex, ey);
+            if (ginf) {
+                g = frow::Pt{ex, ey, L.one};
+                ginf = false;
+            } else {
+                frow::madd(g, ex, ey, f);
+            }
+        }
+        frow::pt_store(S.pt[wave - 1], g, L);
+        if (lane == 0) S.pinf[wave - 1] = ginf ? 1u : 0u;
+        if (wave == 3) {
+            row_post(&S.post[2]);
+        } else {  // wave 2: the two halves
+            row_wait(&S.post[2]);
+            frow::Pt Q, R;
+            bool rinf;
+            frow::pt_load(Q, S.pt[2], L);
+            frow::add_full(R, rinf, g, ginf, Q, sgpr(S.pinf[2]) != 0u, slot, f);
+            frow::pt_store(S.pt[1], R, L);
+            if (lane == 0) S.pinf[1] = rinf ? 1u : 0u;
+        }
+    }
+    // ---------------------------------------------------------------- phase C: t P on wave 0
+    if (wave == 0) {
+        row_wait(&S.post[0]);
+        fe k;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) k.v[q] = sgpr(ok ? t.v[q] : (q == 0 ? 1u : 0u));
+        frow::Pt acc{0u, 0u, 0u};
+        const bool fin = frow::sm2_chain(acc, k, &S.tab[0][0][0], S.zc[L.k], slot, f);
+        frow::pt_store(S.pt[0], acc, L);
+        if (lane == 0) S.pinf[0] = fin ? 0u : 1u;
+    }
+    __syncthreads();
+    if (wave == 0) {  // Q = t P + s G, x(Q) == c or c + n, projectively
+        frow::Pt P, Q, R;
+        bool rinf;
+        frow::pt_load(P, S.pt[0], L);
+        frow::pt_load(Q, S.pt[1], L);
+        frow::add_full(R, rinf, P, sgpr(S.pinf[0]) != 0u, Q, sgpr(S.pinf[1]) != 0u, slot, f);
+        const uint32_t z2 = f.mul(R.Z, R.Z);
+        fe26 c26;
+        fe cw;
+        get8(cw, S.c[0]);
+        fe26_from_words(c26, cw.v);
+        bool match = frow::is_zero_sm2(f.template sub<13>(f.mul(frow::from_fe26(c26, L), z2), R.X), slot, L);
+        if (sgpr(S.cflag) != 0u) {
+            get8(cw, S.c[1]);
+            fe26_from_words(c26, cw.v);
+            match = match || frow::is_zero_sm2(f.template sub<13>(f.mul(frow::from_fe26(c26, L), z2), R.X), slot, L);
+        }
+        const bool ok2 = (sgpr(S.kflag) | sgpr(S.rflag)) == 3u && !rinf && match;
+        uint32_t ad[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) ad[q] = ok2 ? S.ad[q] : 0u;
+        if (lane == 0) io.finish(i, ok2, ad, &px, &py);
+    }
+}
+
+template <class IO>
+int launch_sm2_verify_row(const IO& io, uint64_t n, hipStream_t st) {
+    if (n == 0) return 0;
+    const uint32_t *k1, *sm2;
+    int bits = 8;
+    const int rc = tables(&k1, &sm2, &bits);
+    if (rc) return rc;
+    hipLaunchKernelGGL(sm2_verify_row_kernel<IO>, dim3(static_cast<unsigned>(n)), dim3(256), 0, st, io, n, sm2, bits);
+    return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
+}
+template int launch_sm2_verify_row<TxIO>(const TxIO&, uint64_t, hipStream_t);
+template int launch_sm2_verify_row<SigIO>(const SigIO&, uint64_t, hipStream_t);
+template int launch_sm2_verify_row<KeyIO>(const KeyIO&, uint64_t, hipStream_t);
 
 template <class IO>
 int launch_recover_row(const IO& io, uint64_t n, hipStream_t st) {

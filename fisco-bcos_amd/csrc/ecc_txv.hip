@@ -62,9 +62,13 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
 // has the row kernel (ecc_row.hip, one signature per workgroup): its first round of one signature per
 // CU costs kRowLat of the trio's round and each further round kRowLatN (two workgroups share a CU:
 // tools/small_sweep.py, profiles/r05_small_sweep_row.json: 0.149 / 0.176 / 0.275 / 0.365 / 0.428 ms at
-// 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.378).
+// 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.378); SM2 its own row kernel, whose
+// latency is its one-wave chain's, so two workgroups per CU overlap whole: its rounds hold 2 signatures
+// per CU, at kRowLatSM2 / kRowLatNSM2 of the SM2 trio's round (profiles/r05_small_sweep_row_sm2.json:
+// 0.336 / 0.363 / 0.364 / 0.702 ms at 1 / 256 / 512 / 1024 signatures against the trio's 0.577).
 // Returns 3 (row), 2 (trio), 1 (pair), 0 (one-lane, occupancy 1) or -2 (one-lane, occupancy 2).
 static constexpr double kRowLat = 0.42, kRowLatN = 0.28;
+static constexpr double kRowLatSM2 = 0.60, kRowLatNSM2 = 0.61;
 static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_ok) {
     const bool sm2 = suite == BCOSGPU_SUITE_SM2;
     //                    occ 2,              occ 1,              pair,               trio
@@ -85,8 +89,10 @@ static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_o
             best = code[k];
         }
     }
-    if (row_ok && !sm2 && small_ok) {
-        const double c = kRowLat + static_cast<double>((n + cus - 1) / cus - 1) * kRowLatN;
+    if (row_ok && small_ok) {
+        const double r1 = sm2 ? kRowLatSM2 : kRowLat, rn = sm2 ? kRowLatNSM2 : kRowLatN;
+        const uint64_t per_round = (sm2 ? 2ull : 1ull) * cus;
+        const double c = r1 + static_cast<double>((n + per_round - 1) / per_round - 1) * rn;
         if (c < cost) best = 3;
     }
     return best;
@@ -106,12 +112,14 @@ int launch_verify(int suite, const IO& io, uint64_t n, hipStream_t st) {
     bool small = pol.split >= 0 ? pol.split == 1 : n <= (1ull << 15);
     int occ = pol.occ;
     if (pol.split < 0 && pol.coop == 2 && pol.f26) {
-        // the row kernel recovers (TxIO, SigIO, EcrecIO); BCOSGPU_TXV_ROW=0 leaves it out of the choice
+        // the row kernels: secp256k1 recovery (TxIO, SigIO, EcrecIO; its known-key verify is chosen in
+        // ecc_sig.hip) and SM2 verification (TxIO, SigIO, KeyIO); BCOSGPU_TXV_ROW=0 leaves them out
         static const bool row_env = [] {
             const char* e = getenv("BCOSGPU_TXV_ROW");
             return !(e && atoi(e) == 0);
         }();
-        const int k = auto_kernel(suite, n, cu_count(), n <= (1ull << 16), row_env && !std::is_same_v<IO, KeyIO>);
+        const bool row_io = suite == BCOSGPU_SUITE_SM2 || !std::is_same_v<IO, KeyIO>;
+        const int k = auto_kernel(suite, n, cu_count(), n <= (1ull << 16), row_env && row_io);
         small = k > 0;
         if (small) pol.coop = k;
         else if (!occ) occ = k == -2 ? 2 : 1;

@@ -118,9 +118,10 @@ __device__ __forceinline__ uint32_t reduce(uint64_t lo, uint64_t hi, const Lane&
     return (static_cast<uint32_t>(t) & L.keep9) + shr<1>(c5);
 }
 
-// r = a * b (both spread over the row, magnitudes <= 16).  Two accumulators (even / odd steps) halve
-// the dependent chain of 64-bit multiply-adds.
-__device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b, const Lane& L) {
+// the product's 19 columns of a * b (both spread over the row, magnitudes <= 16): lo = columns 0..15 on
+// lanes 0..15, hi = columns 16..18 on lanes 0..2.  Two accumulators (even / odd steps) halve the
+// dependent chain of 64-bit multiply-adds.
+__device__ __forceinline__ void conv(uint32_t a, uint32_t b, const Lane& L, uint64_t& lo, uint64_t& hi) {
     uint32_t t1 = ror<1>(b);
     uint64_t e = mad(bcast<0>(a), b, 0), o = mad(bcast<1>(a), t1, 0);
     uint32_t t2 = ror<2>(b);
@@ -140,8 +141,13 @@ __device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b, const Lane& L) {
     t1 = ror<2>(t1);
     wo = mad(bcast<9>(a), t1, wo);
     const uint64_t w = we + wo;
-    const uint64_t lo = e + o + bsel64(L.ge3, w, 0);
-    const uint64_t hi = bsel64(L.ge3, 0, w);
+    lo = e + o + bsel64(L.ge3, w, 0);
+    hi = bsel64(L.ge3, 0, w);
+}
+// r = a * b in secp256k1's field (magnitudes <= 16 -> 1)
+__device__ __forceinline__ uint32_t mul(uint32_t a, uint32_t b, const Lane& L) {
+    uint64_t lo, hi;
+    conv(a, b, L, lo, hi);
     return reduce(lo, hi, L);
 }
 
@@ -154,6 +160,93 @@ template <int K>
 __device__ __forceinline__ uint32_t neg(uint32_t a, const Lane& L) { return K * L.q - a; }
 template <int C>
 __device__ __forceinline__ uint32_t mul_int(uint32_t a) { return a * C; }
+
+// ------------------------------------------------------------------ SM2's field on the rows
+// p = 2^256 - 2^224 - 2^96 + 2^64 - 1 has no small 2^260 residue (2^260 = 2^228 + 2^100 - 2^68 + 2^4 mod
+// p: folding by it alone would take eight rounds), so the high columns H_j (weight 2^(26 (10 + j)),
+// j = 0..10) fold through their FULL residues M_j = 2^(26 (10 + j)) mod p: lane k adds
+// sum_j H_j M_j[k] -- eleven broadcasts and multiply-adds, each M_j[k] < 2^26 a per-lane constant, the
+// sum < 2^56.5; one parallel carry; then the carries into lanes 10, 11 (weights 2^260, 2^286: M_0 and
+// M_1 are < 2^229 and < 2^255) and lane 9's bits from 2^256 (D = 2^256 mod p) fold once more, which
+// leaves a value < 2^257, and two carry rounds bring every limb under B.  Same magnitude contracts as
+// the secp256k1 field; sub<K> adds K Q2 with Q2 = 16 p in digits within 2^-4 of 2^26, so K Q2 >= b limb
+// by limb for b.m <= K - 1 up to K = 15.  Checked on the GPU by tools/rowbench.hip against a host
+// reference, and in Python (every bound above) at magnitude 16.
+// 2^(26 (10 + j)) mod p for j = 0..10, D = 2^256 mod p and Q2 = 16 p (digit 2 raised by 2^26, digit 3
+// lowered by 1, so every digit is within 2^-4 of 2^26), radix-2^26 digits per lane (lanes 10..15: 0)
+__device__ __constant__ static const uint32_t kSm2RowM[11][16] = {
+    {0x10u, 0x0u, 0x3ff0000u, 0x3fffffu, 0x0u, 0x0u, 0x0u, 0x0u, 0x100000u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+    {0x0u, 0x10u, 0x0u, 0x3ff0000u, 0x3fffffu, 0x0u, 0x0u, 0x0u, 0x0u, 0x100000u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+    {0x1000000u, 0x0u, 0x10u, 0x3fffc00u, 0x3ffffffu, 0x3fffffu, 0x0u, 0x0u, 0x0u, 0x4000u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+    {0x40000u, 0x1000000u, 0x0u, 0x0u, 0x0u, 0x0u, 0x400000u, 0x0u, 0x0u, 0x100u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+    {0x1000u, 0x40000u, 0x0u, 0x0u, 0x10u, 0x0u, 0x0u, 0x400000u, 0x0u, 0x4u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+    {0x40u, 0x1000u, 0x0u, 0x1000000u, 0x0u, 0x10u, 0x0u, 0x0u, 0x800000u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+    {0x2u, 0x40u, 0x3fff000u, 0x7ffffu, 0x1000000u, 0x0u, 0x10u, 0x0u, 0x20000u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+    {0x0u, 0x2u, 0x40u, 0x3fff000u, 0x7ffffu, 0x1000000u, 0x0u, 0x10u, 0x0u, 0x20000u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+    {0x200000u, 0x0u, 0x2u, 0x3ffffc0u, 0xfffu, 0x80000u, 0x1000000u, 0x0u, 0x10u, 0x800u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+    {0x8000u, 0x200000u, 0x0u, 0x0u, 0x40u, 0x1000u, 0x80000u, 0x1000000u, 0x0u, 0x30u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+    {0x300u, 0x8000u, 0x3f00000u, 0x3ffffffu, 0x2u, 0x40u, 0x1000u, 0x80000u, 0x0u, 0x1u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u},
+};
+__device__ __constant__ static const uint32_t kSm2RowD[16] = {0x1u, 0x0u, 0x3fff000u, 0x3ffffu, 0x0u, 0x0u, 0x0u, 0x0u, 0x10000u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u};
+__device__ __constant__ static const uint32_t kSm2RowQ[16] = {0x3fffff0u, 0x3ffffffu, 0x400ffffu, 0x3bfffffu, 0x3ffffffu, 0x3ffffffu, 0x3ffffffu, 0x3ffffffu, 0x3efffffu, 0x3ffffffu, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u};
+
+struct Sm2Lane {
+    uint32_t q, d, mask9;  // Q2 and D digits, mask9: all ones on lanes 0..8, 2^22 - 1 on lane 9, 0 above
+    uint32_t m[11];
+    __device__ __forceinline__ explicit Sm2Lane(const Lane& L) {
+        q = kSm2RowQ[L.k];
+        d = kSm2RowD[L.k];
+#pragma unroll
+        for (int j = 0; j < 11; ++j) m[j] = kSm2RowM[j][L.k];
+        mask9 = opaque(L.k < 9 ? 0xffffffffu : L.k == 9 ? 0x3fffffu : 0u);
+    }
+};
+
+template <int J>
+__device__ __forceinline__ uint64_t fold_col(uint32_t H, const Sm2Lane& C, uint64_t r) {
+    return mad(bcast<J>(H), C.m[J], r);
+}
+
+__device__ __forceinline__ uint32_t reduce_sm2(uint64_t lo, uint64_t hi, const Lane& L, const Sm2Lane& C) {
+    // round 1 (as reduce): columns 0..15 in v, 16..20 in w
+    const uint32_t l = static_cast<uint32_t>(lo) & M26, cA = hi26(lo) & M26, cB = static_cast<uint32_t>(lo >> 52);
+    const uint32_t lh = static_cast<uint32_t>(hi) & M26, hA = hi26(hi) & M26, hB = static_cast<uint32_t>(hi >> 52);
+    const uint32_t v = l + shr<1>(cA) + shr<2>(cB);
+    const uint32_t x1 = shr<1>(hA) + ror<1>(cA & L.eq15);
+    const uint32_t x2 = shr<2>(hB) + ror<2>(cB & L.ge14);
+    const uint32_t w = lh + x1 + x2;
+    const uint32_t H = shl<10>(v) + shr<6>(w);  // lanes 0..10: H_j = column 10 + j (< 2^27.01)
+    // pass 1: r_k = v_k + sum_j H_j M_j[k]  (< 2^56.5, lanes 0..9)
+    uint64_t r = v & L.lt10;
+    r = fold_col<0>(H, C, r);
+    r = fold_col<1>(H, C, r);
+    r = fold_col<2>(H, C, r);
+    r = fold_col<3>(H, C, r);
+    r = fold_col<4>(H, C, r);
+    r = fold_col<5>(H, C, r);
+    r = fold_col<6>(H, C, r);
+    r = fold_col<7>(H, C, r);
+    r = fold_col<8>(H, C, r);
+    r = fold_col<9>(H, C, r);
+    r = fold_col<10>(H, C, r);
+    const uint32_t u = (static_cast<uint32_t>(r) & M26) + shr<1>(hi26(r) & M26) + shr<2>(static_cast<uint32_t>(r >> 52));
+    // pass 2: lanes 10, 11 by M_0, M_1; lane 9's bits from 2^256 by D  (< 2^52.1)
+    uint64_t t = mad(bcast<10>(u), C.m[0], u & C.mask9);
+    t = mad(bcast<11>(u), C.m[1], t);
+    t = mad(bcast<9>(u) >> 22, C.d, t);
+    // round A (lane 9 stays < 2^24.8, so nothing leaves it), round B (lanes 0..8 carry)
+    const uint32_t ua = (static_cast<uint32_t>(t) & M26) + shr<1>(hi26(t) & M26) + shr<2>(static_cast<uint32_t>(t >> 52));
+    return ((ua & L.keep9) + shr<1>((ua >> 26) & L.lt9)) & L.lt10;
+}
+__device__ __forceinline__ uint32_t mul_sm2(uint32_t a, uint32_t b, const Lane& L, const Sm2Lane& C) {
+    uint64_t lo, hi;
+    conv(a, b, L, lo, hi);
+    return reduce_sm2(lo, hi, L, C);
+}
+template <int K>
+__device__ __forceinline__ uint32_t sub_sm2(uint32_t a, uint32_t b, const Sm2Lane& C) { return a + (K * C.q - b); }
+template <int K>
+__device__ __forceinline__ uint32_t neg_sm2(uint32_t a, const Sm2Lane& C) { return K * C.q - a; }
 
 // every row receives every row's value: .v[j] = row j's (v_permlane16_swap then v_permlane32_swap)
 struct Rows4 {

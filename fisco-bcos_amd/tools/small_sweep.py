@@ -19,7 +19,7 @@ from bcos_gpu import device, synth
 
 bcos_gpu.ensure_device(0)
 VARIANTS = {"trio": (1, 0, 2, 1), "row": (1, 0, 3, 1), "pair": (1, 0, 1, 1), "occ1": (0, 1, 0, 1),
-            "occ2": (0, 2, 0, 1), "auto": (-1, 0, 2, 1)}  # row: secp256k1 only (ecc_row.hip)
+            "occ2": (0, 2, 0, 1), "auto": (-1, 0, 2, 1)}  # row: ecc_row.hip (secp256k1 recovery, SM2 verify)
 args = sys.argv[1:]
 mode = args.pop(0) if args and args[0] == "verify" else "tx"
 # sizes: one comma-separated argument or several arguments (tools/gpu_run.sh turns commas into spaces)
@@ -87,8 +87,6 @@ for suite in (0, 1):
         snd = torch.empty((n, 20), dtype=torch.uint8, device="cuda")
         st = torch.empty(n, dtype=torch.uint8, device="cuda")
         for name, pol in VARIANTS.items():
-            if name == "row" and suite == 1:
-                continue
             bcos_gpu.set_tx_kernel_policy(*pol)
             for _ in range(30):
                 device.tx_verify(suite, big.pre, po, big.sig, so, th, snd, st)

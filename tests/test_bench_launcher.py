@@ -55,12 +55,16 @@ def test_small_batch_choice_mirrors_library():
     mr = re.search(r"kRowLat = ([\d.]+), kRowLatN = ([\d.]+);", src)
     mbr = re.search(r"ROW_LAT, ROW_LAT_N = ([\d.]+), ([\d.]+)", bsrc)
     assert mr and mbr and mr.groups() == mbr.groups()
+    mr = re.search(r"kRowLatSM2 = ([\d.]+), kRowLatNSM2 = ([\d.]+);", src)
+    mbr = re.search(r"ROW_LAT_SM2, ROW_LAT_N_SM2 = ([\d.]+), ([\d.]+)", bsrc)
+    assert mr and mbr and mr.groups() == mbr.groups()
     ns = {"__name__": "bench_mirror", "__file__": os.path.join(ROOT, "bench.py")}
     exec(bsrc[bsrc.index("ROW_LAT, ROW_LAT_N ="):bsrc.index("def _kernel_name")], ns)
     pick = ns["_auto_kernel"]
     names = {3: "row", 2: "trio", 1: "pair", 0: "occ1", -2: "occ2"}
-    # round 5's sweep adds the row kernel (1 .. 2,048 signatures)
-    for fname, row_ok in (("r04_small_sweep.json", False), ("r05_small_sweep_row.json", True)):
+    # round 5's sweeps add the row kernels (secp256k1 1 .. 2,048 signatures; SM2 1 .. 1,024)
+    for fname, row_ok in (("r04_small_sweep.json", False), ("r05_small_sweep_row.json", True),
+                          ("r05_small_sweep_row_sm2.json", True)):
         path = os.path.join(ROOT, "profiles", fname)
         if not os.path.exists(path):
             continue
@@ -73,5 +77,8 @@ def test_small_batch_choice_mirrors_library():
             cands = [v for v in ("row", "trio", "pair", "occ1", "occ2") if "%s_%d_%s" % (suite_name, n, v) in sweep]
             best = min(sweep["%s_%d_%s" % (suite_name, n, v)] for v in cands)
             # (the round-4 sweep predates the row kernel: the choice among the kernels it timed)
-            chosen = sweep["%s_%d_%s" % (suite_name, n, names[pick(suite, n, 256, n <= (1 << 16), row_ok)])]
+            key = "%s_%d_%s" % (suite_name, n, names[pick(suite, n, 256, n <= (1 << 16), row_ok)])
+            if key not in sweep:  # a kernel this sweep did not time
+                continue
+            chosen = sweep[key]
             assert chosen <= best * 1.05, (key, chosen, best)

@@ -91,3 +91,47 @@ def test_row_recover_crafted_scalars(gpu, oracle, row_policy):
     ok = _check(gpu, oracle, h, sig)
     assert (~ok).sum() >= 20  # the Q = O cases
     assert ok.sum() >= 100
+
+
+# ------------------------------------------------------------------ SM2 (sm2_verify_row_kernel)
+N_SM2 = 0xFFFFFFFEFFFFFFFFFFFFFFFFFFFFFFFF7203DF6B21C6052B53BBF40939D54123
+
+
+@pytest.mark.parametrize("n", [1, 7, 300])
+def test_row_sm2_verify_random_and_edge(gpu, oracle, row_policy, n):
+    """SM2Crypto::recover / verify with the embedded key (r || s || pub) through the SM2 row kernel:
+    valid signatures, bit flips, a wrong hash, r = n, s = 0, r + s = n (t = 0), a key with x >= p, a key
+    off the curve, r + s = n - 2 and n - 4 (t near n: the chain's last addition meets its doubling /
+    infinity cases), against the oracle's verdicts and addresses."""
+    rng = np.random.default_rng(0x5A + n)
+    sk = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    sk[:, 0] &= 0x7F
+    h = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    _, sig, _ = _dev_sign(gpu, 1, sk, h)
+    sig = sig.copy()
+    for i in range(n if n > 1 else 0):
+        kind = i % 10
+        if kind == 1:
+            sig[i, rng.integers(0, 128)] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 2:
+            h[i, 0] ^= 1
+        elif kind == 3:
+            sig[i, 0:32] = np.frombuffer(N_SM2.to_bytes(32, "big"), dtype=np.uint8)
+        elif kind == 4:
+            sig[i, 32:64] = 0
+        elif kind in (5, 8, 9):  # r + s = n, n - 2, n - 4
+            r = int.from_bytes(sig[i, 0:32].tobytes(), "big")
+            off = {5: 0, 8: 2, 9: 4}[kind]
+            sig[i, 32:64] = np.frombuffer(((N_SM2 - off - r) % N_SM2).to_bytes(32, "big"), dtype=np.uint8)
+        elif kind == 6:
+            sig[i, 64:96] = 0xFF
+        elif kind == 7:
+            sig[i, 127] ^= 1
+    _, addr, okg = gpu.SM2Crypto().recover_batch(h, sig, want_address=True)
+    want = oracle.sm2_verify_batch(h, sig, nthreads=8)
+    assert np.array_equal(okg, want)
+    assert not addr[~want].any()
+    for i in np.nonzero(want)[0]:
+        assert addr[i].tobytes() == oracle.sm3(sig[i, 64:].tobytes())[12:], i
+    if n >= 300:  # kind 0 (one in ten) is the valid case; every other kind is rejected
+        assert want.sum() >= n // 12 and (~want).sum() >= n // 2
