@@ -134,7 +134,7 @@ def kernel_source_sha():
 
 
 ROW_LAT, ROW_LAT_N = 0.42, 0.28  # ecc_txv.hip kRowLat, kRowLatN
-ROW_LAT_SM2, ROW_LAT_N_SM2 = 0.60, 0.61  # kRowLatSM2, kRowLatNSM2 (rounds of 2 per CU)
+ROW_LAT_SM2, ROW_LAT_N_SM2 = 0.53, 0.48  # kRowLatSM2, kRowLatNSM2 (rounds of 2 per CU)
 
 
 def _auto_kernel(suite, n, cus, small_ok=True, row_ok=True):

@@ -434,37 +434,55 @@ __device__ __forceinline__ void dbl_m3(Pt& P, const F& f) {
     P.X = X3;
     P.Z = mul_int<2>(W);
 }
-// the window's last doubling, with ZZ = Z3^2, U2 = x ZZ, T = y Z3 for the mixed addition (rows 1, 2 of
-// level 3, beside alpha^2)
+// the chain's doubling with ZZ = Z^2 carried beside the point (m <= 16), so that alpha = 3 (X^2 - ZZ^2)
+// is ready after the first level: 3 levels -- X^2 | gamma = Y^2 | Y Z | ZZ^2, then alpha^2 | beta = X gamma |
+// gamma^2 | gamma ZZ (Z3^2 = 4 gamma ZZ), then alpha (4 beta - X3) -- and (10, 10, 2), ZZ 4
 template <class F>
-__device__ __forceinline__ void dbl_m3_zz(Pt& P, uint32_t x, uint32_t y, uint32_t zc2, uint32_t& ZZ, uint32_t& U2,
-                                          uint32_t& T, uint32_t& U1, const F& f) {
+__device__ __forceinline__ void dbl_m3z(Pt& P, uint32_t& ZZ, const F& f) {
     const Lane& L = f.L;
-    const Rows4 g1 = gather4(f.mul(sel4(L, P.Z, P.Y, P.Y, P.Y), sel4(L, P.Z, P.Y, P.Z, P.Z)));
-    const uint32_t dl = g1.v[0], gm = g1.v[1], W = g1.v[2];
-    const uint32_t xm = f.template sub<2>(P.X, dl), xp = P.X + dl;
-    const Rows4 g2 = gather4(f.mul(sel4(L, P.X, xm, gm, W), sel4(L, gm, xp, gm, W)));  // ... | W^2
-    const uint32_t b4 = mul_int<4>(g2.v[0]), al = mul_int<3>(g2.v[1]), C = g2.v[2];
-    const uint32_t Z3 = mul_int<2>(W);
+    const Rows4 g1 = gather4(f.mul(sel4(L, P.X, P.Y, P.Y, ZZ), sel4(L, P.X, P.Y, P.Z, ZZ)));
+    const uint32_t gm = g1.v[1], W = g1.v[2];
+    const uint32_t al = mul_int<3>(f.template sub<2>(g1.v[0], g1.v[3]));  // 3 (X^2 - Z^4)       m 9
+    const Rows4 g2 = gather4(f.mul(sel4(L, al, P.X, gm, gm), sel4(L, al, gm, gm, ZZ)));
+    const uint32_t b4 = mul_int<4>(g2.v[1]), C = g2.v[2];
+    const uint32_t X3 = f.template sub<9>(g2.v[0], mul_int<2>(b4));  // alpha^2 - 8 beta    m 10
+    const uint32_t t = f.template sub<11>(b4, X3);                   // 4 beta - X3         m 15
+    P.Y = f.template sub<9>(f.mul(al, t), mul_int<8>(C));             // m 10
+    P.X = X3;
+    P.Z = mul_int<2>(W);
     ZZ = mul_int<4>(g2.v[3]);
-    const Rows4 g3 = gather4(f.mul(sel4(L, al, x, y, y), sel4(L, al, ZZ, Z3, Z3)));  // alpha^2 | x ZZ | y Z3
-    const uint32_t X3 = f.template sub<9>(g3.v[0], mul_int<2>(b4));
+}
+// the window's last doubling (dbl_m3z) with, beside alpha (4 beta - X3) in level 3, the addition's
+// U2 = x Z3^2, T = y Z3 and U1 = X3 Zc^2 (the table entry (x, y) is the Jacobian point (x, y, Zc))
+template <class F>
+__device__ __forceinline__ void dbl_m3z_zz(Pt& P, uint32_t& ZZ, uint32_t x, uint32_t y, uint32_t zc2, uint32_t& U2,
+                                           uint32_t& T, uint32_t& U1, const F& f) {
+    const Lane& L = f.L;
+    const Rows4 g1 = gather4(f.mul(sel4(L, P.X, P.Y, P.Y, ZZ), sel4(L, P.X, P.Y, P.Z, ZZ)));
+    const uint32_t gm = g1.v[1];
+    const uint32_t al = mul_int<3>(f.template sub<2>(g1.v[0], g1.v[3]));
+    const uint32_t Z3 = mul_int<2>(g1.v[2]);
+    const Rows4 g2 = gather4(f.mul(sel4(L, al, P.X, gm, gm), sel4(L, al, gm, gm, ZZ)));
+    const uint32_t b4 = mul_int<4>(g2.v[1]), C = g2.v[2];
+    const uint32_t X3 = f.template sub<9>(g2.v[0], mul_int<2>(b4));
     const uint32_t t = f.template sub<11>(b4, X3);
-    uint32_t at;
-    gather01(f.mul(sel4(L, al, X3, X3, X3), sel4(L, t, zc2, zc2, zc2)), at, U1);  // alpha t | X3 Zc^2
-    P.Y = f.template sub<9>(at, mul_int<8>(C));
+    ZZ = mul_int<4>(g2.v[3]);
+    const Rows4 g3 = gather4(f.mul(sel4(L, al, x, y, X3), sel4(L, t, ZZ, Z3, zc2)));  // alpha t | U2 | T | U1
+    P.Y = f.template sub<9>(g3.v[0], mul_int<8>(C));
     P.X = X3;
     P.Z = Z3;
     U2 = g3.v[1];
     T = g3.v[2];
+    U1 = g3.v[3];
 }
 
-// P = P + (x, y, Zc) after dbl_m3_zz: the table entry is a Jacobian point with the table's common Z = Zc
+// P = P + (x, y, Zc) after dbl_m3z_zz: the table entry is a Jacobian point with the table's common Z = Zc
 // (SM2's doubling needs true coordinates: on the co-Z rescaled curve a would become -3 Zc^4), so
-// U1 = X1 Zc^2 (from the doubling), S1 = Y1 Zc^3 and Z3 = 2 Z1 Zc H join the spare rows of madd_zz's
-// three levels.  P (10, 10, 2), (x, y) m <= 2 -> (9, 6, 2); H and rr = (S2 - S1) returned for the tests
+// U1 = X1 Zc^2 (from the doubling), S1 = Y1 Zc^3, Z3 = 2 Z1 Zc H and the next ZZ = Z3^2 join the spare rows
+// of madd_zz's three levels.  P (10, 10, 2), (x, y) m <= 2 -> (9, 6, 2), ZZ 4; H and rr = S2 - S1 returned
+// for the complete last addition
 template <class F>
-__device__ __forceinline__ void add_coz_zz(Pt& P, uint32_t ZZ, uint32_t U2, uint32_t T, uint32_t U1, uint32_t zc,
+__device__ __forceinline__ void add_coz_zz(Pt& P, uint32_t& ZZ, uint32_t U2, uint32_t T, uint32_t U1, uint32_t zc,
                                            uint32_t zc3, const F& f, uint32_t* Ho = nullptr, uint32_t* rro = nullptr) {
     const Lane& L = f.L;
     const uint32_t H = f.template sub<2>(U2, U1);  // m 3
@@ -478,12 +496,13 @@ __device__ __forceinline__ void add_coz_zz(Pt& P, uint32_t ZZ, uint32_t U2, uint
     uint32_t X3 = f.template sub<2>(mul_int<4>(gb.v[2]), J);  // r^2 - J                m 6
     X3 = f.template sub<3>(X3, mul_int<2>(V));                // - 2 V                  m 9
     const uint32_t u = f.template sub<10>(V, X3);             // V - X3                 m 11
-    // Lc: rr (V - X3) | S1 J
-    uint32_t ya, yb;
-    gather01(f.mul(sel4(L, rr, S1, S1, S1), sel4(L, u, J, J, J)), ya, yb);
+    // Lc: rr (V - X3) | S1 J | (Z1 H Zc)^2
+    const uint32_t zh = gb.v[3];
+    const Rows4 gc = gather4(f.mul(sel4(L, rr, S1, zh, zh), sel4(L, u, J, zh, zh)));
     P.X = X3;
-    P.Y = mul_int<2>(f.template sub<2>(ya, yb));  // r (V - X3) - 2 S1 J          m 6
-    P.Z = mul_int<2>(gb.v[3]);                     // 2 Z1 Zc H                   m 2
+    P.Y = mul_int<2>(f.template sub<2>(gc.v[0], gc.v[1]));  // r (V - X3) - 2 S1 J   m 6
+    P.Z = mul_int<2>(zh);                                    // 2 Z1 Zc H            m 2
+    ZZ = mul_int<4>(gc.v[2]);                                // Z3^2                 m 4
     if (Ho) *Ho = H;
     if (rro) *rro = rr;
 }
@@ -546,7 +565,7 @@ __device__ __forceinline__ bool is_zero_sm2(uint32_t x, uint32_t* slot, const La
 
 // t P for a 256-bit t held in SGPRs over the co-Z table tab[8][3][16] (x, y of 1P .. 8P, each the Jacobian
 // point (x, y, Zc): the result is in true coordinates on E): radix-16 Booth
-// windows (the top digit = bit 255, then 64 windows of 4 doublings and one addition).  Before every
+// windows (the top digit = bit 255, then 64 windows of 4 doublings and one addition, 15 levels).  Before every
 // window but the last the accumulator is K P with 16 <= K < n / 16 + 8, which can never meet +-d P
 // (|d| <= 8); at the last window K = t - d may (t = n - 2 |d| gives K = -d), so its addition is
 // complete (zero tests on H and r, the doubling or infinity).  Returns false when the result is infinity.
@@ -556,6 +575,7 @@ __device__ __forceinline__ bool sm2_chain(Pt& acc, fe& k, const uint32_t* tab, u
     const Lane& L = f.L;
     const uint32_t zc2 = f.mul(zc, zc), zc3 = f.mul(zc2, zc);
     bool inf = true;
+    uint32_t ZZ = zc2;
     int d = static_cast<int>(k.v[7] >> 31);
     if (d != 0) {
         acc.X = tab[L.k];
@@ -579,32 +599,35 @@ __device__ __forceinline__ bool sm2_chain(Pt& acc, fe& k, const uint32_t* tab, u
                 acc.X = x;
                 acc.Y = y;
                 acc.Z = zc;
+                ZZ = zc2;
                 inf = false;
             }
             continue;
         }
-        dbl_m3(acc, f);
-        dbl_m3(acc, f);
-        dbl_m3(acc, f);
+        dbl_m3z(acc, ZZ, f);
+        dbl_m3z(acc, ZZ, f);
+        dbl_m3z(acc, ZZ, f);
         if (d != 0) {
-            uint32_t ZZ, U2, T, U1, H, rr;
-            dbl_m3_zz(acc, x, y, zc2, ZZ, U2, T, U1, f);
+            uint32_t U2, T, U1, H, rr;
+            dbl_m3z_zz(acc, ZZ, x, y, zc2, U2, T, U1, f);
             if (w != 0) {
                 add_coz_zz(acc, ZZ, U2, T, U1, zc, zc3, f);
             } else {
                 const Pt before = acc;
+                const uint32_t zzb = ZZ;
                 add_coz_zz(acc, ZZ, U2, T, U1, zc, zc3, f, &H, &rr);
                 if (is_zero_sm2(H, slot, L)) {
                     if (is_zero_sm2(rr, slot, L)) {
                         acc = before;
-                        dbl_m3(acc, f);
+                        ZZ = zzb;
+                        dbl_m3z(acc, ZZ, f);
                     } else {
                         inf = true;
                     }
                 }
             }
         } else {
-            dbl_m3(acc, f);
+            dbl_m3z(acc, ZZ, f);
         }
     }
     return !inf;

@@ -65,10 +65,11 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
 // 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.378); SM2 its own row kernel, whose
 // latency is its one-wave chain's, so two workgroups per CU overlap whole: its rounds hold 2 signatures
 // per CU, at kRowLatSM2 / kRowLatNSM2 of the SM2 trio's round (profiles/r05_small_sweep_row_sm2.json:
-// 0.336 / 0.363 / 0.364 / 0.702 ms at 1 / 256 / 512 / 1024 signatures against the trio's 0.577).
+// 0.278 / 0.304 / 0.305 / 0.571 / 0.583 ms at 1 / 256 / 512 / 768 / 1024 signatures against the trio's
+// 0.577).
 // Returns 3 (row), 2 (trio), 1 (pair), 0 (one-lane, occupancy 1) or -2 (one-lane, occupancy 2).
 static constexpr double kRowLat = 0.42, kRowLatN = 0.28;
-static constexpr double kRowLatSM2 = 0.60, kRowLatNSM2 = 0.61;
+static constexpr double kRowLatSM2 = 0.53, kRowLatNSM2 = 0.48;
 static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_ok) {
     const bool sm2 = suite == BCOSGPU_SUITE_SM2;
     //                    occ 2,              occ 1,              pair,               trio

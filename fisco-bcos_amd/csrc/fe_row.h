@@ -217,23 +217,21 @@ __device__ __forceinline__ uint32_t reduce_sm2(uint64_t lo, uint64_t hi, const L
     const uint32_t w = lh + x1 + x2;
     const uint32_t H = shl<10>(v) + shr<6>(w);  // lanes 0..10: H_j = column 10 + j (< 2^27.01)
     // pass 1: r_k = v_k + sum_j H_j M_j[k]  (< 2^56.5, lanes 0..9)
-    uint64_t r = v & L.lt10;
-    r = fold_col<0>(H, C, r);
-    r = fold_col<1>(H, C, r);
-    r = fold_col<2>(H, C, r);
-    r = fold_col<3>(H, C, r);
-    r = fold_col<4>(H, C, r);
-    r = fold_col<5>(H, C, r);
-    r = fold_col<6>(H, C, r);
-    r = fold_col<7>(H, C, r);
-    r = fold_col<8>(H, C, r);
-    r = fold_col<9>(H, C, r);
-    r = fold_col<10>(H, C, r);
+    // (three accumulators: the multiply-adds' dependent chain is four long instead of eleven)
+    uint64_t ra = fold_col<0>(H, C, v & L.lt10), rb = fold_col<1>(H, C, 0), rc = fold_col<2>(H, C, 0);
+    ra = fold_col<3>(H, C, ra);
+    rb = fold_col<4>(H, C, rb);
+    rc = fold_col<5>(H, C, rc);
+    ra = fold_col<6>(H, C, ra);
+    rb = fold_col<7>(H, C, rb);
+    rc = fold_col<8>(H, C, rc);
+    ra = fold_col<9>(H, C, ra);
+    rb = fold_col<10>(H, C, rb);
+    const uint64_t r = ra + rb + rc;
     const uint32_t u = (static_cast<uint32_t>(r) & M26) + shr<1>(hi26(r) & M26) + shr<2>(static_cast<uint32_t>(r >> 52));
     // pass 2: lanes 10, 11 by M_0, M_1; lane 9's bits from 2^256 by D  (< 2^52.1)
-    uint64_t t = mad(bcast<10>(u), C.m[0], u & C.mask9);
-    t = mad(bcast<11>(u), C.m[1], t);
-    t = mad(bcast<9>(u) >> 22, C.d, t);
+    const uint64_t t = mad(bcast<10>(u), C.m[0], u & C.mask9) + mad(bcast<11>(u), C.m[1], 0) +
+                       mad(bcast<9>(u) >> 22, C.d, 0);
     // round A (lane 9 stays < 2^24.8, so nothing leaves it), round B (lanes 0..8 carry)
     const uint32_t ua = (static_cast<uint32_t>(t) & M26) + shr<1>(hi26(t) & M26) + shr<2>(static_cast<uint32_t>(t >> 52));
     return ((ua & L.keep9) + shr<1>((ua >> 26) & L.lt9)) & L.lt10;
