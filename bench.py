@@ -133,7 +133,7 @@ def kernel_source_sha():
     return h.hexdigest()[:16]
 
 
-ROW_LAT, ROW_LAT_N = 0.42, 0.28  # ecc_txv.hip kRowLat, kRowLatN
+ROW_LAT, ROW_LAT_N = 0.38, 0.20  # ecc_txv.hip kRowLat, kRowLatN
 ROW_LAT_SM2, ROW_LAT_N_SM2 = 0.53, 0.48  # kRowLatSM2, kRowLatNSM2 (rounds of 2 per CU)
 
 

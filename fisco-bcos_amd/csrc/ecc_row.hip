@@ -36,6 +36,7 @@ struct RowLds {
     uint32_t kflags;            // wave 0: bit 0 scalars ok, bit 2 neg1, bit 3 neg2
     uint32_t rflag;             // wave 3: R on the curve (bit 1)
     uint32_t post[4];           // 0: e, 1: k / u1, 2: table of R', 3: table of 2^64 R'
+    alignas(8) uint32_t msg[16];  // wave 0: the 64-byte public key for the cooperative address Keccak
 };
 
 __device__ __forceinline__ void row_post(uint32_t* f) {
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         }
         fe rm, rinv;
         FieldN1::from_plain(rm, inv_of);
-        FieldInv<FieldN1>::inv_pipe(rinv, rm);
+        FieldInv<FieldN1>::inv_var(rinv, rm);  // variable time: every lane holds the same value
         row_wait(&S.post[0]);
         fe e, u1, u2, k1, k2;
         get8(e, S.e);
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         fe z, zi, ax, ay;
         fe26_to_fe(z, Rq.Z);
         ROW_T(4);
-        FieldInv<FieldK1>::inv_pipe(zi, z);
+        FieldInv<FieldK1>::inv_var(zi, z);
         ROW_T(5);
         fe26 zi26, zi2, zi3, AX, AY;
         fe26_from_fe(zi26, zi);
@@ -330,8 +331,30 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         fe26_mul(AY, Rq.Y, zi3);
         fe26_to_fe(ax, AX);
         fe26_to_fe(ay, AY);
+        // the address: Keccak-256 of the 64-byte key over 25 lanes (KeccakCoop: ~60 instead of ~180
+        // instructions a round), the whole wave taking part (wave-uniform branch); keccak_address's
+        // digest words 3..7 = bytes 12..31 are the high half of Keccak lane 1 and lanes 2, 3
         uint32_t ad[5] = {0, 0, 0, 0, 0};
-        if (ok2 && io.want_addr()) keccak_address(ad, ax, ay);
+        if (sgpr(ok2 && io.want_addr() ? 1u : 0u) != 0u) {
+            uint32_t m[16];
+            fe_to_be_words(m, ax);
+            fe_to_be_words(m + 8, ay);
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) S.msg[q] = m[q];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const KeccakCoop kc;
+            uint32_t lo, hi;
+            kc.hash(reinterpret_cast<const uint8_t*>(S.msg), 64u, lo, hi);
+            ad[0] = __builtin_amdgcn_readlane(hi, 1);
+            ad[1] = __builtin_amdgcn_readlane(lo, 2);
+            ad[2] = __builtin_amdgcn_readlane(hi, 2);
+            ad[3] = __builtin_amdgcn_readlane(lo, 3);
+            ad[4] = __builtin_amdgcn_readlane(hi, 3);
+        }
         if (lane == 0) io.finish(i, ok2, ad, &ax, &ay);
         }
     }

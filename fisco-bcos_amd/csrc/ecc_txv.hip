@@ -61,14 +61,13 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
 // 2^16 txs (beyond that the one-lane kernel's throughput wins at any rounding).  secp256k1 recovery also
 // has the row kernel (ecc_row.hip, one signature per workgroup): its first round of one signature per
 // CU costs kRowLat of the trio's round and each further round kRowLatN (two workgroups share a CU:
-// tools/small_sweep.py, profiles/r05_small_sweep_row.json: 0.149 / 0.176 / 0.275 / 0.365 / 0.428 ms at
-// 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.378); SM2 its own row kernel, whose
+// tools/small_sweep.py, profiles/r05_small_sweep_row.json: 0.133 / 0.156 / 0.225 / 0.302 / 0.375 ms at
+// 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.377); SM2 its own row kernel, whose
 // latency is its one-wave chain's, so two workgroups per CU overlap whole: its rounds hold 2 signatures
-// per CU, at kRowLatSM2 / kRowLatNSM2 of the SM2 trio's round (profiles/r05_small_sweep_row_sm2.json:
-// 0.278 / 0.304 / 0.305 / 0.571 / 0.583 ms at 1 / 256 / 512 / 768 / 1024 signatures against the trio's
-// 0.577).
+// per CU, at kRowLatSM2 / kRowLatNSM2 of the SM2 trio's round (same file: 0.275 / 0.304 / 0.306 /
+// 0.572 / 0.583 ms at 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.577).
 // Returns 3 (row), 2 (trio), 1 (pair), 0 (one-lane, occupancy 1) or -2 (one-lane, occupancy 2).
-static constexpr double kRowLat = 0.42, kRowLatN = 0.28;
+static constexpr double kRowLat = 0.38, kRowLatN = 0.20;
 static constexpr double kRowLatSM2 = 0.53, kRowLatNSM2 = 0.48;
 static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_ok) {
     const bool sm2 = suite == BCOSGPU_SUITE_SM2;

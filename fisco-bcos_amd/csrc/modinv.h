@@ -80,6 +80,68 @@ __device__ __forceinline__ int32_t divsteps_30(int32_t zeta, uint32_t f, uint32_
     return zeta;
 }
 
+// 30 divsteps as divsteps_30, in variable time (the var-time loop of libsecp256k1's modinv32, restated):
+// a run of zeros at the bottom of g is one shift (count trailing zeros, capped at the steps left by a
+// sentinel bit), and up to min(eta + 1, steps left, 8) low bits of g are cancelled at once by adding
+// w f, w = -g / f (mod 2^8) with f^-1 by Newton from the 5-bit seed (3 f) ^ 2.  eta = -delta, starting at
+// -1 (the delta = 1 variant: at most 724 divsteps for 256-bit inputs, hence 25 batches).  Same matrix
+// contract as divsteps_30 (u f0 + v g0 = f 2^30, q f0 + r g0 = g 2^30, |u| + |v|, |q| + |r| <= 2^30), so
+// update_fg_30 / update_de_30 apply unchanged.  Lanes run in lockstep: the loop ends when every lane has
+// done its 30 steps, a finished lane's iterations being no-ops (limit 0).  Fastest where every lane
+// holds the same value (the row kernel's one-signature inversions).
+template <int U = 3>
+__device__ __forceinline__ int32_t divsteps_30_var(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
+    uint32_t u = 1, v = 0, q = 0, r = 1;
+    int i = 30;
+    // one step of the loop; once a lane has done its 30 divsteps (i == 0) further steps are no-ops
+    // (zeros 0, no swap, mask 0), so the exit test (a VALU compare feeding a scalar branch, which stalls
+    // a lone wave) runs once per U steps
+    auto step = [&]() {
+        const int zeros = __builtin_ctz(g | (0xffffffffu << i));
+        g >>= zeros;
+        u <<= zeros;
+        v <<= zeros;
+        eta -= zeros;
+        i -= zeros;
+        const bool live = i != 0;
+        const bool sw = live && eta < 0;  // (f, g, u, v, q, r) <- (g, -f, q, r, -u, -v), eta <- -eta
+        const uint32_t nf = 0u - f, nu = 0u - u, nv = 0u - v;
+        eta = sw ? -eta : eta;
+        f = sw ? g : f;
+        g = sw ? nf : g;
+        u = sw ? q : u;
+        q = sw ? nu : q;
+        v = sw ? r : v;
+        r = sw ? nv : r;
+        const int limit = (eta + 1) < i ? (eta + 1) : i;  // >= 1 on a live lane (eta >= 0 here)
+        const uint32_t m = !live ? 0u : limit >= 8 ? 255u : (1u << limit) - 1u;
+        uint32_t x = ((f << 1) + f) ^ 2u;  // f^-1 mod 2^5
+        x *= 2u - f * x;                   // mod 2^10
+        const uint32_t w = (g * (0u - x)) & m;
+        g += f * w;
+        q += u * w;
+        r += v * w;
+    };
+#pragma unroll 1
+    for (;;) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) step();
+        // the zeros after the last elimination (a finished lane's i is 0 already)
+        const int zeros = __builtin_ctz(g | (0xffffffffu << i));
+        g >>= zeros;
+        u <<= zeros;
+        v <<= zeros;
+        eta -= zeros;
+        i -= zeros;
+        if (__builtin_amdgcn_ballot_w64(i != 0) == 0) break;
+    }
+    t[0] = static_cast<int32_t>(u);
+    t[1] = static_cast<int32_t>(v);
+    t[2] = static_cast<int32_t>(q);
+    t[3] = static_cast<int32_t>(r);
+    return eta;
+}
+
 // (f, g) <- t (f, g) / 2^30 (exact)
 __device__ __forceinline__ void update_fg_30(S30& f, S30& g, const int32_t t[4]) {
     const int64_t u = t[0], v = t[1], q = t[2], r = t[3];
@@ -215,6 +277,38 @@ __device__ __forceinline__ void modinv_safegcd_pipe(fe& r, const fe& x, const Mo
     s30_to_fe(r, d);
 }
 
+// r = x^-1 mod m with divsteps_30_var, the (d, e) update pipelined as modinv_safegcd_pipe; up to 25
+// batches (the delta = 1 bound), ending once g == 0 in every lane.
+template <int U = 3>
+__device__ __forceinline__ void modinv_safegcd_var(fe& r, const fe& x, const ModInfo30& mi) {
+    S30 d, e, f, g;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        d.v[i] = 0;
+        e.v[i] = 0;
+        f.v[i] = mi.m[i];
+    }
+    e.v[0] = 1;
+    fe_to_s30(g, x);
+    int32_t t[4];
+    int32_t eta = divsteps_30_var<U>(-1, static_cast<uint32_t>(f.v[0]), static_cast<uint32_t>(g.v[0]), t);
+    update_fg_30(f, g, t);
+#pragma unroll 1
+    for (int it = 1; it < 25; ++it) {
+        int32_t gz = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) gz |= g.v[i];
+        if (__builtin_amdgcn_ballot_w64(gz != 0) == 0) break;
+        int32_t tp[4] = {t[0], t[1], t[2], t[3]};
+        eta = divsteps_30_var<U>(eta, static_cast<uint32_t>(f.v[0]), static_cast<uint32_t>(g.v[0]), t);
+        update_de_30(d, e, tp, mi);
+        update_fg_30(f, g, t);
+    }
+    update_de_30(d, e, t, mi);
+    normalize_30(d, f.v[8], mi);
+    s30_to_fe(r, d);
+}
+
 // Field inversion used by the kernels (plain or Montgomery form in, same form out).
 // For Montgomery fields: safegcd of a*R gives a^-1 R^-1; multiplying by R^3 (Montgomery) gives a^-1 R.
 __device__ __constant__ static const uint32_t kR3P2[8] = {0x00000016u, 0x00000012u, 0xfffffff8u, 0x0000000eu,
@@ -240,11 +334,19 @@ struct FieldInv<FieldK1> {
         FieldK1::normalize(t);
         modinv_safegcd_pipe(r, t, kMod30K1P);
     }
+    __device__ static __forceinline__ void inv_var(fe& r, const fe& a) {
+        fe t;
+        fe_copy(t, a);
+        FieldK1::normalize(t);
+        modinv_safegcd_var(r, t, kMod30K1P);
+    }
 };
-template <class P, bool PIPE = false>
+// PIPE: 0 plain, 1 pipelined, 2 variable time
+template <class P, int PIPE = 0>
 __device__ __forceinline__ void mont_inv_safegcd(fe& r, const fe& a, const ModInfo30& mi, const uint32_t* r3) {
     fe t, k;
-    if constexpr (PIPE) modinv_safegcd_pipe(t, a, mi);
+    if constexpr (PIPE == 2) modinv_safegcd_var(t, a, mi);
+    else if constexpr (PIPE == 1) modinv_safegcd_pipe(t, a, mi);
     else modinv_safegcd(t, a, mi);
     fe_set(k, r3);
     Mont<P>::mul(r, t, k);
@@ -257,7 +359,10 @@ template <>
 struct FieldInv<FieldN1> {
     __device__ static __forceinline__ void inv(fe& r, const fe& a) { mont_inv_safegcd<ParamN1>(r, a, kMod30N1, kR3N1); }
     __device__ static __forceinline__ void inv_pipe(fe& r, const fe& a) {
-        mont_inv_safegcd<ParamN1, true>(r, a, kMod30N1, kR3N1);
+        mont_inv_safegcd<ParamN1, 1>(r, a, kMod30N1, kR3N1);
+    }
+    __device__ static __forceinline__ void inv_var(fe& r, const fe& a) {
+        mont_inv_safegcd<ParamN1, 2>(r, a, kMod30N1, kR3N1);
     }
 };
 template <>

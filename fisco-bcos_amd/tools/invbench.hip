@@ -58,6 +58,28 @@ __global__ void parts_kernel(const fe* in, uint64_t* cyc, int32_t* sink) {
     sink[threadIdx.x] = s;
 }
 
+// the variable-time inversion (modinv_safegcd_var), one timed region per launch: mode 0 per-lane inputs
+// (the wave runs its slowest lane), 1 one value in every lane, 2 that value made uniform (readfirstlane:
+// the compiler may keep it in SGPRs); mode 3 the pipelined constant-time loop on one value in every lane
+template <int U>
+__global__ void var_kernel(const fe* in, fe* out, int which_mod, int mode, uint64_t* cyc) {
+    const ModInfo30& mi = which_mod ? kMod30N1 : kMod30K1P;
+    fe x = in[mode == 0 ? threadIdx.x : 0];
+    if (mode == 2) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x.v[k] = __builtin_amdgcn_readfirstlane(x.v[k]);
+    }
+    fe a;
+    __syncthreads();
+    const uint64_t t0 = clock64();
+    if (mode == 3) modinv_safegcd_pipe(a, x, mi);
+    else modinv_safegcd_var<U>(a, x, mi);
+    out[threadIdx.x] = a;
+    __syncthreads();
+    const uint64_t t1 = clock64();
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
 int main() {
     std::vector<fe> x(64);
     uint64_t s = 0x9E3779B97F4A7C15ull;
@@ -87,6 +109,36 @@ int main() {
         for (int i = 0; i < 64; ++i)
             for (int k = 0; k < 8; ++k) bad += a[i].v[k] != b[i].v[k];
     }
+    // the variable-time loop at four unroll depths: each lane's result against the constant-time one;
+    // cycles [mod][unroll][mode]
+    fe* dv;
+    (void)hipMalloc(&dv, 64 * sizeof(fe));
+    uint64_t cv[2][4][4];
+    for (int m = 0; m < 2; ++m) {
+        hipLaunchKernelGGL(inv_kernel, dim3(1), dim3(64), 0, 0, dx, da, db, m, dc);
+        std::vector<fe> a(64), v(64);
+        (void)hipMemcpy(a.data(), da, 64 * sizeof(fe), hipMemcpyDeviceToHost);
+        for (int uu = 0; uu < 4; ++uu)
+            for (int mode = 0; mode < 4; ++mode) {
+                for (int rep = 0; rep < 2; ++rep) {
+                    if (uu == 0) hipLaunchKernelGGL(var_kernel<2>, dim3(1), dim3(64), 0, 0, dx, dv, m, mode, dc);
+                    else if (uu == 1) hipLaunchKernelGGL(var_kernel<3>, dim3(1), dim3(64), 0, 0, dx, dv, m, mode, dc);
+                    else if (uu == 2) hipLaunchKernelGGL(var_kernel<4>, dim3(1), dim3(64), 0, 0, dx, dv, m, mode, dc);
+                    else hipLaunchKernelGGL(var_kernel<6>, dim3(1), dim3(64), 0, 0, dx, dv, m, mode, dc);
+                    (void)hipMemcpy(&cv[m][uu][mode], dc, 8, hipMemcpyDeviceToHost);
+                }
+                (void)hipMemcpy(v.data(), dv, 64 * sizeof(fe), hipMemcpyDeviceToHost);
+                for (int i = 0; i < 64; ++i)
+                    for (int k = 0; k < 8; ++k) bad += v[i].v[k] != a[mode == 0 ? i : 0].v[k];
+            }
+    }
+    printf("{\"var_mismatched_words\": %d, \"cycles[mod p, n][unroll 2, 3, 4, 6][lanes, same, uniform, const_pipe_same]\": [",
+           bad);
+    for (int m = 0; m < 2; ++m)
+        for (int uu = 0; uu < 4; ++uu)
+            printf("%s[%llu, %llu, %llu, %llu]", (m | uu) ? ", " : "", (unsigned long long)cv[m][uu][0],
+                   (unsigned long long)cv[m][uu][1], (unsigned long long)cv[m][uu][2], (unsigned long long)cv[m][uu][3]);
+    printf("]}\n");
     uint64_t p[3];
     hipLaunchKernelGGL(parts_kernel, dim3(1), dim3(64), 0, 0, dx, dc, dk);
     (void)hipMemcpy(p, dc, 24, hipMemcpyDeviceToHost);

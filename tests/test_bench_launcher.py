@@ -62,9 +62,8 @@ def test_small_batch_choice_mirrors_library():
     exec(bsrc[bsrc.index("ROW_LAT, ROW_LAT_N ="):bsrc.index("def _kernel_name")], ns)
     pick = ns["_auto_kernel"]
     names = {3: "row", 2: "trio", 1: "pair", 0: "occ1", -2: "occ2"}
-    # round 5's sweeps add the row kernels (secp256k1 1 .. 2,048 signatures; SM2 1 .. 1,024)
-    for fname, row_ok in (("r04_small_sweep.json", False), ("r05_small_sweep_row.json", True),
-                          ("r05_small_sweep_row_sm2.json", True)):
+    # round 5's sweep adds the row kernels (1 .. 2,048 signatures, both suites)
+    for fname, row_ok in (("r04_small_sweep.json", False), ("r05_small_sweep_row.json", True)):
         path = os.path.join(ROOT, "profiles", fname)
         if not os.path.exists(path):
             continue
