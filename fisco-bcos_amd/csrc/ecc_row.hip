@@ -37,6 +37,7 @@ struct RowLds {
     uint32_t rflag;             // wave 3: R on the curve (bit 1)
     uint32_t post[4];           // 0: e, 1: k / u1, 2: table of R', 3: table of 2^64 R'
     alignas(8) uint32_t msg[16];  // wave 0: the 64-byte public key for the cooperative address Keccak
+    InvQueue invq;                // phase D: Z^-1 split over waves 0 (divsteps, f, g) and 1 (d, e)
 };
 
 __device__ __forceinline__ void row_post(uint32_t* f) {
@@ -53,6 +54,64 @@ __device__ __forceinline__ void get8(fe& a, const uint32_t* d) {
     for (int q = 0; q < 8; ++q) a.v[q] = d[q];
 }
 __device__ __forceinline__ uint32_t sgpr(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// modinv_var_split_fg with (f, g) spread over the rows: lane k < 9 of every row holds limb k (signed
+// 30-bit form, lanes 9..15 zero), so a batch's (f, g) <- t (f, g) / 2^30 is two lane-parallel rounds
+// instead of nine serial limbs: (1) each lane forms u f_k + v g_k (|.| < 2^60.01), keeps bits 0..29 for
+// the lane below and bits 30.. (|.| < 2^30.01) itself -- the exact division by 2^30 is the shift down
+// by one lane; (2) the sums (< 2^31.01) split once more, their carries (|.| <= 2) one lane up, the top
+// lane keeping its whole signed value.  Limbs stay in [-2, 2^30 + 2) below the top, so the next
+// products stay < 2^61.  f0, g0 for the divsteps are limb 0 + 2^30 limb 1 (mod 2^32); g == 0 is tested
+// as all limbs zero (a redundant zero only costs further batches, which are exact no-ops), and f's sign
+// at the end (f = +-1) from its low word.
+__device__ __forceinline__ int32_t inv_fg_rows(const fe& x, const ModInfo30& mi, InvQueue& q, int lane) {
+    const int k = lane & 15;
+    const uint32_t in9 = frow::mask_if(k < 9), below8 = frow::mask_if(k < 8), top = frow::mask_if(k == 8);
+    S30 gs;
+    fe_to_s30(gs, x);
+    int32_t f = 0, g = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {  // lane k takes limb k (constant indices: no scratch)
+        f = k == i ? mi.m[i] : f;
+        g = k == i ? gs.v[i] : g;
+    }
+    f = static_cast<int32_t>(static_cast<uint32_t>(f) & in9);
+    g = static_cast<int32_t>(static_cast<uint32_t>(g) & in9);
+    auto low32 = [](int32_t a) {  // limb 0 + 2^30 limb 1 (mod 2^32), uniform
+        const uint32_t a0 = __builtin_amdgcn_readlane(static_cast<uint32_t>(a), 0);
+        const uint32_t a1 = __builtin_amdgcn_readlane(static_cast<uint32_t>(a), 1);
+        return a0 + (a1 << 30);
+    };
+    auto apply = [&](int32_t a, int32_t b, int32_t m1, int32_t m2) {  // (m1 a + m2 b) / 2^30 over the row
+        const int64_t c = static_cast<int64_t>(m1) * a + static_cast<int64_t>(m2) * b;
+        const uint32_t lo = static_cast<uint32_t>(c) & 0x3fffffffu;
+        const int32_t hi = static_cast<int32_t>(c >> 30);
+        const int64_t n = static_cast<int64_t>(hi) + frow::shl<1>(lo);  // lane k: bits 30.. of k, 0..29 of k + 1
+        const uint32_t lo2 = static_cast<uint32_t>(n) & 0x3fffffffu;
+        const uint32_t c2 = static_cast<uint32_t>(static_cast<int32_t>(n >> 30)) & below8;
+        const uint32_t keep = frow::bsel(top, static_cast<uint32_t>(n), lo2);
+        return static_cast<int32_t>(keep + frow::shr<1>(c2));
+    };
+    int32_t eta = -1;
+#pragma unroll 1
+    for (int it = 0; it < 25; ++it) {
+        int32_t t[4];
+        eta = divsteps_30_var(eta, low32(f), low32(g), t);
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q.t[it][j] = t[j];
+            __hip_atomic_store(&q.n, static_cast<uint32_t>(it + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        const int32_t u = __builtin_amdgcn_readfirstlane(t[0]), v = __builtin_amdgcn_readfirstlane(t[1]);
+        const int32_t qq = __builtin_amdgcn_readfirstlane(t[2]), r = __builtin_amdgcn_readfirstlane(t[3]);
+        const int32_t fn = apply(f, g, u, v), gn = apply(f, g, qq, r);
+        f = fn;
+        g = gn;
+        if (__builtin_amdgcn_ballot_w64(g != 0) == 0) break;
+    }
+    if (lane == 0) __hip_atomic_store(&q.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return low32(f) == 1u ? 0 : -1;  // f = +-1
+}
 
 }  // namespace
 
@@ -84,6 +143,7 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
     const uint64_t i = blockIdx.x;  // one signature per workgroup (the grid is n)
     ROW_T(0);
     if (threadIdx.x < 4) S.post[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) invq_reset(S.invq);
     __syncthreads();
     fe r, s, kx, ky;
     uint32_t v = 0;
@@ -320,8 +380,11 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         } else {
         fe z, zi, ax, ay;
         fe26_to_fe(z, Rq.Z);
+        FieldK1::normalize(z);
         ROW_T(4);
-        FieldInv<FieldK1>::inv_var(zi, z);
+        // Z^-1: divsteps and (f, g) over the rows here, the (d, e) updates on wave 1 (modinv_var_split_de)
+        const int32_t fsign = inv_fg_rows(z, kMod30K1P, S.invq, lane);
+        modinv_var_split_finish(zi, fsign, kMod30K1P, S.invq);
         ROW_T(5);
         fe26 zi26, zi2, zi3, AX, AY;
         fe26_from_fe(zi26, zi);
@@ -357,6 +420,8 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
         }
         if (lane == 0) io.finish(i, ok2, ad, &ax, &ay);
         }
+    } else if (!kVer && wave == 1) {  // the (d, e) half of wave 0's Z^-1
+        modinv_var_split_de(kMod30K1P, S.invq, lane);
     }
     ROW_T(3);
 }

@@ -113,11 +113,15 @@ __device__ __forceinline__ int32_t divsteps_30_var(int32_t eta, uint32_t f, uint
         q = sw ? nu : q;
         v = sw ? r : v;
         r = sw ? nv : r;
-        const int limit = (eta + 1) < i ? (eta + 1) : i;  // >= 1 on a live lane (eta >= 0 here)
-        const uint32_t m = !live ? 0u : limit >= 8 ? 255u : (1u << limit) - 1u;
-        uint32_t x = ((f << 1) + f) ^ 2u;  // f^-1 mod 2^5
-        x *= 2u - f * x;                   // mod 2^10
-        const uint32_t w = (g * (0u - x)) & m;
+        // limit = min(eta + 1, i) >= 1 on a live lane (eta >= 0 here), 0 on a finished one (i == 0):
+        // one v_med3 clamp, the mask of its low bits one v_bfm, capped at 8 bits
+        const int lim = (eta + 1) < i ? (eta + 1) : i;
+        const uint32_t m = ((1u << (lim < 0 ? 0 : lim)) - 1u) & 255u;
+        // f^-1 mod 2^10 by Newton from the 5-bit seed (3 f) ^ 2, and w = -g / f mod 2^8: only low bits
+        // matter, so 24-bit multiplies (full rate) suffice
+        uint32_t x = ((f << 1) + f) ^ 2u;
+        x = (x & 0xffffffu) * ((2u - (f & 0xffffffu) * (x & 0xffffffu)) & 0xffffffu);
+        const uint32_t w = ((g & 0xffffffu) * ((0u - x) & 0xffffffu)) & m;
         g += f * w;
         q += u * w;
         r += v * w;
@@ -306,6 +310,90 @@ __device__ __forceinline__ void modinv_safegcd_var(fe& r, const fe& x, const Mod
     }
     update_de_30(d, e, t, mi);
     normalize_30(d, f.v[8], mi);
+    s30_to_fe(r, d);
+}
+
+// modinv_safegcd_var split over two waves of a workgroup, for a value every lane of the producing wave
+// holds (the row kernel's Z^-1): the producer runs the divsteps and the (f, g) updates -- the serial
+// part -- and posts each batch's matrix to an LDS queue; a second wave applies the (d, e) updates from
+// the queue meanwhile (in the one-wave loop they could no longer hide beside the divsteps, whose loop
+// ends in a branch), and the producer takes d back at the end.  Same result as modinv_safegcd.
+struct InvQueue {
+    int32_t t[25][4];
+    int32_t d[9];
+    uint32_t n, done, ready;  // batches posted, all posted, d written (zero before the producer starts)
+};
+__device__ __forceinline__ void invq_reset(InvQueue& q) {
+    q.n = 0u;
+    q.done = 0u;
+    q.ready = 0u;
+}
+// producer: returns f's top limb (its sign gives the result's) for modinv_var_split_finish
+__device__ __forceinline__ int32_t modinv_var_split_fg(const fe& x, const ModInfo30& mi, InvQueue& q, int lane) {
+    S30 f, g;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) f.v[i] = mi.m[i];
+    fe_to_s30(g, x);
+    int32_t eta = -1;
+#pragma unroll 1
+    for (int it = 0; it < 25; ++it) {
+        int32_t t[4];
+        eta = divsteps_30_var(eta, static_cast<uint32_t>(f.v[0]), static_cast<uint32_t>(g.v[0]), t);
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q.t[it][k] = t[k];
+            __hip_atomic_store(&q.n, static_cast<uint32_t>(it + 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        update_fg_30(f, g, t);
+        int32_t gz = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) gz |= g.v[i];
+        if (__builtin_amdgcn_ballot_w64(gz != 0) == 0) break;
+    }
+    if (lane == 0) __hip_atomic_store(&q.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return f.v[8];
+}
+// consumer (the other wave): every posted batch's (d, e) update, then d to the queue
+__device__ __forceinline__ void modinv_var_split_de(const ModInfo30& mi, InvQueue& q, int lane) {
+    S30 d, e;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        d.v[i] = 0;
+        e.v[i] = 0;
+    }
+    e.v[0] = 1;
+#pragma unroll 1
+    for (uint32_t b = 0; b < 25u; ++b) {
+        uint32_t n;
+        for (;;) {
+            n = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&q.n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (n > b) break;
+            if (__builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(&q.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0u) {
+                n = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&q.n, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (n <= b) break;  // all posted batches applied
+        int32_t t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = q.t[b][k];
+        update_de_30(d, e, t, mi);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) q.d[i] = d.v[i];
+        __hip_atomic_store(&q.ready, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+__device__ __forceinline__ void modinv_var_split_finish(fe& r, int32_t fsign, const ModInfo30& mi, InvQueue& q) {
+    while (__hip_atomic_load(&q.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        __builtin_amdgcn_s_sleep(1);
+    S30 d;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d.v[i] = q.d[i];
+    normalize_30(d, fsign, mi);
     s30_to_fe(r, d);
 }
 
