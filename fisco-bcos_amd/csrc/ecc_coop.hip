@@ -1424,7 +1424,11 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             COOP_T(4);
             fe z, zi;
             fe26_to_fe(z, acc.Zs);
+#if BCOSGPU_TRIO_INV_VAR  // A/B: the variable-time loop (every lane its own Z: the wave runs its slowest)
+            FieldInv<FieldK1>::inv_var(zi, z);
+#else
             FieldInv<FieldK1>::inv_pipe(zi, z);
+#endif
             COOP_T(5);
             fe26 zi26, zi2, zi3, X, Y;  // lane 2 holds X (Xs), Y (S1), Z
             fe26_from_fe(zi26, zi);

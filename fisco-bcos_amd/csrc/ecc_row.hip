@@ -430,9 +430,10 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
 // SM2Crypto::verify / recover with the key (SM2Crypto.cpp:66-92, sm2_do_verify: fast_sm2.cpp:139-227)
 // for the smallest batches: Q = s G + t P (t = r + s mod n), accept iff x(Q) = r - e (mod n), e =
 // SM3(Z_A || hash).  SM2 has no endomorphism, so t P is ONE chain of 64 radix-16 windows (doublings of
-// 4 product levels for a = -3: 19 levels a window) on wave 0; wave 1 builds the key's table (its
-// on-curve check on the rows) while wave 0 hashes Z_A and e, waves 2 and 3 each take half of the s G
-// comb windows (the comb entries are FieldP2 Montgomery words: one row product by R^-1 each).  The
+// 3 product levels for a = -3 with Z^2 carried: 15 levels a window) on wave 0, which starts it as soon
+// as wave 1 has built the key's table (its on-curve check on the rows); wave 3 hashes Z_A and e, wave 2
+// the key's address, and then each takes half of the s G comb windows (the comb entries are FieldP2
+// Montgomery words: one row product by R^-1 each).  The
 // x-check is projective (X == c Z^2), so there is no inversion.  Outputs bit-identical to every other
 // SM2 verification kernel (tests/test_gpu_row.py, the kernel-variant tests).
 __device__ __constant__ static const uint32_t kSm2RowRinv[16] = {0x4u, 0x3fffe40u, 0x6fffu, 0x3f40000u, 0x2ffffffu,
@@ -479,33 +480,10 @@ __global__ __launch_bounds__(256, 1) void sm2_verify_row_kernel(IO io, uint64_t 
     const bool ok = sgpr(okp ? 1u : 0u) != 0u;
     const uint32_t rinv = kSm2RowRinv[L.k];
     // ---------------------------------------------------------------- phase A
-    if (wave == 0) {  // e, c = r - e (mod n), the address of the key
-        fe h, e, c, c2;
-        io.template digest<SM3>(i, h);
-        uint32_t eb[8];
-        sm2_e(eb, X, Y, h);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) e.v[q] = eb[7 - q];
-        reduce_once(e, ParamN2::M);
-        FieldN2::sub(c, r, e);
-        const uint32_t carry = fe_add_k(c2, c, ParamN2::M);
-        const bool second = carry == 0u && fe_lt_k(c2, ParamP2::M);
-        put8(S.c[0], c, lane);
-        put8(S.c[1], c2, lane);
-        uint32_t ad[5] = {0, 0, 0, 0, 0};
-        if (io.want_addr()) sm3_address(ad, px, py);
-        if (lane < 5) {
-            uint32_t a = 0;
-#pragma unroll
-            for (int q = 0; q < 5; ++q) a = lane == q ? ad[q] : a;
-            S.ad[lane] = a;
-        }
-        if (lane == 0) {
-            S.cflag = second ? 1u : 0u;
-            S.kflag = ok ? 1u : 0u;
-        }
-        row_post(&S.post[1]);
-    } else if (wave == 1) {  // the key on the rows, its curve check and its table
+    // wave 0 only waits for the key's table (wave 1) and then runs the chain: the hashing the final
+    // x-check needs -- e = SM3(Z_A || hash), c = r - e -- runs on wave 3 and the key's address on wave 2,
+    // each before its half of the s G comb
+    if (wave == 1) {  // the key on the rows, its curve check and its table
         fe26 X26, Y26;
         fe26_from_words(X26, px.v);
         fe26_from_words(Y26, py.v);
@@ -526,7 +504,35 @@ __global__ __launch_bounds__(256, 1) void sm2_verify_row_kernel(IO io, uint64_t 
         if (lane == 0) S.rflag = on ? 2u : 0u;
         frow::build_table<frow::FSM2, false>(S.tab, S.zc, frow::Pt{Xr, Yr, L.one}, 0u, f);
         row_post(&S.post[0]);
-    } else {  // waves 2, 3: s G over half of the comb windows each (no P = +-Q inside a half)
+    } else if (wave >= 2) {  // waves 2, 3: the hashing, then s G over half of the comb windows each (no
+                             // P = +-Q inside a half)
+        if (wave == 3) {  // e, c = r - e (mod n)
+            fe h, e, c, c2;
+            io.template digest<SM3>(i, h);
+            uint32_t eb[8];
+            sm2_e(eb, X, Y, h);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) e.v[q] = eb[7 - q];
+            reduce_once(e, ParamN2::M);
+            FieldN2::sub(c, r, e);
+            const uint32_t carry = fe_add_k(c2, c, ParamN2::M);
+            const bool second = carry == 0u && fe_lt_k(c2, ParamP2::M);
+            put8(S.c[0], c, lane);
+            put8(S.c[1], c2, lane);
+            if (lane == 0) {
+                S.cflag = second ? 1u : 0u;
+                S.kflag = ok ? 1u : 0u;
+            }
+        } else {  // the address of the key
+            uint32_t ad[5] = {0, 0, 0, 0, 0};
+            if (io.want_addr()) sm3_address(ad, px, py);
+            if (lane < 5) {
+                uint32_t a = 0;
+#pragma unroll
+                for (int q = 0; q < 5; ++q) a = lane == q ? ad[q] : a;
+                S.ad[lane] = a;
+            }
+        }
         const int W = tab_bits == kWideBits ? 256 / kWideBits : 32, bits = tab_bits == kWideBits ? kWideBits : 8;
         const int lo = (wave - 2) * (W / 2), hi = lo + W / 2;
         frow::Pt g{0u, 0u, 0u};
