@@ -133,8 +133,9 @@ def kernel_source_sha():
     return h.hexdigest()[:16]
 
 
-ROW_LAT, ROW_LAT_N = 0.38, 0.20  # ecc_txv.hip kRowLat, kRowLatN
-ROW_LAT_SM2, ROW_LAT_N_SM2 = 0.53, 0.48  # kRowLatSM2, kRowLatNSM2 (rounds of 2 per CU)
+ROW_LAT, ROW_LAT_N = 0.38, 0.18  # ecc_txv.hip kRowLat, kRowLatN
+ROW_LAT_SM2, ROW_LAT_N_SM2 = 0.53, 0.55  # kRowLatSM2, kRowLatNSM2
+ROW_PER_CU_SM2 = 3  # kRowPerCuSM2
 
 
 def _auto_kernel(suite, n, cus, small_ok=True, row_ok=True):
@@ -154,7 +155,7 @@ def _auto_kernel(suite, n, cus, small_ok=True, row_ok=True):
         if c < cost:
             best, cost = code[k], c
     r1, rn = (ROW_LAT_SM2, ROW_LAT_N_SM2) if suite == 1 else (ROW_LAT, ROW_LAT_N)
-    per_round = (2 if suite == 1 else 1) * cus
+    per_round = (ROW_PER_CU_SM2 if suite == 1 else 1) * cus
     if row_ok and small_ok and r1 + (-(-n // per_round) - 1) * rn < cost:
         best = 3
     return best

@@ -61,14 +61,16 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
 // 2^16 txs (beyond that the one-lane kernel's throughput wins at any rounding).  secp256k1 recovery also
 // has the row kernel (ecc_row.hip, one signature per workgroup): its first round of one signature per
 // CU costs kRowLat of the trio's round and each further round kRowLatN (two workgroups share a CU:
-// tools/small_sweep.py, profiles/r05_small_sweep_row.json: 0.133 / 0.156 / 0.225 / 0.302 / 0.375 ms at
-// 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.377); SM2 its own row kernel, whose
-// latency is its one-wave chain's, so two workgroups per CU overlap whole: its rounds hold 2 signatures
-// per CU, at kRowLatSM2 / kRowLatNSM2 of the SM2 trio's round (same file: 0.275 / 0.304 / 0.306 /
-// 0.572 / 0.583 ms at 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.577).
+// tools/small_sweep.py, profiles/r05_small_sweep_row.json: 0.127 / 0.153 / 0.211 / 0.280 / 0.347 ms at
+// 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.378); SM2 its own row kernel, whose
+// latency is its one-wave chain's, so the workgroups resident on a CU (three) overlap whole: its rounds
+// hold kRowPerCuSM2 signatures per CU, at kRowLatSM2 / kRowLatNSM2 of the SM2 trio's round (same file:
+// 0.258 / 0.288 / 0.294 / 0.321 / 0.566 ms at 1 / 256 / 512 / 768 / 1024 signatures against the trio's
+// 0.577).
 // Returns 3 (row), 2 (trio), 1 (pair), 0 (one-lane, occupancy 1) or -2 (one-lane, occupancy 2).
-static constexpr double kRowLat = 0.38, kRowLatN = 0.20;
-static constexpr double kRowLatSM2 = 0.53, kRowLatNSM2 = 0.48;
+static constexpr double kRowLat = 0.38, kRowLatN = 0.18;
+static constexpr double kRowLatSM2 = 0.53, kRowLatNSM2 = 0.55;
+static constexpr uint64_t kRowPerCuSM2 = 3;
 static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_ok) {
     const bool sm2 = suite == BCOSGPU_SUITE_SM2;
     //                    occ 2,              occ 1,              pair,               trio
@@ -91,7 +93,7 @@ static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_o
     }
     if (row_ok && small_ok) {
         const double r1 = sm2 ? kRowLatSM2 : kRowLat, rn = sm2 ? kRowLatNSM2 : kRowLatN;
-        const uint64_t per_round = (sm2 ? 2ull : 1ull) * cus;
+        const uint64_t per_round = (sm2 ? kRowPerCuSM2 : 1ull) * cus;
         const double c = r1 + static_cast<double>((n + per_round - 1) / per_round - 1) * rn;
         if (c < cost) best = 3;
     }
