@@ -1018,7 +1018,10 @@ struct Trio26Lds {
     uint32_t ys[8][64];
     uint32_t rflag[64];
     uint32_t post[3];
+    uint32_t invq[2][4];  // phase D: Z^-1 over wave pairs (0, 1) and (2, 3): posted, consumed, d ready
 };
+// phase D's Z^-1 ring and d (two wave pairs) live in pt, which is free by then
+static_assert(2 * (kInvRing * 4 * 64 + 9 * 64) <= sizeof(Trio26Lds::pt) / 4, "Z^-1 queue exceeds pt");
 __device__ __forceinline__ void lds_store_limbs26(uint32_t (*dst)[64], const fe26& a, int lane) {
     fe26 t;
     fe26_copy(t, a);
@@ -1117,6 +1120,9 @@ enum { kRecover = 0, kVerify = 1 };
 #ifndef kTrioDblUnroll
 #define kTrioDblUnroll 3  // phase C doublings per window unrolled (rolled, 1: 0.385 vs 0.383 ms)
 #endif
+#ifndef BCOSGPU_TRIO_INV_SPLIT
+#define BCOSGPU_TRIO_INV_SPLIT 1  // phase-D Z^-1 over wave pairs (0 = the one-wave pipelined loop, A/B)
+#endif
 template <bool TRIO, int MODE, class IO>
 __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint32_t* __restrict__ tab, int tab_bits) {
     static_assert(MODE == kRecover || TRIO, "known-key verify runs on the trio kernel only");
@@ -1131,6 +1137,10 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
         L.post[0] = 0u;
         L.post[1] = 0u;
         L.post[2] = 0u;
+        if constexpr (TRIO) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) (&L.invq[0][0])[q] = 0u;
+        }
     }
     __syncthreads();
     // ---------------------------------------------------------------- phase A (as tx_verify_coop_kernel)
@@ -1424,8 +1434,16 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
             COOP_T(4);
             fe z, zi;
             fe26_to_fe(z, acc.Zs);
-#if BCOSGPU_TRIO_INV_VAR  // A/B: the variable-time loop (every lane its own Z: the wave runs its slowest)
-            FieldInv<FieldK1>::inv_var(zi, z);
+#if BCOSGPU_TRIO_INV_SPLIT
+            // Z^-1 over the wave pair: the divsteps and (f, g) here, the (d, e) updates on the chain-1
+            // partner (same txs, same lanes), through a ring in the chain points' LDS (free after the
+            // barrier above): modinv_pair_*
+            FieldK1::normalize(z);
+            int32_t* const pq = reinterpret_cast<int32_t*>(&L.pt[0][0][0]);
+            int32_t* const ring = pq + (wave >> 1) * (kInvRing * 4 * 64);
+            int32_t* const dq = pq + 2 * kInvRing * 4 * 64 + (wave >> 1) * 9 * 64;
+            const int32_t fs = modinv_pair_fg(z, kMod30K1P, ring, L.invq[wave >> 1], lane);
+            modinv_pair_finish(zi, fs, kMod30K1P, dq, L.invq[wave >> 1], lane);
 #else
             FieldInv<FieldK1>::inv_pipe(zi, z);
 #endif
@@ -1446,6 +1464,14 @@ __device__ __forceinline__ void coop26_body(const IO& io, uint64_t n, const uint
                 for (int q = 0; q < 16; ++q) mbuf[16 * tl + q] = m[q];
             }
         }
+#if BCOSGPU_TRIO_INV_SPLIT
+        else if (!kVer) {  // chain 1: the (d, e) half of the partner's Z^-1
+            const int32_t* const pq = reinterpret_cast<const int32_t*>(&L.pt[0][0][0]);
+            modinv_pair_de(kMod30K1P, pq + (wave >> 1) * (kInvRing * 4 * 64),
+                           reinterpret_cast<int32_t*>(&L.pt[0][0][0]) + 2 * kInvRing * 4 * 64 + (wave >> 1) * 9 * 64,
+                           L.invq[wave >> 1], lane);
+        }
+#endif
         __syncthreads();
         if (chain == 0 && io.want_addr()) {  // Keccak256(x || y) on lane pairs: tx j = lane / 2 of the wave
             const KeccakPair kp;

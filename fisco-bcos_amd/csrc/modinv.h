@@ -397,6 +397,89 @@ __device__ __forceinline__ void modinv_var_split_finish(fe& r, int32_t fsign, co
     s30_to_fe(r, d);
 }
 
+// modinv_safegcd split over a wave PAIR for per-lane values (the lane-trio kernel's phase-D Z^-1, one
+// value per lane): the producer wave runs the constant-time divsteps and the (f, g) updates and posts
+// each batch's matrix, per lane, to a ring of kInvRing slots in LDS; its partner wave, whose lanes hold
+// the same values' places, applies the (d, e) updates from the ring meanwhile and returns d.  The
+// producer waits only when the ring is full (the consumer's update is the shorter).  Same result as
+// modinv_safegcd.  ring: [kInvRing][4][64] words, dq: [9][64] words, ctr: 3 words zeroed beforehand
+// (batches posted, batches consumed, d ready; posted | 0x80000000 once the producer is done).
+constexpr int kInvRing = 8;
+__device__ __forceinline__ int32_t modinv_pair_fg(const fe& x, const ModInfo30& mi, int32_t* ring, uint32_t* ctr,
+                                                  int lane) {
+    S30 f, g;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) f.v[i] = mi.m[i];
+    fe_to_s30(g, x);
+    int32_t zeta = -1;
+    uint32_t it = 0;
+#pragma unroll 1
+    for (; it < 20u; ++it) {
+        int32_t t[4];
+        zeta = divsteps_30(zeta, static_cast<uint32_t>(f.v[0]), static_cast<uint32_t>(g.v[0]), t);
+        if (it >= static_cast<uint32_t>(kInvRing)) {  // the slot's previous batch must be consumed
+            while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&ctr[1], __ATOMIC_ACQUIRE,
+                                                                    __HIP_MEMORY_SCOPE_WORKGROUP)) + kInvRing <= it)
+                __builtin_amdgcn_s_sleep(1);
+        }
+        int32_t* slot = ring + (it % kInvRing) * 4 * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) slot[k * 64] = t[k];
+        if (lane == 0) __hip_atomic_store(&ctr[0], it + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        update_fg_30(f, g, t);
+        int32_t gz = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) gz |= g.v[i];
+        if (__builtin_amdgcn_ballot_w64(gz != 0) == 0) {
+            ++it;
+            break;
+        }
+    }
+    if (lane == 0) __hip_atomic_store(&ctr[0], it | 0x80000000u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return f.v[8];
+}
+__device__ __forceinline__ void modinv_pair_de(const ModInfo30& mi, const int32_t* ring, int32_t* dq, uint32_t* ctr,
+                                               int lane) {
+    S30 d, e;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        d.v[i] = 0;
+        e.v[i] = 0;
+    }
+    e.v[0] = 1;
+#pragma unroll 1
+    for (uint32_t b = 0; b < 20u; ++b) {
+        uint32_t n;
+        for (;;) {
+            n = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ctr[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if ((n & 0x7fffffffu) > b || (n & 0x80000000u) != 0u) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if ((n & 0x7fffffffu) <= b) break;  // the producer is done and every batch is applied
+        const int32_t* slot = ring + (b % kInvRing) * 4 * 64 + lane;
+        int32_t t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = slot[k * 64];
+        // the slot is free once read: the loads complete before the release store below
+        if (lane == 0) __hip_atomic_store(&ctr[1], b + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        update_de_30(d, e, t, mi);
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) dq[i * 64 + lane] = d.v[i];
+    if (lane == 0) __hip_atomic_store(&ctr[2], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void modinv_pair_finish(fe& r, int32_t fsign, const ModInfo30& mi, const int32_t* dq,
+                                                   uint32_t* ctr, int lane) {
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&ctr[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) ==
+           0u)
+        __builtin_amdgcn_s_sleep(1);
+    S30 d;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d.v[i] = dq[i * 64 + lane];
+    normalize_30(d, fsign, mi);
+    s30_to_fe(r, d);
+}
+
 // Field inversion used by the kernels (plain or Montgomery form in, same form out).
 // For Montgomery fields: safegcd of a*R gives a^-1 R^-1; multiplying by R^3 (Montgomery) gives a^-1 R.
 __device__ __constant__ static const uint32_t kR3P2[8] = {0x00000016u, 0x00000012u, 0xfffffff8u, 0x0000000eu,
