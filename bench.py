@@ -134,8 +134,8 @@ def kernel_source_sha():
 
 
 ROW_LAT, ROW_LAT_N = 0.38, 0.18  # ecc_txv.hip kRowLat, kRowLatN
-ROW_LAT_SM2, ROW_LAT_N_SM2 = 0.53, 0.55  # kRowLatSM2, kRowLatNSM2
-ROW_PER_CU_SM2 = 3  # kRowPerCuSM2
+ROW_LAT_SM2, ROW_LAT_N_SM2 = 0.43, 0.14  # kRowLatSM2, kRowLatNSM2
+ROW_RESIDENT_SM2 = 4  # kRowResidentSM2
 
 
 def _auto_kernel(suite, n, cus, small_ok=True, row_ok=True):
@@ -155,8 +155,10 @@ def _auto_kernel(suite, n, cus, small_ok=True, row_ok=True):
         if c < cost:
             best, cost = code[k], c
     r1, rn = (ROW_LAT_SM2, ROW_LAT_N_SM2) if suite == 1 else (ROW_LAT, ROW_LAT_N)
-    per_round = (ROW_PER_CU_SM2 if suite == 1 else 1) * cus
-    if row_ok and small_ok and r1 + (-(-n // per_round) - 1) * rn < cost:
+    m = -(-n // cus)
+    res = ROW_RESIDENT_SM2 if suite == 1 else m
+    rounds = -(-m // res)
+    if row_ok and small_ok and rounds * r1 + (m - rounds) * rn < cost:
         best = 3
     return best
 

@@ -429,27 +429,31 @@ __global__ __launch_bounds__(256, 1) void recover_row_kernel(IO io, uint64_t n, 
 // ------------------------------------------------------------------ SM2 verify on the rows
 // SM2Crypto::verify / recover with the key (SM2Crypto.cpp:66-92, sm2_do_verify: fast_sm2.cpp:139-227)
 // for the smallest batches: Q = s G + t P (t = r + s mod n), accept iff x(Q) = r - e (mod n), e =
-// SM3(Z_A || hash).  SM2 has no endomorphism, so t P is ONE chain of 64 radix-16 windows (doublings of
-// 3 product levels for a = -3 with Z^2 carried: 15 levels a window) on wave 0, which starts it as soon
-// as wave 1 has built the key's table (its on-curve check on the rows); wave 3 hashes Z_A and e, wave 2
-// the key's address, and then each takes half of the s G comb windows (the comb entries are FieldP2
-// Montgomery words: one row product by R^-1 each).  The
+// SM3(Z_A || hash).  SM2 has no endomorphism, so t P is split by bit position, t = t_lo + 2^212 t_hi:
+// wave 0 builds the key's table and runs t_lo's 53 radix-16 windows (doublings of 3 product levels for
+// a = -3 with Z^2 carried: 15 levels a window), while wave 1 doubles the key 212 times, builds that
+// point's table and runs t_hi's 11 windows -- about 830 levels each against 995 for one 256-bit chain;
+// both check the key on the curve on the rows.  Wave 3 hashes Z_A and e, wave 2 the key's address, and
+// then each takes half of the s G comb windows (the comb entries are FieldP2 Montgomery words: one row
+// product by R^-1 each); wave 0 adds the three points with complete additions.  The
 // x-check is projective (X == c Z^2), so there is no inversion.  Outputs bit-identical to every other
 // SM2 verification kernel (tests/test_gpu_row.py, the kernel-variant tests).
 __device__ __constant__ static const uint32_t kSm2RowRinv[16] = {0x4u, 0x3fffe40u, 0x6fffu, 0x3f40000u, 0x2ffffffu,
                                                                  0x0u, 0x3ffffc0u, 0x17ffu, 0x3fb0000u, 0x3fffffu,
                                                                  0x0u, 0x0u, 0x0u, 0x0u, 0x0u, 0x0u};
+// t = t_lo + 2^kSm2RowSplit t_hi (the SM2 row kernel's two chains, see there)
+constexpr int kSm2RowSplit = 212;
 namespace {
 struct Sm2RowLds {
-    uint32_t tab[8][3][16];  // the key's table: x, y (row limbs, magnitude 1; slot 2 unused)
-    uint32_t zc[16];
-    uint32_t pt[3][3][16];   // the chain's point, the two comb halves
-    uint32_t pinf[3];
+    uint32_t tab[2][8][3][16];  // the tables of P and of 2^kSm2RowSplit P: x, y (row limbs, magnitude 1)
+    uint32_t zc[2][16];
+    uint32_t pt[4][3][16];      // the low chain's point, the two comb halves, the high chain's point
+    uint32_t pinf[4];
     uint32_t slot[4][16];
     uint32_t c[2][8];        // c = (r - e) mod n and c + n (canonical words)
     uint32_t cflag, kflag, rflag;
     uint32_t ad[5];
-    uint32_t post[3];        // 0: table, 1: scalars, 2: comb half of wave 3
+    uint32_t post[3];        // 2: comb half of wave 3
 };
 }  // namespace
 
@@ -483,7 +487,7 @@ __global__ __launch_bounds__(256, 1) void sm2_verify_row_kernel(IO io, uint64_t 
     // wave 0 only waits for the key's table (wave 1) and then runs the chain: the hashing the final
     // x-check needs -- e = SM3(Z_A || hash), c = r - e -- runs on wave 3 and the key's address on wave 2,
     // each before its half of the s G comb
-    if (wave == 1) {  // the key on the rows, its curve check and its table
+    if (wave <= 1) {  // the key on the rows and its curve check, on both waves; then the two chains
         fe26 X26, Y26;
         fe26_from_words(X26, px.v);
         fe26_from_words(Y26, py.v);
@@ -501,9 +505,36 @@ __global__ __launch_bounds__(256, 1) void sm2_verify_row_kernel(IO io, uint64_t 
             Xr = gx;
             Yr = gy;
         }
-        if (lane == 0) S.rflag = on ? 2u : 0u;
-        frow::build_table<frow::FSM2, false>(S.tab, S.zc, frow::Pt{Xr, Yr, L.one}, 0u, f);
-        row_post(&S.post[0]);
+        if (wave == 1 && lane == 0) S.rflag = on ? 2u : 0u;
+        // t = t_lo + 2^kSm2RowSplit t_hi: wave 0 runs t_lo over the table of P, wave 1 first doubles P
+        // kSm2RowSplit times (3 levels each) and runs t_hi over the table of that point; the split
+        // balances the two (3 levels a doubled bit against 3.75 a chain bit)
+        fe tt, k;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tt.v[q] = sgpr(ok ? t.v[q] : (q == 0 ? 1u : 0u));
+        fe_zero(k);
+        constexpr int kw = kSm2RowSplit / 32, kb = kSm2RowSplit % 32;
+        static_assert(kw == 6 && kb > 0, "t_hi below takes the bits of words 6 and 7");
+        frow::Pt P{Xr, Yr, L.one};
+        if (wave == 0) {
+#pragma unroll
+            for (int q = 0; q < kw; ++q) k.v[q] = tt.v[q];
+            k.v[kw] = tt.v[kw] & ((1u << kb) - 1u);
+        } else {
+            k.v[0] = (tt.v[6] >> kb) | (tt.v[7] << (32 - kb));
+            k.v[1] = tt.v[7] >> kb;
+            uint32_t zz = L.one;
+#pragma unroll 1
+            for (int q = 0; q < kSm2RowSplit; ++q) frow::dbl_m3z(P, zz, f);
+        }
+        frow::build_table<frow::FSM2, false>(S.tab[wave], S.zc[wave], P, 0u, f);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        frow::Pt acc{0u, 0u, 0u};
+        const bool fin = frow::sm2_chain(acc, k, &S.tab[wave][0][0][0], S.zc[wave][L.k], slot, f);
+        frow::pt_store(S.pt[wave == 0 ? 0 : 3], acc, L);
+        if (lane == 0) S.pinf[wave == 0 ? 0 : 3] = fin ? 0u : 1u;
     } else if (wave >= 2) {  // waves 2, 3: the hashing, then s G over half of the comb windows each (no
                              // P = +-Q inside a half)
         if (wave == 3) {  // e, c = r - e (mod n)
@@ -573,24 +604,17 @@ __global__ __launch_bounds__(256, 1) void sm2_verify_row_kernel(IO io, uint64_t 
             if (lane == 0) S.pinf[1] = rinf ? 1u : 0u;
         }
     }
-    // ---------------------------------------------------------------- phase C: t P on wave 0
-    if (wave == 0) {
-        row_wait(&S.post[0]);
-        fe k;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) k.v[q] = sgpr(ok ? t.v[q] : (q == 0 ? 1u : 0u));
-        frow::Pt acc{0u, 0u, 0u};
-        const bool fin = frow::sm2_chain(acc, k, &S.tab[0][0][0], S.zc[L.k], slot, f);
-        frow::pt_store(S.pt[0], acc, L);
-        if (lane == 0) S.pinf[0] = fin ? 0u : 1u;
-    }
     __syncthreads();
-    if (wave == 0) {  // Q = t P + s G, x(Q) == c or c + n, projectively
+    if (wave == 0) {  // Q = t_lo P + t_hi 2^kSm2RowSplit P + s G, x(Q) == c or c + n, projectively
         frow::Pt P, Q, R;
         bool rinf;
         frow::pt_load(P, S.pt[0], L);
+        frow::pt_load(Q, S.pt[3], L);
+        frow::add_full(R, rinf, P, sgpr(S.pinf[0]) != 0u, Q, sgpr(S.pinf[3]) != 0u, slot, f);
+        P = R;
+        const bool pinf = rinf;
         frow::pt_load(Q, S.pt[1], L);
-        frow::add_full(R, rinf, P, sgpr(S.pinf[0]) != 0u, Q, sgpr(S.pinf[1]) != 0u, slot, f);
+        frow::add_full(R, rinf, P, pinf, Q, sgpr(S.pinf[1]) != 0u, slot, f);
         const uint32_t z2 = f.mul(R.Z, R.Z);
         fe26 c26;
         fe cw;

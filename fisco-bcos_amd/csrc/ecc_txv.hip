@@ -62,15 +62,14 @@ __global__ __launch_bounds__(256, OCC) void tx_verify_kernel(IO io, uint64_t n, 
 // has the row kernel (ecc_row.hip, one signature per workgroup): its first round of one signature per
 // CU costs kRowLat of the trio's round and each further round kRowLatN (two workgroups share a CU:
 // tools/small_sweep.py, profiles/r05_small_sweep_row.json: 0.127 / 0.153 / 0.211 / 0.280 / 0.347 ms at
-// 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.378); SM2 its own row kernel, whose
-// latency is its one-wave chain's, so the workgroups resident on a CU (three) overlap whole: its rounds
-// hold kRowPerCuSM2 signatures per CU, at kRowLatSM2 / kRowLatNSM2 of the SM2 trio's round (same file:
-// 0.258 / 0.288 / 0.294 / 0.321 / 0.566 ms at 1 / 256 / 512 / 768 / 1024 signatures against the trio's
-// 0.577).
+// 1 / 256 / 512 / 768 / 1024 signatures against the trio's 0.378); SM2 its own row kernel, at
+// kRowLatSM2 for one signature per CU and kRowLatNSM2 per further one while kRowResidentSM2 workgroups
+// share a CU, a new round beyond (same file: 0.221 / 0.250 / 0.384 / 0.401 / 0.485 / 0.754 ms at 1 / 256 /
+// 512 / 768 / 1024 / 1280 signatures against the trio's 0.578).
 // Returns 3 (row), 2 (trio), 1 (pair), 0 (one-lane, occupancy 1) or -2 (one-lane, occupancy 2).
 static constexpr double kRowLat = 0.38, kRowLatN = 0.18;
-static constexpr double kRowLatSM2 = 0.53, kRowLatNSM2 = 0.55;
-static constexpr uint64_t kRowPerCuSM2 = 3;
+static constexpr double kRowLatSM2 = 0.43, kRowLatNSM2 = 0.14;
+static constexpr uint64_t kRowResidentSM2 = 4;
 static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_ok) {
     const bool sm2 = suite == BCOSGPU_SUITE_SM2;
     //                    occ 2,              occ 1,              pair,               trio
@@ -92,9 +91,11 @@ static int auto_kernel(int suite, uint64_t n, int cus, bool small_ok, bool row_o
         }
     }
     if (row_ok && small_ok) {
+        // m signatures per CU; a round holds `res` of them per CU (secp256k1: linear in m throughout)
         const double r1 = sm2 ? kRowLatSM2 : kRowLat, rn = sm2 ? kRowLatNSM2 : kRowLatN;
-        const uint64_t per_round = (sm2 ? kRowPerCuSM2 : 1ull) * cus;
-        const double c = r1 + static_cast<double>((n + per_round - 1) / per_round - 1) * rn;
+        const uint64_t m = (n + cus - 1) / cus, res = sm2 ? kRowResidentSM2 : m;
+        const uint64_t rounds = (m + res - 1) / res;
+        const double c = static_cast<double>(rounds) * r1 + static_cast<double>(m - rounds) * rn;
         if (c < cost) best = 3;
     }
     return best;

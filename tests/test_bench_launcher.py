@@ -58,8 +58,8 @@ def test_small_batch_choice_mirrors_library():
     mr = re.search(r"kRowLatSM2 = ([\d.]+), kRowLatNSM2 = ([\d.]+);", src)
     mbr = re.search(r"ROW_LAT_SM2, ROW_LAT_N_SM2 = ([\d.]+), ([\d.]+)", bsrc)
     assert mr and mbr and mr.groups() == mbr.groups()
-    mr = re.search(r"kRowPerCuSM2 = (\d+);", src)
-    mbr = re.search(r"ROW_PER_CU_SM2 = (\d+)", bsrc)
+    mr = re.search(r"kRowResidentSM2 = (\d+);", src)
+    mbr = re.search(r"ROW_RESIDENT_SM2 = (\d+)", bsrc)
     assert mr and mbr and mr.groups() == mbr.groups()
     ns = {"__name__": "bench_mirror", "__file__": os.path.join(ROOT, "bench.py")}
     exec(bsrc[bsrc.index("ROW_LAT, ROW_LAT_N ="):bsrc.index("def _kernel_name")], ns)
