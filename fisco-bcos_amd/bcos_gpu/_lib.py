@@ -74,6 +74,10 @@ _SIGS = {
     "bcosgpu_tx_verify_batch_dev": (_I, [_I, _P, _P, _P, _P, _SZ, _P, _P, _P, _P]),
     "bcosgpu_tx_preimage_size": (ctypes.c_uint64, [_P, _SZ]),
     "bcosgpu_pack_tx_preimages": (_I, [_P, _SZ, _P, ctypes.c_uint64, _P]),
+    "bcosgpu_receipt_preimage_size": (ctypes.c_uint64, [_P, _SZ]),
+    "bcosgpu_pack_receipt_preimages": (_I, [_P, _SZ, _P, ctypes.c_uint64, _P]),
+    "bcosgpu_apply_receipt_data_hashes": (None, [_P, _SZ, _P]),
+    "bcosgpu_receipt_roots": (_I, [_I, _P, _P, _SZ, _P, _P]),
     "bcosgpu_tars_decode_work_size": (ctypes.c_uint64, [_SZ]),
     "bcosgpu_tars_tx_decode_dev": (_I, [_P, _P, _SZ, _P, _P, _P, _P, _P, _P, ctypes.c_uint64, _P]),
     "bcosgpu_tars_tx_verify_batch": (_I, [_I, _P, _P, _SZ, _I, _I, _P, _P, _P]),

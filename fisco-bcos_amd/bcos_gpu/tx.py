@@ -223,25 +223,95 @@ def verify_transactions(suite: CryptoSuite, txs):
     return status
 
 
-def _hashes_of(suite: CryptoSuite, items):
-    """impl_calculate over tx / receipt objects: a set dataHash is used as is (TarsHashable.h:20-24,
-    :47-51), the rest are hashed on the GPU in one batch."""
-    out = [bytes(getattr(it, "data_hash", b"") or b"") for it in items]
-    todo = [i for i, h in enumerate(out) if not h]
-    if todo:
-        data, off = pack_messages([items[i].data.preimage() for i in todo])
-        hs = suite.hash_impl.hash_packed(data, off)
-        for k, i in enumerate(todo):
-            out[i] = hs[k].tobytes()
-    return out
+class _BytesView(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_char_p), ("len", ctypes.c_size_t)]
+
+
+class _LogView(ctypes.Structure):
+    """bcosgpu_LogEntry (include/bcos_gpu.h)."""
+    _fields_ = [("address", ctypes.c_char_p), ("address_len", ctypes.c_size_t),
+                ("topics", ctypes.POINTER(_BytesView)), ("ntopics", ctypes.c_size_t),
+                ("data", ctypes.c_char_p), ("data_len", ctypes.c_size_t)]
+
+
+class _ReceiptView(ctypes.Structure):
+    """bcosgpu_TransactionReceiptData (include/bcos_gpu.h): pointers into the caller's fields."""
+    _fields_ = [("version", ctypes.c_int32),
+                ("gas_used", ctypes.c_char_p), ("gas_used_len", ctypes.c_size_t),
+                ("contract_address", ctypes.c_char_p), ("contract_address_len", ctypes.c_size_t),
+                ("status", ctypes.c_int32),
+                ("output", ctypes.c_char_p), ("output_len", ctypes.c_size_t),
+                ("logs", ctypes.POINTER(_LogView)), ("nlogs", ctypes.c_size_t),
+                ("block_number", ctypes.c_int64),
+                ("data_hash", ctypes.c_char_p), ("data_hash_len", ctypes.c_size_t)]
+
+
+def _receipt_views(receipts):
+    """ctypes views of TransactionReceipt objects; returns (views array, keep-alive list)."""
+    n = len(receipts)
+    views = (_ReceiptView * max(n, 1))()
+    keep = []
+    for i, r in enumerate(receipts):
+        d, v = r.data, views[i]
+        fields = [d.gas_used.encode(), d.contract_address.encode(), bytes(d.output), bytes(r.data_hash or b"")]
+        keep.append(fields)
+        v.version, v.status, v.block_number = d.version, d.status, d.block_number
+        for name, b in zip(("gas_used", "contract_address", "output", "data_hash"), fields):
+            setattr(v, name, b)
+            setattr(v, name + "_len", len(b))
+        logs = d.log_entries or []
+        if logs:
+            la = (_LogView * len(logs))()
+            for k, lg in enumerate(logs):
+                addr, data, topics = lg.address.encode(), bytes(lg.data), [bytes(t) for t in lg.topic or []]
+                ta = (_BytesView * max(len(topics), 1))()
+                for j, t in enumerate(topics):
+                    ta[j].data, ta[j].len = t, len(t)
+                keep.append((addr, data, topics, ta))
+                la[k].address, la[k].address_len = addr, len(addr)
+                la[k].data, la[k].data_len = data, len(data)
+                la[k].topics, la[k].ntopics = ta, len(topics)
+            keep.append(la)
+            v.logs, v.nlogs = la, len(logs)
+    return views, keep
+
+
+def pack_receipt_preimages(receipts):
+    """The native receipt packer (bcosgpu_pack_receipt_preimages, host C++): list[TransactionReceipt] ->
+    (uint8 packed preimages, uint64 offsets[n+1]); a receipt with a dataHash gets an empty preimage."""
+    views, keep = _receipt_views(receipts)
+    n = len(receipts)
+    size = int(lib().bcosgpu_receipt_preimage_size(views, n))
+    out = np.zeros(max(size, 1), dtype=np.uint8)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    check(lib().bcosgpu_pack_receipt_preimages(views, n, _ptr(out), size, _ptr(off)))
+    del keep
+    return out[:size], off
+
+
+def receipt_roots(hasher, receipts, block_off):
+    """bcosgpu_receipt_roots: calculateReceiptRoot for many blocks in one engine call (block b = receipts
+    [block_off[b], block_off[b+1])).  Returns (roots uint8[nblocks, 32], receipt hashes uint8[n, 32])."""
+    ensure_device()
+    bo = np.ascontiguousarray(block_off, dtype=np.uint64)
+    nb = bo.size - 1
+    views, keep = _receipt_views(receipts)
+    n = len(receipts)
+    roots = np.zeros((max(nb, 1), 32), dtype=np.uint8)
+    hashes = np.zeros((max(n, 1), 32), dtype=np.uint8)
+    check(lib().bcosgpu_receipt_roots(hasher, views, _ptr(bo), nb, _ptr(roots), _ptr(hashes)))
+    del keep
+    return roots[:nb], hashes[:n]
 
 
 def calculate_receipt_root(suite: CryptoSuite, receipts) -> bytes:
-    """BlockImpl::calculateReceiptRoot (BlockImpl.h:156-183): width-2 Merkle over the receipt hashes;
+    """BlockImpl::calculateReceiptRoot (BlockImpl.h:156-183) through bcosgpu_receipt_roots: receipts packed
+    by the native packer, hashed on the GPU (a set dataHash used as is, TarsHashable.h:47-51), width-2 root;
     no receipts -> the zero hash (:159-163)."""
     if len(receipts) == 0:
         return bytes(32)
-    return Merkle(suite.hash_impl, 2).root(_hashes_of(suite, receipts))
+    roots, _ = receipt_roots(suite.hash_impl.kind, receipts, [0, len(receipts)])
+    return roots[0].tobytes()
 
 
 def calculate_roots_batch(suite: CryptoSuite, blocks_of_hashes):

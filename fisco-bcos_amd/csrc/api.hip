@@ -42,6 +42,23 @@ struct DevBuf {
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// Grow-only pinned host buffer (staging for packers that write straight into DMA-able memory).
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes < 65536 ? 65536 : bytes + bytes / 4;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
 // One workspace per device for the synchronous host-pointer API; the mutex makes those entry
 // points safe to call from the reference's concurrent verifier pools (TxPool.h:48-49).
 struct Workspace {
@@ -49,6 +66,7 @@ struct Workspace {
     bool ready = false;
     hipStream_t stream = nullptr;
     DevBuf b[8];
+    HostBuf h[2];
 };
 std::mutex g_mu;
 std::vector<Workspace*> g_ws;
@@ -335,6 +353,57 @@ int bcosgpu_merkle_roots_batch(int hasher, int width, const uint8_t* leaves32, c
                                    w->b[2].as<uint8_t>(), w->stream);
     if (rc) return hip_err(hipGetLastError(), "merkle roots launch");
     HIP_OK(hipMemcpyAsync(roots32, w->b[2].p, nblocks * 32, hipMemcpyDeviceToHost, w->stream));
+    HIP_OK(hipStreamSynchronize(w->stream));
+    return 0;
+}
+
+// calculateReceiptRoot for many blocks (BlockImpl.h:156-183): the receipt preimages are packed
+// (pack.cpp, TarsHashable.h:54-73) straight into pinned staging, one H2D, one hash launch, the dataHash
+// short-circuits (TarsHashable.h:47-51) patched in, then the many-tree root kernel.
+int bcosgpu_receipt_roots(int hasher, const bcosgpu_TransactionReceiptData* receipts, const uint64_t* block_off,
+                          size_t nblocks, uint8_t* roots32, uint8_t* hashes32) {
+    if (hasher != BCOSGPU_KECCAK256 && hasher != BCOSGPU_SM3) return set_err(BCOSGPU_E_ARG, "bad hasher");
+    if (nblocks == 0) return 0;
+    if (int rc = check_block_off(block_off, nblocks)) return rc;
+    if (block_off[0] != 0) return set_err(BCOSGPU_E_ARG, "block_off[0] must be 0");
+    const uint64_t n = block_off[nblocks];
+    if (!roots32 || (n && !receipts)) return set_err(BCOSGPU_E_ARG, "null pointer");
+    Workspace* w;
+    int rc = get_ws(&w);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(w->mu);
+    const uint64_t bytes = bcosgpu_receipt_preimage_size(receipts, n);
+    bool patched = false;
+    for (uint64_t i = 0; i < n && !patched; ++i) patched = receipts[i].data_hash_len != 0;
+    HIP_OK(w->h[0].ensure(bytes + 8 * (n + 1) + 16));
+    if (patched) HIP_OK(w->h[1].ensure(32 * n + 32));
+    uint64_t* off = w->h[0].as<uint64_t>();
+    uint8_t* pre = reinterpret_cast<uint8_t*>(off + n + 1);
+    if (bcosgpu_pack_receipt_preimages(receipts, n, pre, bytes, off))
+        return set_err(BCOSGPU_E_ARG, "bad receipt view (null field with a length, or a dataHash over 32 bytes)");
+    HIP_OK(w->b[0].ensure(bytes + 8 * (n + 1) + 16));
+    HIP_OK(w->b[1].ensure(32 * n + 32));
+    HIP_OK(w->b[2].ensure(merkle_roots_work_bytes(n, nblocks, 2)));
+    HIP_OK(w->b[3].ensure(nblocks * 32));
+    uint8_t* d_hash = w->b[1].as<uint8_t>();
+    if (n) {
+        HIP_OK(hipMemcpyAsync(w->b[0].p, off, bytes + 8 * (n + 1), hipMemcpyHostToDevice, w->stream));
+        const uint64_t* d_off = w->b[0].as<uint64_t>();
+        if (launch_hash_batch(hasher, reinterpret_cast<const uint8_t*>(d_off + n + 1), d_off, n, d_hash, w->stream))
+            return hip_err(hipGetLastError(), "receipt hash launch");
+        if (patched) {  // the dataHash receipts: hashes round-trip through the host once
+            uint8_t* h = w->h[1].as<uint8_t>();
+            HIP_OK(hipMemcpyAsync(h, d_hash, 32 * n, hipMemcpyDeviceToHost, w->stream));
+            HIP_OK(hipStreamSynchronize(w->stream));
+            bcosgpu_apply_receipt_data_hashes(receipts, n, h);
+            HIP_OK(hipMemcpyAsync(d_hash, h, 32 * n, hipMemcpyHostToDevice, w->stream));
+        }
+    }
+    rc = launch_merkle_roots_batch(hasher, 2, d_hash, block_off, nblocks, w->b[2].as<uint8_t>(), w->b[3].as<uint8_t>(),
+                                   w->stream);
+    if (rc) return hip_err(hipGetLastError(), "merkle roots launch");
+    HIP_OK(hipMemcpyAsync(roots32, w->b[3].p, nblocks * 32, hipMemcpyDeviceToHost, w->stream));
+    if (hashes32 && n) HIP_OK(hipMemcpyAsync(hashes32, d_hash, 32 * n, hipMemcpyDeviceToHost, w->stream));
     HIP_OK(hipStreamSynchronize(w->stream));
     return 0;
 }

@@ -291,6 +291,51 @@ uint64_t bcosgpu_tx_preimage_size(const bcosgpu_TransactionData* txs, size_t n);
 int bcosgpu_pack_tx_preimages(const bcosgpu_TransactionData* txs, size_t n, uint8_t* out, uint64_t cap,
                               uint64_t* offsets);
 
+/* ---------------------------------------------------------------- receipts (calculateReceiptRoot) */
+/* Views of bcostars::LogEntry / TransactionReceiptData / TransactionReceipt.dataHash
+ * (bcos-tars-protocol/bcos-tars-protocol/tars/TransactionReceipt.tars:2-23): pointers into the caller's
+ * decoded receipt.  topic is vector<vector<byte>>: ntopics byte strings. */
+typedef struct { const uint8_t* data; size_t len; } bcosgpu_Bytes;
+typedef struct {
+    const char* address;   size_t address_len;
+    const bcosgpu_Bytes* topics; size_t ntopics;
+    const uint8_t* data;   size_t data_len;
+} bcosgpu_LogEntry;
+typedef struct {
+    int32_t version;
+    const char* gas_used;          size_t gas_used_len;
+    const char* contract_address;  size_t contract_address_len;
+    int32_t status;
+    const uint8_t* output;         size_t output_len;
+    const bcosgpu_LogEntry* logs;  size_t nlogs;
+    int64_t block_number;
+    /* TransactionReceipt.dataHash: when non-empty it IS the receipt hash (TarsHashable.h:47-51) and the
+     * fields above are not read.  At most 32 bytes (the reference's assignTo into a 32-byte hash throws
+     * NoEnoughSpace beyond that); a shorter one fills the leading bytes, the rest are zero here (the
+     * reference leaves them uninitialised, BlockImpl.h:171). */
+    const uint8_t* data_hash;      size_t data_hash_len;
+} bcosgpu_TransactionReceiptData;
+/* Total preimage bytes of n receipts (0 for a receipt with a dataHash). */
+uint64_t bcosgpu_receipt_preimage_size(const bcosgpu_TransactionReceiptData* receipts, size_t n);
+/* Packs the receipt-hash preimages impl_calculate<Hasher>(TransactionReceipt) hashes
+ * (TarsHashable.h:54-73: be32(version) || gasUsed || contractAddress || be32(status) || output ||
+ * per log (address || topic_0 .. topic_k || data) || be64(blockNumber)) back to back into out (cap bytes)
+ * and writes offsets[n+1]; a receipt with a dataHash gets an empty preimage.  Host only, multithreaded
+ * for large batches.  BCOSGPU_E_ARG if cap is too small, a field pointer is null with a non-zero length,
+ * or a dataHash is longer than 32 bytes. */
+int bcosgpu_pack_receipt_preimages(const bcosgpu_TransactionReceiptData* receipts, size_t n, uint8_t* out,
+                                   uint64_t cap, uint64_t* offsets);
+/* hashes32[i] = receipt i's dataHash for every receipt that has one (host only; the step after hashing
+ * the packed preimages). */
+void bcosgpu_apply_receipt_data_hashes(const bcosgpu_TransactionReceiptData* receipts, size_t n, uint8_t* hashes32);
+/* BlockImpl::calculateReceiptRoot (bcos-tars-protocol/.../protocol/BlockImpl.h:156-183) for nblocks blocks
+ * in one call: block b's receipts are receipts[block_off[b] .. block_off[b+1]) (HOST array, block_off[0] =
+ * 0); every receipt hashed on the GPU with `hasher` (impl_calculate, dataHash short-circuit), then
+ * roots32 + 32 b = Merkle<H, 2> root of block b's receipt hashes (zero hash for a block without
+ * receipts, BlockImpl.h:159-163).  hashes32 (nullable) receives the block_off[nblocks] receipt hashes. */
+int bcosgpu_receipt_roots(int hasher, const bcosgpu_TransactionReceiptData* receipts, const uint64_t* block_off,
+                          size_t nblocks, uint8_t* roots32, uint8_t* hashes32);
+
 /* ---------------------------------------------------------------- single calls on an explicit device */
 /* One signature per call, for the reference's per-transaction call sites: TxPool's submitter threads
  * (TxPool.h:48-49) -> TxValidator::verify (TxValidator.cpp:56) -> Transaction::verify (Transaction.h:68-82)

@@ -228,6 +228,33 @@ inline std::vector<HashType> calculateRoots(const std::vector<std::vector<HashTy
     return roots;
 }
 
+/* BlockImpl::calculateReceiptRoot (BlockImpl.h:156-183) for many blocks in one engine call: every receipt
+ * hashed on the GPU (impl_calculate<Hasher>(TransactionReceipt), TarsHashable.h:43-75, a set dataHash
+ * used as is), then each block's width-2 root; a block without receipts gives the zero hash.
+ * receiptHashes (nullable) receives every receipt's hash, blocks back to back. */
+template <int HASHER>
+inline std::vector<HashType> calculateReceiptRoots(const std::vector<std::vector<bcosgpu_TransactionReceiptData>>& blocks,
+                                                   std::vector<HashType>* receiptHashes = nullptr) {
+    std::vector<uint64_t> off(blocks.size() + 1, 0);
+    std::vector<bcosgpu_TransactionReceiptData> all;
+    for (size_t b = 0; b < blocks.size(); ++b) {
+        all.insert(all.end(), blocks[b].begin(), blocks[b].end());
+        off[b + 1] = all.size();
+    }
+    std::vector<HashType> roots(blocks.size());
+    if (receiptHashes) receiptHashes->assign(all.size(), HashType{});
+    if (blocks.empty()) return roots;
+    check(bcosgpu_receipt_roots(HASHER, all.data(), off.data(), blocks.size(), roots[0].data(),
+                                receiptHashes && !all.empty() ? (*receiptHashes)[0].data() : nullptr));
+    return roots;
+}
+
+/* BlockImpl::calculateReceiptRoot for one block */
+template <int HASHER>
+inline HashType calculateReceiptRoot(const std::vector<bcosgpu_TransactionReceiptData>& receipts) {
+    return calculateReceiptRoots<HASHER>({receipts})[0];
+}
+
 /* EVM ecRecover precompile (bcos-executor/src/vm/Precompiled.cpp:443-482): {true, 32-byte output}
  * on success, {true, {}} on failure; `in` is read as 128 zero-padded bytes. */
 inline std::pair<bool, bytes> ecRecover(const uint8_t* in, size_t len) {
