@@ -705,9 +705,12 @@ def cpu_baseline(batches, threads):
                     "unbuildable here, BASELINE.md 3): OpenSSL libcrypto EC and the oracle's 4x64 Montgomery port"}
 
 
-def host_api_rate(b, suite, n, reps=5):
-    """The same batch through the host-pointer ABI (bcosgpu_tx_verify_batch: H2D copy, kernel, D2H,
-    synchronise) -- the PCIe-inclusive rate a caller holding host buffers sees.  Not `value`."""
+def host_api_rate(b, suite, n, reps=20):
+    """The same batch through the host-pointer ABI (bcosgpu_tx_verify_batch: the chunked copy / compute
+    pipeline of csrc/txpipe.hip -- H2D, kernel, D2H, synchronise) -- the PCIe-inclusive rate a caller
+    holding host buffers sees.  Not `value`.  The caller's output arrays are reused across calls (a node
+    keeps its batch buffers); `fresh_outputs_ms` is the same call into newly allocated arrays each time
+    (their first-touch page faults land inside the call)."""
     import numpy as np
     import bcos_gpu
     from bcos_gpu import tx
@@ -716,13 +719,21 @@ def host_api_rate(b, suite, n, reps=5):
     sig = np.ascontiguousarray(b.sig.cpu().numpy())
     sig_off = np.ascontiguousarray(b.sig_off[: n + 1].cpu().numpy().astype(np.uint64))
     suite_obj = bcos_gpu.sm_suite() if suite else bcos_gpu.secp256k1_suite()
-    tx.verify_packed(suite_obj, pre, pre_off, sig, sig_off)  # warm-up (workspace growth)
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        tx.verify_packed(suite_obj, pre, pre_off, sig, sig_off)
-    dt = (time.perf_counter() - t0) / reps
-    return {"value": n / dt, "unit": "tx/s", "ms_per_batch": dt * 1e3,
-            "path": "bcosgpu_tx_verify_batch (host buffers: H2D + kernel + D2H + sync)"}
+    out = tx.verify_packed(suite_obj, pre, pre_off, sig, sig_off)  # warm-up (pipeline buffers)
+
+    def med(f):
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            f()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return ts[len(ts) // 2]
+    dt = med(lambda: tx.verify_packed(suite_obj, pre, pre_off, sig, sig_off, out=out))
+    fresh = med(lambda: tx.verify_packed(suite_obj, pre, pre_off, sig, sig_off))
+    return {"value": n / dt, "unit": "tx/s", "ms_per_batch": dt * 1e3, "fresh_outputs_ms": fresh * 1e3,
+            "path": "bcosgpu_tx_verify_batch (host buffers: pinned-staged H2D + kernel + D2H + sync; median of %d)"
+                    % reps}
 
 
 def interface_legs(batches, threads=(16, 64, 256), calls=1000, reps=20):
@@ -1027,18 +1038,22 @@ def devset_legs(devices, min_seconds=1.0):
     per = WORKLOADS["c5"]["n"] // WORKLOADS["c5"]["blocks"]
     n4 = WORKLOADS["c4"]["n"]
 
-    def c4(devs):
-        return tx.verify_packed_multi(devs, suite, pre, po[: n4 + 1], sg, so[: n4 + 1], width=2)
+    nall = len(po) - 1
+    bufs = (np.zeros((nall, 32), np.uint8), np.zeros((nall, 20), np.uint8), np.zeros(nall, np.uint8))
+
+    def c4(devs, out=None):
+        return tx.verify_packed_multi(devs, suite, pre, po[: n4 + 1], sg, so[: n4 + 1], width=2, out=out)
 
     nblk = WORKLOADS["c5"]["blocks"]
     bo = np.arange(nblk + 1, dtype=np.uint64) * np.uint64(per)
 
-    def c5(devs):  # the 64 blocks in one call, whole blocks per device (bcosgpu_blocks_verify_multi)
-        return tx.blocks_verify_multi(devs, suite, pre, po, sg, so, bo, width=2)
+    def c5(devs, out=None):  # the 64 blocks in one call, whole blocks per device (bcosgpu_blocks_verify_multi)
+        return tx.blocks_verify_multi(devs, suite, pre, po, sg, so, bo, width=2, out=out)
 
-    def c5_seq(devs):  # one block at a time, each sharded over the devices (bcosgpu_block_verify_multi)
+    def c5_seq(devs, out=None):  # one block at a time, each sharded over the devices (bcosgpu_block_verify_multi)
         return [tx.verify_packed_multi(devs, suite, pre, po[k * per: (k + 1) * per + 1], sg,
-                                       so[k * per: (k + 1) * per + 1], width=2)
+                                       so[k * per: (k + 1) * per + 1], width=2,
+                                       out=None if out is None else tuple(x[k * per:(k + 1) * per] for x in out))
                 for k in range(nblk)]
 
     def _same(g, w):
@@ -1049,13 +1064,18 @@ def devset_legs(devices, min_seconds=1.0):
         want = fn([devices[0]])
         got = fn(devices)
         same = _same(got, want) if wl != "c5_seq" else all(_same(g, w) for g, w in zip(got, want))
-        steps, t0 = 0, time.perf_counter()
-        while steps < 2 or time.perf_counter() - t0 < min_seconds:
-            fn(devices)
-            steps += 1
-        dt = (time.perf_counter() - t0) / steps
-        out[wl] = {"tx_s": WORKLOADS[wl.split("_")[0]]["n"] / dt, "ms_per_step": dt * 1e3, "steps": steps,
+        ts = []
+        t0 = time.perf_counter()
+        while len(ts) < 3 or time.perf_counter() - t0 < min_seconds:
+            t1 = time.perf_counter()
+            fn(devices, out=bufs)  # the caller's reused output buffers
+            ts.append(time.perf_counter() - t1)
+        ts.sort()
+        dt = ts[len(ts) // 2]
+        out[wl] = {"tx_s": WORKLOADS[wl.split("_")[0]]["n"] / dt, "ms_per_step": dt * 1e3, "steps": len(ts),
                    "matches_single_device": bool(same)}
+    out["note"] = ("host buffers in and out through the chunked copy / compute pipeline (csrc/txpipe.hip); "
+                   "median call, output arrays reused across calls as a node reuses its batch buffers")
     return out
 
 
@@ -1093,7 +1113,7 @@ def summarize(full, head_name):
     if ds:
         out["devset"] = {"devices": ds["devices"], **{k: {"tx_s": _g(v["tx_s"]), "ms": _g(v["ms_per_step"]),
                                                           "ok": v["matches_single_device"]}
-                                                      for k, v in ds.items() if k != "devices"}}
+                                                      for k, v in ds.items() if isinstance(v, dict)}}
     itf = full.get("interface") or {}
     sc = {}
     for k, v in itf.items():

@@ -129,13 +129,22 @@ def pack_preimages(datas):
     return out[:size], off
 
 
-def verify_packed(suite: CryptoSuite, pre, pre_off, sig, sig_off):
+def _outputs(n, out):
+    """(txhash uint8[n,32], sender uint8[n,20], status uint8[n]): `out` (a caller's reused buffers, as a node
+    keeps its batch arrays; at least n rows each) or fresh zeroed arrays."""
+    if out is None:
+        return np.zeros((n, 32), dtype=np.uint8), np.zeros((n, 20), dtype=np.uint8), np.zeros(n, dtype=np.uint8)
+    txhash, sender, status = out
+    assert txhash.shape[0] >= n and sender.shape[0] >= n and status.shape[0] >= n
+    assert all(a.flags.c_contiguous and a.dtype == np.uint8 for a in out)
+    return txhash[:n], sender[:n], status[:n]
+
+
+def verify_packed(suite: CryptoSuite, pre, pre_off, sig, sig_off, out=None):
     """Batched Transaction::verify over packed buffers.
-    Returns (txhash uint8[n,32], sender uint8[n,20], status uint8[n])."""
+    Returns (txhash uint8[n,32], sender uint8[n,20], status uint8[n]) -- written into `out` when given."""
     n = len(pre_off) - 1
-    txhash = np.zeros((n, 32), dtype=np.uint8)
-    sender = np.zeros((n, 20), dtype=np.uint8)
-    status = np.zeros(n, dtype=np.uint8)
+    txhash, sender, status = _outputs(n, out)
     if n:
         ensure_device()
         p = pre if len(pre) else np.zeros(1, dtype=np.uint8)
@@ -151,16 +160,14 @@ def _devices(devices):
     return d
 
 
-def verify_packed_multi(devices, suite: CryptoSuite, pre, pre_off, sig, sig_off, width=None):
+def verify_packed_multi(devices, suite: CryptoSuite, pre, pre_off, sig, sig_off, width=None, out=None):
     """verify_packed over a device set in ONE process (bcosgpu_tx_verify_batch_multi): the batch split by
     index over `devices` (an index may repeat: two shards on one GPU, distinct streams).  With `width`,
     also the block's tx root (bcosgpu_block_verify_multi: per-GPU frontiers gathered on devices[0]).
     Returns (txhash, sender, status) or (txhash, sender, status, root)."""
     d = _devices(devices)
     n = len(pre_off) - 1
-    txhash = np.zeros((n, 32), dtype=np.uint8)
-    sender = np.zeros((n, 20), dtype=np.uint8)
-    status = np.zeros(n, dtype=np.uint8)
+    txhash, sender, status = _outputs(n, out)
     p = pre if len(pre) else np.zeros(1, dtype=np.uint8)
     s = sig if len(sig) else np.zeros(1, dtype=np.uint8)
     po = np.ascontiguousarray(pre_off, dtype=np.uint64)
@@ -175,16 +182,14 @@ def verify_packed_multi(devices, suite: CryptoSuite, pre, pre_off, sig, sig_off,
     return txhash, sender, status, root.tobytes()
 
 
-def blocks_verify_multi(devices, suite: CryptoSuite, pre, pre_off, sig, sig_off, block_off, width=2):
+def blocks_verify_multi(devices, suite: CryptoSuite, pre, pre_off, sig, sig_off, block_off, width=2, out=None):
     """Many blocks in one call over a device set (bcosgpu_blocks_verify_multi): block b = txs
     [block_off[b], block_off[b+1]).  Returns (txhash, sender, status, roots uint8[nblocks, 32])."""
     d = _devices(devices)
     bo = np.ascontiguousarray(block_off, dtype=np.uint64)
     nb = bo.size - 1
     n = int(bo[-1]) if nb >= 0 else 0
-    txhash = np.zeros((max(n, 1), 32), dtype=np.uint8)
-    sender = np.zeros((max(n, 1), 20), dtype=np.uint8)
-    status = np.zeros(max(n, 1), dtype=np.uint8)
+    txhash, sender, status = _outputs(max(n, 1), out)
     roots = np.zeros((max(nb, 1), 32), dtype=np.uint8)
     p = pre if len(pre) else np.zeros(1, dtype=np.uint8)
     s = sig if len(sig) else np.zeros(1, dtype=np.uint8)

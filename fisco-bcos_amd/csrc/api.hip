@@ -670,6 +670,9 @@ int bcosgpu_tx_verify_batch_dev(int suite, const uint8_t* d_pre, const uint64_t*
     return rc ? set_err(rc, "tx verify launch failed") : 0;
 }
 
+// The batch site TransactionSync::importDownloadedTxs (TransactionSync.cpp:516-548) holds host memory:
+// the chunked copy / compute pipeline of txpipe.hip on a pipeline of the calling thread's device (its own
+// streams and buffers: concurrent callers overlap).
 int bcosgpu_tx_verify_batch(int suite, const uint8_t* pre, const uint64_t* pre_off,
                             const uint8_t* sig, const uint64_t* sig_off, size_t n,
                             uint8_t* txhash32, uint8_t* sender20, uint8_t* status) {
@@ -677,36 +680,25 @@ int bcosgpu_tx_verify_batch(int suite, const uint8_t* pre, const uint64_t* pre_o
     if (n == 0) return 0;
     if (!pre || !pre_off || !sig || !sig_off || !txhash32 || !sender20 || !status)
         return set_err(BCOSGPU_E_ARG, "null pointer");
-    for (size_t i = 0; i < n; ++i)
-        if (pre_off[i + 1] < pre_off[i] || sig_off[i + 1] < sig_off[i] || pre_off[i + 1] - pre_off[i] > 0xFFFFFFFFull)
-            return set_err(BCOSGPU_E_ARG, "offsets must be non-decreasing");
-    const uint64_t pb = pre_off[0], pbytes = pre_off[n] - pb, sb = sig_off[0], sbytes = sig_off[n] - sb;
-    Workspace* w;
-    int rc = get_ws(&w);
-    if (rc) return rc;
-    std::lock_guard<std::mutex> g(w->mu);
-    HIP_OK(w->b[0].ensure(pbytes + 8));
-    HIP_OK(w->b[1].ensure((n + 1) * 8));
-    HIP_OK(w->b[2].ensure(sbytes + 8));
-    HIP_OK(w->b[3].ensure((n + 1) * 8));
-    HIP_OK(w->b[4].ensure(n * 32));
-    HIP_OK(w->b[5].ensure(n * 20));
-    HIP_OK(w->b[6].ensure(n));
-    std::vector<uint64_t> po(n + 1), so(n + 1);
-    for (size_t i = 0; i <= n; ++i) { po[i] = pre_off[i] - pb; so[i] = sig_off[i] - sb; }
-    HIP_OK(hipMemcpyAsync(w->b[0].p, pre + pb, pbytes, hipMemcpyHostToDevice, w->stream));
-    HIP_OK(hipMemcpyAsync(w->b[1].p, po.data(), (n + 1) * 8, hipMemcpyHostToDevice, w->stream));
-    HIP_OK(hipMemcpyAsync(w->b[2].p, sig + sb, sbytes, hipMemcpyHostToDevice, w->stream));
-    HIP_OK(hipMemcpyAsync(w->b[3].p, so.data(), (n + 1) * 8, hipMemcpyHostToDevice, w->stream));
-    rc = launch_tx_verify(suite, w->b[0].as<uint8_t>(), w->b[1].as<uint64_t>(), w->b[2].as<uint8_t>(),
-                          w->b[3].as<uint64_t>(), n, w->b[4].as<uint8_t>(), w->b[5].as<uint8_t>(),
-                          w->b[6].as<uint8_t>(), w->stream);
-    if (rc) return set_err(rc, "tx verify launch failed");
-    HIP_OK(hipMemcpyAsync(txhash32, w->b[4].p, n * 32, hipMemcpyDeviceToHost, w->stream));
-    HIP_OK(hipMemcpyAsync(sender20, w->b[5].p, n * 20, hipMemcpyDeviceToHost, w->stream));
-    HIP_OK(hipMemcpyAsync(status, w->b[6].p, n, hipMemcpyDeviceToHost, w->stream));
-    HIP_OK(hipStreamSynchronize(w->stream));
-    return 0;
+    int dev = 0;  // (the offsets are checked by the pipeline, chunk by chunk)
+    if (int rc = calling_device(&dev)) return rc;
+    TxPipe* p = tx_pipe_acquire(dev);
+    if (!p) return hip_err(hipGetLastError(), "tx pipeline setup");
+    HostTxRange t;
+    t.suite = suite;
+    t.pre = pre;
+    t.pre_off = pre_off;
+    t.sig = sig;
+    t.sig_off = sig_off;
+    t.lo = 0;
+    t.hi = n;
+    t.txhash32 = txhash32;
+    t.sender20 = sender20;
+    t.status = status;
+    std::string msg;
+    const int rc = tx_pipeline(*p, t, nullptr, msg);
+    tx_pipe_release(p);
+    return rc ? set_err(rc, msg) : 0;
 }
 
 // ------------------------------------------------------------------ Tars-encoded transactions

@@ -3,7 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <condition_variable>
+#include <functional>
 #include <string>
+#include <vector>
 #include "../../include/bcos_gpu.h"
 
 namespace bcosgpu {
@@ -98,6 +100,47 @@ int coalesced_run(int device, SigJob& job);
 int api_set_err(int code, const std::string& msg);
 int api_ready_device(int device);
 int api_run_job(int device, SigJob& job);
+
+// txpipe.hip: the host-pointer tx-verify batches as a chunked copy / compute pipeline (see the file header)
+struct PipeBuf {  // grow-only device buffer
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes);
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+struct PipeHostBuf {  // grow-only pinned host buffer
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes);
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+struct TxPipe {
+    int device = -1;
+    hipStream_t compute = nullptr, compute2 = nullptr, copy = nullptr;  // chunks alternate compute streams
+    std::vector<hipEvent_t> ev;  // 2 per chunk: inputs landed, kernel done
+    PipeBuf b[8];                // 0-4 the pipeline's (inputs, outputs); 5-7 free for a tail's work
+    PipeHostBuf hin, host;       // input / output staging of small batches
+};
+// txs [lo, hi) of a host batch (the caller's indexing: offsets, outputs at row i for tx i)
+struct HostTxRange {
+    int suite = 0;
+    const uint8_t* pre = nullptr;
+    const uint64_t* pre_off = nullptr;
+    const uint8_t* sig = nullptr;
+    const uint64_t* sig_off = nullptr;
+    uint64_t lo = 0, hi = 0;
+    uint8_t* txhash32 = nullptr;
+    uint8_t* sender20 = nullptr;
+    uint8_t* status = nullptr;
+};
+// queued on p.compute after every chunk's kernel, before the last download: d_hash = the range's
+// (hi - lo) x 32 tx hashes on the device
+using PipeTail = std::function<int(TxPipe& p, const uint8_t* d_hash, std::string& msg)>;
+TxPipe* tx_pipe_acquire(int device);  // nullptr on a HIP failure; the calling thread's device is kept
+void tx_pipe_release(TxPipe* p);
+uint64_t tx_pipe_chunk(uint64_t m);
+// on the calling thread's current device == p.device; returns after every output is in host memory
+int tx_pipeline(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::string& msg);
 
 // tars_kernels.hip
 uint64_t tars_decode_work_bytes(uint64_t n);

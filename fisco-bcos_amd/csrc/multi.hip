@@ -280,6 +280,39 @@ int sig_multi(const int* devices, int ndev, int kind, size_t n, const uint8_t* h
     });
 }
 
+// shards' pipelines (txpipe.hip) from each device's pool, returned when the call ends
+struct Pipes {
+    std::vector<TxPipe*> p;
+    ~Pipes() {
+        for (TxPipe* x : p) tx_pipe_release(x);
+    }
+    int acquire(const int* devices, int ndev) {
+        p.assign(ndev, nullptr);
+        for (int k = 0; k < ndev; ++k) {
+            p[k] = tx_pipe_acquire(devices[k]);
+            if (!p[k]) return api_set_err(BCOSGPU_E_HIP, "tx pipeline setup on a device of the set failed");
+        }
+        return 0;
+    }
+};
+
+HostTxRange host_range(int suite, const uint8_t* pre, const uint64_t* pre_off, const uint8_t* sig,
+                       const uint64_t* sig_off, uint64_t lo, uint64_t hi, uint8_t* txhash32, uint8_t* sender20,
+                       uint8_t* status) {
+    HostTxRange t;
+    t.suite = suite;
+    t.pre = pre;
+    t.pre_off = pre_off;
+    t.sig = sig;
+    t.sig_off = sig_off;
+    t.lo = lo;
+    t.hi = hi;
+    t.txhash32 = txhash32;
+    t.sender20 = sender20;
+    t.status = status;
+    return t;
+}
+
 int tx_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off, const uint8_t* sig,
              const uint64_t* sig_off, size_t n, int width, uint8_t* txhash32, uint8_t* sender20, uint8_t* status,
              uint8_t* root32) {
@@ -291,76 +324,51 @@ int tx_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const 
     }
     if (!pre || !pre_off || !sig || !sig_off || !txhash32 || !sender20 || !status)
         return api_set_err(BCOSGPU_E_ARG, "null pointer");
-    for (size_t i = 0; i < n; ++i)
-        if (pre_off[i + 1] < pre_off[i] || sig_off[i + 1] < sig_off[i] || pre_off[i + 1] - pre_off[i] > 0xFFFFFFFFull)
-            return api_set_err(BCOSGPU_E_ARG, "offsets must be non-decreasing");
+    if (pre_off[n] < pre_off[0] || sig_off[n] < sig_off[0])
+        return api_set_err(BCOSGPU_E_ARG, "offsets must be non-decreasing");  // (each shard's pipeline checks the rest)
     if (int rc = check_set(devices, ndev)) return rc;
     if (root32) enable_peers(devices, ndev);
     const int hasher = suite == BCOSGPU_SUITE_SM2 ? BCOSGPU_SM3 : BCOSGPU_KECCAK256;
     const Plan p = make_plan(n, ndev, root32 ? width : 0);
-    std::vector<ShardCtx*> ctx = contexts(devices, ndev);
+    Pipes pipes;
+    if (int rc = pipes.acquire(devices, ndev)) return rc;
     ShardCtx* top = root32 ? shard_ctx(devices[0], -1) : nullptr;
-    std::vector<ShardCtx*> all = ctx;
-    if (top) all.push_back(top);
-    auto locks = lock_all(all);
+    std::unique_lock<std::mutex> top_lock;
+    if (top) top_lock = std::unique_lock<std::mutex>(top->mu);
     std::vector<const uint8_t*> frontier(ndev, nullptr);
     int rc = run_shards(ndev, [&](int k, std::string& msg) -> int {
         const uint64_t lo = p.lo[k], hi = p.hi[k], m = hi - lo;
         if (!m) return 0;
-        ShardCtx* c = ctx[k];
-        DeviceGuard dg(c->device);
+        TxPipe& c = *pipes.p[k];
+        DeviceGuard dg(c.device);
         SHARD_HIP(dg.err);
-        SHARD_HIP(ensure_stream(c));
-        const uint64_t pb = pre_off[lo], pbytes = pre_off[hi] - pb, sb = sig_off[lo], sbytes = sig_off[hi] - sb;
-        SHARD_HIP(c->b[0].ensure(pbytes + 8));
-        SHARD_HIP(c->b[1].ensure((m + 1) * 8));
-        SHARD_HIP(c->b[2].ensure(sbytes + 8));
-        SHARD_HIP(c->b[3].ensure((m + 1) * 8));
-        SHARD_HIP(c->b[4].ensure(m * 32));
-        SHARD_HIP(c->b[5].ensure(m * 20));
-        SHARD_HIP(c->b[6].ensure(m));
-        std::vector<uint64_t> po(m + 1), so(m + 1);
-        for (uint64_t i = 0; i <= m; ++i) {
-            po[i] = pre_off[lo + i] - pb;
-            so[i] = sig_off[lo + i] - sb;
-        }
-        SHARD_HIP(hipMemcpyAsync(c->b[0].p, pre + pb, pbytes, hipMemcpyHostToDevice, c->stream));
-        SHARD_HIP(hipMemcpyAsync(c->b[1].p, po.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
-        SHARD_HIP(hipMemcpyAsync(c->b[2].p, sig + sb, sbytes, hipMemcpyHostToDevice, c->stream));
-        SHARD_HIP(hipMemcpyAsync(c->b[3].p, so.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
-        int lrc = launch_tx_verify(suite, c->b[0].as<uint8_t>(), c->b[1].as<uint64_t>(), c->b[2].as<uint8_t>(),
-                                   c->b[3].as<uint64_t>(), m, c->b[4].as<uint8_t>(), c->b[5].as<uint8_t>(),
-                                   c->b[6].as<uint8_t>(), c->stream);
-        if (lrc) {
-            msg = hip_msg(hipGetLastError(), "tx verify launch");
-            return lrc;
-        }
-        if (root32 && p.levels > 0) {
-            SHARD_HIP(c->b[7].ensure(64 * ((m + width - 1) / width)));
-            SHARD_HIP(c->b[8].ensure(32 * p.count(k)));
-            lrc = launch_merkle_levels(hasher, width, c->b[4].as<uint8_t>(), m, p.levels, c->b[7].as<uint8_t>(),
-                                       c->b[8].as<uint8_t>(), c->stream);
-            if (lrc) {
-                msg = hip_msg(hipGetLastError(), "merkle frontier launch");
-                return lrc;
+        // the shard's level-L frontier (or its hashes, L = 0), queued behind the last chunk's kernel
+        PipeTail tail = [&](TxPipe& q, const uint8_t* d_hash, std::string& m2) -> int {
+            if (!root32) return 0;
+            if (p.levels == 0) {
+                frontier[k] = d_hash;
+                return 0;
             }
-            frontier[k] = c->b[8].as<uint8_t>();
-        } else if (root32) {
-            frontier[k] = c->b[4].as<uint8_t>();  // L = 0: the tx hashes are the frontier
-        }
-        SHARD_HIP(hipMemcpyAsync(txhash32 + 32 * lo, c->b[4].p, m * 32, hipMemcpyDeviceToHost, c->stream));
-        SHARD_HIP(hipMemcpyAsync(sender20 + 20 * lo, c->b[5].p, m * 20, hipMemcpyDeviceToHost, c->stream));
-        SHARD_HIP(hipMemcpyAsync(status + lo, c->b[6].p, m, hipMemcpyDeviceToHost, c->stream));
-        SHARD_HIP(hipStreamSynchronize(c->stream));
-        return 0;
+            if (q.b[5].ensure(64 * ((m + width - 1) / width)) != hipSuccess || q.b[6].ensure(32 * p.count(k)) != hipSuccess) {
+                m2 = "frontier buffers: out of device memory";
+                return BCOSGPU_E_HIP;
+            }
+            const int lrc = launch_merkle_levels(hasher, width, d_hash, m, p.levels, q.b[5].as<uint8_t>(),
+                                                 q.b[6].as<uint8_t>(), q.compute);
+            if (lrc) m2 = hip_msg(hipGetLastError(), "merkle frontier launch");
+            frontier[k] = q.b[6].as<uint8_t>();
+            return lrc;
+        };
+        return tx_pipeline(c, host_range(suite, pre, pre_off, sig, sig_off, lo, hi, txhash32, sender20, status), tail, msg);
     });
     if (rc || !root32) return rc;
     return gather_root(devices, ndev, p, frontier, hasher, width, top, root32);
 }
 
 // Many blocks at once over the device set (a sync catch-up or a replay: configs[4]): whole blocks per
-// device, contiguous ranges balanced by tx count; each device verifies its txs and computes its blocks'
-// roots with the many-tree level kernel (launch_merkle_roots_batch); no exchange.
+// device, contiguous ranges balanced by tx count; each device verifies its txs through the chunked
+// pipeline and computes its blocks' roots with the many-tree level kernel (launch_merkle_roots_batch)
+// behind the last chunk; no exchange.
 int blocks_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const uint64_t* pre_off, const uint8_t* sig,
                  const uint64_t* sig_off, const uint64_t* block_off, size_t nblocks, int width, uint8_t* txhash32,
                  uint8_t* sender20, uint8_t* status, uint8_t* roots32) {
@@ -375,9 +383,8 @@ int blocks_multi(const int* devices, int ndev, int suite, const uint8_t* pre, co
     const uint64_t n = block_off[nblocks];
     if (n && (!pre || !pre_off || !sig || !sig_off || !txhash32 || !sender20 || !status))
         return api_set_err(BCOSGPU_E_ARG, "null pointer");
-    for (uint64_t i = 0; i < n; ++i)
-        if (pre_off[i + 1] < pre_off[i] || sig_off[i + 1] < sig_off[i] || pre_off[i + 1] - pre_off[i] > 0xFFFFFFFFull)
-            return api_set_err(BCOSGPU_E_ARG, "offsets must be non-decreasing");
+    if (n && (pre_off[n] < pre_off[0] || sig_off[n] < sig_off[0]))
+        return api_set_err(BCOSGPU_E_ARG, "offsets must be non-decreasing");  // (each shard's pipeline checks the rest)
     if (int rc = check_set(devices, ndev)) return rc;
     const int hasher = suite == BCOSGPU_SUITE_SM2 ? BCOSGPU_SM3 : BCOSGPU_KECCAK256;
     // block ranges [bl[k], bl[k + 1]): device k's share ends at the first block boundary past (k + 1) n / ndev
@@ -389,63 +396,34 @@ int blocks_multi(const int* devices, int ndev, int suite, const uint8_t* pre, co
         while (b < nblocks && block_off[b] < want) ++b;
         bl[k] = b;
     }
-    std::vector<ShardCtx*> ctx = contexts(devices, ndev);
-    auto locks = lock_all(ctx);
+    Pipes pipes;
+    if (int rc = pipes.acquire(devices, ndev)) return rc;
     return run_shards(ndev, [&](int k, std::string& msg) -> int {
-        const size_t b0 = bl[k], b1 = bl[k + 1];
-        if (b0 == b1) return 0;
+        const size_t b0 = bl[k], b1 = bl[k + 1], nb = b1 - b0;
+        if (nb == 0) return 0;
         const uint64_t lo = block_off[b0], hi = block_off[b1], m = hi - lo;
-        ShardCtx* c = ctx[k];
-        DeviceGuard dg(c->device);
+        if (m == 0) {  // only empty blocks: zero roots (BlockImpl.h:114-119)
+            std::memset(roots32 + 32 * b0, 0, 32 * nb);
+            return 0;
+        }
+        TxPipe& c = *pipes.p[k];
+        DeviceGuard dg(c.device);
         SHARD_HIP(dg.err);
-        SHARD_HIP(ensure_stream(c));
-        const uint64_t pb = m ? pre_off[lo] : 0, pbytes = m ? pre_off[hi] - pb : 0;
-        const uint64_t sb = m ? sig_off[lo] : 0, sbytes = m ? sig_off[hi] - sb : 0;
-        const size_t nb = b1 - b0;
-        SHARD_HIP(c->b[0].ensure(pbytes + 8));
-        SHARD_HIP(c->b[1].ensure((m + 1) * 8));
-        SHARD_HIP(c->b[2].ensure(sbytes + 8));
-        SHARD_HIP(c->b[3].ensure((m + 1) * 8));
-        SHARD_HIP(c->b[4].ensure(m * 32 + 32));
-        SHARD_HIP(c->b[5].ensure(m * 20 + 4));
-        SHARD_HIP(c->b[6].ensure(m + 4));
-        SHARD_HIP(c->b[7].ensure(merkle_roots_work_bytes(m, nb, width)));
-        SHARD_HIP(c->b[8].ensure(nb * 32));
         std::vector<uint64_t> boff(nb + 1);
         for (size_t b = 0; b <= nb; ++b) boff[b] = block_off[b0 + b] - lo;
-        if (m) {
-            std::vector<uint64_t> po(m + 1), so(m + 1);
-            for (uint64_t i = 0; i <= m; ++i) {
-                po[i] = pre_off[lo + i] - pb;
-                so[i] = sig_off[lo + i] - sb;
-            }
-            SHARD_HIP(hipMemcpyAsync(c->b[0].p, pre + pb, pbytes, hipMemcpyHostToDevice, c->stream));
-            SHARD_HIP(hipMemcpyAsync(c->b[1].p, po.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
-            SHARD_HIP(hipMemcpyAsync(c->b[2].p, sig + sb, sbytes, hipMemcpyHostToDevice, c->stream));
-            SHARD_HIP(hipMemcpyAsync(c->b[3].p, so.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
-            const int lrc = launch_tx_verify(suite, c->b[0].as<uint8_t>(), c->b[1].as<uint64_t>(), c->b[2].as<uint8_t>(),
-                                             c->b[3].as<uint64_t>(), m, c->b[4].as<uint8_t>(), c->b[5].as<uint8_t>(),
-                                             c->b[6].as<uint8_t>(), c->stream);
-            if (lrc) {
-                msg = hip_msg(hipGetLastError(), "tx verify launch");
-                return lrc;
-            }
-            // (the pageable po / so must outlive their copies: wait before they go out of scope)
-            SHARD_HIP(hipStreamSynchronize(c->stream));
-        }
-        const int rrc = launch_merkle_roots_batch(hasher, width, c->b[4].as<uint8_t>(), boff.data(), nb,
-                                                  c->b[7].as<uint8_t>(), c->b[8].as<uint8_t>(), c->stream);
-        if (rrc) {
-            msg = hip_msg(hipGetLastError(), "merkle roots launch");
+        SHARD_HIP(c.b[5].ensure(merkle_roots_work_bytes(m, nb, width)));
+        SHARD_HIP(c.b[6].ensure(nb * 32));
+        PipeTail tail = [&](TxPipe& q, const uint8_t* d_hash, std::string& m2) -> int {
+            const int rrc = launch_merkle_roots_batch(hasher, width, d_hash, boff.data(), nb, q.b[5].as<uint8_t>(),
+                                                      q.b[6].as<uint8_t>(), q.compute);
+            if (rrc) m2 = hip_msg(hipGetLastError(), "merkle roots launch");
             return rrc;
-        }
-        if (m) {
-            SHARD_HIP(hipMemcpyAsync(txhash32 + 32 * lo, c->b[4].p, m * 32, hipMemcpyDeviceToHost, c->stream));
-            SHARD_HIP(hipMemcpyAsync(sender20 + 20 * lo, c->b[5].p, m * 20, hipMemcpyDeviceToHost, c->stream));
-            SHARD_HIP(hipMemcpyAsync(status + lo, c->b[6].p, m, hipMemcpyDeviceToHost, c->stream));
-        }
-        SHARD_HIP(hipMemcpyAsync(roots32 + 32 * b0, c->b[8].p, nb * 32, hipMemcpyDeviceToHost, c->stream));
-        SHARD_HIP(hipStreamSynchronize(c->stream));
+        };
+        const int rc = tx_pipeline(c, host_range(suite, pre, pre_off, sig, sig_off, lo, hi, txhash32, sender20, status),
+                                   tail, msg);
+        if (rc) return rc;
+        SHARD_HIP(hipMemcpyAsync(roots32 + 32 * b0, c.b[6].p, nb * 32, hipMemcpyDeviceToHost, c.copy));
+        SHARD_HIP(hipStreamSynchronize(c.copy));
         return 0;
     });
 }

@@ -1,0 +1,290 @@
+// txpipe.hip -- the host-pointer tx-verify batches (bcosgpu_tx_verify_batch, the device-set shards of
+// multi.hip) as a copy / compute pipeline.  The reference hands its batch sites host memory
+// (TransactionSync.cpp:516-548 verifies a downloaded vector of transactions, BlockImpl.h:111-154 roots
+// the block's hashes), so every such call pays PCIe both ways.  Measured on MI355X
+// (tools/copybench.hip, profiles/r06_copybench.json): a pageable hipMemcpyAsync reaches the pinned rate
+// (~56 GB/s) from ~27 MB up, returns only when its data has moved, and overlaps a kernel running on
+// another stream.  So a batch is cut into chunks of one full round of the one-lane kernel at occupancy 2
+// (512 txs per CU); while chunk k's kernel runs, the host thread copies chunk k+1 in and chunk k-1's
+// results out, and only the first chunk's upload and the last chunk's download stay exposed.  Chunks
+// alternate between two compute streams, so a chunk's kernel can start in the previous one's tail.
+//
+//  - Device buffers hold the whole range, so no chunk ever overwrites a buffer in use: chunk k's inputs go
+//    to their final place, its kernel reads them through the range's own offsets (the device preimage
+//    pointer is pre_off[lo] bytes before the buffer, so offsets need no host rebasing), its outputs land
+//    at k's rows.
+//  - Large batches: pageable H2D straight from the caller on the copy stream (the host blocks while they
+//    move, i.e. while the previous chunk computes), an event, the chunk's compute stream waits on it;
+//    once chunk k-1's kernel event has completed, pageable D2H straight into the caller's arrays (so no
+//    copy waits on the GPU while holding the host thread).
+//  - Small batches (<= 65536 txs, one launch: C2's 10k): staged through pinned memory on one stream, the
+//    signatures and offsets gathered while the preimages' DMA runs, one DMA of the outputs back (three
+//    pageable D2H of a 10k batch cost ~65 us, profiles/r06_pipe_trace_10k.txt).
+//  - Pipelines come from a per-device pool: concurrent callers (the reference's verifier pools,
+//    TxPool.h:48-49) each get their own streams and buffers, so their round trips overlap instead of
+//    serialising behind one workspace mutex.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+#include "engine.h"
+
+namespace bcosgpu {
+
+hipError_t PipeBuf::ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    const hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+}
+
+hipError_t PipeHostBuf::ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = bytes < 65536 ? 65536 : bytes + bytes / 4;
+    const hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+}
+
+namespace {
+
+std::mutex g_pool_mu;
+std::vector<std::vector<TxPipe*>> g_free;  // per device; pipes are never freed (no teardown races)
+
+struct DevGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DevGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            (void)hipGetLastError();
+            prev = -1;
+        }
+        if (prev != dev) err = hipSetDevice(dev);
+    }
+    ~DevGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+hipError_t ensure_events(TxPipe& p, size_t need) {
+    while (p.ev.size() < need) {
+        hipEvent_t e;
+        const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        if (r != hipSuccess) return r;
+        p.ev.push_back(e);
+    }
+    return hipSuccess;
+}
+
+#define PIPE_HIP(call)                                               \
+    do {                                                             \
+        const hipError_t e_ = (call);                                \
+        if (e_ != hipSuccess) {                                      \
+            msg = std::string(#call) + ": " + hipGetErrorString(e_); \
+            return BCOSGPU_E_HIP;                                    \
+        }                                                            \
+    } while (0)
+
+}  // namespace
+
+TxPipe* tx_pipe_acquire(int device) {
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        if (device >= 0 && static_cast<size_t>(device) < g_free.size() && !g_free[device].empty()) {
+            TxPipe* p = g_free[device].back();
+            g_free[device].pop_back();
+            return p;
+        }
+    }
+    DevGuard dg(device);
+    if (dg.err != hipSuccess) return nullptr;
+    TxPipe* p = new TxPipe();
+    p->device = device;
+    if (hipStreamCreateWithFlags(&p->compute, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&p->compute2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&p->copy, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;  // (a pipe without streams is dropped; the caller reports the failure)
+    }
+    return p;
+}
+
+void tx_pipe_release(TxPipe* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (g_free.size() <= static_cast<size_t>(p->device)) g_free.resize(p->device + 1);
+    g_free[p->device].push_back(p);
+}
+
+uint64_t tx_pipe_chunk(uint64_t m) {
+    // BCOSGPU_PIPE_CHUNK (read per call; a test hook): force a chunk size, so chunk boundaries can be
+    // tested at oracle-sized batches
+    if (const char* e = std::getenv("BCOSGPU_PIPE_CHUNK")) {
+        const long long v = std::atoll(e);
+        if (v > 0) return std::min<uint64_t>(m, std::max<uint64_t>(static_cast<uint64_t>(v), (m + 4095) / 4096));
+    }
+    const uint64_t cus = static_cast<uint64_t>(cu_count());
+    const uint64_t c = 512 * cus;  // one round of the occupancy-2 one-lane kernel
+    // below two rounds one launch: its kernel choice beats chunks (two co-running halves of C2's 10k
+    // trio round measured 0.604 ms against 0.557 for one launch, profiles/r06_hostpath_probe.json: the
+    // second half's launch waits for its inputs and its trio round is as long as the whole batch's)
+    return m >= 2 * c ? c : m;
+}
+
+namespace {
+// One launch of a small batch (<= 65536 txs, one chunk), staged through pinned memory on ONE stream (no
+// cross-stream events: an event wait added ~16 us before the kernel started).  Device layout =
+// pinned layout: [preimages | signatures | pad | pre_off[m+1] | sig_off[m+1]] and the outputs
+// [txhash | sender | status].  The host copies the preimages into the staging buffer, starts their DMA,
+// copies the signatures and offsets while it runs and starts the second DMA; kernel, the follow-on tail,
+// one D2H of the outputs, one synchronisation, three host copies out.
+int tx_small(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::string& msg) {
+    const uint64_t lo = t.lo, hi = t.hi, m = hi - lo;
+    for (uint64_t i = lo; i < hi; ++i)
+        if (t.pre_off[i + 1] < t.pre_off[i] || t.sig_off[i + 1] < t.sig_off[i] ||
+            t.pre_off[i + 1] - t.pre_off[i] > 0xFFFFFFFFull) {
+            msg = "offsets must be non-decreasing";
+            return BCOSGPU_E_ARG;
+        }
+    const uint64_t pb = t.pre_off[lo], pbytes = t.pre_off[hi] - pb;
+    const uint64_t sb = t.sig_off[lo], sbytes = t.sig_off[hi] - sb;
+    const uint64_t spo = (pbytes + sbytes + 15) & ~7ull, sso = spo + 8 * (m + 1), total = sso + 8 * (m + 1);
+    PIPE_HIP(p.b[0].ensure(total));
+    PIPE_HIP(p.b[4].ensure(53 * m + 8));
+    PIPE_HIP(p.hin.ensure(total));
+    PIPE_HIP(p.host.ensure(53 * m));
+    uint8_t* h = p.hin.as<uint8_t>();
+    uint8_t* d = p.b[0].as<uint8_t>();
+    hipStream_t st = p.compute;
+    std::memcpy(h, t.pre + pb, pbytes);
+    if (pbytes) PIPE_HIP(hipMemcpyAsync(d, h, pbytes, hipMemcpyHostToDevice, st));
+    std::memcpy(h + pbytes, t.sig + sb, sbytes);
+    std::memcpy(h + spo, t.pre_off + lo, 8 * (m + 1));
+    std::memcpy(h + sso, t.sig_off + lo, 8 * (m + 1));
+    PIPE_HIP(hipMemcpyAsync(d + pbytes, h + pbytes, total - pbytes, hipMemcpyHostToDevice, st));
+    uint8_t* d_out = p.b[4].as<uint8_t>();
+    const int lrc = launch_tx_verify(t.suite, d - pb, reinterpret_cast<const uint64_t*>(d + spo), d + pbytes - sb,
+                                     reinterpret_cast<const uint64_t*>(d + sso), m, d_out, d_out + 32 * m,
+                                     d_out + 52 * m, st);
+    if (lrc) {
+        msg = std::string("tx verify launch: ") + hipGetErrorString(hipGetLastError());
+        return lrc;
+    }
+    if (tail)
+        if (int rc = tail(p, d_out, msg)) return rc;
+    uint8_t* o = p.host.as<uint8_t>();
+    PIPE_HIP(hipMemcpyAsync(o, d_out, 53 * m, hipMemcpyDeviceToHost, st));
+    PIPE_HIP(hipStreamSynchronize(st));
+    std::memcpy(t.txhash32 + 32 * lo, o, 32 * m);
+    std::memcpy(t.sender20 + 20 * lo, o + 32 * m, 20 * m);
+    std::memcpy(t.status + lo, o + 52 * m, m);
+    return 0;
+}
+}  // namespace
+
+int tx_pipeline(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::string& msg) {
+    const uint64_t lo = t.lo, hi = t.hi, m = hi - lo;
+    if (m == 0) return 0;
+    // offsets are validated chunk by chunk, right before the chunk is sent (for 1M txs the 16 MB of offsets
+    // take ~0.5 ms to check: that check now overlaps the previous chunk's kernel); the endpoints size the
+    // device buffers, so they are checked first
+    if (t.pre_off[hi] < t.pre_off[lo] || t.sig_off[hi] < t.sig_off[lo]) {
+        msg = "offsets must be non-decreasing";
+        return BCOSGPU_E_ARG;
+    }
+    const uint64_t chunk = tx_pipe_chunk(m);
+    bool small = m <= 65536 && chunk == m;
+    if (const char* e = std::getenv("BCOSGPU_PIPE_STAGED")) small = small && e[0] != '0';  // A/B hook
+    if (small) return tx_small(p, t, tail, msg);
+    const uint64_t pb = t.pre_off[lo], pbytes = t.pre_off[hi] - pb;
+    const uint64_t sb = t.sig_off[lo], sbytes = t.sig_off[hi] - sb;
+    // outputs contiguous: txhash [m][32] | sender [m][20] | status [m]  (sender stays 4-byte aligned)
+    PIPE_HIP(p.b[0].ensure(pbytes + 8));
+    PIPE_HIP(p.b[1].ensure((m + 1) * 8));
+    PIPE_HIP(p.b[2].ensure(sbytes + 8));
+    PIPE_HIP(p.b[3].ensure((m + 1) * 8));
+    PIPE_HIP(p.b[4].ensure(53 * m + 8));
+    const uint64_t nchunks = (m + chunk - 1) / chunk;
+    PIPE_HIP(ensure_events(p, 2 * nchunks));
+    // device views of the whole range: the byte buffers shifted back by the range's first offset, so the
+    // caller's offsets index them directly
+    const uint8_t* d_pre = p.b[0].as<uint8_t>() - pb;
+    const uint8_t* d_sig = p.b[2].as<uint8_t>() - sb;
+    uint64_t* d_po = p.b[1].as<uint64_t>();
+    uint64_t* d_so = p.b[3].as<uint64_t>();
+    uint8_t* d_out = p.b[4].as<uint8_t>();
+    uint8_t *d_hash = d_out, *d_snd = d_out + 32 * m, *d_st = d_out + 52 * m;
+    hipStream_t cs[2] = {p.compute, p.compute2};
+    if (const char* e = std::getenv("BCOSGPU_PIPE_STREAMS"))  // A/B hook: 1 = every chunk on one stream
+        if (e[0] == '1') cs[1] = p.compute;
+    auto drain = [&](uint64_t k) -> int {  // the large path: chunk k's outputs once its kernel is done
+        const uint64_t a = k * chunk, e = std::min(m, a + chunk), c = e - a;
+        PIPE_HIP(hipEventSynchronize(p.ev[2 * k + 1]));
+        PIPE_HIP(hipMemcpyAsync(t.txhash32 + 32 * (lo + a), d_hash + 32 * a, 32 * c, hipMemcpyDeviceToHost, p.copy));
+        PIPE_HIP(hipMemcpyAsync(t.sender20 + 20 * (lo + a), d_snd + 20 * a, 20 * c, hipMemcpyDeviceToHost, p.copy));
+        PIPE_HIP(hipMemcpyAsync(t.status + lo + a, d_st + a, c, hipMemcpyDeviceToHost, p.copy));
+        return 0;
+    };
+    for (uint64_t k = 0; k < nchunks; ++k) {
+        const uint64_t a = k * chunk, e = std::min(m, a + chunk), c = e - a;
+        const uint64_t ga = lo + a, ge = lo + e;  // the chunk in the caller's indexing
+        for (uint64_t i = ga; i < ge; ++i)
+            if (t.pre_off[i + 1] < t.pre_off[i] || t.sig_off[i + 1] < t.sig_off[i] ||
+                t.pre_off[i + 1] - t.pre_off[i] > 0xFFFFFFFFull || t.pre_off[i + 1] > t.pre_off[hi] ||
+                t.sig_off[i + 1] > t.sig_off[hi]) {
+                (void)hipStreamSynchronize(cs[0]);  // the chunks already launched finish before the error returns
+                (void)hipStreamSynchronize(cs[1]);
+                (void)hipStreamSynchronize(p.copy);
+                msg = "offsets must be non-decreasing";
+                return BCOSGPU_E_ARG;
+            }
+        const uint64_t p0 = t.pre_off[ga], p1 = t.pre_off[ge], s0 = t.sig_off[ga], s1 = t.sig_off[ge];
+        hipStream_t st = cs[k & 1];
+        // pageable copies straight from the caller (they return once their data has moved)
+        if (p1 > p0)
+            PIPE_HIP(hipMemcpyAsync(p.b[0].as<uint8_t>() + (p0 - pb), t.pre + p0, p1 - p0, hipMemcpyHostToDevice,
+                                    p.copy));
+        if (s1 > s0)
+            PIPE_HIP(hipMemcpyAsync(p.b[2].as<uint8_t>() + (s0 - sb), t.sig + s0, s1 - s0, hipMemcpyHostToDevice,
+                                    p.copy));
+        PIPE_HIP(hipMemcpyAsync(d_po + a, t.pre_off + ga, (c + 1) * 8, hipMemcpyHostToDevice, p.copy));
+        PIPE_HIP(hipMemcpyAsync(d_so + a, t.sig_off + ga, (c + 1) * 8, hipMemcpyHostToDevice, p.copy));
+        PIPE_HIP(hipEventRecord(p.ev[2 * k], p.copy));
+        PIPE_HIP(hipStreamWaitEvent(st, p.ev[2 * k], 0));
+        const int lrc = launch_tx_verify(t.suite, d_pre, d_po + a, d_sig, d_so + a, c, d_hash + 32 * a, d_snd + 20 * a,
+                                         d_st + a, st);
+        if (lrc) {
+            msg = std::string("tx verify launch: ") + hipGetErrorString(hipGetLastError());
+            return lrc;
+        }
+        PIPE_HIP(hipEventRecord(p.ev[2 * k + 1], st));
+        if (k + 1 == nchunks) {
+            // compute stream 0 joins the other stream's last chunk, then the follow-on kernels over the
+            // whole range's hashes (roots, frontier)
+            if (nchunks >= 2) {
+                const uint64_t j = (k & 1) ? k : k - 1;  // the last chunk that ran on stream 1
+                PIPE_HIP(hipStreamWaitEvent(cs[0], p.ev[2 * j + 1], 0));
+            }
+            if (tail)
+                if (int rc = tail(p, d_hash, msg)) return rc;
+        }
+        if (k >= 1)
+            if (int rc = drain(k - 1)) return rc;
+    }
+    if (int rc = drain(nchunks - 1)) return rc;
+    PIPE_HIP(hipStreamSynchronize(p.copy));
+    PIPE_HIP(hipStreamSynchronize(cs[0]));
+    PIPE_HIP(hipStreamSynchronize(cs[1]));
+    return 0;
+}
+
+}  // namespace bcosgpu
