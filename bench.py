@@ -250,6 +250,52 @@ def _block_plan(nblocks, world, rank):
     return min(rank * per, nblocks), min((rank + 1) * per, nblocks)
 
 
+def launcher_selftest_plans(ctx, dist):
+    """The multi-rank plumbing of the GPU run, on the CPU (gloo): every rank derives its C4 shard exactly as
+    run_leg does (parallel.choose_levels / shard_plan: width^L-aligned tx ranges of configs[3]'s 1M txs) and
+    its C5 block range (_block_plan over configs[4]'s 64 blocks), builds its level-L frontier over stand-in
+    leaves (leaf i = blake2b-256 of i; a stand-in hash, this checks the plan and the gather, not Keccak --
+    blake2b also builds the levels), and the frontiers go through parallel.sharded_merkle_root's
+    count-prefixed all-gather as on RCCL; rank 0 reports every rank's ranges, the gathered root, the
+    device list the one-process device-set legs would take and the per-GPU kernel choice at C4."""
+    import hashlib as hl
+    import torch
+    from bcos_gpu import parallel
+    world, rank = ctx.world, ctx.rank
+    n4, width = WORKLOADS["c4"]["n"], 2
+    levels = parallel.choose_levels(n4, world, width)
+    plan = parallel.shard_plan(n4, world, width, levels)
+
+    def h2(x):
+        return hl.blake2b(x, digest_size=32).digest()
+
+    def frontier_fn(lo, hi):
+        cur = [h2(i.to_bytes(8, "little")) for i in range(lo, hi)]
+        for _ in range(levels):
+            cur = [h2(b"".join(cur[k:k + width])) for k in range(0, len(cur), width)]
+        return torch.tensor(list(b"".join(cur)), dtype=torch.uint8).view(-1, 32)
+
+    def root_fn(frontier):
+        cur = [bytes(r.tolist()) for r in frontier]
+        while len(cur) > 1:
+            cur = [h2(b"".join(cur[k:k + width])) for k in range(0, len(cur), width)]
+        return torch.tensor(list(cur[0]), dtype=torch.uint8)
+    root = parallel.sharded_merkle_root(frontier_fn, root_fn, n4, width, levels, rank, world, "cpu")
+    blo, bhi = _block_plan(WORKLOADS["c5"]["blocks"], world, rank)
+    mine = torch.tensor([plan[rank][0], plan[rank][1], blo, bhi], dtype=torch.int64)
+    allr = [torch.zeros(4, dtype=torch.int64) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(allr, mine)
+    else:
+        allr = [mine]
+    per = plan[0][1] - plan[0][0]
+    return {"c4": {"levels": levels, "block": width ** levels, "ranges": [[int(x[0]), int(x[1])] for x in allr],
+                   "per_gpu_txs": per, "kernel_per_gpu": _kernel_name(0, per),
+                   "standin_root_blake2b": bytes(root.tolist()).hex()},
+            "c5": {"block_ranges": [[int(x[2]), int(x[3])] for x in allr]},
+            "devset": list(range(world)) if world > 1 else [0, 0]}
+
+
 def spawn_ranks(args):
     """--gpus N without a launcher: run this script under torch.distributed.run (one process per GPU,
     RCCL rendezvous on 127.0.0.1) as a child -- before this process touches the GPU -- and return its
@@ -1220,8 +1266,10 @@ def main():
             dist.init_process_group("gloo")
         ctx = Ctx(world, rank, dist)
         slowest = ctx.max(rank)
+        rec = launcher_selftest_plans(ctx, dist)
         if rank == 0:
-            print(json.dumps({"n_gpus": world, "max_over_ranks": slowest, "launcher_selftest": True}), flush=True)
+            print(json.dumps({"n_gpus": world, "max_over_ranks": slowest, "launcher_selftest": True, **rec}),
+                  flush=True)
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()

@@ -199,8 +199,12 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
     const int vsuite = kind == kSigJobVerifySM2 ? BCOSGPU_SUITE_SM2 : BCOSGPU_SUITE_SECP256K1;
     if (verify) {
         const uint8_t* pubs = kind == kSigJobVerifySM2 ? in + 32 * n + 64 : in;
+        // only calls that name their keys (SignatureCrypto::verify: the sealer path) promote keys; SM2 recover
+        // (admission: the key is the sender's, embedded in the signature) only looks them up
+        bool named = true;
+        for (SigJob* j : batch) named = named && (kind == kSigJobVerifyK1 || j->pub64 != nullptr);
         const int krc = keyed_slots(vsuite, pubs, kind == kSigJobVerifySM2 ? 128 : 64, n,
-                                    reinterpret_cast<int32_t*>(in + slots_at), false, &keyed, slot.stream, &gen);
+                                    reinterpret_cast<int32_t*>(in + slots_at), false, &keyed, slot.stream, &gen, named);
         if (krc) keyed = false;  // a failed table build leaves the generic path
     }
     if (!zero_copy) BATCH_HIP(hipMemcpyAsync(slot.d_in, slot.h_in, in_bytes, hipMemcpyHostToDevice, slot.stream));

@@ -24,11 +24,15 @@
 // pick u1, u2 so that two partial sums coincide.
 //
 // Host side: a per-(device, suite) cache of key tables, filled by bcosgpu_register_keys (the node's
-// consensus list) and by promotion of keys seen in three calls; never evicted while the process runs
-// (bcosgpu_clear_keys drains the device first), so a table is never rewritten under a launch that reads
-// it.  The coalesced host-pointer verify calls take this path when every key of the batch is cached.
+// consensus list) and by promotion of keys named in three verify calls (counted once per call; SM2
+// recover -- admission, the sender's own key -- never promotes; at most 16 builds a call, in at most half
+// the capacity); never evicted while the process runs (bcosgpu_clear_keys drains the device first), so a
+// table is never rewritten under a launch that reads it.  Slot ids carry the cache generation: an id from
+// before a clear fails in the kernel instead of naming whichever key now has its index.  The coalesced
+// host-pointer verify calls take this path when every key of the batch is cached.
 #include <array>
 #include <unordered_map>
+#include <unordered_set>
 #include "ecc_device.h"
 
 namespace bcosgpu {
@@ -273,7 +277,7 @@ __device__ __forceinline__ void keyed_add_entry(JacP26& acc, const uint32_t* tab
 // key's SM3 address) may be null.  One 64-thread workgroup = 4 signatures.
 template <int SUITE>
 __global__ __launch_bounds__(64) void sig_verify_keyed_kernel(const uint32_t* __restrict__ arena, uint32_t cap,
-                                                              const int32_t* __restrict__ slots,
+                                                              uint32_t gen15, const int32_t* __restrict__ slots,
                                                               const uint8_t* __restrict__ hash,
                                                               const uint8_t* __restrict__ sig, uint32_t stride,
                                                               uint64_t n, const uint32_t* __restrict__ gtab, int gbits,
@@ -283,9 +287,12 @@ __global__ __launch_bounds__(64) void sig_verify_keyed_kernel(const uint32_t* __
     const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * 4u + (lane >> 4);
     const bool live = i0 < n;
     const uint64_t i = live ? i0 : n - 1;  // a spare row re-runs the last signature (nothing stored)
+    // a slot id is (generation << 16) | index (keyed_slots): an id handed out before a bcosgpu_clear_keys
+    // names an old generation and fails here, even once its index holds another key's table
     const int32_t sl = slots[i];
-    const bool slot_ok = sl >= 0 && static_cast<uint32_t>(sl) < cap;
-    const uint32_t* key = arena + static_cast<size_t>(slot_ok ? sl : 0) * kKeySlotWords;
+    const uint32_t idx = static_cast<uint32_t>(sl) & 0xFFFFu;
+    const bool slot_ok = sl >= 0 && (static_cast<uint32_t>(sl) >> 16) == gen15 && idx < cap;
+    const uint32_t* key = arena + static_cast<size_t>(slot_ok ? idx : 0) * kKeySlotWords;
     const uint32_t* ktab = key + kKeyHdrWords;
     fe h;
     load_be256(h, hash + 32 * i);
@@ -451,6 +458,14 @@ int capacity_env() {
     return cap;
 }
 
+// the 15-bit generation tag of public slot ids: id = (tag << 16) | index (capacity <= 65536 keys)
+inline uint32_t gen_tag(uint64_t gen) { return static_cast<uint32_t>(gen & 0x7FFFu); }
+inline int32_t slot_id(uint64_t gen, int32_t index) { return static_cast<int32_t>((gen_tag(gen) << 16) | uint32_t(index)); }
+
+// tables built by promotion in one call at most: a build runs synchronously under the cache mutex, so
+// this bounds the stall one batch can cause every caller of the device
+constexpr int kPromoteBuildsPerCall = 16;
+
 int promote_after() {
     static const int k = [] {
         // calls that must see a key before it is cached (0 = never).  3: a sealer's key is cached by its
@@ -529,10 +544,14 @@ int build_keys(KeyCache& c, int suite, const std::vector<Key64>& todo, std::vect
 
 }  // namespace
 
-// Slots of n keys (pub i at pubs + pub_stride * i) on the current device; keys not cached are built when
-// `force`, or when seen in promote_after() calls.  Returns 0 and *all = every key has a slot, or < 0.
+// Slot ids of n keys (pub i at pubs + pub_stride * i) on the current device; keys not cached are built
+// when `force` (registration), or -- when `promote` -- once seen in promote_after() calls.  A key counts
+// once per call however often it occurs in it, and only calls that name their keys explicitly promote
+// (the sealer path: SignatureCrypto::verify(pub, ...)); admission (SM2 recover, whose key is the
+// sender's) only looks keys up.  At most kPromoteBuildsPerCall tables are built per call.  Ids carry the
+// cache generation (slot_id).  Returns 0 and *all = every key has a slot, or < 0.
 int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int32_t* out, bool force, bool* all,
-                hipStream_t st, uint64_t* gen) {
+                hipStream_t st, uint64_t* gen, bool promote) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BCOSGPU_E_NODEV;
     *all = false;
@@ -543,25 +562,42 @@ int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int
     KeyCache& c = *cache_of(dev, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
     std::lock_guard<std::mutex> g(c.mu);
     if (gen) *gen = c.gen;
-    if (!force && c.slot_of.empty() && promote_after() <= 0) return 0;
+    promote = promote && !force && promote_after() > 0;
+    if (!force && c.slot_of.empty() && !promote) return 0;
     std::vector<Key64> todo;
     std::vector<size_t> todo_at;
+    std::unordered_set<Key64, Key64Hash> first, counted;  // this call's keys being built / already counted
     bool every = true;
     for (size_t i = 0; i < n; ++i) {
         Key64 k;
         std::memcpy(k.data(), pubs + pub_stride * i, 64);
         auto it = c.slot_of.find(k);
         if (it != c.slot_of.end()) {
-            out[i] = it->second;
+            out[i] = slot_id(c.gen, it->second);
             continue;
         }
         out[i] = -1;
+        if (!force && !promote) {
+            every = false;
+            continue;
+        }
+        if (first.count(k)) {  // a repeat within this call: it follows its first occurrence's build
+            todo.push_back(k);
+            todo_at.push_back(i);
+            continue;
+        }
+        if (!force && !counted.insert(k).second) {  // counted once already in this call, not built
+            every = false;
+            continue;
+        }
         bool build = force;
-        if (!build && promote_after() > 0 && c.promoted + static_cast<int>(todo.size()) < capacity_env() / 2) {
+        if (!build && c.promoted + static_cast<int>(first.size()) < capacity_env() / 2 &&
+            static_cast<int>(first.size()) < kPromoteBuildsPerCall) {
             if (c.seen.size() > (1u << 16)) c.seen.clear();  // a bounded sketch of recent keys
             build = ++c.seen[k] >= static_cast<uint32_t>(promote_after());
         }
         if (build) {
+            first.insert(k);
             todo.push_back(k);
             todo_at.push_back(i);
         } else {
@@ -575,7 +611,7 @@ int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int
         if (rc) return rc;
         (force ? c.registered : c.promoted) += static_cast<int>(c.slot_of.size()) - before;
         for (size_t q = 0; q < todo.size(); ++q) {
-            out[todo_at[q]] = got[q];
+            out[todo_at[q]] = got[q] < 0 ? -1 : slot_id(c.gen, got[q]);
             if (got[q] < 0) every = false;
             else c.seen.erase(todo[q]);
         }
@@ -596,11 +632,12 @@ int launch_sig_verify_keyed(int suite, const int32_t* d_slots, const uint8_t* d_
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BCOSGPU_E_NODEV;
     KeyCache& c = *cache_of(dev, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
     const uint32_t* arena;
-    uint32_t cap;
+    uint32_t cap, gen15;
     {
         std::lock_guard<std::mutex> g(c.mu);
         arena = c.arena;
         cap = static_cast<uint32_t>(c.slot_of.size());
+        gen15 = gen_tag(c.gen);
     }
     if (!arena) return BCOSGPU_E_ARG;  // no key registered on this device
     const dim3 grid(static_cast<unsigned>((n + 3) / 4)), block(64);
@@ -608,13 +645,13 @@ int launch_sig_verify_keyed(int suite, const int32_t* d_slots, const uint8_t* d_
         const uint32_t* tab;
         int bits;
         if (int rc = tables_sm2_26(&tab, &bits)) return rc;
-        hipLaunchKernelGGL(sig_verify_keyed_kernel<BCOSGPU_SUITE_SM2>, grid, block, 0, st, arena, cap, d_slots, d_hash,
+        hipLaunchKernelGGL(sig_verify_keyed_kernel<BCOSGPU_SUITE_SM2>, grid, block, 0, st, arena, cap, gen15, d_slots, d_hash,
                            d_sig, stride, n, tab, bits, d_ok, d_addr);
     } else {
         const uint32_t *k1, *sm2;
         int bits;
         if (int rc = tables(&k1, &sm2, &bits)) return rc;
-        hipLaunchKernelGGL(sig_verify_keyed_kernel<BCOSGPU_SUITE_SECP256K1>, grid, block, 0, st, arena, cap, d_slots,
+        hipLaunchKernelGGL(sig_verify_keyed_kernel<BCOSGPU_SUITE_SECP256K1>, grid, block, 0, st, arena, cap, gen15, d_slots,
                            d_hash, d_sig, stride, n, k1, bits, d_ok, d_addr);
     }
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;

@@ -67,7 +67,7 @@ int launch_tx_verify(int suite, const uint8_t* d_pre, const uint64_t* d_pre_off,
 
 // ecc_keyed.hip: verification against registered keys (per-key comb tables in HBM)
 int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int32_t* out, bool force, bool* all,
-                hipStream_t st, uint64_t* gen = nullptr);
+                hipStream_t st, uint64_t* gen = nullptr, bool promote = false);
 uint64_t keyed_generation(int suite);  // of the current device's cache
 int launch_sig_verify_keyed(int suite, const int32_t* d_slots, const uint8_t* d_hash, const uint8_t* d_sig,
                             uint32_t stride, uint64_t n, uint8_t* d_ok, uint8_t* d_addr, hipStream_t st);

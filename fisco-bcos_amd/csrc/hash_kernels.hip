@@ -9,6 +9,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <mutex>
 #include <utility>
 #include <thread>
@@ -590,7 +591,22 @@ struct PerThreadSlots {
     std::vector<std::pair<size_t, size_t>> held;  // (pool, slot)
     ~PerThreadSlots() {
         if (held.empty()) return;
-        (void)hipStreamSynchronize(hipStreamPerThread);  // its last launches have reset their counters
+        // drain this thread's per-thread stream on EVERY device it held a slot on (its last launches there
+        // have reset their counters) before the slots go back: a slot is reused without a memset
+        std::vector<int> devs;
+        {
+            std::lock_guard<std::mutex> g(g_slot_mu);
+            for (auto& h : held) devs.push_back(slot_pools()[h.first].device);
+        }
+        int prev = -1;
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        std::vector<int> done;
+        for (int d : devs) {
+            if (std::find(done.begin(), done.end(), d) != done.end()) continue;
+            done.push_back(d);
+            if (hipSetDevice(d) == hipSuccess) (void)hipStreamSynchronize(hipStreamPerThread);
+        }
+        if (prev >= 0) (void)hipSetDevice(prev);
         (void)hipGetLastError();
         std::lock_guard<std::mutex> g(g_slot_mu);
         for (auto& h : held) slot_pools()[h.first].owners[h.second].kind = -1;

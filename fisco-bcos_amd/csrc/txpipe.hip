@@ -19,7 +19,7 @@
 //    copy waits on the GPU while holding the host thread).
 //  - Small batches (<= 65536 txs, one launch: C2's 10k): staged through pinned memory on one stream, the
 //    signatures and offsets gathered while the preimages' DMA runs, one DMA of the outputs back (three
-//    pageable D2H of a 10k batch cost ~65 us, profiles/r06_pipe_trace_10k.txt).
+//    pageable D2H of a 10k batch cost ~65 us, profiles/r06_pipe_trace.txt).
 //  - Pipelines come from a per-device pool: concurrent callers (the reference's verifier pools,
 //    TxPool.h:48-49) each get their own streams and buffers, so their round trips overlap instead of
 //    serialising behind one workspace mutex.

@@ -72,9 +72,10 @@ int bcosgpu_init_ex(int device, int flags);
  * read once from BCOSGPU_TXV_SPLIT / _OCC / _COOP and BCOSGPU_K1_F26 at the first init, never per launch):
  * split -1 by size (secp256k1 batches <= 2^15 run the small-batch kernels), 0 never, 1 always;
  * occupancy 0 by size (2 waves/SIMD for n >= 2^17), 1 or 2 forced; coop (secp256k1 small batches)
- * 3 the row kernel (recovery: one signature per workgroup on row-spread field elements, ecc_row.hip),
- * 2 lane-trio (default; needs field 1; with split -1 the automatic choice among row, lane-trio, pair and
- * one-lane kernels by rounds x latency), 1 cooperative-pair, 0 split (SM2: 3 and 2 lane-trio, 1 pair
+ * 3 the row kernels (one signature per workgroup on row-spread field elements, ecc_row.hip: recovery,
+ * and known-key verify through bcosgpu_verify_batch*), 2 lane-trio (default; needs field 1; with split -1
+ * the automatic choice among row, lane-trio, pair and one-lane kernels by rounds x latency),
+ * 1 cooperative-pair, 0 split (SM2: 3 the SM2 row kernel sm2_verify_row_kernel, 2 lane-trio, 1 pair
  * kernel, 0 the one-lane kernel);
  * field (secp256k1 throughput kernels) 1 the 10 x 26-bit point arithmetic (default), 0 the 8 x 32-bit
  * one, -1 unchanged.  Every variant returns identical results. */
@@ -205,19 +206,22 @@ int bcosgpu_verify_batch_dev(int suite, const uint8_t* d_pub64, const uint8_t* d
  * its multiples in HBM (512 KiB, built once), so verifying against it needs table lookups and ~7 point
  * additions instead of a variable-base multiplication (~10x shorter per signature; same verdicts).
  *   bcosgpu_register_keys: tables for n keys (pub64 + 64 i) of `suite` on `device`; slots[i] = the key's
- *     slot, or -1 when the cache is full (BCOSGPU_KEY_CACHE keys per device and suite, default 256).
- *     Returns the number of keys cached (< 0 on error).  Registering a cached key is a lookup.
+ *     slot id (opaque, >= 0), or -1 when the cache is full (BCOSGPU_KEY_CACHE keys per device and suite,
+ *     default 256).  Returns the number of keys cached (< 0 on error).  Registering a cached key is a lookup.
  *   Host-pointer verify calls (bcosgpu_verify_batch, bcosgpu_secp256k1_verify, bcosgpu_sm2_verify, the
  *     device-set batches, SM2 recover) take the registered-key kernel when every key of the coalesced
- *     batch is cached; a key seen in BCOSGPU_KEY_PROMOTE (default 3) calls is cached automatically (in at
- *     most half the capacity: the other half is kept for registrations).
- *   bcosgpu_verify_keyed_batch_dev: ok[i] = verify(key of d_slots[i], d_hash32 + 32 i, d_sig +
- *     sig_stride i) on the calling thread's device, stream-ordered; a slot that is not registered fails.
+ *     batch is cached.  A key NAMED (pub64 given: the sealer path) in BCOSGPU_KEY_PROMOTE (default 3;
+ *     0 = never) verify calls is cached automatically -- counted once per call, at most 16 new tables per
+ *     call, in at most half the capacity (the other half is kept for registrations); SM2 recover
+ *     (admission, the sender's embedded key) only looks keys up.
+ *   bcosgpu_verify_keyed_batch_dev: ok[i] = verify(key of slot id d_slots[i], d_hash32 + 32 i, d_sig +
+ *     sig_stride i) on the calling thread's device, stream-ordered; an id that names no registered key
+ *     fails (ok = 0) -- including every id handed out before a bcosgpu_clear_keys: ids carry the cache
+ *     generation, so an old id never verifies against a key registered later in the same index.
  *   bcosgpu_key_cache_info: out5 = {keys cached, capacity, verified on the keyed path, verified
  *     elsewhere, tables built}.  bcosgpu_clear_keys: drains the device, then forgets every key (a
- *     consensus membership change); slots are reassigned by later registrations (a coalesced batch that
- *     looked its keys up before the clear runs again on the generic kernels; callers of
- *     bcosgpu_verify_keyed_batch_dev must not clear while their launches are in flight). */
+ *     consensus membership change); later registrations get new ids (a coalesced batch that looked its
+ *     keys up before the clear runs again on the generic kernels). */
 int bcosgpu_register_keys(int device, int suite, const uint8_t* pub64, size_t n, int32_t* slots);
 int bcosgpu_verify_keyed_batch_dev(int suite, const int32_t* d_slots, const uint8_t* d_hash32, const uint8_t* d_sig,
                                    size_t sig_stride, size_t n, uint8_t* d_ok, void* stream);

@@ -84,3 +84,36 @@ def test_small_batch_choice_mirrors_library():
                 continue
             chosen = sweep[key]
             assert chosen <= best * 1.05, (key, chosen, best)
+
+
+def test_gpus_8_plans_and_gather():
+    """bench.py --gpus 8 as the driver's 8-GPU scaling run starts it (8 ranks spawned by the script itself,
+    rendezvous on 127.0.0.1), gloo on the CPU: the line parses with n_gpus 8; the C4 shards tile configs[3]'s
+    1M txs in width^L-aligned ranges (per-GPU batch 125k -> the one-lane kernel at occupancy 2, one partial
+    round); the C5 block ranges tile the 64 blocks; the frontier all-gather of parallel.sharded_merkle_root
+    (stand-in hash) gives the single-process root; the device-set legs would take devices 0..7."""
+    import hashlib
+    p = _run("--gpus", "8")
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["max_over_ranks"] == 7.0
+    c4 = d["c4"]
+    n, blk = 1_000_000, c4["block"]
+    assert blk == 2 ** c4["levels"] and c4["levels"] >= 1
+    rs = c4["ranges"]
+    assert len(rs) == 8 and rs[0][0] == 0 and rs[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(rs, rs[1:])) and all(r[0] % blk == 0 for r in rs)
+    assert 124_000 <= c4["per_gpu_txs"] <= 126_000
+    assert c4["kernel_per_gpu"].startswith("tx_verify_kernel<0,2")
+    br = d["c5"]["block_ranges"]
+    assert br[0][0] == 0 and br[-1][1] == 64 and all(a[1] == b[0] for a, b in zip(br, br[1:]))
+    assert d["devset"] == list(range(8))
+
+    def h2(x):
+        return hashlib.blake2b(x, digest_size=32).digest()
+    cur = [h2(i.to_bytes(8, "little")) for i in range(n)]
+    while len(cur) > 1:
+        cur = [h2(b"".join(cur[k:k + 2])) for k in range(0, len(cur), 2)]
+    assert c4["standin_root_blake2b"] == cur[0].hex()

@@ -182,6 +182,18 @@ def test_registered_key_exceptional_additions(gpu, oracle):
     assert (slots >= 0).all()
     assert np.array_equal(_keyed_dev(0, slots, h, sig), want)
     assert np.array_equal(gpu.Secp256k1Crypto().verify_batch(pubs, h, sig), want)
+    # the generic known-key kernels on the same owner-crafted cases: keys forgotten, then the row verify
+    # kernel (policy coop 3) and the lane-trio kernel (coop 2), each checked to have left the keyed path
+    for policy in ((1, 0, 3, 1), (1, 0, 2, 1)):
+        gpu.clear_keys(0)
+        gpu.set_tx_kernel_policy(*policy)
+        try:
+            k0 = gpu.key_cache_info(0)["keyed"]
+            assert np.array_equal(gpu.Secp256k1Crypto().verify_batch(pubs, h, sig), want), policy
+            assert gpu.key_cache_info(0)["keyed"] == k0, policy
+        finally:
+            gpu.set_tx_kernel_policy()
+    gpu.clear_keys(0)
 
 
 def test_promotion_single_calls_and_sm2_recover(gpu, oracle):
@@ -253,8 +265,12 @@ def test_clear_and_reregister(gpu, oracle):
         gpu.clear_keys(suite)
         assert gpu.key_cache_info(suite)["keys"] == 0
         slots_b = gpu.register_keys(suite, pb)
-        assert sorted(slots_b.tolist()) == list(range(5))  # numbering restarts: earlier slots are reused
-        assert (slots_a >= 0).all()
+        assert sorted((slots_b & 0xFFFF).tolist()) == list(range(5))  # table indices restart: reused
+        assert (slots_a >= 0).all() and not set(slots_a.tolist()) & set(slots_b.tolist())  # ids do not
+        # an id from before the clear names an old generation: it fails in the kernel even though its index
+        # now holds one of the new keys' tables (B's valid signatures through A's ids stay rejected)
+        assert not _keyed_dev(suite, slots_a, h, sb).any()
+        assert not _keyed_dev(suite, slots_a, h, sa).any()
         k0 = gpu.key_cache_info(suite)
         assert np.array_equal(crypto.verify_batch(pa, h, sa), want_a)   # forgotten: generic
         k1 = gpu.key_cache_info(suite)
@@ -262,3 +278,30 @@ def test_clear_and_reregister(gpu, oracle):
         assert np.array_equal(crypto.verify_batch(pb, h, sb), want_b)   # registered: keyed
         assert gpu.key_cache_info(suite)["keyed"] - k1["keyed"] == 5
         assert np.array_equal(_keyed_dev(suite, slots_b, h, sb), want_b)
+
+
+def test_promotion_counts_calls_not_occurrences(gpu, oracle):
+    """A key repeated within one call counts once toward promotion (three copies in one batch promote
+    nothing), and SM2 recover -- admission, whose key is the sender's own, embedded in the signature --
+    never promotes, however often a key recurs; verdicts equal the oracle's throughout."""
+    rng = np.random.default_rng(99)
+    for suite in (0, 1):
+        gpu.clear_keys(suite)
+        crypto = gpu.SM2Crypto() if suite else gpu.Secp256k1Crypto()
+        sk = _keys(rng, 2)
+        h = rng.integers(0, 256, size=(2, 32), dtype=np.uint8)
+        pub, sig, ok = _dev_sign(gpu, suite, sk, h)
+        assert ok.all()
+        rep = np.array([0, 0, 0, 1, 1, 1])
+        b0 = gpu.key_cache_info(suite)["built"]
+        assert crypto.verify_batch(pub[rep], h[rep], sig[rep]).all()
+        assert crypto.verify_batch(pub[rep], h[rep], sig[rep]).all()
+        assert gpu.key_cache_info(suite)["built"] == b0  # two calls: not yet, despite six occurrences
+        if suite == 1:  # SM2 recover with the same embedded keys, many times: lookups only
+            for _ in range(4):
+                _, addr, okr = crypto.recover_batch(h[rep], sig[rep], want_address=True)
+                assert okr.all()
+            assert gpu.key_cache_info(suite)["built"] == b0
+        assert crypto.verify_batch(pub[rep], h[rep], sig[rep]).all()  # third named call: promoted
+        assert gpu.key_cache_info(suite)["built"] - b0 == 2
+        gpu.clear_keys(suite)

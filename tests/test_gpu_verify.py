@@ -17,9 +17,10 @@ P_SECP = 2**256 - 2**32 - 977
 
 # Every kernel a verify / ecRecover batch can take (bcosgpu_set_tx_kernel_policy(split, occupancy, coop,
 # field)): the automatic choice, the lane-trio kernels (sig_verify_trio26_kernel, the SM2 trio kernel over
-# KeyIO, the recovery trio kernel over EcrecIO), the row kernel (ecRecover; known-key verify keeps the
-# lane-trio kernels under it), the pair kernels, the one-lane kernels at occupancy 1
-# and 2, and the 8 x 32-bit field variants.
+# KeyIO, the recovery trio kernel over EcrecIO), the row kernels (coop 3: ecRecover on recover_row_kernel,
+# secp256k1 known-key verify on its verify mode -- ecc_sig.hip launch_sig_verify -- and SM2 on
+# sm2_verify_row_kernel), the pair kernels, the one-lane kernels at occupancy 1 and 2, and the 8 x 32-bit
+# field variants.
 SIG_VARIANTS = {"auto": (-1, 0, 2, 1), "trio": (1, 0, 2, 1), "row": (1, 0, 3, 1), "pair": (1, 0, 1, 1),
                 "onelane_occ1": (0, 1, 2, 1), "onelane_occ2": (0, 2, 2, 1), "fe32": (-1, 0, 2, 0)}
 

@@ -168,3 +168,34 @@ def test_c4_1m_block_on_two_shards_through_cpp(gpu, oracle, tmp_path):
     r = subprocess.run([exe, data, "0,0"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "multi_test: ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_eight_entry_device_list_peer_branch(gpu, oracle, monkeypatch):
+    """The list an 8-GPU node passes, {0} x 8 on this one-GPU box, with BCOSGPU_MULTI_PEER=1 (the
+    cross-device branches: peer-access probe, hipMemcpyPeerAsync frontier gather): one block through
+    bcosgpu_block_verify_multi (8 shards, width 2 and 16) and 64 blocks of 0 .. 700 txs through
+    bcosgpu_blocks_verify_multi (whole blocks per entry) -- every hash, sender, verdict and root against the
+    oracle."""
+    from bcos_gpu import synth, tx
+    monkeypatch.setenv("BCOSGPU_MULTI_PEER", "1")
+    rng = np.random.default_rng(0x8E)
+    sizes = [int(x) for x in rng.integers(0, 700, size=64)]
+    sizes[0], sizes[17], sizes[63] = 0, 1, 0
+    bo = np.zeros(len(sizes) + 1, dtype=np.uint64)
+    bo[1:] = np.cumsum(sizes)
+    n = int(bo[-1])
+    b = synth.make_batch(0, n, seed=0x8E8, flip_frac=0.05, bad_v_frac=0.02)
+    pre, po, sg, so = _host(b)
+    wh, ws, wst = oracle.tx_verify_packed(0, pre, po, sg, so, nthreads=_threads())
+    s = gpu.secp256k1_suite()
+    devs = [0] * 8
+    for width in (2, 16):
+        th, snd, st, root = tx.verify_packed_multi(devs, s, pre, po, sg, so, width=width)
+        assert np.array_equal(th, wh) and np.array_equal(snd, ws) and np.array_equal(st, wst), width
+        assert root == oracle.merkle(oracle.KECCAK256, width, wh), width
+    th, snd, st, roots = tx.blocks_verify_multi(devs, s, pre, po, sg, so, bo, width=2)
+    assert np.array_equal(th, wh) and np.array_equal(snd, ws) and np.array_equal(st, wst)
+    want = [oracle.merkle(oracle.KECCAK256, 2, wh[int(bo[k]):int(bo[k + 1])]) if sizes[k] else bytes(32)
+            for k in range(len(sizes))]
+    assert [r.tobytes() for r in roots] == want
