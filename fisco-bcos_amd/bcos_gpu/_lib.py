@@ -86,6 +86,7 @@ _SIGS = {
     "bcosgpu_secp256k1_recover": (_I, [_I, _P, _P, _SZ, _P]),
     "bcosgpu_secp256k1_verify": (_I, [_I, _P, _P, _P, _SZ]),
     "bcosgpu_sm2_verify": (_I, [_I, _P, _P, _P]),
+    "bcosgpu_coalesce_stats": (_I, [_I, _P, _I]),
     "bcosgpu_init_devices": (_I, [_P, _I]),
     "bcosgpu_secp256k1_recover_batch_multi": (_I, [_P, _I, _P, _P, _SZ, _P, _P, _P]),
     "bcosgpu_sm2_verify_batch_multi": (_I, [_P, _I, _P, _P, _SZ, _P, _P]),

@@ -835,6 +835,12 @@ int bcosgpu_sm2_verify(int device, const uint8_t* pub64, const uint8_t* hash32, 
     return ok ? 1 : 0;
 }
 
+int bcosgpu_coalesce_stats(int device, uint64_t* out10, int reset) {
+    if (!out10) return set_err(BCOSGPU_E_ARG, "null pointer");
+    const int rc = coalesce_stats(device, out10, 10, reset);
+    return rc ? set_err(rc, "bad device") : 0;
+}
+
 // ------------------------------------------------------------------ wedpr-ABI shims
 // On the calling thread's current device.  0 = WEDPR_SUCCESS, -1 = WEDPR_ERROR (invalid input or
 // signature), BCOSGPU_WEDPR_ENGINE_ERROR = the engine failed (no device, HIP error): the message is in

@@ -12,6 +12,8 @@
 // (leader / follower), so nothing runs when nobody calls and nothing needs shutting down.  Up to
 // slots_in_use() batches can be in flight per device at once, each on its own stream: small
 // latency-bound batches occupy a few CUs each, so they overlap on the device instead of queueing.
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -51,12 +53,37 @@ struct Slot {
     size_t d_in_cap = 0, d_out_cap = 0;
 };
 
+// Where a coalesced call's time goes (bcosgpu_coalesce_stats): per device, summed over calls / batches,
+// in nanoseconds.  All updated under the queue mutex except the batch phases (one leader each, atomics).
+enum CoalesceStat {
+    kStBatches = 0,   // batches launched
+    kStJobs,          // calls completed
+    kStItems,         // signatures
+    kStQueueNs,       // per call: enqueue -> its batch taken by a leader
+    kStLeadNs,        // per batch: the leader's host work before the launch (staging, key lookup)
+    kStGpuNs,         // per batch: first launch -> results synchronised (kernel + copies + queue)
+    kStScatterNs,     // per batch: results copied out to the callers
+    kStWakeNs,        // per woken follower / leader: notify -> running again (scheduler latency)
+    kStWakes,         // wake-ups counted in kStWakeNs
+    kStLockNs,        // per call: waiting for the queue mutex on entry
+    kStCount
+};
+
 struct DeviceQueue {
     std::mutex mu;
     uint64_t next_seq = 0;
     std::deque<SigJob*> pending[kSigJobKinds];
     Slot slots[kMaxSlots];
+    std::atomic<uint64_t> stat[kStCount];
+    DeviceQueue() {
+        for (auto& x : stat) x.store(0, std::memory_order_relaxed);
+    }
 };
+
+inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 std::mutex g_qmu;
 DeviceQueue* g_queues[64] = {};  // never freed: no teardown races with the HIP runtime at exit
@@ -122,7 +149,9 @@ int fail(std::vector<SigJob*>& batch, int rc, const std::string& msg) {
     } while (0)
 
 // One coalesced launch for `batch` (all of one kind) on `slot` of `device`.
-int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
+int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch, std::atomic<uint64_t>* stat) {
+    const int64_t t_lead = now_ns();
+    int64_t t_launch = 0, t_synced = 0;
     size_t n = 0;
     bool want_addr = false, want_pub = false;
     for (SigJob* j : batch) {
@@ -210,6 +239,7 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
     if (!zero_copy) BATCH_HIP(hipMemcpyAsync(slot.d_in, slot.h_in, in_bytes, hipMemcpyHostToDevice, slot.stream));
     const uint8_t* di = zero_copy ? slot.hd_in : slot.d_in;
     uint8_t* dout = zero_copy ? slot.hd_out : slot.d_out;
+    t_launch = now_ns();
     for (int attempt = 0; attempt < 2; ++attempt) {
         int rc;
         if (keyed && kind == kSigJobVerifySM2)
@@ -237,6 +267,7 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
         if (!keyed || keyed_generation(vsuite) == gen) break;
         keyed = false;
     }
+    t_synced = now_ns();
     // scatter
     const uint8_t* out = slot.h_out;
     at = 0;
@@ -255,6 +286,11 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
         j->rc = 0;
         at += m;
     }
+    stat[kStBatches].fetch_add(1, std::memory_order_relaxed);
+    stat[kStItems].fetch_add(n, std::memory_order_relaxed);
+    stat[kStLeadNs].fetch_add(static_cast<uint64_t>(t_launch - t_lead), std::memory_order_relaxed);
+    stat[kStGpuNs].fetch_add(static_cast<uint64_t>(t_synced - t_launch), std::memory_order_relaxed);
+    stat[kStScatterNs].fetch_add(static_cast<uint64_t>(now_ns() - t_synced), std::memory_order_relaxed);
     return 0;
 }
 
@@ -264,7 +300,21 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch) {
 // free slot the owner of the oldest queued job (of any kind) to lead the next batch.  (A broadcast on
 // every completion woke all callers -- 256 submitter threads on the box's 16 cores -- per batch: at
 // 256 threads secp256k1 single calls fell to 30k/s with a p99 of 87 ms, profiles/r04_bench_first.json.)
-static void wake_leaders(DeviceQueue& q) {
+// An owner sleeps on its job's own mutex, and a leader marks its batch's jobs done and wakes their owners
+// AFTER releasing the device queue's mutex: at 256 callers on 16 cores, notifying ~20 owners under that
+// mutex held it ~0.1 ms per batch and every new call queued behind it (tools/callbench_sweep.py,
+// profiles/r06_callbench_sweep.json: lock wait 0.17 -> 0.75 ms per call when only the wait moved).
+// A job's owner returns only after taking the job's mutex once its done flag is set, so the leader's
+// notify (under that mutex) has finished with the job before the owner's stack frame goes away.
+static void notify_job(SigJob* j, bool done, int64_t t) {
+    std::lock_guard<std::mutex> g(j->m);
+    if (done) j->done.store(true, std::memory_order_release);
+    else j->woken = true;
+    j->t_notify = t;
+    j->cv.notify_one();
+}
+
+static void wake_leaders(DeviceQueue& q) {  // under q.mu
     int free_slots = 0;
     for (int k = 0; k < slots_in_use(); ++k) free_slots += !q.slots[k].busy;
     for (int pass = 0; pass < kSigJobKinds && free_slots > 0; ++pass) {
@@ -276,10 +326,15 @@ static void wake_leaders(DeviceQueue& q) {
             if (!best || pend.front()->seq < best->seq) best = pend.front();
         }
         if (!best) return;
-        best->woken = true;
-        best->cv.notify_one();
+        notify_job(best, false, now_ns());
         --free_slots;
     }
+}
+
+// done: return only after the notifier has released the job's mutex (see above)
+static int finish(SigJob& job) {
+    std::lock_guard<std::mutex> g(job.m);
+    return job.rc;
 }
 
 int coalesced_run(int device, SigJob& job) {
@@ -289,15 +344,23 @@ int coalesced_run(int device, SigJob& job) {
     }
     if (job.n == 0) return job.rc = 0;
     DeviceQueue& q = *queue_of(device);
+    const int64_t t_call = now_ns();
     std::unique_lock<std::mutex> lk(q.mu);
-    job.done = false;
+    job.t_enq = now_ns();
+    q.stat[kStLockNs].fetch_add(static_cast<uint64_t>(job.t_enq - t_call), std::memory_order_relaxed);
+    job.done.store(false, std::memory_order_relaxed);
     job.queued = true;
     job.woken = false;
+    job.t_notify = 0;
     job.seq = q.next_seq++;
     q.pending[job.kind].push_back(&job);
     // A caller leads only while its own job is still queued (a caller whose job is in flight just waits
     // for its batch to finish).
-    while (!job.done) {
+    while (true) {
+        if (job.done.load(std::memory_order_acquire)) {
+            lk.unlock();
+            return finish(job);
+        }
         Slot* free_slot = nullptr;
         for (int k = 0; k < slots_in_use(); ++k)
             if (!q.slots[k].busy) {
@@ -305,17 +368,33 @@ int coalesced_run(int device, SigJob& job) {
                 break;
             }
         if (!free_slot || !job.queued) {
-            job.cv.wait(lk);
-            job.woken = false;
+            lk.unlock();
+            bool done;
+            {
+                std::unique_lock<std::mutex> jl(job.m);
+                job.cv.wait(jl, [&] { return job.done.load(std::memory_order_acquire) || job.woken; });
+                if (job.t_notify) {  // a targeted wake-up: its scheduler latency
+                    q.stat[kStWakeNs].fetch_add(static_cast<uint64_t>(now_ns() - job.t_notify),
+                                                std::memory_order_relaxed);
+                    q.stat[kStWakes].fetch_add(1, std::memory_order_relaxed);
+                    job.t_notify = 0;
+                }
+                done = job.done.load(std::memory_order_acquire);
+            }
+            if (done) return finish(job);
+            lk.lock();
+            job.woken = false;  // (wake_leaders sets it under q.mu)
             continue;
         }
         // lead: take every queued job of this kind, oldest first, up to kMaxBatch items (at least one)
         auto& pend = q.pending[job.kind];
         std::vector<SigJob*> batch;
         size_t items = 0;
+        const int64_t t_take = now_ns();
         while (!pend.empty() && (batch.empty() || items + pend.front()->n <= kMaxBatch)) {
             items += pend.front()->n;
             pend.front()->queued = false;
+            q.stat[kStQueueNs].fetch_add(static_cast<uint64_t>(t_take - pend.front()->t_enq), std::memory_order_relaxed);
             batch.push_back(pend.front());
             pend.pop_front();
         }
@@ -324,7 +403,7 @@ int coalesced_run(int device, SigJob& job) {
         // a host exception (std::bad_alloc from the staging vectors) fails this batch only: the slot is
         // released and every job of the batch is completed with the error, so no caller waits forever
         try {
-            run_batch(device, job.kind, *free_slot, batch);
+            run_batch(device, job.kind, *free_slot, batch, q.stat);
         } catch (const std::exception& e) {
             fail(batch, BCOSGPU_E_HIP, std::string("signature batch failed on the host: ") + e.what());
         } catch (...) {
@@ -332,13 +411,34 @@ int coalesced_run(int device, SigJob& job) {
         }
         lk.lock();
         free_slot->busy = false;
-        for (SigJob* j : batch) {
-            j->done = true;
-            if (j != &job) j->cv.notify_one();
-        }
         wake_leaders(q);
+        lk.unlock();
+        const int64_t t_done = now_ns();
+        bool mine = false;
+        for (SigJob* j : batch) {
+            if (j == &job) {
+                mine = true;
+                continue;
+            }
+            notify_job(j, true, t_done);  // j's owner may return (and j go away) once this releases j->m
+        }
+        q.stat[kStJobs].fetch_add(batch.size(), std::memory_order_relaxed);
+        if (mine) {
+            job.done.store(true, std::memory_order_release);
+            return job.rc;
+        }
+        lk.lock();  // the batch was full before this caller's own job: lead or wait again
     }
-    return job.rc;
+}
+
+int coalesce_stats(int device, uint64_t* out, int n, int reset) {
+    if (device < 0 || device >= 64 || !out) return BCOSGPU_E_ARG;
+    DeviceQueue& q = *queue_of(device);
+    for (int k = 0; k < kStCount; ++k) {
+        const uint64_t v = reset ? q.stat[k].exchange(0, std::memory_order_relaxed) : q.stat[k].load(std::memory_order_relaxed);
+        if (k < n) out[k] = v;
+    }
+    return 0;
 }
 
 }  // namespace bcosgpu

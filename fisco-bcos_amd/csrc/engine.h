@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include <condition_variable>
 #include <functional>
 #include <string>
@@ -89,11 +90,15 @@ struct SigJob {
     uint8_t* out_ok = nullptr;        // n bytes: 1 valid, 0 invalid
     int rc = 0;                       // filled in by the engine: 0 or BCOSGPU_E_*, with err
     std::string err;
-    bool queued = false, done = false, woken = false;
+    bool queued = false, woken = false;
+    std::atomic<bool> done{false};
     uint64_t seq = 0;                 // arrival order in its device queue
-    std::condition_variable cv;       // its owner sleeps on it (under the device queue's mutex)
+    int64_t t_enq = 0, t_notify = 0;  // steady-clock ns: queued, last notified (coalescer statistics)
+    std::mutex m;                     // its owner sleeps on cv under m (not under the device queue's mutex):
+    std::condition_variable cv;       // done / woken are written under both, read by the owner under m
 };
 int coalesced_run(int device, SigJob& job);
+int coalesce_stats(int device, uint64_t* out, int n, int reset);
 
 // api.hip internals the device-set entry points (multi.hip) share: the calling thread's error message,
 // one-time device initialisation without changing the calling thread's device, a coalesced job

@@ -46,6 +46,8 @@ int main(int argc, char** argv) {
         printf("{\"error\": \"%s\"}\n", bcosgpu_last_error());
         return 1;
     }
+    uint64_t st[10];
+    bcosgpu_coalesce_stats(dev, st, 1);  // zero the coalescer's counters: the timed calls only
     std::atomic<long> mismatches{0}, errors{0};
     std::vector<std::vector<float>> lat(threads);
     std::vector<std::thread> pool;
@@ -71,9 +73,17 @@ int main(int argc, char** argv) {
     for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
     std::sort(all.begin(), all.end());
     const long total = static_cast<long>(threads) * calls;
+    bcosgpu_coalesce_stats(dev, st, 0);
+    // per call: mutex wait, queue wait; per batch: leader's host work, GPU round trip, scatter; per wake-up:
+    // scheduler latency (notify -> running); busy = fraction of the wall time some batch was in flight
+    const double b = st[0] ? double(st[0]) : 1.0, c = st[1] ? double(st[1]) : 1.0, w = st[8] ? double(st[8]) : 1.0;
     printf("{\"suite\": %u, \"threads\": %d, \"calls\": %ld, \"seconds\": %.4f, \"calls_per_s\": %.1f, "
-           "\"latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}, \"mismatches\": %ld, \"engine_errors\": %ld}\n",
+           "\"latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}, \"mismatches\": %ld, \"engine_errors\": %ld, "
+           "\"coalescer\": {\"batches\": %llu, \"calls_per_batch\": %.2f, \"lock_us_per_call\": %.2f, "
+           "\"queue_us_per_call\": %.2f, \"lead_us_per_batch\": %.2f, \"gpu_us_per_batch\": %.2f, "
+           "\"scatter_us_per_batch\": %.2f, \"wake_us\": %.2f, \"wakes_per_call\": %.2f, \"batches_in_flight\": %.3f}}\n",
            suite, threads, total, dt, total / dt, all[all.size() / 2], all[all.size() * 99 / 100], all.back(),
-           mismatches.load(), errors.load());
+           mismatches.load(), errors.load(), (unsigned long long)st[0], st[1] / b, st[9] / c / 1e3, st[3] / c / 1e3,
+           st[4] / b / 1e3, st[5] / b / 1e3, st[6] / b / 1e3, st[7] / w / 1e3, st[8] / c, st[5] / 1e9 / dt);
     return mismatches.load() || errors.load() ? 1 : 0;
 }

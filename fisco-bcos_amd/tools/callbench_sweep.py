@@ -1,5 +1,5 @@
 """Single-call coalescing sweep (tools/callbench.cpp over the coalesced C ABI): host threads x batches
-in flight (BCOSGPU_COALESCE_SLOTS), per suite.  Writes the callbench data file (C2-size synthetic batch,
+in flight (BCOSGPU_COALESCE_SLOTS), per suite, with the coalescer's phase breakdown (bcosgpu_coalesce_stats).  Writes the callbench data file (C2-size synthetic batch,
 expected results from the batch path) to argv[1] and prints one JSON line per configuration."""
 import json
 import os
@@ -34,12 +34,12 @@ def write_data(path, suite, n=8192):
 
 def main():
     out_dir = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-    configs = [(t, sl, zc) for t in (1, 64, 256) for sl in (4, 6) for zc in (0, 2048)]
+    configs = [(t, sl, 2048) for t in (16, 64, 256) for sl in (4, 8)]
     for suite in (0, 1):
         path = os.path.join(out_dir, "callbench_%d.bin" % suite)
         write_data(path, suite)
         for threads, slots, prio in configs:
-            calls = max(20, int(3000 * (0.5 if suite else 1) * min(threads, 64) / 64 / max(threads / 64, 1) ))
+            calls = 1000
             env = dict(os.environ, BCOSGPU_COALESCE_SLOTS=str(slots), BCOSGPU_COALESCE_ZEROCOPY=str(prio))
             r = subprocess.run([EXE, path, str(threads), str(calls)], capture_output=True, text=True, timeout=120,
                                env=env)

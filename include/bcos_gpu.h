@@ -357,6 +357,12 @@ int bcosgpu_secp256k1_verify(int device, const uint8_t* pub64, const uint8_t* ha
                              size_t sig_len);
 /* SM2Crypto::verify (SM2Crypto.cpp:66-79) -> fast_sm2_verify: sig64 = r||s, with the given key. */
 int bcosgpu_sm2_verify(int device, const uint8_t* pub64, const uint8_t* hash32, const uint8_t* sig64);
+/* Where the coalesced calls' time goes on `device` (diagnostics; counters since start or the last reset):
+ * out10 = {batches, calls, signatures, queue ns (sum over calls: enqueued -> taken into a batch), leader ns
+ * (sum over batches: staging and key lookup before the launch), GPU ns (launch -> results synchronised),
+ * scatter ns (results copied to the callers), wake ns (sum over targeted wake-ups: notify -> running),
+ * wake-ups, lock ns (sum over calls: waiting for the queue mutex)}; reset != 0 zeroes them. */
+int bcosgpu_coalesce_stats(int device, uint64_t* out10, int reset);
 
 /* ---------------------------------------------------------------- device sets (one process, several GPUs) */
 /* A FISCO node is ONE process with one CryptoSuite (libinitializer/ProtocolInitializer.cpp:102-124) whose
