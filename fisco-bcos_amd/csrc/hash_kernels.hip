@@ -764,11 +764,16 @@ struct ClimbTree {
     int pair;
 };
 
-template <int H, int W>
+// X (SM3, latency-sized trees of width > 2): the in-workgroup levels above level 1 and the climb steps'
+// levels expand their blocks in parallel first (sm3_level_x, as merkle_wg_kernel's X variant), so C1's SM3
+// root (width 16) runs as ONE launch -- the last workgroup to finish its level-3 node climbs to the root --
+// instead of merkle_wg_kernel + merkle_top_kernel
+template <int H, int W, bool X = false>
 __global__ __launch_bounds__(256) void merkle_climb_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w,
                                                            uint8_t* __restrict__ tree, const ClimbTree f,
                                                            uint8_t* __restrict__ root, uint32_t* __restrict__ ctr) {
     __shared__ uint4 lds[2][256][2];
+    __shared__ uint4 wxs[X ? kWgXBlocks * kSm3Exp / 4 : 1];
     __shared__ uint32_t arrived_s;
     const TreeLevels& t = f.t;
     const uint32_t width = W ? W : static_cast<uint32_t>(w);
@@ -780,7 +785,8 @@ __global__ __launch_bounds__(256) void merkle_climb_kernel(const uint8_t* __rest
         for (int k = 1; k < 8; ++k) e[k] = 0;
     }
     uint64_t j;  // this workgroup's node at level l - 1 (LDS buffer cur, entry 0)
-    int cur = wg_levels<H, W>(lds, leaves, n, width, f.kin, f.B, tree, t, f.pair, f.coop_max, f.pair_max, j);
+    int cur = wg_levels<H, W, X>(lds, leaves, n, width, f.kin, f.B, tree, t, f.pair, f.coop_max, f.pair_max, j,
+                                 reinterpret_cast<uint32_t*>(&wxs[0]));
     int l = f.kin + 1 < t.nlev ? f.kin + 1 : t.nlev;  // next level to compute
     __syncthreads();
     if (l < t.nlev && tid < 8)  // publish it (device-coherent)
@@ -818,6 +824,9 @@ __global__ __launch_bounds__(256) void merkle_climb_kernel(const uint8_t* __rest
                 const uint32_t gq = tid / 32;
                 coop_level_pass<W>(kc, in, nin, width, gq, nn, tree + 32ull * (t.pos[l + i] + 1 + b + gq),
                                    reinterpret_cast<uint8_t*>(&lds[cur ^ 1][gq < 8 ? gq : 0][0]));
+            } else if (X && sm3_level_fits(nn, width, kWgXBlocks)) {  // SM3, blocks expanded at once
+                sm3_level_x(in, nin, width, nn, reinterpret_cast<uint32_t*>(&wxs[0]),
+                            tree + 32ull * (t.pos[l + i] + 1 + b), reinterpret_cast<uint8_t*>(&lds[cur ^ 1][0][0]));
             } else if (tid < nn) {  // SM3: one lane per node (nn <= 64)
                 uint32_t d[8];
                 const uint32_t c = nin - tid * width < width ? nin - tid * width : width;
@@ -876,7 +885,7 @@ static constexpr int kClimbMaxWidth = 4;  // widths the four-wave path takes at 
 
 // returns 1 when it does not apply (too many counters or workgroups, no counter slot)
 static int launch_merkle_climb(int hasher, int width, const uint8_t* d_leaves, uint64_t n, uint8_t* d_tree,
-                               uint8_t* d_root, const TreeLevels& t0, hipStream_t st) {
+                               uint8_t* d_root, const TreeLevels& t0, hipStream_t st, bool sm3x = false) {
     ClimbTree f{};
     f.B = 1;
     f.kin = 0;
@@ -941,12 +950,16 @@ static int launch_merkle_climb(int hasher, int width, const uint8_t* d_leaves, u
     }
     const dim3 g(static_cast<unsigned>(wgs)), b(256);
 #define CLIMB(HH, WW) hipLaunchKernelGGL((merkle_climb_kernel<HH, WW>), g, b, 0, st, d_leaves, n, width, d_tree, f, d_root, ctr)
-    if (hasher == SM3) {
+#define CLIMBX(HH, WW) hipLaunchKernelGGL((merkle_climb_kernel<HH, WW, true>), g, b, 0, st, d_leaves, n, width, d_tree, f, d_root, ctr)
+    if (hasher == SM3 && sm3x && width > 2 && latency) {
+        if (width == 16) CLIMBX(SM3, 16); else CLIMBX(SM3, 0);
+    } else if (hasher == SM3) {
         if (width == 2) CLIMB(SM3, 2); else if (width == 16) CLIMB(SM3, 16); else CLIMB(SM3, 0);
     } else {
         if (width == 2) CLIMB(KECCAK256, 2); else if (width == 16) CLIMB(KECCAK256, 16); else CLIMB(KECCAK256, 0);
     }
 #undef CLIMB
+#undef CLIMBX
     return hipGetLastError() == hipSuccess ? 0 : BCOSGPU_E_HIP;
 }
 
@@ -996,10 +1009,20 @@ int launch_merkle(int hasher, int width, const uint8_t* d_leaves, uint64_t n, ui
     // only narrow Keccak trees (SM3's one-lane levels measured no faster than the two-launch path,
     // profiles/r04_merkle_paths_ab_sm3.json; width 16 has the one-wave kernel)
     const bool big = t.cnt[0] > 256ull * static_cast<uint64_t>(cu_count());
+    // SM3 trees of width > 2 at latency sizes (C1: 100k leaves, width 16) on the climb kernel with expanded
+    // blocks -- one launch instead of merkle_wg_kernel + merkle_top_kernel -- measured no faster (C1 SM3
+    // 0.1058 vs 0.1038 ms, profiles/r06_merkle_sm3_climbx_ab.json: the critical path is 38 serial
+    // compressions either way, and the second launch's gap is a few us), so it is opt-in
+    // (BCOSGPU_MERKLE_SM3CLIMB=1, read once)
+    static const bool sm3climb_env = [] {
+        const char* e = getenv("BCOSGPU_MERKLE_SM3CLIMB");
+        return e && e[0] == '1';
+    }();
+    const bool sm3_climb = hasher == SM3 && width > 2 && !big && sm3climb_env;
     if (fused_env != 1 &&
-        (climb_env == 1 ||
+        (climb_env == 1 || sm3_climb ||
          (climb_env < 0 && ((width <= kClimbMaxWidth && (hasher == KECCAK256 || big)) || (width <= 16 && big))))) {
-        const int rc = launch_merkle_climb(hasher, width, d_leaves, n, d_tree, d_root, t, st);
+        const int rc = launch_merkle_climb(hasher, width, d_leaves, n, d_tree, d_root, t, st, sm3_climb);
         if (rc <= 0) return rc;
     }
     if (fused_env == 1 || (fused_env < 0 && hasher == KECCAK256)) {

@@ -3,14 +3,17 @@ switches (read once per process) times bcosgpu_merkle_root on random leaves per 
 mean of back-to-back launches after a warm-up, as bench.py's Merkle legs -- and checks every root
 against the first path's.  The parent never touches the GPU.  One JSON line.
   merkle_ab.py [HASHER [NxWIDTH ...]]     HASHER 0 = Keccak256 (default), 1 = SM3
-paths: climb (four-wave one-launch), fused (one-wave one-launch), twolaunch (workgroup + top kernels)"""
+paths: default (the library's choice), sm3_climbx (round 6's SM3 climb kernel with expanded blocks, opt-in),
+climb (four-wave one-launch), fused (one-wave one-launch), twolaunch (workgroup + top kernels)"""
 import json
 import os
 import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-PATHS = {"climb": {"BCOSGPU_MERKLE_CLIMB": "1"},
+PATHS = {"default": {},
+         "sm3_climbx": {"BCOSGPU_MERKLE_SM3CLIMB": "1"},
+         "climb": {"BCOSGPU_MERKLE_CLIMB": "1"},
          "fused": {"BCOSGPU_MERKLE_CLIMB": "0", "BCOSGPU_MERKLE_FUSED": "1"},
          "twolaunch": {"BCOSGPU_MERKLE_CLIMB": "0", "BCOSGPU_MERKLE_FUSED": "0"}}
 
