@@ -17,9 +17,8 @@
 //    move, i.e. while the previous chunk computes), an event, the chunk's compute stream waits on it;
 //    once chunk k-1's kernel event has completed, pageable D2H straight into the caller's arrays (so no
 //    copy waits on the GPU while holding the host thread).
-//  - Small batches (<= 65536 txs, one launch: C2's 10k): staged through pinned memory on one stream, the
-//    signatures and offsets gathered while the preimages' DMA runs, one DMA of the outputs back (three
-//    pageable D2H of a 10k batch cost ~65 us, profiles/r06_pipe_trace.txt).
+//  - Small batches (<= 65536 txs, one launch: C2's 10k): staged through pinned memory on one stream, one
+//    DMA in, one DMA of the outputs back (three pageable D2H of a 10k batch cost ~65 us).
 //  - Pipelines come from a per-device pool: concurrent callers (the reference's verifier pools,
 //    TxPool.h:48-49) each get their own streams and buffers, so their round trips overlap instead of
 //    serialising behind one workspace mutex.
@@ -144,9 +143,10 @@ namespace {
 // One launch of a small batch (<= 65536 txs, one chunk), staged through pinned memory on ONE stream (no
 // cross-stream events: an event wait added ~16 us before the kernel started).  Device layout =
 // pinned layout: [preimages | signatures | pad | pre_off[m+1] | sig_off[m+1]] and the outputs
-// [txhash | sender | status].  The host copies the preimages into the staging buffer, starts their DMA,
-// copies the signatures and offsets while it runs and starts the second DMA; kernel, the follow-on tail,
-// one D2H of the outputs, one synchronisation, three host copies out.
+// [txhash | sender | status].  The host gathers everything into the staging buffer and sends it as ONE
+// DMA (two DMAs -- the preimages' started while the rest was gathered -- measured an ~9 us gap between
+// them in the copy queue, profiles/r06_pipe_trace.txt); kernel, the follow-on tail, one D2H of the
+// outputs, one synchronisation, three host copies out.
 int tx_small(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::string& msg) {
     const uint64_t lo = t.lo, hi = t.hi, m = hi - lo;
     for (uint64_t i = lo; i < hi; ++i)
@@ -166,11 +166,10 @@ int tx_small(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::string&
     uint8_t* d = p.b[0].as<uint8_t>();
     hipStream_t st = p.compute;
     std::memcpy(h, t.pre + pb, pbytes);
-    if (pbytes) PIPE_HIP(hipMemcpyAsync(d, h, pbytes, hipMemcpyHostToDevice, st));
     std::memcpy(h + pbytes, t.sig + sb, sbytes);
     std::memcpy(h + spo, t.pre_off + lo, 8 * (m + 1));
     std::memcpy(h + sso, t.sig_off + lo, 8 * (m + 1));
-    PIPE_HIP(hipMemcpyAsync(d + pbytes, h + pbytes, total - pbytes, hipMemcpyHostToDevice, st));
+    PIPE_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, st));
     uint8_t* d_out = p.b[4].as<uint8_t>();
     const int lrc = launch_tx_verify(t.suite, d - pb, reinterpret_cast<const uint64_t*>(d + spo), d + pbytes - sb,
                                      reinterpret_cast<const uint64_t*>(d + sso), m, d_out, d_out + 32 * m,

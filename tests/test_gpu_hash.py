@@ -308,3 +308,44 @@ def test_merkle_one_launch_per_thread_streams(gpu, oracle):
     for width, _, _, roots, want in cases:
         got = roots.cpu().numpy()
         assert all(got[r].tobytes() == want for r in range(30)), width
+
+
+SM3_CLIMBX_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1]]
+import bcos_gpu
+bcos_gpu.ensure_device(0)
+rng = np.random.default_rng(int(sys.argv[2]))
+H = bcos_gpu.SM3()
+for spec in sys.argv[3:]:
+    n, w = (int(x) for x in spec.split("x"))
+    leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    got = bcos_gpu.Merkle(H, w).generate_merkle([leaves[i].tobytes() for i in range(n)])
+    sys.stdout.write(spec + " " + __import__("hashlib").sha256(b"".join(got)).hexdigest() + "\n")
+"""
+
+
+def test_merkle_sm3_climb_expanded_opt_in(gpu, oracle):
+    """The opt-in one-launch SM3 path (BCOSGPU_MERKLE_SM3CLIMB=1, read once per process: a child process):
+    merkle_climb_kernel<SM3, W, true> with the in-workgroup and climb-step levels' blocks expanded at once,
+    widths 3 .. 33 and sizes around the workgroup / climb-group boundaries, C1 included; every entry of the
+    output vector (compared through its SHA-256) equals the oracle's."""
+    import hashlib
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    specs = ["%dx%d" % (n, w) for w, ns in ((3, (10, 244, 6562, 59050)), (5, (626, 3126, 70001)),
+                                             (16, (257, 4097, 65537, 100000)), (17, (290, 4914)), (33, (1090, 40000)))
+             for n in ns]
+    env = dict(os.environ, BCOSGPU_MERKLE_SM3CLIMB="1")
+    r = subprocess.run([sys.executable, "-c", SM3_CLIMBX_CHILD, os.path.join(root, "fisco-bcos_amd"), "83"] + specs,
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = dict(line.split() for line in r.stdout.splitlines())
+    rng = np.random.default_rng(83)
+    for spec in specs:
+        n, w = (int(x) for x in spec.split("x"))
+        leaves = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        _, want = oracle.merkle(1, w, leaves, want_tree=True)
+        assert got[spec] == hashlib.sha256(want.tobytes()).hexdigest(), spec
