@@ -212,7 +212,17 @@ int tx_pipeline(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::stri
     PIPE_HIP(p.b[2].ensure(sbytes + 8));
     PIPE_HIP(p.b[3].ensure((m + 1) * 8));
     PIPE_HIP(p.b[4].ensure(53 * m + 8));
-    const uint64_t nchunks = (m + chunk - 1) / chunk;
+    // chunk boundaries: a quarter-round head chunk first (its upload is the pipeline's exposed start; its
+    // kernel is less efficient, but the next chunk's kernel fills the rest of the GPU beside it on the
+    // other compute stream), then whole rounds (BCOSGPU_PIPE_HEAD=0: no head chunk, an A/B hook)
+    std::vector<uint64_t> cb{0};
+    {
+        const char* he = std::getenv("BCOSGPU_PIPE_HEAD");
+        const bool head = chunk < m && !std::getenv("BCOSGPU_PIPE_CHUNK") && !(he && he[0] == '0');
+        if (head) cb.push_back(chunk / 4);
+        while (cb.back() < m) cb.push_back(std::min(m, cb.back() + chunk));
+    }
+    const uint64_t nchunks = cb.size() - 1;
     PIPE_HIP(ensure_events(p, 2 * nchunks));
     // device views of the whole range: the byte buffers shifted back by the range's first offset, so the
     // caller's offsets index them directly
@@ -226,7 +236,7 @@ int tx_pipeline(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::stri
     if (const char* e = std::getenv("BCOSGPU_PIPE_STREAMS"))  // A/B hook: 1 = every chunk on one stream
         if (e[0] == '1') cs[1] = p.compute;
     auto drain = [&](uint64_t k) -> int {  // the large path: chunk k's outputs once its kernel is done
-        const uint64_t a = k * chunk, e = std::min(m, a + chunk), c = e - a;
+        const uint64_t a = cb[k], e = cb[k + 1], c = e - a;
         PIPE_HIP(hipEventSynchronize(p.ev[2 * k + 1]));
         PIPE_HIP(hipMemcpyAsync(t.txhash32 + 32 * (lo + a), d_hash + 32 * a, 32 * c, hipMemcpyDeviceToHost, p.copy));
         PIPE_HIP(hipMemcpyAsync(t.sender20 + 20 * (lo + a), d_snd + 20 * a, 20 * c, hipMemcpyDeviceToHost, p.copy));
@@ -234,7 +244,7 @@ int tx_pipeline(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::stri
         return 0;
     };
     for (uint64_t k = 0; k < nchunks; ++k) {
-        const uint64_t a = k * chunk, e = std::min(m, a + chunk), c = e - a;
+        const uint64_t a = cb[k], e = cb[k + 1], c = e - a;
         const uint64_t ga = lo + a, ge = lo + e;  // the chunk in the caller's indexing
         for (uint64_t i = ga; i < ge; ++i)
             if (t.pre_off[i + 1] < t.pre_off[i] || t.sig_off[i + 1] < t.sig_off[i] ||

@@ -20,7 +20,7 @@ from hostpath_probe import med  # noqa: E402
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+    n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1_000_000
     reps = 5
     bcos_gpu.ensure_device(0)
     b = synth.make_batch(0, n, seed=0xC4)
@@ -52,13 +52,18 @@ def main():
 
     def bare():
         check(lib().bcosgpu_tx_verify_batch(0, _ptr(pre), _ptr(po), _ptr(sg), _ptr(so), n, _ptr(h), _ptr(s2), _ptr(t2)))
-    for c in (131072, 262144, 524288):
-        for ns in ("1", "2"):
-            os.environ["BCOSGPU_PIPE_CHUNK"], os.environ["BCOSGPU_PIPE_STREAMS"] = str(c), ns
-            out["host_chunk%d_s%s" % (c, ns)] = med(bare, reps)
-    os.environ.pop("BCOSGPU_PIPE_CHUNK")
-    os.environ.pop("BCOSGPU_PIPE_STREAMS")
-    out["host_default"] = med(bare, reps)
+    if "--quick" not in sys.argv:
+        for c in (131072, 262144, 524288):
+            for ns in ("1", "2"):
+                os.environ["BCOSGPU_PIPE_CHUNK"], os.environ["BCOSGPU_PIPE_STREAMS"] = str(c), ns
+                out["host_chunk%d_s%s" % (c, ns)] = med(bare, reps)
+        os.environ.pop("BCOSGPU_PIPE_CHUNK")
+        os.environ.pop("BCOSGPU_PIPE_STREAMS")
+    for rep in range(2):  # alternated A/B of the head chunk
+        os.environ["BCOSGPU_PIPE_HEAD"] = "0"
+        out["host_no_head_%d" % rep] = med(bare, reps)
+        os.environ.pop("BCOSGPU_PIPE_HEAD")
+        out["host_default_%d" % rep] = med(bare, reps)
     out["matches"] = bool(np.array_equal(t2, st.cpu().numpy()) and np.array_equal(h, th.cpu().numpy()))
     print(json.dumps(out), flush=True)
 

@@ -58,9 +58,10 @@ def test_pipeline_chunk_boundaries_vs_oracle(gpu, oracle, suite, monkeypatch):
 
 @pytest.mark.timeout(600)
 def test_pipeline_default_chunks_full_size(gpu, oracle):
-    """2 x 512 x CUs + 1 secp256k1 txs (3 chunks: two full rounds of the occupancy-2 kernel, then one tx)
-    through the host-pointer path == the device-resident single launch; the oracle on every tx around both
-    chunk boundaries and on a 1-in-509 sample."""
+    """2 x 512 x CUs + 1 secp256k1 txs through the host-pointer path (the default chunking: a quarter-round
+    head chunk, a full round of the occupancy-2 kernel, the rest) == the device-resident single launch, and
+    with the head chunk off (two full rounds, then one tx); the oracle on every tx around every chunk
+    boundary and on a 1-in-509 sample."""
     import torch
     from bcos_gpu import device, synth, tx
     cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -73,11 +74,19 @@ def test_pipeline_default_chunks_full_size(gpu, oracle):
     device.tx_verify(0, b.pre, b.pre_off, b.sig, b.sig_off, th_d, snd_d, st_d)
     torch.cuda.synchronize()
     pre, po, sg, so = _host(b)
-    th, snd, st = tx.verify_packed(gpu.secp256k1_suite(), pre, po, sg, so)
-    assert np.array_equal(th, th_d.cpu().numpy())
-    assert np.array_equal(snd, snd_d.cpu().numpy())
-    assert np.array_equal(st, st_d.cpu().numpy())
-    idx = sorted(set(range(c - 3, c + 3)) | set(range(2 * c - 3, n)) | set(range(0, n, 509)))
+    import os
+    for head in ("1", "0"):
+        os.environ["BCOSGPU_PIPE_HEAD"] = head
+        try:
+            th, snd, st = tx.verify_packed(gpu.secp256k1_suite(), pre, po, sg, so)
+        finally:
+            os.environ.pop("BCOSGPU_PIPE_HEAD")
+        assert np.array_equal(th, th_d.cpu().numpy()), head
+        assert np.array_equal(snd, snd_d.cpu().numpy()), head
+        assert np.array_equal(st, st_d.cpu().numpy()), head
+    q = c // 4
+    idx = sorted(set(range(q - 3, q + 3)) | set(range(q + c - 3, q + c + 3)) | set(range(c - 3, c + 3))
+                 | set(range(2 * c - 3, n)) | set(range(0, n, 509)))
     idx = np.array(idx)
     pre_l = [pre[int(po[i]):int(po[i + 1])].tobytes() for i in idx]
     sig_l = [sg[int(so[i]):int(so[i + 1])].tobytes() for i in idx]
