@@ -245,7 +245,12 @@ def test_merkle_sm3_expanded_levels(gpu, oracle):
 
 def test_merkle_one_launch_repeat_two_streams(gpu, oracle):
     """The one-launch path's arrival counters reset themselves (back-to-back launches on one stream) and
-    are per stream (two torch streams at once): 40 C1-sized roots per stream, each equal to the oracle."""
+    are per stream (two torch streams at once): 40 C1-sized roots per stream, each equal to the oracle.
+    Every tensor a side stream writes is held until the final synchronize and is ready (default-stream
+    fill) before that stream starts: a tree freed while its stream still runs goes back to torch's caching
+    allocator, which may hand its memory to the next allocation (the other stream's roots) while the first
+    stream's kernels still write it.  tools/merkle_stream_diag.py runs this with the two streams measured
+    overlapping (profiles/r06_merkle_two_stream_overlap.json)."""
     import torch
     from bcos_gpu import device
     rng = np.random.default_rng(78)
@@ -259,12 +264,13 @@ def test_merkle_one_launch_repeat_two_streams(gpu, oracle):
         width, d_leaves, _ = cases[k]
         tree = torch.empty((device.merkle_size(100_000, width), 32), dtype=torch.uint8, device="cuda")
         roots = torch.zeros((40, 32), dtype=torch.uint8, device="cuda")
-        outs.append(roots)
+        outs.append((roots, tree))  # both held until the synchronize below
+        st.wait_stream(torch.cuda.current_stream())  # after the zero fill
         with torch.cuda.stream(st):
             for r in range(40):
                 device.merkle_root(device.KECCAK256, width, d_leaves, tree, roots[r], st)
     torch.cuda.synchronize()
-    for (width, _, want), roots in zip(cases, outs):
+    for (width, _, want), (roots, _) in zip(cases, outs):
         got = roots.cpu().numpy()
         assert all(got[r].tobytes() == want for r in range(40)), width
 
