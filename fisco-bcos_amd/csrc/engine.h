@@ -137,6 +137,9 @@ struct HostTxRange {
     uint8_t* txhash32 = nullptr;
     uint8_t* sender20 = nullptr;
     uint8_t* status = nullptr;
+    // a quarter-round head chunk first (txpipe.hip); off for a shard that shares its device with another
+    // shard of the same call, whose first chunk already fills the GPU beside it
+    bool head = true;
 };
 // queued on p.compute after every chunk's kernel, before the last download: d_hash = the range's
 // (hi - lo) x 32 tx hashes on the device

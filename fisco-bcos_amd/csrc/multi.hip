@@ -296,6 +296,13 @@ struct Pipes {
     }
 };
 
+// whether shard k is the only shard with work on its device (its pipeline's head chunk pays only then)
+bool sole_on_device(const int* devices, int ndev, int k, const std::function<bool(int)>& has_work) {
+    for (int j = 0; j < ndev; ++j)
+        if (j != k && devices[j] == devices[k] && has_work(j)) return false;
+    return true;
+}
+
 HostTxRange host_range(int suite, const uint8_t* pre, const uint64_t* pre_off, const uint8_t* sig,
                        const uint64_t* sig_off, uint64_t lo, uint64_t hi, uint8_t* txhash32, uint8_t* sender20,
                        uint8_t* status) {
@@ -359,7 +366,9 @@ int tx_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const 
             frontier[k] = q.b[6].as<uint8_t>();
             return lrc;
         };
-        return tx_pipeline(c, host_range(suite, pre, pre_off, sig, sig_off, lo, hi, txhash32, sender20, status), tail, msg);
+        HostTxRange r = host_range(suite, pre, pre_off, sig, sig_off, lo, hi, txhash32, sender20, status);
+        r.head = sole_on_device(devices, ndev, k, [&](int j) { return p.hi[j] > p.lo[j]; });
+        return tx_pipeline(c, r, tail, msg);
     });
     if (rc || !root32) return rc;
     return gather_root(devices, ndev, p, frontier, hasher, width, top, root32);
@@ -419,8 +428,9 @@ int blocks_multi(const int* devices, int ndev, int suite, const uint8_t* pre, co
             if (rrc) m2 = hip_msg(hipGetLastError(), "merkle roots launch");
             return rrc;
         };
-        const int rc = tx_pipeline(c, host_range(suite, pre, pre_off, sig, sig_off, lo, hi, txhash32, sender20, status),
-                                   tail, msg);
+        HostTxRange r = host_range(suite, pre, pre_off, sig, sig_off, lo, hi, txhash32, sender20, status);
+        r.head = sole_on_device(devices, ndev, k, [&](int j) { return block_off[bl[j + 1]] > block_off[bl[j]]; });
+        const int rc = tx_pipeline(c, r, tail, msg);
         if (rc) return rc;
         SHARD_HIP(hipMemcpyAsync(roots32 + 32 * b0, c.b[6].p, nb * 32, hipMemcpyDeviceToHost, c.copy));
         SHARD_HIP(hipStreamSynchronize(c.copy));

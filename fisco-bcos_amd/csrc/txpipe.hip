@@ -214,11 +214,15 @@ int tx_pipeline(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::stri
     PIPE_HIP(p.b[4].ensure(53 * m + 8));
     // chunk boundaries: a quarter-round head chunk first (its upload is the pipeline's exposed start; its
     // kernel is less efficient, but the next chunk's kernel fills the rest of the GPU beside it on the
-    // other compute stream), then whole rounds (BCOSGPU_PIPE_HEAD=0: no head chunk, an A/B hook)
+    // other compute stream), then whole rounds.  Not for a shard sharing its device with another shard of
+    // the call (t.head false): there the other shard's first chunk already fills the GPU, and the head's
+    // partial round only adds a launch (C5 on {0,0}: 71.6M tx/s without it, 68.5M with it;
+    // profiles/r06_devset_head_ab.json).  BCOSGPU_PIPE_HEAD=0/1 forces it off/on (A/B hook).
     std::vector<uint64_t> cb{0};
     {
         const char* he = std::getenv("BCOSGPU_PIPE_HEAD");
-        const bool head = chunk < m && !std::getenv("BCOSGPU_PIPE_CHUNK") && !(he && he[0] == '0');
+        const bool want = he && (he[0] == '0' || he[0] == '1') ? he[0] == '1' : t.head;
+        const bool head = chunk < m && !std::getenv("BCOSGPU_PIPE_CHUNK") && want;
         if (head) cb.push_back(chunk / 4);
         while (cb.back() < m) cb.push_back(std::min(m, cb.back() + chunk));
     }

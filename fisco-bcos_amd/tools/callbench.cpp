@@ -15,7 +15,14 @@
 #include <thread>
 #include <vector>
 
+#include <sched.h>
+#include <sys/resource.h>
+
 #include "../../include/bcos_gpu.h"
+
+static double cpu_seconds(const rusage& r) {
+    return r.ru_utime.tv_sec + r.ru_stime.tv_sec + 1e-6 * (r.ru_utime.tv_usec + r.ru_stime.tv_usec);
+}
 
 int main(int argc, char** argv) {
     if (argc < 4) {
@@ -51,6 +58,8 @@ int main(int argc, char** argv) {
     std::atomic<long> mismatches{0}, errors{0};
     std::vector<std::vector<float>> lat(threads);
     std::vector<std::thread> pool;
+    rusage ru0{}, ru1{};
+    getrusage(RUSAGE_SELF, &ru0);
     const auto t0 = std::chrono::steady_clock::now();
     for (int t = 0; t < threads; ++t) {
         pool.emplace_back([&, t] {
@@ -69,6 +78,14 @@ int main(int argc, char** argv) {
     }
     for (auto& th : pool) th.join();
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    getrusage(RUSAGE_SELF, &ru1);
+    // the host side: CPUs this process may run on, CPU time it used over the timed calls (user + sys, all
+    // threads) as busy cores, and the preemptions (involuntary context switches) per call
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    const int cpus = sched_getaffinity(0, sizeof(cs), &cs) == 0 ? CPU_COUNT(&cs) : -1;
+    const double busy = (cpu_seconds(ru1) - cpu_seconds(ru0)) / dt;
+    const double nivcsw = double(ru1.ru_nivcsw - ru0.ru_nivcsw), nvcsw = double(ru1.ru_nvcsw - ru0.ru_nvcsw);
     std::vector<float> all;
     for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
     std::sort(all.begin(), all.end());
@@ -81,9 +98,12 @@ int main(int argc, char** argv) {
            "\"latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f}, \"mismatches\": %ld, \"engine_errors\": %ld, "
            "\"coalescer\": {\"batches\": %llu, \"calls_per_batch\": %.2f, \"lock_us_per_call\": %.2f, "
            "\"queue_us_per_call\": %.2f, \"lead_us_per_batch\": %.2f, \"gpu_us_per_batch\": %.2f, "
-           "\"scatter_us_per_batch\": %.2f, \"wake_us\": %.2f, \"wakes_per_call\": %.2f, \"batches_in_flight\": %.3f}}\n",
+           "\"scatter_us_per_batch\": %.2f, \"wake_us\": %.2f, \"wakes_per_call\": %.2f, \"batches_in_flight\": %.3f}, "
+           "\"host\": {\"cpus_allowed\": %d, \"cores_busy\": %.2f, \"cpu_us_per_call\": %.2f, "
+           "\"preemptions_per_call\": %.3f, \"voluntary_switches_per_call\": %.3f}}\n",
            suite, threads, total, dt, total / dt, all[all.size() / 2], all[all.size() * 99 / 100], all.back(),
            mismatches.load(), errors.load(), (unsigned long long)st[0], st[1] / b, st[9] / c / 1e3, st[3] / c / 1e3,
-           st[4] / b / 1e3, st[5] / b / 1e3, st[6] / b / 1e3, st[7] / w / 1e3, st[8] / c, st[5] / 1e9 / dt);
+           st[4] / b / 1e3, st[5] / b / 1e3, st[6] / b / 1e3, st[7] / w / 1e3, st[8] / c, st[5] / 1e9 / dt,
+           cpus, busy, busy * dt / total * 1e6, nivcsw / total, nvcsw / total);
     return mismatches.load() || errors.load() ? 1 : 0;
 }
