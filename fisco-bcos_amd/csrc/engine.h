@@ -113,8 +113,9 @@ struct PipeBuf {  // grow-only device buffer
     hipError_t ensure(size_t bytes);
     template <class T> T* as() const { return static_cast<T*>(p); }
 };
-struct PipeHostBuf {  // grow-only pinned host buffer
+struct PipeHostBuf {  // grow-only pinned host buffer, mapped into the device's address space (hd)
     void* p = nullptr;
+    void* hd = nullptr;
     size_t cap = 0;
     hipError_t ensure(size_t bytes);
     template <class T> T* as() const { return static_cast<T*>(p); }
