@@ -25,7 +25,9 @@ class InvalidSignature(Exception):
 
 
 def _ptr(a):
-    return a.ctypes.data_as(ctypes.c_void_p)
+    """the array's data address as an int (every ABI pointer parameter is declared c_void_p, which takes
+    one; ~2 us cheaper per argument than ctypes.data_as on the host-pointer batch calls)"""
+    return a.__array_interface__["data"][0]
 
 
 def _u8(a, shape=None):
