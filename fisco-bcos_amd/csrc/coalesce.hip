@@ -21,6 +21,9 @@
 #include <vector>
 #include <cstdlib>
 #include <cstring>
+#include <sched.h>
+#include <sys/prctl.h>
+#include <time.h>
 #include "engine.h"
 
 namespace bcosgpu {
@@ -39,10 +42,30 @@ int slots_in_use() {
     return n;
 }
 
+// How a leader waits for its batch (BCOSGPU_COALESCE_WAIT, read once): 0 hipStreamSynchronize (the
+// runtime spins on the completion signal), 1 a blocking-sync event (the thread sleeps until the GPU's
+// interrupt), 2 poll the event and yield the CPU between polls, 3 poll the event and sleep ~15 us between
+// polls (1 us timer slack on the leader thread), 4 (default) as 3 until 25 us before the batch's expected
+// end (a running average of the GPU time of the last batches of its kind), then poll without sleeping.
+// hipStreamSynchronize and even a blocking-sync event spin on the CPU for a batch's whole ~0.13-0.35 ms
+// (one core per batch in flight: a lone caller's process used 1.0 core); mode 4 keeps the spin's latency
+// (p50 132.1 vs 132.0 us for one caller) on 0.26 of a core, and 1.6 / 3.9 cores instead of 4.1 / 6.2 at
+// 16 / 64 callers -- cores a node's executor and consensus threads get back -- for throughput within
+// 2-5 % (tools/callbench_sweep.py, profiles/r06_coalesce_wait_ab.jsonl)
+int wait_mode() {
+    static const int m = [] {
+        const char* e = getenv("BCOSGPU_COALESCE_WAIT");
+        const int v = e ? atoi(e) : 4;
+        return v < 0 || v > 4 ? 4 : v;
+    }();
+    return m;
+}
+
 struct Slot {
     int index = 0;
     bool busy = false;
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;  // wait modes 1 and 2
     uint8_t* h_in = nullptr;  // pinned, device-mapped staging
     uint8_t* h_out = nullptr;
     uint8_t* hd_in = nullptr;  // their device addresses (zero-copy small batches)
@@ -178,6 +201,9 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch, std
         const int levels = least >= greatest ? least - greatest + 1 : 1;
         BATCH_HIP(hipStreamCreateWithPriority(&slot.stream, hipStreamNonBlocking, least - slot.index % levels));
     }
+    if (!slot.done && wait_mode() != 0)
+        BATCH_HIP(hipEventCreateWithFlags(&slot.done, hipEventDisableTiming |
+                                                          (wait_mode() == 1 ? hipEventBlockingSync : 0u)));
     // verify kinds stage the keys' cache slots (int32 per item) after the input (registered-key path)
     const bool verify = kind == kSigJobVerifyK1 || kind == kSigJobVerifySM2;
     const size_t slots_at = kInPer[kind] * n;
@@ -261,7 +287,34 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch, std
         }
         if (!zero_copy)
             BATCH_HIP(hipMemcpyAsync(slot.h_out, slot.d_out, out_bytes, hipMemcpyDeviceToHost, slot.stream));
-        BATCH_HIP(hipStreamSynchronize(slot.stream));
+        if (wait_mode() == 0) {
+            BATCH_HIP(hipStreamSynchronize(slot.stream));
+        } else {
+            BATCH_HIP(hipEventRecord(slot.done, slot.stream));
+            if (wait_mode() == 1) {
+                BATCH_HIP(hipEventSynchronize(slot.done));
+            } else {
+                static thread_local bool slack = false;
+                if (wait_mode() >= 3 && !slack) {
+                    (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+                    slack = true;
+                }
+                static std::atomic<int64_t> expect_ns[kSigJobKinds];  // running average GPU time per kind
+                const int64_t sleep_until = wait_mode() == 4 ? t_launch + expect_ns[kind].load(std::memory_order_relaxed) - 25000
+                                                             : INT64_MAX;
+                const timespec nap{0, 15000};
+                hipError_t qe;
+                while ((qe = hipEventQuery(slot.done)) == hipErrorNotReady) {
+                    if (wait_mode() == 2) sched_yield();
+                    else if (now_ns() < sleep_until) nanosleep(&nap, nullptr);
+                }
+                BATCH_HIP(qe);
+                if (wait_mode() == 4) {
+                    const int64_t took = now_ns() - t_launch, e = expect_ns[kind].load(std::memory_order_relaxed);
+                    expect_ns[kind].store(e == 0 ? took : e + (took - e) / 8, std::memory_order_relaxed);
+                }
+            }
+        }
         // the key cache was cleared (bcosgpu_clear_keys) between the lookup and the launch: its slots may
         // have been rebuilt for other keys meanwhile, so this batch runs again on the generic kernels
         if (!keyed || keyed_generation(vsuite) == gen) break;

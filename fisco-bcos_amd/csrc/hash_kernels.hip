@@ -896,8 +896,19 @@ static int launch_merkle_climb(int hasher, int width, const uint8_t* d_leaves, u
     // more workgroups than CUs: the subtree kernel first for levels 0..k (width^k <= 64 level-0 nodes per
     // thread), so that the climb kernel starts with one workgroup per CU
     const uint64_t cus = static_cast<uint64_t>(cu_count());
+    // A/B hooks (read once): BCOSGPU_MERKLE_NOSUB=1 never runs the subtree kernel first (the climb kernel
+    // takes the leaves itself, two workgroups on some CUs); BCOSGPU_MERKLE_LATSCHED=1 keeps the latency
+    // schedule (25-lane groups from eight nodes down) even with more workgroups than CUs
+    static const bool nosub_env = [] {
+        const char* e = getenv("BCOSGPU_MERKLE_NOSUB");
+        return e && e[0] == '1';
+    }();
+    static const bool latsched_env = [] {
+        const char* e = getenv("BCOSGPU_MERKLE_LATSCHED");
+        return e && e[0] == '1';
+    }();
     int k = -1;
-    if ((t0.cnt[0] + f.B - 1) / f.B > cus) {
+    if (!nosub_env && (t0.cnt[0] + f.B - 1) / f.B > cus) {
         uint64_t span = 1;
         for (int q = 0; q + 2 < t0.nlev && span <= 64; ++q, span *= width)
             if ((t0.cnt[q + 1] + f.B - 1) / f.B <= cus) {
@@ -924,7 +935,7 @@ static int launch_merkle_climb(int hasher, int width, const uint8_t* d_leaves, u
     // one lane per node only for level 1's 256); more: every SIMD runs several waves, so each level takes
     // the fewest wave-cycles -- one lane per node (a wave pass of 64 nodes: 22k cycles) down to 64 nodes,
     // lane pairs (32 nodes: 15k) down to 4, 25-lane groups (2 nodes: 9.4k) below
-    const bool latency = wgs <= static_cast<uint64_t>(cu_count());
+    const bool latency = wgs <= static_cast<uint64_t>(cu_count()) || latsched_env;
     f.coop_max = latency ? 8u : 2u;
     f.pair_max = latency ? 128u : 32u;
     f.pair = 1;

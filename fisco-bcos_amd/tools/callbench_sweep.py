@@ -34,17 +34,22 @@ def write_data(path, suite, n=8192):
 
 def main():
     out_dir = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-    configs = [(t, sl, 2048) for t in (16, 64, 256) for sl in (4, 8)]
+    # argv[2]: thread counts, argv[3]: slot counts, argv[4]: BCOSGPU_COALESCE_WAIT modes (comma lists)
+    ths = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [16, 64, 256]
+    sls = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [4, 8]
+    waits = sys.argv[4].split(",") if len(sys.argv) > 4 else [os.environ.get("BCOSGPU_COALESCE_WAIT", "0")]
+    configs = [(t, sl, 2048, w) for t in ths for sl in sls for w in waits]
     for suite in (0, 1):
         path = os.path.join(out_dir, "callbench_%d.bin" % suite)
         write_data(path, suite)
-        for threads, slots, prio in configs:
+        for threads, slots, prio, wait in configs:
             calls = 1000
-            env = dict(os.environ, BCOSGPU_COALESCE_SLOTS=str(slots), BCOSGPU_COALESCE_ZEROCOPY=str(prio))
+            env = dict(os.environ, BCOSGPU_COALESCE_SLOTS=str(slots), BCOSGPU_COALESCE_ZEROCOPY=str(prio),
+                       BCOSGPU_COALESCE_WAIT=wait)
             r = subprocess.run([EXE, path, str(threads), str(calls)], capture_output=True, text=True, timeout=120,
                                env=env)
             res = json.loads(r.stdout.strip().splitlines()[-1]) if r.stdout.strip() else {"rc": r.returncode}
-            res.update(slots=slots, zerocopy=prio, rc=r.returncode)
+            res.update(slots=slots, zerocopy=prio, wait=int(wait), rc=r.returncode)
             print(json.dumps(res), flush=True)
 
 

@@ -4,7 +4,8 @@ mean of back-to-back launches after a warm-up, as bench.py's Merkle legs -- and 
 against the first path's.  The parent never touches the GPU.  One JSON line.
   merkle_ab.py [HASHER [NxWIDTH ...]]     HASHER 0 = Keccak256 (default), 1 = SM3
 paths: default (the library's choice), sm3_climbx (round 6's SM3 climb kernel with expanded blocks, opt-in),
-climb (four-wave one-launch), fused (one-wave one-launch), twolaunch (workgroup + top kernels)"""
+climb (four-wave one-launch), fused (one-wave one-launch), twolaunch (workgroup + top kernels), nosub (the climb
+kernel on the leaves without the subtree kernel first), nosub_lat (nosub on the latency schedule)"""
 import json
 import os
 import subprocess
@@ -15,7 +16,9 @@ PATHS = {"default": {},
          "sm3_climbx": {"BCOSGPU_MERKLE_SM3CLIMB": "1"},
          "climb": {"BCOSGPU_MERKLE_CLIMB": "1"},
          "fused": {"BCOSGPU_MERKLE_CLIMB": "0", "BCOSGPU_MERKLE_FUSED": "1"},
-         "twolaunch": {"BCOSGPU_MERKLE_CLIMB": "0", "BCOSGPU_MERKLE_FUSED": "0"}}
+         "twolaunch": {"BCOSGPU_MERKLE_CLIMB": "0", "BCOSGPU_MERKLE_FUSED": "0"},
+         "nosub": {"BCOSGPU_MERKLE_NOSUB": "1"},
+         "nosub_lat": {"BCOSGPU_MERKLE_NOSUB": "1", "BCOSGPU_MERKLE_LATSCHED": "1"}}
 
 CHILD = r"""
 import sys, time, torch
