@@ -46,7 +46,8 @@ int slots_in_use() {
 // runtime spins on the completion signal), 1 a blocking-sync event (the thread sleeps until the GPU's
 // interrupt), 2 poll the event and yield the CPU between polls, 3 poll the event and sleep ~15 us between
 // polls (1 us timer slack on the leader thread), 4 (default) as 3 until 25 us before the batch's expected
-// end (a running average of the GPU time of the last batches of its kind), then poll without sleeping.
+// end (a running average of the GPU time of the last batches of its kind, kernel family -- registered-key
+// or not -- and size class), then poll without sleeping.
 // hipStreamSynchronize and even a blocking-sync event spin on the CPU for a batch's whole ~0.13-0.35 ms
 // (one core per batch in flight: a lone caller's process used 1.0 core); mode 4 keeps the spin's latency
 // (p50 132.1 vs 132.0 us for one caller) on 0.26 of a core, and 1.6 / 3.9 cores instead of 4.1 / 6.2 at
@@ -299,8 +300,12 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch, std
                     (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
                     slack = true;
                 }
-                static std::atomic<int64_t> expect_ns[kSigJobKinds];  // running average GPU time per kind
-                const int64_t sleep_until = wait_mode() == 4 ? t_launch + expect_ns[kind].load(std::memory_order_relaxed) - 25000
+                // running average GPU time per (kind, registered-key kernel or not, batch size by powers of 2)
+                static std::atomic<int64_t> expect[kSigJobKinds][2][18];
+                int lg = 0;
+                while (lg < 17 && (size_t{1} << (lg + 1)) <= n) ++lg;
+                std::atomic<int64_t>& expect_ns = expect[kind][keyed ? 1 : 0][lg];
+                const int64_t sleep_until = wait_mode() == 4 ? t_launch + expect_ns.load(std::memory_order_relaxed) - 25000
                                                              : INT64_MAX;
                 const timespec nap{0, 15000};
                 hipError_t qe;
@@ -310,8 +315,8 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch, std
                 }
                 BATCH_HIP(qe);
                 if (wait_mode() == 4) {
-                    const int64_t took = now_ns() - t_launch, e = expect_ns[kind].load(std::memory_order_relaxed);
-                    expect_ns[kind].store(e == 0 ? took : e + (took - e) / 8, std::memory_order_relaxed);
+                    const int64_t took = now_ns() - t_launch, e = expect_ns.load(std::memory_order_relaxed);
+                    expect_ns.store(e == 0 ? took : e + (took - e) / 8, std::memory_order_relaxed);
                 }
             }
         }
