@@ -96,9 +96,9 @@ PEAK_ALU_PER_S = 3.7497e13      # full-rate 32-bit VALU (v_alignbit_b32)
 # SURVEY §8d ALU ops per permutation / compression
 KECCAK_F_OPS = 6240
 SM3_C_OPS = 2100
-PMC_GLOB = "r05_pmc_{}.json"
+PMC_GLOB = "r06_pmc_{}.json"
 # per-leg PMC summary of the Merkle and hash legs (tools/leg_run.py under rocprofv3, tools/leg_prof.py)
-LEG_PMC = "r05_pmc_legs.json"
+LEG_PMC = "r06_pmc_legs.json"
 KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_device.h", "fisco-bcos_amd/csrc/ecc_tables.hip", "fisco-bcos_amd/csrc/ecc_sig.hip",
               "fisco-bcos_amd/csrc/ecc_txv.hip", "fisco-bcos_amd/csrc/ecc_coop.hip", "fisco-bcos_amd/csrc/ecc_pair.hip",
               "fisco-bcos_amd/csrc/fe_asm.h", "fisco-bcos_amd/csrc/fe.h",
@@ -106,7 +106,8 @@ KERNEL_SRC = ["fisco-bcos_amd/csrc/ecc_device.h", "fisco-bcos_amd/csrc/ecc_table
               "fisco-bcos_amd/csrc/fe26.h", "fisco-bcos_amd/csrc/ec26.h", "fisco-bcos_amd/csrc/recover26.h",
               "fisco-bcos_amd/csrc/fp26.h", "fisco-bcos_amd/csrc/ecp26.h", "fisco-bcos_amd/csrc/verify_sm2_26.h",
               "fisco-bcos_amd/csrc/ec26_trio.h", "fisco-bcos_amd/csrc/ecp26_trio.h", "fisco-bcos_amd/csrc/ecc_row.hip",
-              "fisco-bcos_amd/csrc/fe_row.h", "fisco-bcos_amd/csrc/ec_row.h"]
+              "fisco-bcos_amd/csrc/fe_row.h", "fisco-bcos_amd/csrc/ec_row.h", "fisco-bcos_amd/csrc/hash_kernels.hip",
+              "fisco-bcos_amd/csrc/sm3_x.h"]
 
 WORKLOADS = {
     "c2": dict(suite=0, n=10_000, scaling="weak",
