@@ -145,11 +145,12 @@ uint64_t tx_pipe_chunk(uint64_t m) {
 }
 
 namespace {
-// The small path's gather into pinned staging, split over the calling thread and a few persistent helper
-// threads: on one core the 2.3 MB of C2's 10k-tx inputs take ~47 us to copy into pinned memory (a
-// quarter of the call's host time; threads spawned per call cost more than they save).  One gather at a
-// time uses the helpers; a concurrent caller copies on its own thread.  BCOSGPU_PIPE_COPY_THREADS =
-// helper count (default 3; 0: the caller alone), read once.
+// The small path's host work -- the offsets check and the gather into pinned staging, the copy of the
+// outputs back -- split over the calling thread and a few persistent helper threads: on one core the
+// 2.3 MB of C2's 10k-tx inputs take ~47 us to copy into pinned memory (a quarter of the call's host time;
+// threads spawned per call cost more than they save).  One call at a time uses the helpers; a concurrent
+// caller works on its own thread.  BCOSGPU_PIPE_COPY_THREADS = helper count (default 3; 0: the caller
+// alone), read once.
 struct CopySeg {
     uint8_t* dst;
     const uint8_t* src;
@@ -164,36 +165,33 @@ void copy_range(const CopySeg* s, int nseg, size_t a, size_t b) {  // bytes [a, 
     }
 }
 
-class CopyPool {
+class HostPool {
 public:
-    static CopyPool& get() {
-        static CopyPool* p = new CopyPool();  // never destroyed: its threads live as long as the process
+    static HostPool& get() {
+        static HostPool* p = new HostPool();  // never destroyed: its threads live as long as the process
         return *p;
     }
-    void run(const CopySeg* segs, int nseg) {
-        size_t total = 0;
-        for (int k = 0; k < nseg; ++k) total += segs[k].n;
+    // fn(part, parts) for part = 0 .. parts - 1, part 0 on the calling thread; parts = 1 (the caller alone)
+    // when `wide` is false, there are no helpers or another caller has them
+    void run(const std::function<void(int, int)>& fn, bool wide) {
         std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
-        if (helpers_ == 0 || total < (256u << 10) || !busy.owns_lock()) {
-            copy_range(segs, nseg, 0, total);
+        if (!wide || helpers_ == 0 || !busy.owns_lock()) {
+            fn(0, 1);
             return;
         }
-        const int parts = helpers_ + 1;
         {
             std::lock_guard<std::mutex> g(mu_);
-            segs_ = segs;
-            nseg_ = nseg;
-            total_ = total;
+            fn_ = &fn;
             left_.store(helpers_, std::memory_order_relaxed);
             ++gen_;
         }
         cv_.notify_all();
-        copy_range(segs, nseg, 0, total / parts);
+        fn(0, helpers_ + 1);
         while (left_.load(std::memory_order_acquire) != 0) sched_yield();
     }
 
 private:
-    CopyPool() {
+    HostPool() {
         const char* e = std::getenv("BCOSGPU_PIPE_COPY_THREADS");
         helpers_ = e ? std::max(0, std::min(15, std::atoi(e))) : 3;
         for (int i = 0; i < helpers_; ++i) std::thread([this, i] { worker(i + 1); }).detach();
@@ -201,19 +199,14 @@ private:
     void worker(int part) {
         uint64_t seen = 0;
         while (true) {
-            const CopySeg* segs;
-            int nseg;
-            size_t total;
+            const std::function<void(int, int)>* fn;
             {
                 std::unique_lock<std::mutex> g(mu_);
                 cv_.wait(g, [&] { return gen_ != seen; });
                 seen = gen_;
-                segs = segs_;
-                nseg = nseg_;
-                total = total_;
+                fn = fn_;
             }
-            const size_t parts = static_cast<size_t>(helpers_) + 1;
-            copy_range(segs, nseg, total * part / parts, total * (part + 1) / parts);
+            (*fn)(part, helpers_ + 1);
             left_.fetch_sub(1, std::memory_order_release);
         }
     }
@@ -221,9 +214,7 @@ private:
     std::mutex run_mu_, mu_;
     std::condition_variable cv_;
     uint64_t gen_ = 0;
-    const CopySeg* segs_ = nullptr;
-    int nseg_ = 0;
-    size_t total_ = 0;
+    const std::function<void(int, int)>* fn_ = nullptr;
     std::atomic<int> left_{0};
 };
 
@@ -236,12 +227,6 @@ private:
 // outputs, one synchronisation, three host copies out.
 int tx_small(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::string& msg) {
     const uint64_t lo = t.lo, hi = t.hi, m = hi - lo;
-    for (uint64_t i = lo; i < hi; ++i)
-        if (t.pre_off[i + 1] < t.pre_off[i] || t.sig_off[i + 1] < t.sig_off[i] ||
-            t.pre_off[i + 1] - t.pre_off[i] > 0xFFFFFFFFull) {
-            msg = "offsets must be non-decreasing";
-            return BCOSGPU_E_ARG;
-        }
     const uint64_t pb = t.pre_off[lo], pbytes = t.pre_off[hi] - pb;
     const uint64_t sb = t.sig_off[lo], sbytes = t.sig_off[hi] - sb;
     const uint64_t spo = (pbytes + sbytes + 15) & ~7ull, sso = spo + 8 * (m + 1), total = sso + 8 * (m + 1);
@@ -252,11 +237,29 @@ int tx_small(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::string&
     uint8_t* h = p.hin.as<uint8_t>();
     uint8_t* d = p.b[0].as<uint8_t>();
     hipStream_t st = p.compute;
+    // each part checks its share of the offsets (nothing is launched unless all pass; the copy spans the
+    // range's endpoints, checked by tx_pipeline, so it is safe either way) and gathers its share of bytes
     const CopySeg segs[4] = {{h, t.pre + pb, pbytes},
                              {h + pbytes, t.sig + sb, sbytes},
                              {h + spo, reinterpret_cast<const uint8_t*>(t.pre_off + lo), 8 * (m + 1)},
                              {h + sso, reinterpret_cast<const uint8_t*>(t.sig_off + lo), 8 * (m + 1)}};
-    CopyPool::get().run(segs, 4);
+    const size_t gather = pbytes + sbytes + 16 * (m + 1);
+    std::atomic<bool> bad{false};
+    HostPool::get().run(
+        [&](int part, int parts) {
+            for (uint64_t i = lo + m * part / parts, e = lo + m * (part + 1) / parts; i < e; ++i)
+                if (t.pre_off[i + 1] < t.pre_off[i] || t.sig_off[i + 1] < t.sig_off[i] ||
+                    t.pre_off[i + 1] - t.pre_off[i] > 0xFFFFFFFFull) {
+                    bad.store(true, std::memory_order_relaxed);
+                    break;
+                }
+            copy_range(segs, 4, gather * part / parts, gather * (part + 1) / parts);
+        },
+        gather >= (256u << 10));
+    if (bad.load()) {
+        msg = "offsets must be non-decreasing";
+        return BCOSGPU_E_ARG;
+    }
     PIPE_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, st));
     // without a tail the kernel writes its outputs straight into the mapped pinned buffer (no D2H copy and
     // no second wait on the copy engine); a tail reads the hashes on the device.  BCOSGPU_PIPE_ZCOUT=0
@@ -279,9 +282,10 @@ int tx_small(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::string&
     uint8_t* o = p.host.as<uint8_t>();
     if (!zc) PIPE_HIP(hipMemcpyAsync(o, d_out, 53 * m, hipMemcpyDeviceToHost, st));
     PIPE_HIP(hipStreamSynchronize(st));
-    std::memcpy(t.txhash32 + 32 * lo, o, 32 * m);
-    std::memcpy(t.sender20 + 20 * lo, o + 32 * m, 20 * m);
-    std::memcpy(t.status + lo, o + 52 * m, m);
+    const CopySeg outs[3] = {{t.txhash32 + 32 * lo, o, 32 * m}, {t.sender20 + 20 * lo, o + 32 * m, 20 * m},
+                             {t.status + lo, o + 52 * m, m}};
+    HostPool::get().run([&](int part, int parts) { copy_range(outs, 3, 53 * m * part / parts, 53 * m * (part + 1) / parts); },
+                        53 * m >= (256u << 10));
     return 0;
 }
 }  // namespace
