@@ -138,16 +138,17 @@ struct HostTxRange {
     uint8_t* txhash32 = nullptr;
     uint8_t* sender20 = nullptr;
     uint8_t* status = nullptr;
-    // a quarter-round head chunk first (txpipe.hip); off for a shard that shares its device with another
-    // shard of the same call, whose first chunk already fills the GPU beside it
-    bool head = true;
+    // shards of the same call with work on this range's device (txpipe.hip): alone (1), the pipeline
+    // starts with a quarter-round head chunk and then takes whole rounds; shared, no head chunk (the other
+    // shards' first chunks already fill the GPU beside it) and chunks of one round / share
+    int share = 1;
 };
 // queued on p.compute after every chunk's kernel, before the last download: d_hash = the range's
 // (hi - lo) x 32 tx hashes on the device
 using PipeTail = std::function<int(TxPipe& p, const uint8_t* d_hash, std::string& msg)>;
 TxPipe* tx_pipe_acquire(int device);  // nullptr on a HIP failure; the calling thread's device is kept
 void tx_pipe_release(TxPipe* p);
-uint64_t tx_pipe_chunk(uint64_t m);
+uint64_t tx_pipe_chunk(uint64_t m, int share = 1);
 // on the calling thread's current device == p.device; returns after every output is in host memory
 int tx_pipeline(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::string& msg);
 

@@ -296,11 +296,12 @@ struct Pipes {
     }
 };
 
-// whether shard k is the only shard with work on its device (its pipeline's head chunk pays only then)
-bool sole_on_device(const int* devices, int ndev, int k, const std::function<bool(int)>& has_work) {
+// shards with work on shard k's device, k included (its pipeline's chunking: txpipe.hip)
+int shards_on_device(const int* devices, int ndev, int k, const std::function<bool(int)>& has_work) {
+    int n = 1;
     for (int j = 0; j < ndev; ++j)
-        if (j != k && devices[j] == devices[k] && has_work(j)) return false;
-    return true;
+        if (j != k && devices[j] == devices[k] && has_work(j)) ++n;
+    return n;
 }
 
 HostTxRange host_range(int suite, const uint8_t* pre, const uint64_t* pre_off, const uint8_t* sig,
@@ -367,7 +368,7 @@ int tx_multi(const int* devices, int ndev, int suite, const uint8_t* pre, const 
             return lrc;
         };
         HostTxRange r = host_range(suite, pre, pre_off, sig, sig_off, lo, hi, txhash32, sender20, status);
-        r.head = sole_on_device(devices, ndev, k, [&](int j) { return p.hi[j] > p.lo[j]; });
+        r.share = shards_on_device(devices, ndev, k, [&](int j) { return p.hi[j] > p.lo[j]; });
         return tx_pipeline(c, r, tail, msg);
     });
     if (rc || !root32) return rc;
@@ -429,7 +430,7 @@ int blocks_multi(const int* devices, int ndev, int suite, const uint8_t* pre, co
             return rrc;
         };
         HostTxRange r = host_range(suite, pre, pre_off, sig, sig_off, lo, hi, txhash32, sender20, status);
-        r.head = sole_on_device(devices, ndev, k, [&](int j) { return block_off[bl[j + 1]] > block_off[bl[j]]; });
+        r.share = shards_on_device(devices, ndev, k, [&](int j) { return block_off[bl[j + 1]] > block_off[bl[j]]; });
         const int rc = tx_pipeline(c, r, tail, msg);
         if (rc) return rc;
         SHARD_HIP(hipMemcpyAsync(roots32 + 32 * b0, c.b[6].p, nb * 32, hipMemcpyDeviceToHost, c.copy));

@@ -129,7 +129,7 @@ void tx_pipe_release(TxPipe* p) {
     g_free[p->device].push_back(p);
 }
 
-uint64_t tx_pipe_chunk(uint64_t m) {
+uint64_t tx_pipe_chunk(uint64_t m, int share) {
     // BCOSGPU_PIPE_CHUNK (read per call; a test hook): force a chunk size, so chunk boundaries can be
     // tested at oracle-sized batches
     if (const char* e = std::getenv("BCOSGPU_PIPE_CHUNK")) {
@@ -137,7 +137,10 @@ uint64_t tx_pipe_chunk(uint64_t m) {
         if (v > 0) return std::min<uint64_t>(m, std::max<uint64_t>(static_cast<uint64_t>(v), (m + 4095) / 4096));
     }
     const uint64_t cus = static_cast<uint64_t>(cu_count());
-    const uint64_t c = 512 * cus;  // one round of the occupancy-2 one-lane kernel
+    // one round of the occupancy-2 one-lane kernel, split between the shards sharing the device (two
+    // shards on {0, 0} with half rounds: C4 68.5M against 67.9M tx/s with whole ones,
+    // profiles/r06_devset_chunk_ab.json)
+    const uint64_t c = 512 * cus / static_cast<uint64_t>(share < 1 ? 1 : share);
     // below two rounds one launch: its kernel choice beats chunks (two co-running halves of C2's 10k
     // trio round measured 0.604 ms against 0.557 for one launch, profiles/r06_hostpath_probe.json: the
     // second half's launch waits for its inputs and its trio round is as long as the whole batch's)
@@ -300,7 +303,7 @@ int tx_pipeline(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::stri
         msg = "offsets must be non-decreasing";
         return BCOSGPU_E_ARG;
     }
-    const uint64_t chunk = tx_pipe_chunk(m);
+    const uint64_t chunk = tx_pipe_chunk(m, t.share);
     bool small = m <= 65536 && chunk == m;
     if (const char* e = std::getenv("BCOSGPU_PIPE_STAGED")) small = small && e[0] != '0';  // A/B hook
     if (small) return tx_small(p, t, tail, msg);
@@ -315,13 +318,13 @@ int tx_pipeline(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::stri
     // chunk boundaries: a quarter-round head chunk first (its upload is the pipeline's exposed start; its
     // kernel is less efficient, but the next chunk's kernel fills the rest of the GPU beside it on the
     // other compute stream), then whole rounds.  Not for a shard sharing its device with another shard of
-    // the call (t.head false): there the other shard's first chunk already fills the GPU, and the head's
+    // the call (t.share > 1): there the other shard's first chunk already fills the GPU, and the head's
     // partial round only adds a launch (C5 on {0,0}: 71.6M tx/s without it, 68.5M with it;
     // profiles/r06_devset_head_ab.json).  BCOSGPU_PIPE_HEAD=0/1 forces it off/on (A/B hook).
     std::vector<uint64_t> cb{0};
     {
         const char* he = std::getenv("BCOSGPU_PIPE_HEAD");
-        const bool want = he && (he[0] == '0' || he[0] == '1') ? he[0] == '1' : t.head;
+        const bool want = he && (he[0] == '0' || he[0] == '1') ? he[0] == '1' : t.share <= 1;
         const bool head = chunk < m && !std::getenv("BCOSGPU_PIPE_CHUNK") && want;
         if (head) cb.push_back(chunk / 4);
         while (cb.back() < m) cb.push_back(std::min(m, cb.back() + chunk));
