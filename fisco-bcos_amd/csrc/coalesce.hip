@@ -21,8 +21,11 @@
 #include <vector>
 #include <cstdlib>
 #include <cstring>
+#include <linux/futex.h>
 #include <sched.h>
 #include <sys/prctl.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <time.h>
 #include "engine.h"
 
@@ -358,18 +361,31 @@ int run_batch(int device, int kind, Slot& slot, std::vector<SigJob*>& batch, std
 // free slot the owner of the oldest queued job (of any kind) to lead the next batch.  (A broadcast on
 // every completion woke all callers -- 256 submitter threads on the box's 16 cores -- per batch: at
 // 256 threads secp256k1 single calls fell to 30k/s with a p99 of 87 ms, profiles/r04_bench_first.json.)
-// An owner sleeps on its job's own mutex, and a leader marks its batch's jobs done and wakes their owners
-// AFTER releasing the device queue's mutex: at 256 callers on 16 cores, notifying ~20 owners under that
-// mutex held it ~0.1 ms per batch and every new call queued behind it (tools/callbench_sweep.py,
-// profiles/r06_callbench_sweep.json: lock wait 0.17 -> 0.75 ms per call when only the wait moved).
-// A job's owner returns only after taking the job's mutex once its done flag is set, so the leader's
-// notify (under that mutex) has finished with the job before the owner's stack frame goes away.
+// An owner sleeps on its job's own futex word, and a leader marks its batch's jobs done and wakes their
+// owners AFTER releasing the device queue's mutex: at 256 callers on 16 cores, notifying ~20 owners under
+// that mutex held it ~0.1 ms per batch and every new call queued behind it (tools/callbench_sweep.py,
+// profiles/r06_callbench_sweep.json: lock wait 0.17 -> 0.75 ms per call when only the wait moved).  The
+// word, not a mutex + condition variable: a notify under the job's mutex woke the owner only for it to
+// block again on that mutex (two context switches per wake-up).  The notifier's last access to the job is
+// the release fetch_or that publishes the bit (rc, outputs and t_notify are written before it); the
+// FUTEX_WAKE after it names only the word's address, so an owner that has already seen the bit and
+// returned (its SigJob gone) costs at most a spurious wake-up of whatever waits there later, which every
+// futex waiter tolerates.
+static constexpr uint32_t kSigWake = 1, kSigDone = 2;
+
+static void futex_wait(std::atomic<uint32_t>& a, uint32_t v) {
+    (void)syscall(SYS_futex, reinterpret_cast<uint32_t*>(&a), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
+}
+static void futex_wake(uint32_t* a) {
+    (void)syscall(SYS_futex, a, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
+
 static void notify_job(SigJob* j, bool done, int64_t t) {
-    std::lock_guard<std::mutex> g(j->m);
-    if (done) j->done.store(true, std::memory_order_release);
-    else j->woken = true;
-    j->t_notify = t;
-    j->cv.notify_one();
+    uint32_t* word = reinterpret_cast<uint32_t*>(&j->wake);
+    if (!done) j->woken = true;  // (under q.mu: wake_leaders)
+    j->t_notify.store(t, std::memory_order_relaxed);
+    j->wake.fetch_or(done ? kSigDone : kSigWake, std::memory_order_release);  // last access to *j
+    futex_wake(word);
 }
 
 static void wake_leaders(DeviceQueue& q) {  // under q.mu
@@ -389,12 +405,6 @@ static void wake_leaders(DeviceQueue& q) {  // under q.mu
     }
 }
 
-// done: return only after the notifier has released the job's mutex (see above)
-static int finish(SigJob& job) {
-    std::lock_guard<std::mutex> g(job.m);
-    return job.rc;
-}
-
 int coalesced_run(int device, SigJob& job) {
     if (device < 0 || device >= 64 || job.kind < 0 || job.kind >= kSigJobKinds) {
         job.err = "bad device or job kind";
@@ -406,19 +416,16 @@ int coalesced_run(int device, SigJob& job) {
     std::unique_lock<std::mutex> lk(q.mu);
     job.t_enq = now_ns();
     q.stat[kStLockNs].fetch_add(static_cast<uint64_t>(job.t_enq - t_call), std::memory_order_relaxed);
-    job.done.store(false, std::memory_order_relaxed);
+    job.wake.store(0, std::memory_order_relaxed);
     job.queued = true;
     job.woken = false;
-    job.t_notify = 0;
+    job.t_notify.store(0, std::memory_order_relaxed);
     job.seq = q.next_seq++;
     q.pending[job.kind].push_back(&job);
     // A caller leads only while its own job is still queued (a caller whose job is in flight just waits
     // for its batch to finish).
     while (true) {
-        if (job.done.load(std::memory_order_acquire)) {
-            lk.unlock();
-            return finish(job);
-        }
+        if (job.wake.load(std::memory_order_acquire) & kSigDone) return job.rc;  // (lk released on return)
         Slot* free_slot = nullptr;
         for (int k = 0; k < slots_in_use(); ++k)
             if (!q.slots[k].busy) {
@@ -427,19 +434,15 @@ int coalesced_run(int device, SigJob& job) {
             }
         if (!free_slot || !job.queued) {
             lk.unlock();
-            bool done;
-            {
-                std::unique_lock<std::mutex> jl(job.m);
-                job.cv.wait(jl, [&] { return job.done.load(std::memory_order_acquire) || job.woken; });
-                if (job.t_notify) {  // a targeted wake-up: its scheduler latency
-                    q.stat[kStWakeNs].fetch_add(static_cast<uint64_t>(now_ns() - job.t_notify),
-                                                std::memory_order_relaxed);
-                    q.stat[kStWakes].fetch_add(1, std::memory_order_relaxed);
-                    job.t_notify = 0;
-                }
-                done = job.done.load(std::memory_order_acquire);
+            uint32_t s;
+            while (((s = job.wake.load(std::memory_order_acquire)) & (kSigWake | kSigDone)) == 0) futex_wait(job.wake, s);
+            const int64_t tn = job.t_notify.exchange(0, std::memory_order_relaxed);
+            if (tn) {  // a targeted wake-up: its scheduler latency
+                q.stat[kStWakeNs].fetch_add(static_cast<uint64_t>(now_ns() - tn), std::memory_order_relaxed);
+                q.stat[kStWakes].fetch_add(1, std::memory_order_relaxed);
             }
-            if (done) return finish(job);
+            if (s & kSigDone) return job.rc;
+            job.wake.fetch_and(~kSigWake, std::memory_order_relaxed);
             lk.lock();
             job.woken = false;  // (wake_leaders sets it under q.mu)
             continue;
@@ -478,13 +481,10 @@ int coalesced_run(int device, SigJob& job) {
                 mine = true;
                 continue;
             }
-            notify_job(j, true, t_done);  // j's owner may return (and j go away) once this releases j->m
+            notify_job(j, true, t_done);  // j's owner may return (and j go away) once the bit is set
         }
         q.stat[kStJobs].fetch_add(batch.size(), std::memory_order_relaxed);
-        if (mine) {
-            job.done.store(true, std::memory_order_release);
-            return job.rc;
-        }
+        if (mine) return job.rc;
         lk.lock();  // the batch was full before this caller's own job: lead or wait again
     }
 }

@@ -90,12 +90,11 @@ struct SigJob {
     uint8_t* out_ok = nullptr;        // n bytes: 1 valid, 0 invalid
     int rc = 0;                       // filled in by the engine: 0 or BCOSGPU_E_*, with err
     std::string err;
-    bool queued = false, woken = false;
-    std::atomic<bool> done{false};
-    uint64_t seq = 0;                 // arrival order in its device queue
-    int64_t t_enq = 0, t_notify = 0;  // steady-clock ns: queued, last notified (coalescer statistics)
-    std::mutex m;                     // its owner sleeps on cv under m (not under the device queue's mutex):
-    std::condition_variable cv;       // done / woken are written under both, read by the owner under m
+    bool queued = false, woken = false;  // under the device queue's mutex
+    uint64_t seq = 0;                    // arrival order in its device queue
+    int64_t t_enq = 0;                   // steady-clock ns: queued (coalescer statistics)
+    std::atomic<int64_t> t_notify{0};    // ... last notified
+    std::atomic<uint32_t> wake{0};       // the owner's futex word: bit 0 woken to lead, bit 1 done (coalesce.hip)
 };
 int coalesced_run(int device, SigJob& job);
 int coalesce_stats(int device, uint64_t* out, int n, int reset);
