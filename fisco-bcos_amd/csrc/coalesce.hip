@@ -12,6 +12,7 @@
 // (leader / follower), so nothing runs when nobody calls and nothing needs shutting down.  Up to
 // slots_in_use() batches can be in flight per device at once, each on its own stream: small
 // latency-bound batches occupy a few CUs each, so they overlap on the device instead of queueing.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -65,6 +66,20 @@ int wait_mode() {
     return m;
 }
 
+// Batches in flight: slots_in_use() while fewer than kDeepCallers callers are inside the device's queue,
+// 2 beyond (with ~256 submitter threads on the box's 16 cores more concurrent leaders only add host CPU
+// -- polling leaders, smaller batches, more wake-ups -- to a process already at its CPU quota:
+// tools/callbench_sweep.py, profiles/r06_callbench_slots.jsonl: secp256k1 at 256 threads 245k calls/s
+// with 4 slots, 347k with 2; at 16 / 64 threads 4 slots stay ahead, 80k / 266k against 72k / 254k).
+// BCOSGPU_COALESCE_DEEP = the caller count (default 128; 0 keeps slots_in_use() always), read once.
+int deep_callers() {
+    static const int n = [] {
+        const char* e = getenv("BCOSGPU_COALESCE_DEEP");
+        return e ? atoi(e) : 128;
+    }();
+    return n;
+}
+
 struct Slot {
     int index = 0;
     bool busy = false;
@@ -98,6 +113,7 @@ enum CoalesceStat {
 
 struct DeviceQueue {
     std::mutex mu;
+    std::atomic<int> callers{0};  // callers inside coalesced_run on this device
     uint64_t next_seq = 0;
     std::deque<SigJob*> pending[kSigJobKinds];
     Slot slots[kMaxSlots];
@@ -388,9 +404,14 @@ static void notify_job(SigJob* j, bool done, int64_t t) {
     futex_wake(word);
 }
 
+static int slots_now(const DeviceQueue& q) {
+    const int deep = deep_callers();
+    return deep > 0 && q.callers.load(std::memory_order_relaxed) >= deep ? std::min(2, slots_in_use()) : slots_in_use();
+}
+
 static void wake_leaders(DeviceQueue& q) {  // under q.mu
     int free_slots = 0;
-    for (int k = 0; k < slots_in_use(); ++k) free_slots += !q.slots[k].busy;
+    for (int k = 0, cap = slots_now(q); k < cap; ++k) free_slots += !q.slots[k].busy;
     for (int pass = 0; pass < kSigJobKinds && free_slots > 0; ++pass) {
         // the kind whose front job has waited longest first (jobs carry their arrival order)
         SigJob* best = nullptr;
@@ -412,6 +433,11 @@ int coalesced_run(int device, SigJob& job) {
     }
     if (job.n == 0) return job.rc = 0;
     DeviceQueue& q = *queue_of(device);
+    struct Inside {
+        std::atomic<int>& c;
+        explicit Inside(std::atomic<int>& x) : c(x) { c.fetch_add(1, std::memory_order_relaxed); }
+        ~Inside() { c.fetch_sub(1, std::memory_order_relaxed); }
+    } inside(q.callers);
     const int64_t t_call = now_ns();
     std::unique_lock<std::mutex> lk(q.mu);
     job.t_enq = now_ns();
@@ -427,7 +453,7 @@ int coalesced_run(int device, SigJob& job) {
     while (true) {
         if (job.wake.load(std::memory_order_acquire) & kSigDone) return job.rc;  // (lk released on return)
         Slot* free_slot = nullptr;
-        for (int k = 0; k < slots_in_use(); ++k)
+        for (int k = 0, cap = slots_now(q); k < cap; ++k)
             if (!q.slots[k].busy) {
                 free_slot = &q.slots[k];
                 break;
