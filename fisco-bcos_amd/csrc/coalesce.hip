@@ -116,12 +116,16 @@ enum CoalesceStat {
 struct DeviceQueue {
     std::mutex mu;
     std::atomic<int> callers{0};  // callers inside coalesced_run on this device
+    // arrivals push their job here without the mutex; whoever holds the mutex moves them to pending
+    std::atomic<SigJob*> incoming{nullptr};
+    std::atomic<int> idle{0};     // slots free within the current cap (written under mu)
     uint64_t next_seq = 0;
     std::deque<SigJob*> pending[kSigJobKinds];
     Slot slots[kMaxSlots];
     std::atomic<uint64_t> stat[kStCount];
     DeviceQueue() {
         for (auto& x : stat) x.store(0, std::memory_order_relaxed);
+        idle.store(slots_in_use(), std::memory_order_relaxed);
     }
 };
 
@@ -411,6 +415,43 @@ static int slots_now(const DeviceQueue& q) {
     return deep > 0 && q.callers.load(std::memory_order_relaxed) >= deep ? std::min(2, slots_in_use()) : slots_in_use();
 }
 
+// Arrivals without the queue mutex (BCOSGPU_COALESCE_LOCKFREE, default 1, read once): a caller pushes its
+// job on q.incoming and takes the mutex only when a slot is free (q.idle > 0); otherwise it sleeps at once,
+// and every holder of the mutex moves the arrivals to pending first.  No arrival is stranded: a leader
+// stores q.idle after freeing its slot and only then drains, while an arrival pushes and only then reads
+// q.idle (all sequentially consistent), so either the leader's drain sees the job or the arrival sees the
+// free slot and comes to lead.  At 256 submitter threads every arrival used to queue on the mutex (tens of
+// us per call under the box's CPU quota, its holders preempted).
+static bool lockfree_arrivals() {
+    static const bool v = [] {
+        const char* e = getenv("BCOSGPU_COALESCE_LOCKFREE");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
+static void refresh_idle(DeviceQueue& q) {  // under q.mu
+    int free_slots = 0;
+    for (int k = 0, cap = slots_now(q); k < cap; ++k) free_slots += !q.slots[k].busy;
+    q.idle.store(free_slots, std::memory_order_seq_cst);
+}
+
+static void drain(DeviceQueue& q) {  // under q.mu: arrivals to pending, in arrival order
+    SigJob* h = q.incoming.exchange(nullptr, std::memory_order_seq_cst);
+    SigJob* fifo = nullptr;
+    while (h) {
+        SigJob* n = h->next;
+        h->next = fifo;
+        fifo = h;
+        h = n;
+    }
+    for (SigJob* j = fifo; j; j = j->next) {
+        j->queued = true;
+        j->seq = q.next_seq++;
+        q.pending[j->kind].push_back(j);
+    }
+}
+
 static void wake_leaders(DeviceQueue& q) {  // under q.mu
     int free_slots = 0;
     for (int k = 0, cap = slots_now(q); k < cap; ++k) free_slots += !q.slots[k].busy;
@@ -440,28 +481,47 @@ int coalesced_run(int device, SigJob& job) {
         explicit Inside(std::atomic<int>& x) : c(x) { c.fetch_add(1, std::memory_order_relaxed); }
         ~Inside() { c.fetch_sub(1, std::memory_order_relaxed); }
     } inside(q.callers);
-    const int64_t t_call = now_ns();
-    std::unique_lock<std::mutex> lk(q.mu);
-    job.t_enq = now_ns();
-    q.stat[kStLockNs].fetch_add(static_cast<uint64_t>(job.t_enq - t_call), std::memory_order_relaxed);
     job.wake.store(0, std::memory_order_relaxed);
-    job.queued = true;
+    job.queued = false;
     job.woken = false;
     job.t_notify.store(0, std::memory_order_relaxed);
-    job.seq = q.next_seq++;
-    q.pending[job.kind].push_back(&job);
+    job.t_enq = now_ns();
+    std::unique_lock<std::mutex> lk(q.mu, std::defer_lock);
+    bool sleep_first = false;
+    if (lockfree_arrivals()) {
+        SigJob* h = q.incoming.load(std::memory_order_relaxed);
+        do {
+            job.next = h;
+        } while (!q.incoming.compare_exchange_weak(h, &job, std::memory_order_seq_cst, std::memory_order_relaxed));
+        sleep_first = q.idle.load(std::memory_order_seq_cst) == 0;  // every slot busy: a leader will drain
+    }
+    if (!sleep_first) {
+        const int64_t t_call = now_ns();
+        lk.lock();
+        q.stat[kStLockNs].fetch_add(static_cast<uint64_t>(now_ns() - t_call), std::memory_order_relaxed);
+        if (lockfree_arrivals()) {
+            drain(q);
+        } else {
+            job.queued = true;
+            job.seq = q.next_seq++;
+            q.pending[job.kind].push_back(&job);
+        }
+    }
     // A caller leads only while its own job is still queued (a caller whose job is in flight just waits
     // for its batch to finish).
     while (true) {
-        if (job.wake.load(std::memory_order_acquire) & kSigDone) return job.rc;  // (lk released on return)
         Slot* free_slot = nullptr;
-        for (int k = 0, cap = slots_now(q); k < cap; ++k)
-            if (!q.slots[k].busy) {
-                free_slot = &q.slots[k];
-                break;
-            }
-        if (!free_slot || !job.queued) {
-            lk.unlock();
+        if (!sleep_first) {
+            if (job.wake.load(std::memory_order_acquire) & kSigDone) return job.rc;  // (lk released on return)
+            for (int k = 0, cap = slots_now(q); k < cap; ++k)
+                if (!q.slots[k].busy) {
+                    free_slot = &q.slots[k];
+                    break;
+                }
+        }
+        if (sleep_first || !free_slot || !job.queued) {
+            if (!sleep_first) lk.unlock();
+            sleep_first = false;
             uint32_t s;
             while (((s = job.wake.load(std::memory_order_acquire)) & (kSigWake | kSigDone)) == 0) futex_wait(job.wake, s);
             const int64_t tn = job.t_notify.exchange(0, std::memory_order_relaxed);
@@ -472,10 +532,12 @@ int coalesced_run(int device, SigJob& job) {
             if (s & kSigDone) return job.rc;
             job.wake.fetch_and(~kSigWake, std::memory_order_relaxed);
             lk.lock();
+            drain(q);
             job.woken = false;  // (wake_leaders sets it under q.mu)
             continue;
         }
         // lead: take every queued job of this kind, oldest first, up to kMaxBatch items (at least one)
+        drain(q);
         auto& pend = q.pending[job.kind];
         std::vector<SigJob*> batch;
         size_t items = 0;
@@ -488,6 +550,7 @@ int coalesced_run(int device, SigJob& job) {
             pend.pop_front();
         }
         free_slot->busy = true;
+        refresh_idle(q);
         lk.unlock();
         // a host exception (std::bad_alloc from the staging vectors) fails this batch only: the slot is
         // released and every job of the batch is completed with the error, so no caller waits forever
@@ -500,6 +563,8 @@ int coalesced_run(int device, SigJob& job) {
         }
         lk.lock();
         free_slot->busy = false;
+        refresh_idle(q);  // before the drain (see lockfree_arrivals)
+        drain(q);
         wake_leaders(q);
         lk.unlock();
         const int64_t t_done = now_ns();
@@ -514,6 +579,7 @@ int coalesced_run(int device, SigJob& job) {
         q.stat[kStJobs].fetch_add(batch.size(), std::memory_order_relaxed);
         if (mine) return job.rc;
         lk.lock();  // the batch was full before this caller's own job: lead or wait again
+        drain(q);
     }
 }
 

@@ -95,6 +95,7 @@ struct SigJob {
     int64_t t_enq = 0;                   // steady-clock ns: queued (coalescer statistics)
     std::atomic<int64_t> t_notify{0};    // ... last notified
     std::atomic<uint32_t> wake{0};       // the owner's futex word: bit 0 woken to lead, bit 1 done (coalesce.hip)
+    SigJob* next = nullptr;              // the device queue's lock-free arrival stack
 };
 int coalesced_run(int device, SigJob& job);
 int coalesce_stats(int device, uint64_t* out, int n, int reset);
