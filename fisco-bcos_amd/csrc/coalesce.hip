@@ -72,7 +72,9 @@ int wait_mode() {
 // tools/callbench_sweep.py, profiles/r06_callbench_slots.jsonl: secp256k1 at 256 threads 245k calls/s
 // with 4 slots, 347k with 2; at 16 / 64 threads 4 slots stay ahead, 80k / 266k against 72k / 254k;
 // the cap against none on one box, profiles/r06_coalesce_deep_ab.json: 257-273k against 187-219k, p99
-// 2 ms against 60 ms).
+// 2 ms against 60 ms).  Measured before the lock-free arrivals below; with them the CPU is no longer the
+// bound, the cap is neutral for secp256k1 and still worth ~6 % for SM2's longer batches at 256 threads
+// (profiles/r06_coalesce_deep_ab2.json), so it stays.
 // BCOSGPU_COALESCE_DEEP = the caller count (default 128; 0 keeps slots_in_use() always), read once.
 int deep_callers() {
     static const int n = [] {
