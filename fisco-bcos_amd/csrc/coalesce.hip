@@ -8,7 +8,8 @@
 // that finds a free launch slot takes EVERY queued job of its kind (up to kMaxBatch items) and runs them
 // as one batch -- assemble into pinned staging, one H2D copy, one launch (the same rounds x latency
 // kernel choice as the tx path, ecc_txv.hip launch_verify), one D2H copy, synchronise, scatter -- while
-// the other callers sleep on the queue.  No dispatcher thread: the callers themselves lead batches
+// the other callers sleep, each on its own job (see notify_job and lockfree_arrivals).  No dispatcher
+// thread: the callers themselves lead batches
 // (leader / follower), so nothing runs when nobody calls and nothing needs shutting down.  Up to
 // slots_in_use() batches can be in flight per device at once, each on its own stream: small
 // latency-bound batches occupy a few CUs each, so they overlap on the device instead of queueing.
