@@ -30,6 +30,7 @@
 // table is never rewritten under a launch that reads it.  Slot ids carry the cache generation: an id from
 // before a clear fails in the kernel instead of naming whichever key now has its index.  The coalesced
 // host-pointer verify calls take this path when every key of the batch is cached.
+#include <algorithm>
 #include <array>
 #include <unordered_map>
 #include <unordered_set>
@@ -437,6 +438,10 @@ struct KeyCache {
     int promoted = 0;  // slots taken by promotion: at most half the capacity, the rest stays for registrations
     int registered = 0;
     uint64_t gen = 0;  // bumped by keyed_clear: a slot looked up under another generation may name another key
+    // the builds' key / slot upload buffer, grow-only: a build under mu costs its upload, the table kernel
+    // and one stream sync, not a hipMalloc + hipFree (a hipFree can wait for the whole device)
+    uint8_t* scratch = nullptr;
+    size_t scratch_cap = 0;
 };
 
 std::mutex g_kc_mu;
@@ -514,8 +519,17 @@ int build_keys(KeyCache& c, int suite, const std::vector<Key64>& todo, std::vect
     std::vector<uint8_t> host(kb + sb);
     for (size_t q = 0; q < keys.size(); ++q) std::memcpy(host.data() + 64 * q, keys[q].data(), 64);
     std::memcpy(host.data() + kb, slots.data(), sb);
-    uint8_t* d = nullptr;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&d), kb + sb);
+    hipError_t e = hipSuccess;
+    if (c.scratch_cap < kb + sb) {
+        if (c.scratch) (void)hipFree(c.scratch);
+        c.scratch = nullptr;
+        c.scratch_cap = 0;
+        const size_t want = std::max<size_t>(kb + sb, (64 + 4) * 64);
+        e = hipMalloc(reinterpret_cast<void**>(&c.scratch), want);
+        if (e == hipSuccess) c.scratch_cap = want;
+        else c.scratch = nullptr;
+    }
+    uint8_t* d = c.scratch;
     if (e == hipSuccess) e = hipMemcpyAsync(d, host.data(), kb + sb, hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
         const uint64_t lanes = static_cast<uint64_t>(keys.size()) * kKeyEntriesPerKey;
@@ -530,7 +544,6 @@ int build_keys(KeyCache& c, int suite, const std::vector<Key64>& todo, std::vect
         const hipError_t e2 = hipStreamSynchronize(st);
         if (e == hipSuccess) e = e2;
     }
-    if (d) (void)hipFree(d);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         for (const Key64& k : keys) c.slot_of.erase(k);
