@@ -327,6 +327,15 @@ int tx_pipeline(TxPipe& p, const HostTxRange& t, const PipeTail& tail, std::stri
         const bool want = he && (he[0] == '0' || he[0] == '1') ? he[0] == '1' : t.share <= 1;
         const bool head = chunk < m && !std::getenv("BCOSGPU_PIPE_CHUNK") && want;
         if (head) cb.push_back(chunk / 4);
+        // a shard sharing its device takes its partial chunk FIRST (BCOSGPU_PIPE_REMFIRST=0/1 forces it
+        // off/on): its small kernel then overlaps the next chunks, where as the last chunk it ran
+        // alone at partial occupancy once the other shard had finished (a 1M C4 block on {0, 0}: ~1 ms of a
+        // lone 41k-tx kernel, tools/trace_timeline.py over tools/pipe_trace.py devset; read per call, as
+        // BCOSGPU_PIPE_HEAD)
+        const char* re = std::getenv("BCOSGPU_PIPE_REMFIRST");
+        const int remfirst_env = re && (re[0] == '0' || re[0] == '1') ? re[0] - '0' : -1;
+        const bool remfirst = !head && chunk < m && m % chunk && (remfirst_env >= 0 ? remfirst_env == 1 : t.share > 1);
+        if (remfirst) cb.push_back(m % chunk);
         while (cb.back() < m) cb.push_back(std::min(m, cb.back() + chunk));
     }
     const uint64_t nchunks = cb.size() - 1;

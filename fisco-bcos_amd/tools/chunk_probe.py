@@ -59,10 +59,13 @@ def main():
                 out["host_chunk%d_s%s" % (c, ns)] = med(bare, reps)
         os.environ.pop("BCOSGPU_PIPE_CHUNK")
         os.environ.pop("BCOSGPU_PIPE_STREAMS")
-    for rep in range(2):  # alternated A/B of the head chunk
+    for rep in range(2):  # alternated A/B of the head chunk and of the partial chunk first
         os.environ["BCOSGPU_PIPE_HEAD"] = "0"
         out["host_no_head_%d" % rep] = med(bare, reps)
+        os.environ["BCOSGPU_PIPE_REMFIRST"] = "1"
+        out["host_remainder_first_%d" % rep] = med(bare, reps)
         os.environ.pop("BCOSGPU_PIPE_HEAD")
+        os.environ.pop("BCOSGPU_PIPE_REMFIRST")
         out["host_default_%d" % rep] = med(bare, reps)
     out["matches"] = bool(np.array_equal(t2, st.cpu().numpy()) and np.array_equal(h, th.cpu().numpy()))
     print(json.dumps(out), flush=True)
