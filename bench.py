@@ -1143,6 +1143,18 @@ def devset_legs(devices, min_seconds=1.0):
     return out
 
 
+def _safe(name, fn):
+    """A rank-0 extra leg: its record, or {"error": ...} (traceback on stderr) when it raises -- one failing
+    extra leg must not cost the run its line.  (The tx legs run on every rank, collectives included, and
+    are not wrapped: a rank that skipped one would hang the others.)"""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        traceback.print_exc()
+        return {"error": "%s: %s" % (type(e).__name__, e), "leg": name}
+
+
 def _g(x, k=4):
     return float("%.*g" % (k, x)) if isinstance(x, (int, float)) and not isinstance(x, bool) else x
 
@@ -1165,6 +1177,10 @@ def summarize(full, head_name):
     out[head_name] = leg(full["head"])
     for k, rec in (full.get("legs") or {}).items():
         out[k] = leg(rec)
+    errs = {k: v["error"] for k, v in full.items() if isinstance(v, dict) and "error" in v}
+    if errs:
+        out["errors"] = {k: v[:200] for k, v in errs.items()}
+    full = {k: v for k, v in full.items() if k not in errs}
     hs = full.get("hashes") or {}
     if hs:
         out["hashes[h/s,frac,useful]"] = {k: [_g(v["hashes_per_s"]), _g(v["roofline"]["frac"], 3),
@@ -1230,6 +1246,8 @@ def compact_line(full):
         "work": "%d txs x %s" % (rf["units_per_launch"], rf["work_per_unit"].split(" (")[0]),
         "evidence": rf.get("traffic_source")}
     cb = full.get("cpu_baseline")
+    if isinstance(cb, dict) and "error" in cb:
+        cb = None
     line["cpu_baseline"] = None if not cb else {
         "value": _g(cb["value"], 5), "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"],
         "sample": cb["sample"], "full_host_estimate": _g(cb["full_host_estimate"]["value"], 4),
@@ -1346,7 +1364,7 @@ def main():
         else:
             devset = [int(x) for x in args.devset.split(",")]
     if devset is not None and rank == 0:
-        full["devset"] = devset_legs(devset)
+        full["devset"] = _safe("devset", lambda: devset_legs(devset))
     if devset is not None and world > 1:
         store = dist.distributed_c10d._get_default_store()
         if rank == 0:
@@ -1357,23 +1375,28 @@ def main():
         threads = cpu_threads()
         if not args.no_extras:
             b = head_state["batch"]
-            full["pcie_inclusive"] = host_api_rate(b, b.suite, head_state["n"])
-            full["create_transaction"] = create_transaction_leg(b, b.suite, head_state["n"], head_state["status"])
+            full["pcie_inclusive"] = _safe("pcie_inclusive", lambda: host_api_rate(b, b.suite, head_state["n"]))
+            full["create_transaction"] = _safe("create_transaction", lambda: create_transaction_leg(
+                b, b.suite, head_state["n"], head_state["status"]))
             from bcos_gpu import synth
-            sm2b = synth.make_batch(1, 10_000, seed=0x5A3)
-            full["interface"] = interface_legs([(0, b), (1, sm2b)])
-            full["sealer_verify"] = sealer_verify_leg(threads)
+            full["interface"] = _safe("interface", lambda: interface_legs(
+                [(0, b), (1, synth.make_batch(1, 10_000, seed=0x5A3))]))
+            full["sealer_verify"] = _safe("sealer_verify", lambda: sealer_verify_leg(threads))
         if not args.no_hashes:
-            full["hashes"] = hash_legs()
+            full["hashes"] = _safe("hashes", hash_legs)
         if not args.no_merkle:
-            full["merkle"] = merkle_legs(0 if args.no_cpu_baseline else threads)
+            full["merkle"] = _safe("merkle", lambda: merkle_legs(0 if args.no_cpu_baseline else threads))
         if not args.no_cpu_baseline:
-            from bcos_gpu import synth
-            batches = [(0, head_state["batch"], min(head_state["n"], 20000))]
-            sm2 = states.get("c3", {}).get("batch") or synth.make_batch(1, 20000, seed=0x5A2)
-            batches.append((1, sm2, 20000))
-            full["cpu_baseline"] = cpu_baseline(batches, threads)
-            full["cpu_baseline"]["merkle"] = (full.get("merkle") or {}).pop("cpu_baseline", None)
+            def cpu_leg():
+                from bcos_gpu import synth
+                batches = [(0, head_state["batch"], min(head_state["n"], 20000))]
+                sm2 = states.get("c3", {}).get("batch") or synth.make_batch(1, 20000, seed=0x5A2)
+                batches.append((1, sm2, 20000))
+                cb = cpu_baseline(batches, threads)
+                mk = full.get("merkle") or {}
+                cb["merkle"] = mk.pop("cpu_baseline", None) if "error" not in mk else None
+                return cb
+            full["cpu_baseline"] = _safe("cpu_baseline", cpu_leg)
     if rank == 0:
         full["head"] = {k: v for k, v in head.items()}
         full["detail_path"] = args.detail_out

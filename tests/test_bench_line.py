@@ -92,3 +92,26 @@ def test_roofline_fracs_of_recorded_legs_do_not_exceed_one():
         fracs += [v["roofline"]["frac"] for v in (full.get(grp) or {}).values()
                   if isinstance(v, dict) and "roofline" in v]
     assert all(f is None or 0 < f <= 1 for f in fracs), fracs
+
+
+def test_line_survives_failed_extra_legs():
+    """An extra rank-0 leg that raised is recorded as {"error": ...} (bench._safe): the line still parses,
+    lists the failed legs under summary.errors, and keeps every other leg; a failed CPU baseline leaves
+    cpu_baseline null."""
+    full = copy.deepcopy(_records()[-1][1])
+    for k in ("devset", "pcie_inclusive", "interface", "merkle", "cpu_baseline"):
+        full[k] = {"error": "RuntimeError: boom " + "x" * 300, "leg": k}
+    text = bench.dumps_line(bench.compact_line(full))
+    back = json.loads(text)
+    assert back["cpu_baseline"] is None
+    assert set(back["summary"]["errors"]) == {"devset", "pcie_inclusive", "interface", "merkle", "cpu_baseline"}
+    assert all(len(v) <= 200 for v in back["summary"]["errors"].values())
+    assert "hashes[h/s,frac,useful]" in back["summary"] and back["value"] == full["value"]
+    assert len(text) < bench.LINE_MAX
+
+
+def test_safe_returns_error_record(capsys):
+    assert bench._safe("x", lambda: {"ok": 1}) == {"ok": 1}
+    r = bench._safe("x", lambda: 1 / 0)
+    assert r["leg"] == "x" and r["error"].startswith("ZeroDivisionError")
+    assert "Traceback" in capsys.readouterr().err
