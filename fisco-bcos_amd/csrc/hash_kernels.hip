@@ -268,6 +268,15 @@ __device__ __forceinline__ int level_mode(uint64_t nout, uint32_t threads, int p
 // the tree's level 1 leaves most of the GPU idle; a throughput-sized level 1 stays one lane per node,
 // which costs fewer instructions per node)
 // X (SM3): levels whose blocks fit kWgXBlocks at once expand them in parallel (sm3_level_x, wx)
+#ifdef BCOSGPU_MERKLE_PROBE  // tools/fusedprobe.hip, climbprobe.hip: per-wave / per-workgroup global timestamps (s_memrealtime, 100 MHz)
+__device__ uint64_t g_mp[4096][40];
+#define MP(k) \
+    if (threadIdx.x == 0 && blockIdx.x < 4096 && (k) < 40) g_mp[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define MP(k) \
+    do {      \
+    } while (0)
+#endif
 static constexpr uint32_t kWgXBlocks = 256, kTopXBlocks = 448;
 template <int H, int W, bool X = false>
 __device__ __forceinline__ int wg_levels(uint4 (*lds)[256][2], const uint8_t* __restrict__ leaves, uint64_t n,
@@ -290,6 +299,7 @@ __device__ __forceinline__ int wg_levels(uint4 (*lds)[256][2], const uint8_t* __
         store_digest(H, reinterpret_cast<uint8_t*>(&lds[0][tid][0]), d);
     }
     int cur = 0;
+    MP(20);
     const int top = kin + 1 < t.nlev ? kin + 1 : t.nlev;  // levels this kernel produces
     for (int l = 1; l < top; ++l) {
         __syncthreads();
@@ -320,6 +330,7 @@ __device__ __forceinline__ int wg_levels(uint4 (*lds)[256][2], const uint8_t* __
         nodes = nn;
         base = nbase;
         B = (B + width - 1) / width;
+        MP(20 + l);
     }
     return cur;
 }
@@ -476,15 +487,7 @@ __device__ __forceinline__ void fused_level(const uint8_t* in, uint64_t nin, uin
     }
 }
 
-#ifdef BCOSGPU_MERKLE_PROBE  // tools/fusedprobe.hip: per-wave global timestamps (s_memrealtime, 100 MHz)
-__device__ uint64_t g_mp[4096][40];
-#define MP(k) \
-    if (threadIdx.x == 0 && blockIdx.x < 4096 && (k) < 40) g_mp[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime()
-#else
-#define MP(k) \
-    do {      \
-    } while (0)
-#endif
+
 template <int H, int W>
 __global__ __launch_bounds__(64) void merkle_fused_kernel(const uint8_t* __restrict__ leaves, uint64_t n, int w,
                                                           uint8_t* __restrict__ tree, const FusedTree f,
@@ -785,8 +788,11 @@ __global__ __launch_bounds__(256) void merkle_climb_kernel(const uint8_t* __rest
         for (int k = 1; k < 8; ++k) e[k] = 0;
     }
     uint64_t j;  // this workgroup's node at level l - 1 (LDS buffer cur, entry 0)
+    MP(0);
     int cur = wg_levels<H, W, X>(lds, leaves, n, width, f.kin, f.B, tree, t, f.pair, f.coop_max, f.pair_max, j,
                                  reinterpret_cast<uint32_t*>(&wxs[0]));
+    MP(1);
+    [[maybe_unused]] int step = 0;  // climb steps taken (the probe build's stamps)
     int l = f.kin + 1 < t.nlev ? f.kin + 1 : t.nlev;  // next level to compute
     __syncthreads();
     if (l < t.nlev && tid < 8)  // publish it (device-coherent)
@@ -808,6 +814,7 @@ __global__ __launch_bounds__(256) void merkle_climb_kernel(const uint8_t* __rest
         __syncthreads();
         if (arrived_s != kids) return;  // a sibling's workgroup climbs on
         asm volatile("" ::: "memory");  // the children's loads stay after the counter (compiler order)
+        MP(2 + 2 * step);
         uint32_t* buf = reinterpret_cast<uint32_t*>(&lds[0][0][0]);
         const uint8_t* src = tree + 32ull * (t.pos[l - 1] + 1 + first);
         for (uint32_t q = tid; q < 8u * kids; q += 256u) buf[q] = ld_dev(src + 4u * q);
@@ -840,6 +847,8 @@ __global__ __launch_bounds__(256) void merkle_climb_kernel(const uint8_t* __rest
         }
         j = P;
         l += g;
+        MP(3 + 2 * step);
+        ++step;
         if (l < t.nlev && tid < 8)
             st_dev(tree + 32ull * (t.pos[l - 1] + 1 + j) + 4 * tid, reinterpret_cast<const uint32_t*>(&lds[cur][0][0])[tid]);
     }
