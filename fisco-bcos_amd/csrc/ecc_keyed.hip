@@ -25,13 +25,14 @@
 //
 // Host side: a per-(device, suite) cache of key tables, filled by bcosgpu_register_keys (the node's
 // consensus list) and by promotion of keys named in three verify calls (counted once per call; SM2
-// recover -- admission, the sender's own key -- never promotes; at most 16 builds a call, in at most half
-// the capacity); never evicted while the process runs (bcosgpu_clear_keys drains the device first), so a
+// recover -- admission, the sender's own key -- never promotes; at most 16 keys a build, one build in
+// flight, built asynchronously and published when done, in at most half the capacity); never evicted while the process runs (bcosgpu_clear_keys drains the device first), so a
 // table is never rewritten under a launch that reads it.  Slot ids carry the cache generation: an id from
 // before a clear fails in the kernel instead of naming whichever key now has its index.  The coalesced
 // host-pointer verify calls take this path when every key of the batch is cached.
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <unordered_map>
 #include <unordered_set>
 #include "ecc_device.h"
@@ -429,10 +430,22 @@ struct Key64Hash {
 
 struct KeyCache {
     std::mutex mu;
+    std::mutex init_mu;              // prepare_promotion
+    std::atomic<bool> ready{false};  // ... has run
     uint32_t* arena = nullptr;
     int cap = 0;
     bool alloc_failed = false;
-    std::unordered_map<Key64, int32_t, Key64Hash> slot_of;
+    std::unordered_map<Key64, int32_t, Key64Hash> slot_of;  // published: table built
+    std::unordered_map<Key64, int32_t, Key64Hash> pending;  // promoted, table being built (async)
+    int32_t next = 0;  // arena indices handed out this generation (published, pending, failed builds)
+    // the one promotion build in flight: on its own lowest-priority stream, published (slot_of) by the
+    // first cache call after its event completes (poll_build)
+    bool building = false;
+    uint64_t build_gen = 0;
+    hipStream_t build_stream = nullptr;
+    hipEvent_t build_done = nullptr;
+    std::vector<Key64> build_keys;
+    std::vector<uint8_t> build_host;  // the build's upload source, alive until the build completes
     std::unordered_map<Key64, uint32_t, Key64Hash> seen;
     uint64_t hits = 0, misses = 0, builds = 0;
     int promoted = 0;  // slots taken by promotion: at most half the capacity, the rest stays for registrations
@@ -467,8 +480,7 @@ int capacity_env() {
 inline uint32_t gen_tag(uint64_t gen) { return static_cast<uint32_t>(gen & 0x7FFFu); }
 inline int32_t slot_id(uint64_t gen, int32_t index) { return static_cast<int32_t>((gen_tag(gen) << 16) | uint32_t(index)); }
 
-// tables built by promotion in one call at most: a build runs synchronously under the cache mutex, so
-// this bounds the stall one batch can cause every caller of the device
+// tables built by one promotion build at most (keyed_slots: asynchronous, one in flight)
 constexpr int kPromoteBuildsPerCall = 16;
 
 int promote_after() {
@@ -482,43 +494,30 @@ int promote_after() {
     return k;
 }
 
-// Under c.mu on the current device: give every key of `todo` a slot and build its table on st,
-// synchronously (a build is rare -- registration, promotion -- and the slots become visible to other
-// threads only after c.mu is released, by which time their tables exist).
-int build_keys(KeyCache& c, int suite, const std::vector<Key64>& todo, std::vector<int32_t>& got, hipStream_t st) {
-    got.assign(todo.size(), -1);
-    if (todo.empty()) return 0;
-    if (!c.arena && !c.alloc_failed) {
-        const int cap = capacity_env();
-        if (cap > 0 && hipMalloc(&c.arena, static_cast<size_t>(cap) * kKeySlotWords * 4) == hipSuccess) {
-            c.cap = cap;
-        } else {
-            (void)hipGetLastError();
-            c.arena = nullptr;
-            c.alloc_failed = true;
-        }
+// Under c.mu: the key arena, allocated on first use (capacity_env() tables).
+void ensure_arena(KeyCache& c) {
+    if (c.arena || c.alloc_failed) return;
+    const int cap = capacity_env();
+    if (cap > 0 && hipMalloc(&c.arena, static_cast<size_t>(cap) * kKeySlotWords * 4) == hipSuccess) {
+        c.cap = cap;
+    } else {
+        (void)hipGetLastError();
+        c.arena = nullptr;
+        c.alloc_failed = true;
     }
-    const int32_t old = static_cast<int32_t>(c.slot_of.size());
-    std::vector<Key64> keys;
-    std::vector<int32_t> slots;
-    for (size_t q = 0; q < todo.size(); ++q) {
-        auto it = c.slot_of.find(todo[q]);
-        if (it != c.slot_of.end()) {
-            got[q] = it->second;
-            continue;
-        }
-        const int32_t sl = static_cast<int32_t>(c.slot_of.size());
-        if (!c.arena || sl >= c.cap) continue;  // full: not cached
-        c.slot_of.emplace(todo[q], sl);
-        keys.push_back(todo[q]);
-        slots.push_back(sl);
-        got[q] = sl;
-    }
-    if (keys.empty()) return 0;
-    const size_t kb = 64 * keys.size(), sb = 4 * slots.size();
-    std::vector<uint8_t> host(kb + sb);
+}
+
+// Under c.mu on the current device: build the tables of `keys` at arena indices `idx` on st -- with
+// `async`, record c.build_done after it and return (c.build_host keeps the upload's source), else
+// synchronise st.  One build uses c.scratch at a time: an async one is in flight only while c.building,
+// and a synchronous one (registration) first waits for it (keyed_slots).
+int build_tables(KeyCache& c, int suite, const std::vector<Key64>& keys, const std::vector<int32_t>& idx,
+                 hipStream_t st, bool async) {
+    const size_t kb = 64 * keys.size(), sb = 4 * idx.size();
+    std::vector<uint8_t>& host = c.build_host;
+    host.resize(kb + sb);
     for (size_t q = 0; q < keys.size(); ++q) std::memcpy(host.data() + 64 * q, keys[q].data(), 64);
-    std::memcpy(host.data() + kb, slots.data(), sb);
+    std::memcpy(host.data() + kb, idx.data(), sb);
     hipError_t e = hipSuccess;
     if (c.scratch_cap < kb + sb) {
         if (c.scratch) (void)hipFree(c.scratch);
@@ -541,28 +540,99 @@ int build_keys(KeyCache& c, int suite, const std::vector<Key64>& todo, std::vect
             hipLaunchKernelGGL(key_table_kernel<BCOSGPU_SUITE_SECP256K1>, grid, block, 0, st, c.arena,
                                reinterpret_cast<const int32_t*>(d + kb), d, static_cast<uint32_t>(keys.size()));
         e = hipGetLastError();
-        const hipError_t e2 = hipStreamSynchronize(st);
+        const hipError_t e2 = async ? hipEventRecord(c.build_done, st) : hipStreamSynchronize(st);
         if (e == hipSuccess) e = e2;
     }
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        for (const Key64& k : keys) c.slot_of.erase(k);
-        for (auto& g : got)
-            if (g >= old) g = -1;
         return BCOSGPU_E_HIP;
     }
-    c.builds += keys.size();
     return 0;
+}
+
+// Outside c.mu, once per cache: what the first promotion needs -- the arena, the build stream and event,
+// and the code object holding the table kernel (HIP loads it on first use, ~10 ms) -- so that no lookup
+// waits behind these one-time costs.  Failures leave promotion off (build_stream null).
+void prepare_promotion(KeyCache& c, int suite) {
+    std::unique_lock<std::mutex> i(c.init_mu, std::try_to_lock);  // another caller preparing: skip, this
+    if (!i.owns_lock() || c.ready.load(std::memory_order_acquire)) return;  // call does not promote
+    bool need_arena;
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        need_arena = !c.arena && !c.alloc_failed;
+    }
+    uint32_t* arena = nullptr;
+    const int cap = capacity_env();
+    if (need_arena && (cap <= 0 || hipMalloc(&arena, static_cast<size_t>(cap) * kKeySlotWords * 4) != hipSuccess)) {
+        (void)hipGetLastError();
+        arena = nullptr;
+    }
+    hipStream_t s = nullptr;
+    hipEvent_t ev = nullptr;
+    hipFuncAttributes fa;
+    int least = 0, greatest = 0;
+    bool ok = hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+              hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least) == hipSuccess &&
+              hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+    if (ok && suite == BCOSGPU_SUITE_SM2)
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&key_table_kernel<BCOSGPU_SUITE_SM2>)) == hipSuccess;
+    else if (ok)
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&key_table_kernel<BCOSGPU_SUITE_SECP256K1>)) ==
+             hipSuccess;
+    if (!ok) (void)hipGetLastError();
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        if (need_arena && !c.arena && arena) {
+            c.arena = arena;
+            c.cap = cap;
+            arena = nullptr;
+        } else if (need_arena && !c.arena) {
+            c.alloc_failed = true;
+        }
+        if (ok) {
+            c.build_stream = s;
+            c.build_done = ev;
+        }
+    }
+    if (arena) (void)hipFree(arena);  // a registration allocated the arena meanwhile
+    c.ready.store(true, std::memory_order_release);
+}
+
+// Under c.mu: publish the promotion build in flight once it has completed (`wait`: block until then).
+// A build from before a bcosgpu_clear_keys (another generation) or a failed one publishes nothing.
+void poll_build(KeyCache& c, bool wait) {
+    if (!c.building) return;
+    hipError_t q = wait ? hipEventSynchronize(c.build_done) : hipEventQuery(c.build_done);
+    if (q == hipErrorNotReady) return;
+    c.building = false;
+    const bool live = c.build_gen == c.gen;
+    for (const Key64& k : c.build_keys) {
+        auto it = live ? c.pending.find(k) : c.pending.end();
+        if (it == c.pending.end()) continue;
+        if (q == hipSuccess) {
+            c.slot_of.emplace(k, it->second);
+            c.seen.erase(k);
+            ++c.builds;
+            ++c.promoted;
+        }
+        c.pending.erase(it);
+    }
+    if (q != hipSuccess) (void)hipGetLastError();
+    c.build_keys.clear();
 }
 
 }  // namespace
 
 // Slot ids of n keys (pub i at pubs + pub_stride * i) on the current device; keys not cached are built
-// when `force` (registration), or -- when `promote` -- once seen in promote_after() calls.  A key counts
-// once per call however often it occurs in it, and only calls that name their keys explicitly promote
-// (the sealer path: SignatureCrypto::verify(pub, ...)); admission (SM2 recover, whose key is the
-// sender's) only looks keys up.  At most kPromoteBuildsPerCall tables are built per call.  Ids carry the
-// cache generation (slot_id).  Returns 0 and *all = every key has a slot, or < 0.
+// when `force` (registration, synchronously: the ids returned name built tables), or -- when `promote` --
+// once seen in promote_after() calls.  A key counts once per call however often it occurs in it, and only
+// calls that name their keys explicitly promote (the sealer path: SignatureCrypto::verify(pub, ...));
+// admission (SM2 recover, whose key is the sender's) only looks keys up.  A promotion build runs
+// asynchronously on the cache's own lowest-priority stream, at most kPromoteBuildsPerCall keys and one
+// build at a time: the batch that promotes a key, and every batch until its table is published, takes
+// the generic kernels, so no caller waits for a build (a build is ~0.9 ms, latency-bound, whatever its
+// key count: profiles/r06_tail_ab.json).  Ids carry the cache generation (slot_id).  Returns 0 and
+// *all = every key has a slot, or < 0.
 int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int32_t* out, bool force, bool* all,
                 hipStream_t st, uint64_t* gen, bool promote) {
     int dev = 0;
@@ -573,12 +643,16 @@ int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int
         return 0;
     }
     KeyCache& c = *cache_of(dev, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
-    std::lock_guard<std::mutex> g(c.mu);
-    if (gen) *gen = c.gen;
     promote = promote && !force && promote_after() > 0;
+    if (promote && !c.ready.load(std::memory_order_acquire)) prepare_promotion(c, suite);
+    std::lock_guard<std::mutex> g(c.mu);
+    poll_build(c, force);  // a registration reuses the scratch buffer: the build in flight finishes first
+    if (gen) *gen = c.gen;
+    promote = promote && c.build_stream && c.arena;
     if (!force && c.slot_of.empty() && !promote) return 0;
-    std::vector<Key64> todo;
-    std::vector<size_t> todo_at;
+    std::vector<Key64> keys;      // tables this call builds ...
+    std::vector<int32_t> idx;     // ... at these arena indices
+    std::vector<size_t> want_at;  // (force) positions that take a key built by this call
     std::unordered_set<Key64, Key64Hash> first, counted;  // this call's keys being built / already counted
     bool every = true;
     for (size_t i = 0; i < n; ++i) {
@@ -590,50 +664,57 @@ int keyed_slots(int suite, const uint8_t* pubs, size_t pub_stride, size_t n, int
             continue;
         }
         out[i] = -1;
-        if (!force && !promote) {
-            every = false;
+        if (force && first.count(k)) {  // a repeat within this registration: it follows its first occurrence
+            want_at.push_back(i);
             continue;
         }
-        if (first.count(k)) {  // a repeat within this call: it follows its first occurrence's build
-            todo.push_back(k);
-            todo_at.push_back(i);
-            continue;
-        }
-        if (!force && !counted.insert(k).second) {  // counted once already in this call, not built
-            every = false;
-            continue;
-        }
+        every = false;
+        if (!force && (!promote || c.building || c.pending.count(k) || !counted.insert(k).second)) continue;
         bool build = force;
         if (!build && c.promoted + static_cast<int>(first.size()) < capacity_env() / 2 &&
             static_cast<int>(first.size()) < kPromoteBuildsPerCall) {
             if (c.seen.size() > (1u << 16)) c.seen.clear();  // a bounded sketch of recent keys
             build = ++c.seen[k] >= static_cast<uint32_t>(promote_after());
         }
-        if (build) {
-            first.insert(k);
-            todo.push_back(k);
-            todo_at.push_back(i);
-        } else {
-            every = false;
-        }
+        if (!build) continue;
+        if (force) ensure_arena(c);
+        if (!c.arena || c.next >= c.cap) continue;  // the cache is full: not cached
+        first.insert(k);
+        keys.push_back(k);
+        idx.push_back(c.next++);
+        if (force) want_at.push_back(i);
     }
-    if (!todo.empty()) {
-        std::vector<int32_t> got;
-        const int before = static_cast<int>(c.slot_of.size());
-        const int rc = build_keys(c, suite, todo, got, st);
-        if (rc) return rc;
-        (force ? c.registered : c.promoted) += static_cast<int>(c.slot_of.size()) - before;
-        for (size_t q = 0; q < todo.size(); ++q) {
-            out[todo_at[q]] = got[q] < 0 ? -1 : slot_id(c.gen, got[q]);
-            if (got[q] < 0) every = false;
-            else c.seen.erase(todo[q]);
-        }
+    if (keys.empty()) {
+        (every ? c.hits : c.misses) += n;
+        *all = every;
+        return 0;
     }
-    if (every) {
-        c.hits += n;
-    } else {
+    if (!force) {
+        if (build_tables(c, suite, keys, idx, c.build_stream, true) == 0) {
+            for (size_t q = 0; q < keys.size(); ++q) c.pending.emplace(keys[q], idx[q]);
+            c.build_keys = keys;
+            c.build_gen = c.gen;
+            c.building = true;
+        }
         c.misses += n;
+        return 0;
     }
+    const int rc = build_tables(c, suite, keys, idx, st, false);
+    if (rc) return rc;
+    for (size_t q = 0; q < keys.size(); ++q) {
+        c.slot_of.emplace(keys[q], idx[q]);
+        c.seen.erase(keys[q]);
+    }
+    c.builds += keys.size();
+    c.registered += static_cast<int>(keys.size());
+    every = true;
+    for (size_t i : want_at) {
+        Key64 k;
+        std::memcpy(k.data(), pubs + pub_stride * i, 64);
+        out[i] = slot_id(c.gen, c.slot_of.at(k));
+    }
+    for (size_t i = 0; i < n; ++i) every = every && out[i] >= 0;
+    (every ? c.hits : c.misses) += n;
     *all = every;
     return 0;
 }
@@ -649,7 +730,7 @@ int launch_sig_verify_keyed(int suite, const int32_t* d_slots, const uint8_t* d_
     {
         std::lock_guard<std::mutex> g(c.mu);
         arena = c.arena;
-        cap = static_cast<uint32_t>(c.slot_of.size());
+        cap = static_cast<uint32_t>(c.next);  // a batch holds published ids only; pending ones are below next
         gen15 = gen_tag(c.gen);
     }
     if (!arena) return BCOSGPU_E_ARG;  // no key registered on this device
@@ -682,6 +763,7 @@ int keyed_cache_info(int device, int suite, int64_t out[5]) {
     if (device < 0 || device >= 64) return BCOSGPU_E_ARG;
     KeyCache& c = *cache_of(device, suite == BCOSGPU_SUITE_SM2 ? 1 : 0);
     std::lock_guard<std::mutex> g(c.mu);
+    poll_build(c, false);
     out[0] = static_cast<int64_t>(c.slot_of.size());
     out[1] = c.arena ? c.cap : capacity_env();
     out[2] = static_cast<int64_t>(c.hits);
@@ -702,6 +784,10 @@ int keyed_clear(int device, int suite) {
     if (prev != device) (void)hipSetDevice(prev);
     if (e != hipSuccess) return BCOSGPU_E_HIP;
     c.slot_of.clear();
+    c.pending.clear();  // the device drained: a build in flight has completed, and is dropped unpublished
+    c.building = false;
+    c.build_keys.clear();
+    c.next = 0;
     c.seen.clear();
     c.promoted = c.registered = 0;
     ++c.gen;

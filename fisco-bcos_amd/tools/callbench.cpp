@@ -56,7 +56,7 @@ int main(int argc, char** argv) {
     uint64_t st[10];
     bcosgpu_coalesce_stats(dev, st, 1);  // zero the coalescer's counters: the timed calls only
     std::atomic<long> mismatches{0}, errors{0};
-    std::vector<std::vector<float>> lat(threads);
+    std::vector<std::vector<float>> lat(threads), when(threads);  // latency, start (us since t0)
     std::vector<std::thread> pool;
     rusage ru0{}, ru1{};
     getrusage(RUSAGE_SELF, &ru0);
@@ -64,10 +64,12 @@ int main(int argc, char** argv) {
     for (int t = 0; t < threads; ++t) {
         pool.emplace_back([&, t] {
             lat[t].reserve(calls);
+            when[t].reserve(calls);
             uint8_t pub[64];
             for (int j = 0; j < calls; ++j) {
                 const size_t i = (static_cast<size_t>(j) * threads + t) % m;
                 const auto a = std::chrono::steady_clock::now();
+                when[t].push_back(std::chrono::duration<float, std::micro>(a - t0).count());
                 const int rc = one(i, pub);
                 lat[t].push_back(std::chrono::duration<float, std::micro>(std::chrono::steady_clock::now() - a).count());
                 if (rc < 0) ++errors;
@@ -90,6 +92,17 @@ int main(int argc, char** argv) {
     for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
     std::sort(all.begin(), all.end());
     const long total = static_cast<long>(threads) * calls;
+    // the tail: calls slower than 4 x p50, by the tenth of the timed run they started in
+    const float slow = 4.0f * all[all.size() / 2];
+    long by_tenth[10] = {0};
+    for (int t = 0; t < threads; ++t)
+        for (size_t j = 0; j < lat[t].size(); ++j)
+            if (lat[t][j] > slow) ++by_tenth[std::min(9, static_cast<int>(when[t][j] / (dt * 1e5)))];
+    char tail[256];
+    snprintf(tail, sizeof tail, "{\"p90\": %.1f, \"p95\": %.1f, \"p999\": %.1f, \"slow_us\": %.1f, \"slow_by_tenth\": [%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld,%ld]}",
+             all[all.size() * 90 / 100], all[all.size() * 95 / 100], all[all.size() * 999 / 1000], slow, by_tenth[0],
+             by_tenth[1], by_tenth[2], by_tenth[3], by_tenth[4], by_tenth[5], by_tenth[6], by_tenth[7], by_tenth[8],
+             by_tenth[9]);
     bcosgpu_coalesce_stats(dev, st, 0);
     // per call: mutex wait, queue wait; per batch: leader's host work, GPU round trip, scatter; per wake-up:
     // scheduler latency (notify -> running); busy = fraction of the wall time some batch was in flight
@@ -100,10 +113,10 @@ int main(int argc, char** argv) {
            "\"queue_us_per_call\": %.2f, \"lead_us_per_batch\": %.2f, \"gpu_us_per_batch\": %.2f, "
            "\"scatter_us_per_batch\": %.2f, \"wake_us\": %.2f, \"wakes_per_call\": %.2f, \"batches_in_flight\": %.3f}, "
            "\"host\": {\"cpus_allowed\": %d, \"cores_busy\": %.2f, \"cpu_us_per_call\": %.2f, "
-           "\"preemptions_per_call\": %.3f, \"voluntary_switches_per_call\": %.3f}}\n",
+           "\"preemptions_per_call\": %.3f, \"voluntary_switches_per_call\": %.3f}, \"tail\": %s}\n",
            suite, threads, total, dt, total / dt, all[all.size() / 2], all[all.size() * 99 / 100], all.back(),
            mismatches.load(), errors.load(), (unsigned long long)st[0], st[1] / b, st[9] / c / 1e3, st[3] / c / 1e3,
            st[4] / b / 1e3, st[5] / b / 1e3, st[6] / b / 1e3, st[7] / w / 1e3, st[8] / c, st[5] / 1e9 / dt,
-           cpus, busy, busy * dt / total * 1e6, nivcsw / total, nvcsw / total);
+           cpus, busy, busy * dt / total * 1e6, nivcsw / total, nvcsw / total, tail);
     return mismatches.load() || errors.load() ? 1 : 0;
 }

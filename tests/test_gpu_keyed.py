@@ -103,6 +103,17 @@ def _oracle_verify(oracle, suite, pub, h, sig):
     return oracle.secp256k1_verify(pub, h, sig[:64])
 
 
+def _wait_built(gpu, suite, target, timeout=10.0):
+    """Promotion builds run asynchronously (ecc_keyed.hip keyed_slots): poll the cache until `target` tables
+    have been built and published."""
+    import time
+    t0 = time.monotonic()
+    while gpu.key_cache_info(suite)["built"] < target:
+        assert time.monotonic() - t0 < timeout, "promotion build not published"
+        time.sleep(0.001)
+    return gpu.key_cache_info(suite)
+
+
 def _keyed_dev(suite, slots, h, sig):
     import torch
     from bcos_gpu import device
@@ -197,8 +208,10 @@ def test_registered_key_exceptional_additions(gpu, oracle):
 
 
 def test_promotion_single_calls_and_sm2_recover(gpu, oracle):
-    """Keys seen in three calls are promoted (BCOSGPU_KEY_PROMOTE, default 3): the third batch and the single
-    SignatureCrypto::verify calls after it run on the registered-key kernel with the oracle's verdicts; SM2
+    """Keys seen in three calls are promoted (BCOSGPU_KEY_PROMOTE, default 3): the third batch starts their
+    table build (asynchronous; that batch itself stays on the generic kernels), and the batches and single
+    SignatureCrypto::verify calls after it is published run on the registered-key kernel with the oracle's
+    verdicts; SM2
     recover (SM2Crypto::recover, embedded key) over registered keys returns the same addresses as the
     generic path."""
     rng = np.random.default_rng(777)
@@ -214,9 +227,12 @@ def test_promotion_single_calls_and_sm2_recover(gpu, oracle):
         assert np.array_equal(crypto.verify_batch(pub, h, sig), want)   # first sighting: generic
         assert np.array_equal(crypto.verify_batch(pub, h, sig), want)   # second: generic
         assert gpu.key_cache_info(suite)["built"] == i0["built"]
-        assert np.array_equal(crypto.verify_batch(pub, h, sig), want)   # third: promoted, keyed
+        assert np.array_equal(crypto.verify_batch(pub, h, sig), want)   # third: promoted
+        i1 = _wait_built(gpu, suite, i0["built"] + nk)
+        assert i1["built"] - i0["built"] == nk and i1["keys"] - i0["keys"] == nk
+        assert np.array_equal(crypto.verify_batch(pub, h, sig), want)   # after the build: keyed
+        assert gpu.key_cache_info(suite)["keyed"] - i1["keyed"] >= nk
         i1 = gpu.key_cache_info(suite)
-        assert i1["built"] - i0["built"] == nk and i1["keyed"] - i0["keyed"] >= nk
         for i in range(nk):
             assert crypto.verify(pub[i].tobytes(), h[i].tobytes(), sig[i].tobytes())
             bad = bytearray(sig[i].tobytes())
@@ -303,5 +319,58 @@ def test_promotion_counts_calls_not_occurrences(gpu, oracle):
                 assert okr.all()
             assert gpu.key_cache_info(suite)["built"] == b0
         assert crypto.verify_batch(pub[rep], h[rep], sig[rep]).all()  # third named call: promoted
-        assert gpu.key_cache_info(suite)["built"] - b0 == 2
+        assert _wait_built(gpu, suite, b0 + 2)["built"] - b0 == 2
+        gpu.clear_keys(suite)
+
+
+def test_promotion_under_concurrent_calls(gpu, oracle):
+    """Promotion builds run asynchronously (ecc_keyed.hip keyed_slots: one build in flight, published when
+    its event completes): 24 threads make single SignatureCrypto::verify calls over 48 keys -- each key
+    seen many times, so builds start, complete and publish while other threads look the same keys up --
+    and a registration of half the keys (which waits for a build in flight) lands in the middle.  Every verdict equals the expected one (1 in 4 signatures corrupted), every
+    key ends up with exactly one table, and the registered keys' ids name published tables."""
+    import threading
+    rng = np.random.default_rng(2468)
+    for suite in (0, 1):
+        gpu.clear_keys(suite)
+        crypto = gpu.SM2Crypto() if suite else gpu.Secp256k1Crypto()
+        nk = 48
+        sk = _keys(rng, nk)
+        h = rng.integers(0, 256, size=(nk, 32), dtype=np.uint8)
+        pub, sig, ok = _dev_sign(gpu, suite, sk, h)
+        assert ok.all()
+        sig = sig.copy()
+        bad = np.arange(nk) % 4 == 3
+        sig[bad, 5] ^= 0x10
+        want = np.array([_oracle_verify(oracle, suite, pub[i].tobytes(), h[i].tobytes(), sig[i].tobytes())
+                         for i in range(nk)])
+        assert not want[bad].any() and want[~bad].all()
+        b0 = gpu.key_cache_info(suite)["built"]
+        wrong, errors = [], []
+        start = threading.Barrier(25)
+
+        def caller(t):
+            try:
+                start.wait()
+                for j in range(60):
+                    i = (j * 7 + t * 5) % nk
+                    if crypto.verify(pub[i].tobytes(), h[i].tobytes(), sig[i].tobytes()) != bool(want[i]):
+                        wrong.append((t, j, i))
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=caller, args=(t,)) for t in range(24)]
+        for x in th:
+            x.start()
+        start.wait()
+        slots = gpu.register_keys(suite, pub[::2])
+        for x in th:
+            x.join()
+        assert not errors and not wrong, (errors, wrong[:5])
+        assert (slots >= 0).all()
+        gpu.register_keys(suite, pub[:1])  # registered already: waits for a promotion build still in flight
+        info = gpu.key_cache_info(suite)
+        assert info["keys"] == info["built"] - b0 <= nk
+        assert np.array_equal(_keyed_dev(suite, slots, h[::2], sig[::2]), want[::2])
+        assert np.array_equal(crypto.verify_batch(pub, h, sig), want)
         gpu.clear_keys(suite)
